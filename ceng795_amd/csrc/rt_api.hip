@@ -1,0 +1,433 @@
+// C-ABI implementation (include/ceng795_rt.h): scene upload, render launches, counters.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <exception>
+#include <memory>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/ceng795_rt.h"
+#include "host_scene.h"
+#include "rt_internal.h"
+
+namespace rt {
+hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
+                         const float* normals, const DevMaterial* mats, const DevLight* lights,
+                         bool fast, bool deep, hipStream_t stream);
+int max_supported_depth();
+void write_png(const std::string& path, const float* rgb, int w, int h);
+}  // namespace rt
+
+using namespace rt;
+
+struct rt_scene {
+  HostScene host;
+  int device = 0;
+  int mode = RT_TRAVERSAL_FAST;
+  bool deep = false;
+  bool needs_recursion = false;
+  DevNode* d_nodes = nullptr;
+  DevPrim* d_prims = nullptr;
+  float* d_normals = nullptr;
+  DevMaterial* d_mats = nullptr;
+  DevLight* d_lights = nullptr;
+  unsigned long long* d_counters = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_error;
+
+int set_error(int code, const std::string& msg) {
+  g_error = msg;
+  return code;
+}
+
+struct HipFailure {
+  hipError_t err;
+  const char* what;
+};
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw HipFailure{e, what};
+}
+
+template <typename F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const HipFailure& h) {
+    return set_error(RT_E_HIP, std::string(h.what) + ": " + hipGetErrorString(h.err));
+  } catch (const std::domain_error& e) {
+    return set_error(RT_E_UNSUPPORTED, e.what());
+  } catch (const std::invalid_argument& e) {
+    return set_error(RT_E_INVALID, e.what());
+  } catch (const std::ios_base::failure& e) {
+    return set_error(RT_E_IO, e.what());
+  } catch (const std::runtime_error& e) {
+    return set_error(RT_E_PARSE, e.what());
+  } catch (const std::bad_alloc&) {
+    return set_error(RT_E_INVALID, "out of host memory");
+  } catch (const std::exception& e) {
+    return set_error(RT_E_INVALID, e.what());
+  }
+}
+
+template <typename T>
+T* upload(const std::vector<T>& v, const char* what) {
+  T* p = nullptr;
+  const size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+  hip_check(hipMalloc(&p, bytes), what);
+  if (!v.empty()) hip_check(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice), what);
+  return p;
+}
+
+void free_device(rt_scene* s) {
+  int cur = 0;
+  if (hipGetDevice(&cur) == hipSuccess && cur != s->device) (void)hipSetDevice(s->device);
+  (void)hipFree(s->d_nodes);
+  (void)hipFree(s->d_prims);
+  (void)hipFree(s->d_normals);
+  (void)hipFree(s->d_mats);
+  (void)hipFree(s->d_lights);
+  (void)hipFree(s->d_counters);
+  if (cur != s->device) (void)hipSetDevice(cur);
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    hip_check(hipGetDevice(&prev), "hipGetDevice");
+    if (prev != dev) hip_check(hipSetDevice(dev), "hipSetDevice");
+  }
+  ~DeviceGuard() {
+    int cur;
+    if (hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int create_from_host(rt_scene* s, int device) {
+  if (device < 0) hip_check(hipGetDevice(&device), "hipGetDevice");
+  s->device = device;
+  DeviceGuard g(device);
+  const HostScene& h = s->host;
+  if (h.depth > max_supported_depth())
+    throw std::invalid_argument("BVH deeper than " + std::to_string(max_supported_depth()) +
+                                " levels is not supported");
+  s->deep = h.depth > kLaneStack - 2;
+  for (const DevMaterial& m : h.materials) {
+    const bool mirror = m.mirror[0] != 0 || m.mirror[1] != 0 || m.mirror[2] != 0;
+    const bool glass = m.transparency[0] != 0 || m.transparency[1] != 0 || m.transparency[2] != 0;
+    if ((mirror || glass) && h.max_depth > 0) s->needs_recursion = true;
+  }
+  s->d_nodes = upload(h.nodes, "upload nodes");
+  s->d_prims = upload(h.prims, "upload prims");
+  s->d_normals = upload(h.normals, "upload normals");
+  s->d_mats = upload(h.materials, "upload materials");
+  s->d_lights = upload(h.lights, "upload lights");
+  hip_check(hipMalloc(&s->d_counters, sizeof(unsigned long long) * 4 * kCounterRows),
+            "alloc counters");
+  hip_check(hipMemset(s->d_counters, 0, sizeof(unsigned long long) * 4 * kCounterRows),
+            "zero counters");
+  return RT_OK;
+}
+
+struct TilePlan {
+  int rows, tiles_x, tiles_total;
+};
+
+TilePlan plan(const rt_camera& c, int row0, int row_stride) {
+  TilePlan p;
+  p.rows = row0 < c.height ? (c.height - row0 + row_stride - 1) / row_stride : 0;
+  p.tiles_x = (c.width + kTile - 1) / kTile;
+  p.tiles_total = p.tiles_x * ((p.rows + kTile - 1) / kTile);
+  return p;
+}
+
+RenderParams make_params(const rt_scene* s, int cam, int row0, int row_stride, int tile_begin,
+                         int tile_step, int tile_major, float* out, bool counters) {
+  const HostScene& h = s->host;
+  const rt_camera& c = h.cameras[cam];
+  RenderParams P;
+  std::memset(&P, 0, sizeof P);
+  P.nodes = s->d_nodes;
+  P.prims = s->d_prims;
+  P.normals = s->d_normals;
+  P.materials = s->d_mats;
+  P.lights = s->d_lights;
+  P.num_lights = (int)h.lights.size();
+  P.max_depth = h.max_depth;
+  std::memcpy(P.background, h.background, sizeof P.background);
+  std::memcpy(P.ambient, h.ambient, sizeof P.ambient);
+  P.eps = h.eps;
+  P.root_kind = h.root_kind;
+  P.root_ref = h.root_ref;
+  std::memcpy(P.root_box, h.root_box, sizeof P.root_box);
+  std::memcpy(P.cam_e, c.e, 12);
+  std::memcpy(P.cam_tl, c.top_left, 12);
+  std::memcpy(P.cam_su, c.s_u, 12);
+  std::memcpy(P.cam_sv, c.s_v, 12);
+  P.width = c.width;
+  P.height = c.height;
+  const TilePlan tp = plan(c, row0, row_stride);
+  P.row0 = row0;
+  P.row_stride = row_stride;
+  P.rows = tp.rows;
+  P.tiles_x = tp.tiles_x;
+  P.tiles_total = tp.tiles_total;
+  P.tile_begin = tile_begin;
+  P.tile_step = tile_step;
+  P.num_sel_tiles =
+      tile_begin < tp.tiles_total ? (tp.tiles_total - tile_begin + tile_step - 1) / tile_step : 0;
+  P.tile_major = tile_major;
+  P.out = out;
+  P.counters = counters ? s->d_counters : nullptr;
+  return P;
+}
+
+void check_render_args(const rt_scene* s, int cam, int row0, int row_stride) {
+  if (!s) throw std::invalid_argument("scene is NULL");
+  if (cam < 0 || cam >= (int)s->host.cameras.size())
+    throw std::invalid_argument("camera index out of range");
+  if (row0 < 0 || row_stride < 1) throw std::invalid_argument("bad row selection");
+  if (s->host.cameras[cam].num_samples != 1)
+    throw std::domain_error("NumSamples > 1 (jittered MSAA, HW2/Scene.cpp:32-69) is not supported yet");
+  if (s->needs_recursion)
+    throw std::domain_error("mirror / dielectric recursion (HW2/Scene.cpp:141-194) is not supported yet");
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return CENG795_RT_ABI_VERSION; }
+const char* rt_last_error(void) { return g_error.c_str(); }
+
+int rt_camera_from_view(const float position[3], const float gaze[3], const float up[3],
+                        const float near_plane[4], float near_distance, int width, int height,
+                        int num_samples, rt_camera* out) {
+  if (!position || !gaze || !up || !near_plane || !out || width <= 0 || height <= 0)
+    return set_error(RT_E_INVALID, "rt_camera_from_view: bad argument");
+  camera_from_view(position, gaze, up, near_plane, near_distance, width, height,
+                   num_samples < 1 ? 1 : num_samples, *out);
+  return RT_OK;
+}
+
+int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
+  if (!desc || !out) return set_error(RT_E_INVALID, "rt_scene_create: NULL argument");
+  *out = nullptr;
+  auto s = std::make_unique<rt_scene>();
+  const int rc = guarded([&] {
+    build_host_scene(*desc, s->host);
+    return create_from_host(s.get(), device);
+  });
+  if (rc != RT_OK) {
+    free_device(s.get());
+    return rc;
+  }
+  *out = s.release();
+  return RT_OK;
+}
+
+int rt_scene_load_xml(const char* xml_path, int device, rt_scene** out) {
+  if (!xml_path || !out) return set_error(RT_E_INVALID, "rt_scene_load_xml: NULL argument");
+  *out = nullptr;
+  auto s = std::make_unique<rt_scene>();
+  const int rc = guarded([&] {
+    XmlSceneStorage st;
+    rt_scene_desc d;
+    load_scene_xml(xml_path, st, d);
+    s->host.image_names = st.image_names;
+    build_host_scene(d, s->host);
+    return create_from_host(s.get(), device);
+  });
+  if (rc != RT_OK) {
+    free_device(s.get());
+    return rc;
+  }
+  *out = s.release();
+  return RT_OK;
+}
+
+void rt_scene_destroy(rt_scene* s) {
+  if (!s) return;
+  free_device(s);
+  delete s;
+}
+
+int rt_scene_num_cameras(const rt_scene* s) { return s ? (int)s->host.cameras.size() : 0; }
+int rt_scene_num_lights(const rt_scene* s) { return s ? (int)s->host.lights.size() : 0; }
+int rt_scene_bvh_depth(const rt_scene* s) { return s ? s->host.depth : 0; }
+
+int rt_scene_camera(const rt_scene* s, int cam, rt_camera* out) {
+  if (!s || !out || cam < 0 || cam >= (int)s->host.cameras.size())
+    return set_error(RT_E_INVALID, "rt_scene_camera: bad argument");
+  *out = s->host.cameras[cam];
+  return RT_OK;
+}
+
+const char* rt_scene_image_name(const rt_scene* s, int cam) {
+  if (!s || cam < 0 || cam >= (int)s->host.image_names.size()) return "";
+  return s->host.image_names[cam].c_str();
+}
+
+int rt_scene_dump_bvh(const rt_scene* s, const char* path) {
+  if (!s || !path) return set_error(RT_E_INVALID, "rt_scene_dump_bvh: NULL argument");
+  FILE* f = std::fopen(path, "w");
+  if (!f) return set_error(RT_E_IO, std::string("cannot open ") + path);
+  const std::string d = dump_bvh(s->host);
+  std::fwrite(d.data(), 1, d.size(), f);
+  std::fclose(f);
+  return RT_OK;
+}
+
+int rt_host_dump_bvh_xml(const char* xml_path, const char* out_path) {
+  if (!xml_path || !out_path) return set_error(RT_E_INVALID, "rt_host_dump_bvh_xml: NULL argument");
+  return guarded([&] {
+    XmlSceneStorage st;
+    rt_scene_desc d;
+    load_scene_xml(xml_path, st, d);
+    HostScene h;
+    build_host_scene(d, h);
+    FILE* f = std::fopen(out_path, "w");
+    if (!f) throw std::ios_base::failure(std::string("cannot open ") + out_path);
+    const std::string text = dump_bvh(h);
+    std::fwrite(text.data(), 1, text.size(), f);
+    std::fclose(f);
+    return RT_OK;
+  });
+}
+
+int rt_set_traversal(rt_scene* s, int mode) {
+  if (!s || (mode != RT_TRAVERSAL_FAST && mode != RT_TRAVERSAL_REFERENCE))
+    return set_error(RT_E_INVALID, "rt_set_traversal: bad argument");
+  s->mode = mode;
+  return RT_OK;
+}
+
+int rt_num_tiles(const rt_scene* s, int cam, int row0, int row_stride) {
+  if (!s || cam < 0 || cam >= (int)s->host.cameras.size() || row0 < 0 || row_stride < 1)
+    return set_error(RT_E_INVALID, "rt_num_tiles: bad argument");
+  return plan(s->host.cameras[cam], row0, row_stride).tiles_total;
+}
+
+int rt_render_device(rt_scene* s, int cam, int row0, int row_stride, int tile_begin,
+                     int tile_step, int tile_major, float* d_out, void* stream) {
+  return guarded([&] {
+      check_render_args(s, cam, row0, row_stride);
+      if (tile_begin < 0 || tile_step < 1 || !d_out)
+        throw std::invalid_argument("rt_render_device: bad tile selection / output");
+      DeviceGuard g(s->device);
+      const RenderParams P =
+          make_params(s, cam, row0, row_stride, tile_begin, tile_step, tile_major, d_out, true);
+      hip_check(launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
+                              s->mode == RT_TRAVERSAL_FAST, s->deep, (hipStream_t)stream),
+                "render launch");
+      return RT_OK;
+  });
+}
+
+int rt_collect_stats(rt_scene* s, rt_stats* stats) {
+  if (!s || !stats) return set_error(RT_E_INVALID, "rt_collect_stats: NULL argument");
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    std::vector<unsigned long long> c(4 * kCounterRows);
+    hip_check(hipMemcpy(c.data(), s->d_counters, c.size() * sizeof c[0], hipMemcpyDeviceToHost),
+              "read counters");
+    hip_check(hipMemset(s->d_counters, 0, c.size() * sizeof c[0]), "reset counters");
+    std::memset(stats, 0, sizeof *stats);
+    for (int r = 0; r < kCounterRows; r++) {
+      stats->primary_rays += (long long)c[4 * r];
+      stats->shadow_rays += (long long)c[4 * r + 1];
+      stats->secondary_rays += (long long)c[4 * r + 2];
+      stats->primary_hits += (long long)c[4 * r + 3];
+    }
+    return RT_OK;
+  });
+}
+
+int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt_stats* stats) {
+  return guarded([&] {
+      check_render_args(s, cam, row0, row_stride);
+      if (!out_rgb) throw std::invalid_argument("rt_render: out_rgb is NULL");
+      DeviceGuard g(s->device);
+      const rt_camera& c = s->host.cameras[cam];
+      const TilePlan tp = plan(c, row0, row_stride);
+      if (tp.rows == 0) return RT_OK;
+      const size_t frame = (size_t)c.width * c.height * 3;
+      float* d_out = nullptr;
+      hipStream_t stream = nullptr;
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      auto cleanup = [&] {
+        if (d_out) (void)hipFree(d_out);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        if (stream) (void)hipStreamDestroy(stream);
+      };
+      try {
+        hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream");
+        hip_check(hipMalloc(&d_out, frame * sizeof(float)), "alloc frame");
+        hip_check(hipEventCreate(&e0), "event");
+        hip_check(hipEventCreate(&e1), "event");
+        // Counters are per scene; this call reports its own deltas via a private buffer.
+        unsigned long long* d_cnt = nullptr;
+        hip_check(hipMalloc(&d_cnt, sizeof(unsigned long long) * 4 * kCounterRows), "alloc counters");
+        hip_check(hipMemsetAsync(d_cnt, 0, sizeof(unsigned long long) * 4 * kCounterRows, stream),
+                  "zero counters");
+        RenderParams P = make_params(s, cam, row0, row_stride, 0, 1, 0, d_out, true);
+        P.counters = d_cnt;
+        hip_check(hipEventRecord(e0, stream), "event record");
+        hipError_t le = launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats,
+                                      s->d_lights, s->mode == RT_TRAVERSAL_FAST, s->deep, stream);
+        if (le != hipSuccess) {
+          (void)hipFree(d_cnt);
+          hip_check(le, "render launch");
+        }
+        hip_check(hipEventRecord(e1, stream), "event record");
+        // rows j = row0 + k*row_stride only: a strided 2D copy leaves the others untouched
+        const size_t row_bytes = (size_t)c.width * 3 * sizeof(float);
+        hip_check(hipMemcpy2DAsync(out_rgb + (size_t)row0 * c.width * 3, row_bytes * row_stride,
+                                   d_out + (size_t)row0 * c.width * 3, row_bytes * row_stride,
+                                   row_bytes, tp.rows, hipMemcpyDeviceToHost, stream),
+                  "copy rows");
+        std::vector<unsigned long long> cnt(4 * kCounterRows);
+        hip_check(hipMemcpyAsync(cnt.data(), d_cnt, cnt.size() * sizeof cnt[0],
+                                 hipMemcpyDeviceToHost, stream),
+                  "copy counters");
+        hip_check(hipStreamSynchronize(stream), "synchronize");
+        (void)hipFree(d_cnt);
+        if (stats) {
+          std::memset(stats, 0, sizeof *stats);
+          for (int r = 0; r < kCounterRows; r++) {
+            stats->primary_rays += (long long)cnt[4 * r];
+            stats->shadow_rays += (long long)cnt[4 * r + 1];
+            stats->secondary_rays += (long long)cnt[4 * r + 2];
+            stats->primary_hits += (long long)cnt[4 * r + 3];
+          }
+          float ms = 0;
+          hip_check(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+          stats->kernel_ms = ms;
+        }
+      } catch (...) {
+        cleanup();
+        throw;
+      }
+      cleanup();
+      return RT_OK;
+  });
+}
+
+int rt_write_png(const char* path, const float* rgb, int width, int height) {
+  if (!path || !rgb) return set_error(RT_E_INVALID, "rt_write_png: NULL argument");
+  return guarded([&] {
+    write_png(path, rgb, width, height);
+    return RT_OK;
+  });
+}
+
+}  // extern "C"

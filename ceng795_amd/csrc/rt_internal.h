@@ -1,0 +1,91 @@
+// Internal layouts shared by the host scene builder and the HIP kernels.
+//
+// HBM layout (see DESIGN.md §Data layout):
+//   nodes   : DevNode[num_nodes]    64 B, BVH2 internal nodes in DFS preorder; each holds
+//                                    both CHILD boxes, so one s_load_dwordx16 per visit tests
+//                                    both children (the reference tests a node's own box on
+//                                    entry, HW2/Bounding_volume_hierarchy.cpp:32-35 — same set).
+//   prims   : DevPrim[num_leaves]   48 B, leaves in DFS order: leaf index == the reference's
+//                                    DFS leaf order, which is the closest-hit tie-break key.
+//   normals : float4[num_leaves]     flat normal (Triangle.cpp:14) + material id, read once
+//                                    per pixel for the winning leaf only.
+#ifndef CENG795_RT_INTERNAL_H_
+#define CENG795_RT_INTERNAL_H_
+
+#include <stdint.h>
+
+namespace rt {
+
+constexpr int kTile = 8;          // one wavefront = one 8x8 pixel packet
+constexpr int kWavesPerBlock = 4; // 256-thread workgroups
+constexpr int kLaneStack = 64;    // per-wave traversal stack held one entry per VGPR lane
+constexpr int kCounterRows = 64;  // ray-counter rows (spread atomics)
+
+struct alignas(16) DevNode {
+  float b0[6];   // child 0 box: lo.xyz, hi.xyz (unused if child 0 is a leaf)
+  float b1[6];   // child 1 box
+  int32_t child[2];  // >= 0: internal node index; < 0: leaf index ~child
+  int32_t axis;      // split dimension of THIS node (Bounding_volume_hierarchy.cpp:8)
+  int32_t pad;
+};
+static_assert(sizeof(DevNode) == 64, "node must be one 64-byte scalar load");
+
+enum PrimKind : int32_t { kPrimTriangle = 0, kPrimSphere = 1 };
+
+struct alignas(16) DevPrim {
+  // triangle: v0, a1 = v0 - v1, a2 = v0 - v2 (Triangle.cpp:43-44, same fp32 rounding)
+  // sphere:   v0 = center, a1[0] = radius
+  float v0[3];
+  float a1[3];
+  float a2[3];
+  int32_t kind;
+  int32_t material;
+  int32_t pad;
+};
+static_assert(sizeof(DevPrim) == 48, "prim record is three 16-byte loads");
+
+struct DevMaterial {  // HW2/Material.h
+  float ambient[3], diffuse[3], specular[3], mirror[3], transparency[3];
+  float refraction_index, phong_exponent;
+  float pad[3];
+};
+static_assert(sizeof(DevMaterial) == 80, "");
+
+struct DevLight {
+  float position[3];
+  float intensity[3];
+  float pad[2];
+};
+
+enum RootKind : int32_t { kRootNode = 0, kRootTriangle = 1, kRootSphere = 2 };
+
+struct RenderParams {
+  const DevNode* nodes;
+  const DevPrim* prims;
+  const float* normals;  // float4 per leaf: nx ny nz material(bits)
+  const DevMaterial* materials;
+  const DevLight* lights;
+  int num_lights;
+  int max_depth;
+  float background[3];
+  float ambient[3];
+  float eps;
+  int root_kind;
+  int root_ref;           // kRootNode: node index; else leaf index
+  float root_box[6];
+  // camera (rt_camera)
+  float cam_e[3], cam_tl[3], cam_su[3], cam_sv[3];
+  int width, height;
+  // row subset: image row of logical row k = row0 + k*row_stride
+  int row0, row_stride, rows;
+  // tiles over (rows x width), row-major; this launch does tile_begin + i*tile_step
+  int tiles_x, tiles_total, tile_begin, tile_step, num_sel_tiles;
+  int tile_major;
+  float* out;
+  // kCounterSlots rows of 4: primary rays, shadow rays, secondary rays, primary hits
+  unsigned long long* counters;
+};
+
+}  // namespace rt
+
+#endif

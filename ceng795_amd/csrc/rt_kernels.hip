@@ -1,0 +1,515 @@
+// MI355X (gfx950) render kernels: HW2's Scene::render_image -> trace_ray -> BVH::intersect ->
+// Triangle/Sphere::intersect -> Point_light shading + shadow rays, as one fused kernel.
+//
+// Execution model:
+//   * one wavefront = one 8x8 pixel packet; 4 packets per 256-thread workgroup;
+//   * the wave walks the BVH TOGETHER: the current node index and the 64-bit lane mask of
+//     the rays that accepted every box on the path are wave-uniform (SGPRs), so node and
+//     primitive records come in through the scalar cache (s_load) once per wave, not once
+//     per lane;
+//   * the traversal stack is one entry per VGPR lane (lane-select push, v_readlane pop, 64 deep);
+//     trees deeper than that use a per-wave LDS stack (kDeepStack entries);
+//   * per-lane masks reproduce the reference's per-ray semantics exactly: a ray tests a node
+//     iff it accepted every ancestor's box (HW2/Bounding_volume_hierarchy.cpp:31-55);
+//   * closest hit = lexicographic minimum of (t, DFS leaf index) over accepted leaves, which
+//     is what the reference's left-first recursion with strict `<` returns (appendix A.5), so
+//     any visiting order gives the reference's answer.
+//
+// Numerics: compiled with -ffp-contract=off and this file's pragma; '/' is the correctly
+// rounded fp32 division and sqrtf is correctly rounded on gfx950 (HIP defaults), pow / exp
+// / log are the fp64 ocml functions, matching the reference's double libm islands.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "rt_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace rt {
+
+#define RT_INF __builtin_huge_valf()
+constexpr float kEps = 0.000001f;  // HW2/Vector3.h:7 kEpsilon
+constexpr int kCounterSlots = kCounterRows;
+
+// ------------------------------------------------------------------ vector helpers
+struct V3 {
+  float x, y, z;
+};
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return {x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V3 operator*(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ V3 operator*(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ V3 operator/(V3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return (a.x * b.x) + (a.y * b.y) + (a.z * b.z); }
+__device__ __forceinline__ float length(V3 a) { return __builtin_sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
+__device__ __forceinline__ V3 normalize(V3 a) { return a / length(a); }
+__device__ __forceinline__ V3 ld3(const float* p) { return {p[0], p[1], p[2]}; }
+
+struct LaneRay {
+  V3 o, d;
+  V3 r;       // v_rcp_f32 reciprocals (<= 1 ulp): the approximate slab test only
+  bool skip0, skip1, skip2;  // |d_i| < 1e-6: axis ignored (HW2/bounding_box.cpp:21)
+};
+
+__device__ __forceinline__ LaneRay make_ray(V3 o, V3 d) {
+  LaneRay r;
+  r.o = o;
+  r.d = d;
+  r.r = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+  r.skip0 = __builtin_fabsf(d.x) < kEps;
+  r.skip1 = __builtin_fabsf(d.y) < kEps;
+  r.skip2 = __builtin_fabsf(d.z) < kEps;
+  return r;
+}
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// ------------------------------------------------------------------ slab test
+// Literal HW2/bounding_box.cpp:15-35 + the caller's reject rule (BVH.cpp:32-35).  Used when
+// the fast test below cannot decide.  Its comparisons are the reference's, so NaN / inf
+// inputs behave as there.
+__device__ __forceinline__ bool box_exact(const float* b, const LaneRay& r) {
+  float tmin = -RT_INF, tmax = RT_INF;
+  const float o[3] = {r.o.x, r.o.y, r.o.z};
+  const float d[3] = {r.d.x, r.d.y, r.d.z};
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    if (__builtin_fabsf(d[i]) < kEps) continue;
+    float t0 = (b[i] - o[i]) / d[i];
+    float t1 = (b[i + 3] - o[i]) / d[i];
+    if (d[i] < 0) {
+      const float s = t0;
+      t0 = t1;
+      t1 = s;
+    }
+    if (t0 > tmin) tmin = t0;
+    if (t1 < tmax) tmax = t1;
+    if (tmin > tmax) return false;
+  }
+  const float bt = tmin > 0.0f ? tmin : tmax;
+  return !(bt < 0.0f || bt == RT_INF);
+}
+
+// Fast slab test.  With q = RN(RN(m - o) / d) the reference's quotient and q' = RN(RN(m - o)
+// * rcp(d)) ours, |q' - q| <= 2^-22 |q| and sign(q') == sign(q) exactly.  The reference
+// accepts iff tmin <= tmax and tmax >= 0 (tmin, tmax finite here); the sign test is exact and
+// the order test is decided only outside a 2^-20 relative band — otherwise box_exact.
+// tnear (approximate entry distance) is only used for ordering / culling.
+template <bool SKIP>
+__device__ __forceinline__ bool box_hit(const float* b, const LaneRay& r, float& tnear) {
+  const float ax = (b[0] - r.o.x) * r.r.x, bx = (b[3] - r.o.x) * r.r.x;
+  const float ay = (b[1] - r.o.y) * r.r.y, by = (b[4] - r.o.y) * r.r.y;
+  const float az = (b[2] - r.o.z) * r.r.z, bz = (b[5] - r.o.z) * r.r.z;
+  float nx = __builtin_fminf(ax, bx), fx = __builtin_fmaxf(ax, bx);
+  float ny = __builtin_fminf(ay, by), fy = __builtin_fmaxf(ay, by);
+  float nz = __builtin_fminf(az, bz), fz = __builtin_fmaxf(az, bz);
+  if (SKIP) {
+    nx = r.skip0 ? -RT_INF : nx;
+    fx = r.skip0 ? RT_INF : fx;
+    ny = r.skip1 ? -RT_INF : ny;
+    fy = r.skip1 ? RT_INF : fy;
+    nz = r.skip2 ? -RT_INF : nz;
+    fz = r.skip2 ? RT_INF : fz;
+  }
+  const float tn = __builtin_fmaxf(__builtin_fmaxf(nx, ny), nz);
+  const float tf = __builtin_fminf(__builtin_fminf(fx, fy), fz);
+  tnear = tn;
+  const float band = (__builtin_fabsf(tn) + __builtin_fabsf(tf)) * 0x1p-20f + 0x1p-120f;
+  if (tn < tf - band) return tf >= 0.0f;
+  if (tn > tf + band) return false;
+  return box_exact(b, r);
+}
+
+// ------------------------------------------------------------------ primitives
+// HW2/Triangle.cpp:35-65 with determinant() = Triangle.h:33-38, v0 - v1 / v0 - v2 precomputed
+// on the host with the same fp32 rounding.
+__device__ __forceinline__ float det3(V3 c1, V3 c2, V3 c3) {
+  return c1.x * (c2.y * c3.z - c3.y * c2.z) + c2.x * (c3.y * c1.z - c1.y * c3.z) +
+         c3.x * (c1.y * c2.z - c2.y * c1.z);
+}
+
+__device__ __forceinline__ bool tri_test(V3 v0, V3 a1, V3 a2, const LaneRay& r, float& t) {
+  const float det = det3(a1, a2, r.d);
+  if (det == 0.0f) return false;
+  const V3 b = (v0 - r.o) / det;
+  const float beta = det3(b, a2, r.d);
+  if (beta < 0.0f || beta > 1.0f) return false;
+  const float gamma = det3(a1, b, r.d);
+  if (gamma < 0.0f || beta + gamma > 1.0f) return false;
+  const float tt = det3(a1, a2, b);
+  if (tt > 0.0f) {
+    t = tt;
+    return true;
+  }
+  return false;
+}
+
+// HW2/Sphere.h:26-52 — true for any real root, including a negative one.
+__device__ __forceinline__ bool sphere_test(V3 c, float radius, const LaneRay& r, float& t) {
+  const V3 co = r.o - c;
+  const float a = dot(r.d, r.d);
+  const float b = 2 * dot(r.d, co);
+  const float cc = dot(co, co) - radius * radius;
+  const float disc = b * b - 4 * a * cc;
+  if (disc < -kEps) return false;
+  if (disc < kEps) {
+    t = -b / (2 * a);
+  } else {
+    const float sq = __builtin_sqrtf(disc);  // == (float)sqrt((double)disc)
+    const float t1 = (-b + sq) / (2 * a);
+    const float t2 = (-b - sq) / (2 * a);
+    t = t2 < 0.0f ? t1 : t2;
+  }
+  return true;
+}
+
+__device__ __forceinline__ bool leaf_test(const DevPrim* __restrict__ prims, int leaf,
+                                          const LaneRay& r, float& t) {
+  const DevPrim& p = prims[leaf];
+  const V3 v0 = ld3(p.v0);
+  if (p.kind == kPrimTriangle) return tri_test(v0, ld3(p.a1), ld3(p.a2), r, t);
+  return sphere_test(v0, p.a1[0], r, t);
+}
+
+// ------------------------------------------------------------------ traversal stack
+// Wave-uniform (node, lane-mask) entries.  DEEP == false: entry i lives in VGPR lane i
+// (select-on-lane push / v_readlane pop, no memory traffic, 64 deep).  DEEP == true: a per-wave LDS
+// array of kDeepStack entries for trees deeper than 64 levels (lane 0 writes, all lanes
+// read the broadcast word; LDS ops of one wave complete in order).
+constexpr int kDeepStack = 1024;
+
+template <bool DEEP>
+struct WaveStack {
+  int node = 0;
+  unsigned mlo = 0, mhi = 0;
+  int sp = 0;       // wave-uniform
+  int* lds = nullptr;
+
+  __device__ __forceinline__ void push(int n, uint64_t m) {
+    if (!DEEP) {
+      const bool mine = lane_id() == sp;  // v_cmp + v_cndmask: lane sp takes the entry
+      node = mine ? n : node;
+      mlo = mine ? (unsigned)m : mlo;
+      mhi = mine ? (unsigned)(m >> 32) : mhi;
+    } else if (lane_id() == 0) {
+      lds[3 * sp] = n;
+      lds[3 * sp + 1] = (int)(unsigned)m;
+      lds[3 * sp + 2] = (int)(unsigned)(m >> 32);
+    }
+    sp++;
+  }
+  __device__ __forceinline__ void pop(int& n, uint64_t& m) {
+    sp--;
+    if (!DEEP) {
+      n = __builtin_amdgcn_readlane(node, sp);
+      m = (uint64_t)(unsigned)__builtin_amdgcn_readlane(mlo, sp) |
+          ((uint64_t)(unsigned)__builtin_amdgcn_readlane(mhi, sp) << 32);
+    } else {
+      n = uniform(lds[3 * sp]);
+      m = (uint64_t)(unsigned)uniform(lds[3 * sp + 1]) |
+          ((uint64_t)(unsigned)uniform(lds[3 * sp + 2]) << 32);
+    }
+  }
+};
+
+__device__ __forceinline__ float cull_limit(float t) { return t + t * 0x1p-8f; }
+
+// ------------------------------------------------------------------ closest hit
+// Returns the reference's (t, leaf) for every active lane: best_leaf < 0 = miss.
+template <bool SKIP, bool FAST, bool DEEP>
+__device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode* __restrict__ nodes,
+                            const DevPrim* __restrict__ prims, int* spill, const LaneRay& r,
+                            bool active, float& best_t, int& best_leaf) {
+  best_t = RT_INF;
+  best_leaf = -1;
+  if (P.root_kind != kRootNode) {  // the root IS the primitive (BVH.h:13-14): its own rule
+    float t;
+    if (active && leaf_test(prims, P.root_ref, r, t)) {
+      best_t = t;
+      best_leaf = P.root_ref;
+    }
+    return;
+  }
+  float tn;
+  uint64_t m = ballot(active && box_hit<SKIP>(P.root_box, r, tn));
+  if (m == 0) return;
+  const int lane = lane_id();
+  WaveStack<DEEP> st;
+  st.lds = spill;
+  int node = P.root_ref;
+  for (;;) {
+    const DevNode& N = nodes[node];
+    const bool in = (m >> lane) & 1;
+    const int c0 = N.child[0], c1 = N.child[1];
+    uint64_t m0 = 0, m1 = 0;
+    float t0 = RT_INF, t1 = RT_INF;
+    if (c0 >= 0) {
+      bool h = in && box_hit<SKIP>(N.b0, r, t0);
+      if (FAST) h = h && t0 <= cull_limit(best_t);
+      m0 = ballot(h);
+    } else if (in) {
+      float t;
+      if (leaf_test(prims, ~c0, r, t) && t > 0.0f && t < RT_INF &&
+          (t < best_t || (t == best_t && ~c0 < best_leaf))) {
+        best_t = t;
+        best_leaf = ~c0;
+      }
+    }
+    if (c1 >= 0) {
+      bool h = in && box_hit<SKIP>(N.b1, r, t1);
+      if (FAST) h = h && t1 <= cull_limit(best_t);
+      m1 = ballot(h);
+    } else if (in) {
+      float t;
+      if (leaf_test(prims, ~c1, r, t) && t > 0.0f && t < RT_INF &&
+          (t < best_t || (t == best_t && ~c1 < best_leaf))) {
+        best_t = t;
+        best_leaf = ~c1;
+      }
+    }
+    if (m0 && m1) {
+      // near child first, judged by the first lane that entered both
+      const int f = __builtin_ctzll(m0 & m1 ? (m0 & m1) : m0);
+      const float f0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t0), f));
+      const float f1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t1), f));
+      if (f1 < f0) {
+        st.push(c0, m0);
+        node = c1;
+        m = m1;
+      } else {
+        st.push(c1, m1);
+        node = c0;
+        m = m0;
+      }
+    } else if (m0) {
+      node = c0;
+      m = m0;
+    } else if (m1) {
+      node = c1;
+      m = m1;
+    } else {
+      if (st.sp == 0) break;
+      st.pop(node, m);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ shadow (any hit)
+// Occluded iff some leaf the ray may reach has 0 < t < thr — identical to the reference's
+// closest-hit shadow test `0 < t_closest < dist - eps` (HW2/Scene.cpp:123-127), appendix A.7.
+template <bool SKIP, bool FAST, bool DEEP>
+__device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* __restrict__ nodes,
+                         const DevPrim* __restrict__ prims, int* spill, const LaneRay& r,
+                         bool active, float thr) {
+  if (P.root_kind != kRootNode) {
+    float t;
+    return active && leaf_test(prims, P.root_ref, r, t) && t < thr && t > 0.0f;
+  }
+  bool occ = false;
+  float tn;
+  // thr <= 0 (or NaN): nothing can satisfy 0 < t < thr
+  uint64_t m = ballot(active && thr > 0.0f && box_hit<SKIP>(P.root_box, r, tn));
+  if (m == 0) return false;
+  const int lane = lane_id();
+  WaveStack<DEEP> st;
+  st.lds = spill;
+  int node = P.root_ref;
+  uint64_t alive = m;
+  for (;;) {
+    const DevNode& N = nodes[node];
+    const bool in = (m >> lane) & 1;
+    const int c0 = N.child[0], c1 = N.child[1];
+    uint64_t m0 = 0, m1 = 0;
+    float t0 = RT_INF, t1 = RT_INF;
+    if (c0 >= 0) {
+      bool h = in && box_hit<SKIP>(N.b0, r, t0);
+      if (FAST) h = h && t0 <= cull_limit(thr);
+      m0 = ballot(h);
+    } else if (in) {
+      float t;
+      if (leaf_test(prims, ~c0, r, t) && t > 0.0f && t < thr) occ = true;
+    }
+    if (c1 >= 0) {
+      bool h = in && box_hit<SKIP>(N.b1, r, t1);
+      if (FAST) h = h && t1 <= cull_limit(thr);
+      m1 = ballot(h);
+    } else if (in && !occ) {
+      float t;
+      if (leaf_test(prims, ~c1, r, t) && t > 0.0f && t < thr) occ = true;
+    }
+    alive &= ~ballot(occ);
+    if (alive == 0) break;
+    m0 &= alive;
+    m1 &= alive;
+    if (m0 && m1) {
+      const int f = __builtin_ctzll(m0 & m1 ? (m0 & m1) : m0);
+      const float f0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t0), f));
+      const float f1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t1), f));
+      if (f1 < f0) {
+        st.push(c0, m0);
+        node = c1;
+        m = m1;
+      } else {
+        st.push(c1, m1);
+        node = c0;
+        m = m0;
+      }
+    } else if (m0) {
+      node = c0;
+      m = m0;
+    } else if (m1) {
+      node = c1;
+      m = m1;
+    } else {
+      m = 0;
+      while (m == 0 && st.sp > 0) {
+        st.pop(node, m);
+        m &= alive;
+      }
+      if (m == 0) break;
+    }
+  }
+  return occ;
+}
+
+// ------------------------------------------------------------------ render kernel
+template <bool FAST, bool DEEP>
+__device__ __forceinline__ void render_packet(const RenderParams& P, const DevNode* __restrict__ nodes,
+                              const DevPrim* __restrict__ prims,
+                              const float* __restrict__ normals,
+                              const DevMaterial* __restrict__ mats,
+                              const DevLight* __restrict__ lights, int sel, int* spill) {
+  const int lane = lane_id();
+  const int tile = P.tile_begin + sel * P.tile_step;
+  const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  const int px = tx * kTile + (lane & 7);
+  const int lr = ty * kTile + (lane >> 3);  // logical row
+  const bool valid = px < P.width && lr < P.rows;
+  const int py = P.row0 + lr * P.row_stride;
+
+  // Camera::calculate_ray_at (HW2/Camera.h:30-35); x + 0.5 is exact in fp32 for x < 2^23.
+  const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+  const V3 e = ld3(P.cam_e);
+  const V3 s = (ld3(P.cam_tl) + ld3(P.cam_su) * fx) - ld3(P.cam_sv) * fy;
+  const LaneRay ray = make_ray(e, normalize(s - e));
+
+  const bool skip = ballot(valid && (ray.skip0 || ray.skip1 || ray.skip2)) != 0;
+  float t;
+  int leaf;
+  if (skip)
+    closest_hit<true, FAST, DEEP>(P, nodes, prims, spill, ray, valid, t, leaf);
+  else
+    closest_hit<false, FAST, DEEP>(P, nodes, prims, spill, ray, valid, t, leaf);
+
+  const bool hit = valid && leaf >= 0;
+  V3 color = v3(0.0f, 0.0f, 0.0f);
+  V3 p = v3(0, 0, 0), n = v3(0, 0, 0), w0 = v3(0, 0, 0);
+  const DevMaterial* m = mats;
+  if (hit) {
+    p = ray.o + ray.d * t;  // Ray::point_at = o + t*d
+    const float* nr = normals + 4 * leaf;
+    const DevPrim& pr = prims[leaf];
+    m = mats + pr.material;
+    if (pr.kind == kPrimTriangle)
+      n = ld3(nr);
+    else
+      n = normalize(p - ld3(pr.v0));  // Sphere.h:42,50
+    w0 = normalize(ray.o - p);
+    color = color + ld3(m->ambient) * ld3(P.ambient);
+  } else if (valid) {
+    color = ld3(P.background);  // primary miss: max_recursion_depth == depth
+  }
+  const unsigned long long nhit = __builtin_popcountll(ballot(hit));
+  for (int li = 0; li < P.num_lights; li++) {
+    const DevLight& L = lights[li];
+    const V3 ld = ld3(L.position) - p;
+    const V3 wi = normalize(ld);
+    const float dist = length(ld);
+    const LaneRay sr = make_ray(p + wi * P.eps, wi);
+    const float thr = dist - P.eps;
+    const bool sskip = ballot(hit && (sr.skip0 || sr.skip1 || sr.skip2)) != 0;
+    bool occ;
+    if (sskip)
+      occ = occluded<true, FAST, DEEP>(P, nodes, prims, spill, sr, hit, thr);
+    else
+      occ = occluded<false, FAST, DEEP>(P, nodes, prims, spill, sr, hit, thr);
+    if (hit && !occ) {
+      const V3 I = ld3(L.intensity);
+      const float d2 = dist * dist;
+      const float cos_d = dot(n, wi);
+      color = color + ((ld3(m->diffuse) * I) * cos_d) / d2;
+      const float cos_s = __builtin_fmaxf(dot(n, normalize(w0 + wi)), 0.0f);
+      const float pw = (float)pow((double)cos_s, (double)m->phong_exponent);
+      color = color + ((ld3(m->specular) * I) * pw) / d2;
+    }
+  }
+  if (valid) {
+    float* o;
+    if (P.tile_major)
+      o = P.out + 3 * ((size_t)sel * (kTile * kTile) + lane);
+    else
+      o = P.out + 3 * ((size_t)py * P.width + px);
+    o[0] = 0.0f + color.x;  // Pixel::add_color(color, 1) onto a zeroed pixel
+    o[1] = 0.0f + color.y;
+    o[2] = 0.0f + color.z;
+  } else if (P.tile_major && sel < P.num_sel_tiles) {
+    float* o = P.out + 3 * ((size_t)sel * (kTile * kTile) + lane);
+    o[0] = o[1] = o[2] = 0.0f;
+  }
+  if (P.counters) {  // spread over kCounterSlots rows: no single hot address
+    const unsigned long long nvalid = __builtin_popcountll(ballot(valid));
+    if (lane == 0) {
+      unsigned long long* c = P.counters + 4 * (sel % kCounterSlots);
+      atomicAdd(&c[0], nvalid);
+      atomicAdd(&c[1], nhit * (unsigned long long)P.num_lights);
+      atomicAdd(&c[3], nhit);
+    }
+  }
+}
+
+template <bool FAST, bool DEEP>
+__global__ __launch_bounds__(kWavesPerBlock * 64) void render_kernel(
+    RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims,
+    const float* __restrict__ normals, const DevMaterial* __restrict__ mats,
+    const DevLight* __restrict__ lights) {
+  extern __shared__ __attribute__((aligned(16))) int deep_stack[];
+  // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so hand each
+  // XCD a contiguous run of tiles — neighbouring packets share BVH nodes through its L2.
+  const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+  const int q = nb / 8, rem = nb % 8, x = b % 8;
+  const int logical = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + b / 8;
+  const int wave = (int)threadIdx.x >> 6;
+  const int sel = uniform(logical * kWavesPerBlock + wave);
+  if (sel >= P.num_sel_tiles) return;
+  int* spill = DEEP ? deep_stack + wave * 3 * kDeepStack : nullptr;
+  render_packet<FAST, DEEP>(P, nodes, prims, normals, mats, lights, sel, spill);
+}
+
+template <bool FAST, bool DEEP>
+static void launch_variant(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
+                           const float* normals, const DevMaterial* mats,
+                           const DevLight* lights, int blocks, hipStream_t stream) {
+  const size_t lds = DEEP ? sizeof(int) * 3 * kDeepStack * kWavesPerBlock : 0;
+  hipLaunchKernelGGL((render_kernel<FAST, DEEP>), dim3(blocks), dim3(kWavesPerBlock * 64), lds,
+                     stream, P, nodes, prims, normals, mats, lights);
+}
+
+int max_supported_depth() { return kDeepStack; }
+
+hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
+                         const float* normals, const DevMaterial* mats, const DevLight* lights,
+                         bool fast, bool deep, hipStream_t stream) {
+  if (P.num_sel_tiles <= 0) return hipSuccess;
+  const int blocks = (P.num_sel_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (fast && !deep) launch_variant<true, false>(P, nodes, prims, normals, mats, lights, blocks, stream);
+  else if (fast) launch_variant<true, true>(P, nodes, prims, normals, mats, lights, blocks, stream);
+  else if (!deep) launch_variant<false, false>(P, nodes, prims, normals, mats, lights, blocks, stream);
+  else launch_variant<false, true>(P, nodes, prims, normals, mats, lights, blocks, stream);
+  return hipGetLastError();
+}
+
+}  // namespace rt

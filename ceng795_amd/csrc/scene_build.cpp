@@ -1,0 +1,380 @@
+// Host scene construction: the reference's object list and BVH, flattened for the GPU.
+//
+//   object list order  HW2/Scene.cpp:380-449 (meshes, loose triangles, spheres)
+//   triangle ctor      HW2/Triangle.cpp:4-34 (flat normal, fmin/fmax box)
+//   sphere box         HW2/Sphere.h:17-20
+//   BVH build          HW2/Bounding_volume_hierarchy.cpp:3-29, create_bvh (.h:9-18)
+//   box union          HW2/bounding_box.cpp:2-13
+//
+// The build must reproduce the reference's topology exactly: the leaf order it produces is
+// the closest-hit tie-break order, and the set of boxes on each root-to-leaf path decides
+// which leaves a ray may test at all.  Compiled with -ffp-contract=off (no FMA) so every
+// fp32 expression rounds as on the reference's x86-64 SSE build.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <sstream>
+#include <stdexcept>
+#include <utility>
+
+#include "host_scene.h"
+
+namespace rt {
+namespace {
+
+constexpr float kInf = std::numeric_limits<float>::infinity();
+
+struct F3 {
+  float x, y, z;
+  float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+};
+inline F3 operator+(F3 a, F3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline F3 operator-(F3 a, F3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline F3 operator*(F3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+inline F3 operator/(F3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+inline F3 cross(F3 a, F3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+inline F3 unit(F3 a) { return a / std::sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+inline F3 fmin3(F3 a, F3 b) { return {std::fmin(a.x, b.x), std::fmin(a.y, b.y), std::fmin(a.z, b.z)}; }
+inline F3 fmax3(F3 a, F3 b) { return {std::fmax(a.x, b.x), std::fmax(a.y, b.y), std::fmax(a.z, b.z)}; }
+
+struct Aabb {
+  F3 lo{kInf, kInf, kInf};
+  F3 hi{-kInf, -kInf, -kInf};
+  F3 mid{0, 0, 0};  // (max + min) / 2, as Bounding_box::center
+  static Aabb of(F3 lo, F3 hi) {
+    Aabb b;
+    b.lo = lo;
+    b.hi = hi;
+    b.mid = (hi + lo) / 2.0f;
+    return b;
+  }
+  void grow(const Aabb& o) {
+    lo = fmin3(lo, o.lo);
+    hi = fmax3(hi, o.hi);
+    mid = (hi + lo) / 2.0f;
+  }
+};
+
+// The reference's Shape hierarchy as a tagged list.
+enum ObjKind { kObjBvh, kObjMesh, kObjTri, kObjSphere };
+struct Obj {
+  ObjKind kind;
+  Aabb box;
+  int a = -1, b = -1;  // BVH children; Mesh: a = bvh root
+  int axis = 0;        // BVH split dimension
+  int leaf = -1;       // index into `leaves`
+};
+
+struct Builder {
+  std::vector<Obj> objs;
+  std::vector<LeafSource> leaves;
+  std::vector<F3> normals;
+
+  // create_bvh + BVH::BVH over the object ids in `ids` (permuted in place like the reference).
+  int build(std::vector<int>& ids) {
+    const int n = (int)ids.size();
+    if (n == 0) return -1;
+    if (n == 1) return ids[0];
+    struct Range {
+      int begin, end, axis, node;
+    };
+    std::vector<Range> todo;
+    auto open = [&](int begin, int end, int axis) {
+      Obj o;
+      o.kind = kObjBvh;
+      o.axis = axis;
+      for (int i = begin; i < end; i++) o.box.grow(objs[ids[i]].box);
+      objs.push_back(o);
+      todo.push_back({begin, end, axis, (int)objs.size() - 1});
+      return (int)objs.size() - 1;
+    };
+    const int root = open(0, n, 0);
+    while (!todo.empty()) {
+      const Range r = todo.back();
+      todo.pop_back();
+      const float split = objs[r.node].box.mid[r.axis];
+      int m = r.begin;
+      for (int i = r.begin; i < r.end; i++)
+        if (objs[ids[i]].box.mid[r.axis] < split) std::swap(ids[i], ids[m++]);
+      if (m == r.begin || m == r.end) m = r.begin + (r.end - r.begin) / 2;
+      const int next = (r.axis + 1) % 3;
+      const int left = (r.begin + 1 == m) ? ids[r.begin] : open(r.begin, m, next);
+      const int right = (m + 1 == r.end) ? ids[m] : open(m, r.end, next);
+      objs[r.node].a = left;
+      objs[r.node].b = right;
+    }
+    return root;
+  }
+};
+
+void fail(const std::string& m) { throw std::invalid_argument(m); }
+
+}  // namespace
+
+void camera_from_view(const float pos[3], const float gaze[3], const float up[3],
+                      const float np[4], float dist, int w, int h, int ns, rt_camera& c) {
+  // HW2/Camera.h:19-28
+  const F3 e{pos[0], pos[1], pos[2]};
+  const F3 g{gaze[0], gaze[1], gaze[2]};
+  const F3 u0{up[0], up[1], up[2]};
+  const F3 gn = unit(g);
+  const F3 W{-gn.x, -gn.y, -gn.z};  // w = -(gaze.normalize())
+  const F3 U = unit(cross(unit(u0), W));
+  const F3 V = unit(cross(W, U));
+  const float l = np[0], r = np[1], b = np[2], t = np[3];
+  const F3 tl = ((e - W * dist) + U * l) + V * t;  // e - w*d + l*u + t*v, left to right
+  const F3 su = U * ((r - l) / (float)w);
+  const F3 sv = V * ((t - b) / (float)h);
+  const F3* src[4] = {&e, &tl, &su, &sv};
+  float* dst[4] = {c.e, c.top_left, c.s_u, c.s_v};
+  for (int k = 0; k < 4; k++) {
+    dst[k][0] = src[k]->x;
+    dst[k][1] = src[k]->y;
+    dst[k][2] = src[k]->z;
+  }
+  c.width = w;
+  c.height = h;
+  c.num_samples = ns;
+}
+
+void build_host_scene(const rt_scene_desc& d, HostScene& s) {
+  if (d.num_vertices < 0 || d.num_materials < 0 || d.num_lights < 0 || d.num_cameras < 0 ||
+      d.num_meshes < 0 || d.num_triangles < 0 || d.num_spheres < 0)
+    fail("negative count in scene description");
+  if (d.num_vertices && !d.vertices) fail("vertices == NULL");
+  std::memcpy(s.background, d.background, sizeof s.background);
+  std::memcpy(s.ambient, d.ambient_light, sizeof s.ambient);
+  s.eps = d.shadow_ray_epsilon;
+  s.max_depth = d.max_recursion_depth;
+  if (s.max_depth < 0) fail("MaxRecursionDepth < 0");
+  s.materials.clear();
+  for (int i = 0; i < d.num_materials; i++) {
+    const rt_material& m = d.materials[i];
+    DevMaterial dm{};
+    std::memcpy(dm.ambient, m.ambient, 12);
+    std::memcpy(dm.diffuse, m.diffuse, 12);
+    std::memcpy(dm.specular, m.specular, 12);
+    std::memcpy(dm.mirror, m.mirror, 12);
+    std::memcpy(dm.transparency, m.transparency, 12);
+    dm.refraction_index = m.refraction_index;
+    dm.phong_exponent = m.phong_exponent;
+    s.materials.push_back(dm);
+  }
+  s.lights.clear();
+  for (int i = 0; i < d.num_lights; i++) {
+    DevLight L{};
+    std::memcpy(L.position, d.lights[i].position, 12);
+    std::memcpy(L.intensity, d.lights[i].intensity, 12);
+    s.lights.push_back(L);
+  }
+  s.cameras.assign(d.cameras, d.cameras + d.num_cameras);
+  for (const rt_camera& c : s.cameras)
+    if (c.width <= 0 || c.height <= 0 || c.num_samples <= 0) fail("bad camera resolution");
+  if (s.image_names.size() != s.cameras.size()) s.image_names.assign(s.cameras.size(), "");
+
+  auto vtx = [&](int i) -> F3 {
+    if (i < 0 || i >= d.num_vertices) fail("vertex index out of range");
+    return {d.vertices[3 * i], d.vertices[3 * i + 1], d.vertices[3 * i + 2]};
+  };
+  auto check_material = [&](int m) {
+    if (m < 0 || m >= d.num_materials) fail("material id out of range");
+  };
+
+  Builder B;
+  auto add_triangle = [&](int i0, int i1, int i2, int mat) {
+    check_material(mat);
+    const F3 v0 = vtx(i0), v1 = vtx(i1), v2 = vtx(i2);
+    Obj o;
+    o.kind = kObjTri;
+    o.box = Aabb::of(fmin3(fmin3(v0, v1), v2), fmax3(fmax3(v0, v1), v2));
+    o.leaf = (int)B.leaves.size();
+    LeafSource ls{};
+    ls.kind = kPrimTriangle;
+    ls.i0 = i0;
+    ls.i1 = i1;
+    ls.i2 = i2;
+    ls.material = mat;
+    B.leaves.push_back(ls);
+    B.normals.push_back(unit(cross(v1 - v0, v2 - v0)));
+    B.objs.push_back(o);
+    return (int)B.objs.size() - 1;
+  };
+
+  std::vector<int> top;
+  long long face_base = 0;
+  for (int m = 0; m < d.num_meshes; m++) {
+    const int nf = d.mesh_face_count[m];
+    if (nf <= 0) fail("mesh without faces (the reference dereferences a NULL bvh)");
+    std::vector<int> tris;
+    tris.reserve(nf);
+    for (int f = 0; f < nf; f++) {
+      const int* idx = d.mesh_faces + 3 * (face_base + f);
+      tris.push_back(add_triangle(idx[0], idx[1], idx[2], d.mesh_material[m]));
+    }
+    face_base += nf;
+    const int root = B.build(tris);
+    Obj mo;
+    mo.kind = kObjMesh;
+    mo.a = root;
+    mo.box = B.objs[root].box;
+    B.objs.push_back(mo);
+    top.push_back((int)B.objs.size() - 1);
+  }
+  for (int t = 0; t < d.num_triangles; t++) {
+    const int* idx = d.triangle_indices + 3 * t;
+    top.push_back(add_triangle(idx[0], idx[1], idx[2], d.triangle_material[t]));
+  }
+  for (int k = 0; k < d.num_spheres; k++) {
+    check_material(d.sphere_material[k]);
+    const F3 c = vtx(d.sphere_center[k]);
+    const float r = d.sphere_radius[k];
+    const F3 rr{r, r, r};
+    Obj o;
+    o.kind = kObjSphere;
+    o.box = Aabb::of(c - rr, c + rr);
+    o.leaf = (int)B.leaves.size();
+    LeafSource ls{};
+    ls.kind = kPrimSphere;
+    ls.center[0] = c.x;
+    ls.center[1] = c.y;
+    ls.center[2] = c.z;
+    ls.radius = r;
+    ls.material = d.sphere_material[k];
+    B.leaves.push_back(ls);
+    B.normals.push_back({0, 0, 0});
+    B.objs.push_back(o);
+    top.push_back((int)B.objs.size() - 1);
+  }
+  if (top.empty()) fail("scene has no objects (the reference dereferences a NULL bvh)");
+  int root = B.build(top);
+  while (B.objs[root].kind == kObjMesh) root = B.objs[root].a;  // Mesh::intersect delegates
+
+  // ---- flatten: DFS preorder nodes, DFS-order leaves, meshes spliced out.
+  s.nodes.clear();
+  s.prims.clear();
+  s.normals.clear();
+  s.leaf_src.clear();
+  auto resolve = [&](int id) {
+    while (B.objs[id].kind == kObjMesh) id = B.objs[id].a;
+    return id;
+  };
+  auto emit_leaf = [&](int id) {
+    const Obj& o = B.objs[id];
+    const LeafSource& ls = B.leaves[o.leaf];
+    DevPrim p{};
+    p.kind = ls.kind;
+    p.material = ls.material;
+    if (ls.kind == kPrimTriangle) {
+      const F3 v0 = vtx(ls.i0), v1 = vtx(ls.i1), v2 = vtx(ls.i2);
+      const F3 a1 = v0 - v1, a2 = v0 - v2;
+      const float rec[9] = {v0.x, v0.y, v0.z, a1.x, a1.y, a1.z, a2.x, a2.y, a2.z};
+      std::memcpy(p.v0, rec, sizeof rec);
+    } else {
+      std::memcpy(p.v0, ls.center, 12);
+      p.a1[0] = ls.radius;
+    }
+    const int index = (int)s.prims.size();
+    s.prims.push_back(p);
+    const F3 n = B.normals[o.leaf];
+    int mat_bits = ls.material;
+    float mat_f;
+    std::memcpy(&mat_f, &mat_bits, 4);
+    s.normals.insert(s.normals.end(), {n.x, n.y, n.z, mat_f});
+    s.leaf_src.push_back(ls);
+    return ~index;
+  };
+  auto put_box = [](float* dst, const Aabb& b) {
+    dst[0] = b.lo.x;
+    dst[1] = b.lo.y;
+    dst[2] = b.lo.z;
+    dst[3] = b.hi.x;
+    dst[4] = b.hi.y;
+    dst[5] = b.hi.z;
+  };
+  if (B.objs[root].kind != kObjBvh) {
+    s.root_kind = B.objs[root].kind == kObjTri ? kRootTriangle : kRootSphere;
+    s.root_ref = ~emit_leaf(root);
+    s.depth = 0;
+  } else {
+    s.root_kind = kRootNode;
+    s.root_ref = 0;
+    put_box(s.root_box, B.objs[root].box);
+    struct Frame {
+      int obj, node, stage, depth;
+    };
+    std::vector<Frame> st;
+    s.nodes.push_back(DevNode{});
+    st.push_back({root, 0, 0, 1});
+    s.depth = 1;
+    while (!st.empty()) {
+      Frame& f = st.back();
+      if (f.stage == 2) {
+        st.pop_back();
+        continue;
+      }
+      const int side = f.stage++;
+      const int child = resolve(side == 0 ? B.objs[f.obj].a : B.objs[f.obj].b);
+      const int node = f.node, depth = f.depth;
+      s.nodes[node].axis = B.objs[f.obj].axis;
+      if (B.objs[child].kind == kObjBvh) {
+        const int idx = (int)s.nodes.size();
+        s.nodes.push_back(DevNode{});
+        put_box(side == 0 ? s.nodes[node].b0 : s.nodes[node].b1, B.objs[child].box);
+        s.nodes[node].child[side] = idx;
+        if (depth + 1 > s.depth) s.depth = depth + 1;
+        st.push_back({child, idx, 0, depth + 1});  // invalidates f
+      } else {
+        const int ref = emit_leaf(child);
+        s.nodes[node].child[side] = ref;
+      }
+    }
+  }
+}
+
+std::string dump_bvh(const HostScene& s) {
+  std::ostringstream os;
+  auto hex = [](float f) {
+    unsigned u;
+    std::memcpy(&u, &f, 4);
+    char b[16];
+    std::snprintf(b, sizeof b, "%08x", u);
+    return std::string(b);
+  };
+  auto leaf = [&](int li) {
+    const LeafSource& l = s.leaf_src[li];
+    if (l.kind == kPrimTriangle)
+      os << "T " << l.i0 << " " << l.i1 << " " << l.i2 << " " << l.material << "\n";
+    else
+      os << "S " << hex(l.center[0]) << " " << hex(l.center[1]) << " " << hex(l.center[2])
+         << " " << hex(l.radius) << " " << l.material << "\n";
+  };
+  if (s.root_kind != kRootNode) {
+    leaf(s.root_ref);
+    return os.str();
+  }
+  struct Item {
+    int ref;
+    const float* box;
+  };
+  std::vector<Item> st{{0, s.root_box}};
+  while (!st.empty()) {
+    Item it = st.back();
+    st.pop_back();
+    if (it.ref < 0) {
+      leaf(~it.ref);
+      continue;
+    }
+    os << "N";
+    for (int k = 0; k < 6; k++) os << " " << hex(it.box[k]);
+    os << "\n";
+    const DevNode& n = s.nodes[it.ref];
+    st.push_back({n.child[1], n.b1});
+    st.push_back({n.child[0], n.b0});
+  }
+  return os.str();
+}
+
+}  // namespace rt

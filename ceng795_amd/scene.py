@@ -1,0 +1,142 @@
+"""Scene: the reference's Scene interface (HW2/Scene.h) over the C ABI."""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+
+@dataclass
+class CameraInfo:
+    width: int
+    height: int
+    num_samples: int
+    image_name: str
+    e: tuple
+    top_left: tuple
+    s_u: tuple
+    s_v: tuple
+
+
+class Scene:
+    """HW2 ``Scene``: parse an XML scene and render its cameras on the GPU.
+
+    ``render_image(camera_index, result, starting_row, height_increase)`` has the reference's
+    argument meaning (HW2/Scene.cpp:16-31): rows ``starting_row + k*height_increase`` of
+    ``result`` (an ``(h, w, 3)`` float32 array standing for ``Pixel[w*h]``) receive the fp32
+    radiance ``Pixel::color``; other rows are untouched.  Errors raise ``RTError`` (the
+    reference throws ``std::runtime_error`` from the loader, HW2/Scene.cpp:204,208).
+    """
+
+    def __init__(self, file_name: str, device: int = -1, traversal: str = "fast"):
+        h = C.c_void_p()
+        check(lib().rt_scene_load_xml(str(file_name).encode(), device, C.byref(h)))
+        self._h = h
+        self.set_traversal(traversal)
+
+    @classmethod
+    def _from_handle(cls, h: C.c_void_p) -> "Scene":
+        s = cls.__new__(cls)
+        s._h = h
+        return s
+
+    # ------------------------------------------------------------------ lifetime
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            lib().rt_scene_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ------------------------------------------------------------------ queries
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    @property
+    def num_cameras(self) -> int:
+        return lib().rt_scene_num_cameras(self._h)
+
+    @property
+    def num_lights(self) -> int:
+        return lib().rt_scene_num_lights(self._h)
+
+    @property
+    def bvh_depth(self) -> int:
+        return lib().rt_scene_bvh_depth(self._h)
+
+    def camera(self, i: int) -> CameraInfo:
+        c = _lib.rt_camera()
+        check(lib().rt_scene_camera(self._h, i, C.byref(c)))
+        name = lib().rt_scene_image_name(self._h, i).decode()
+        return CameraInfo(c.width, c.height, c.num_samples, name, tuple(c.e),
+                          tuple(c.top_left), tuple(c.s_u), tuple(c.s_v))
+
+    def set_traversal(self, mode: str) -> None:
+        m = {"fast": _lib.RT_TRAVERSAL_FAST, "reference": _lib.RT_TRAVERSAL_REFERENCE}[mode]
+        check(lib().rt_set_traversal(self._h, m))
+
+    def dump_bvh(self, path: str) -> None:
+        check(lib().rt_scene_dump_bvh(self._h, str(path).encode()))
+
+    # ------------------------------------------------------------------ rendering
+    def new_image(self, camera_index: int) -> np.ndarray:
+        c = self.camera(camera_index)
+        return np.zeros((c.height, c.width, 3), np.float32)
+
+    def render_image(self, camera_index: int, result: Optional[np.ndarray] = None,
+                     starting_row: int = 0, height_increase: int = 1):
+        """Scene::render_image (HW2/Scene.h:34-35).  Returns (result, rt_stats)."""
+        if result is None:
+            result = self.new_image(camera_index)
+        c = self.camera(camera_index)
+        if result.dtype != np.float32 or not result.flags.c_contiguous or \
+                result.size != c.width * c.height * 3:
+            raise ValueError("result must be a C-contiguous float32 array of h*w*3 values")
+        st = _lib.rt_stats()
+        check(lib().rt_render(self._h, camera_index, starting_row, height_increase,
+                              result.ctypes.data, C.byref(st)))
+        return result, st
+
+    def num_tiles(self, camera_index: int, starting_row: int = 0, row_stride: int = 1) -> int:
+        return check(lib().rt_num_tiles(self._h, camera_index, starting_row, row_stride))
+
+    def render_device(self, camera_index: int, out_ptr: int, *, starting_row: int = 0,
+                      row_stride: int = 1, tile_begin: int = 0, tile_step: int = 1,
+                      tile_major: bool = False, stream: int = 0) -> None:
+        """Asynchronous render into device memory at ``out_ptr`` on HIP stream ``stream``."""
+        check(lib().rt_render_device(self._h, camera_index, starting_row, row_stride,
+                                     tile_begin, tile_step, int(tile_major),
+                                     C.c_void_p(out_ptr), C.c_void_p(stream)))
+
+    def collect_stats(self) -> "_lib.rt_stats":
+        st = _lib.rt_stats()
+        check(lib().rt_collect_stats(self._h, C.byref(st)))
+        return st
+
+
+def write_png(path: str, rgb: np.ndarray) -> None:
+    """HW2/main.cpp:43-57: clamp(int(c), 0, 255) per channel."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    h, w = rgb.shape[:2]
+    check(lib().rt_write_png(str(path).encode(), rgb.ctypes.data, w, h))
+
+
+def host_dump_bvh(xml_path: str, out_path: str) -> None:
+    """Host-only: parse + build + flatten the BVH and dump it (no GPU needed)."""
+    check(lib().rt_host_dump_bvh_xml(str(xml_path).encode(), str(out_path).encode()))

@@ -1,0 +1,178 @@
+/* ceng795_rt — MI355X (gfx950) ray-trace hot path behind a C ABI.
+ *
+ * This is the drop-in boundary for the reference's render seam:
+ *
+ *   void Scene::render_image(int camera_index, Pixel* result, int starting_row,
+ *                            int height_increase = 1) const;      HW2/Scene.h:34-35
+ *                                                                 HW2/Scene.cpp:16-70
+ *
+ * The reference calls it from T host threads on a shared const Scene, each thread with a
+ * disjoint row set (HW2/main.cpp:33-36).  Here the whole row set runs as one HIP launch
+ * (or several callers on disjoint rows — rt_render is reentrant).  Everything up to the
+ * seam stays on the host, as in the reference: XML ingest (HW2/Scene.cpp:198-451), the
+ * Camera basis (HW2/Camera.h:10-29) and the BVH build (HW2/Bounding_volume_hierarchy.cpp:3-29)
+ * happen in rt_scene_create / rt_scene_load_xml, untimed like the reference's Scene ctor.
+ *
+ * Plain C types only: no torch, no HIP types in signatures (streams are void*).
+ * Every function returns 0 on success or a negative RT_E* code; the message of the last
+ * failure on the calling thread is in rt_last_error().  No C++ exception crosses the ABI.
+ */
+#ifndef CENG795_RT_H_
+#define CENG795_RT_H_
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CENG795_RT_ABI_VERSION 1
+
+enum {
+  RT_OK = 0,
+  RT_E_INVALID = -1,  /* bad argument or scene description            */
+  RT_E_HIP = -2,      /* HIP runtime error (message has the HIP text)   */
+  RT_E_IO = -3,       /* file could not be read / written                */
+  RT_E_PARSE = -4,    /* scene XML malformed (reference would throw/crash) */
+  RT_E_UNSUPPORTED = -5
+};
+
+/* HW2/Material.h:5-13 (field order kept). */
+typedef struct rt_material {
+  float ambient[3];
+  float diffuse[3];
+  float specular[3];
+  float mirror[3];
+  float transparency[3];
+  float refraction_index;
+  float phong_exponent;
+} rt_material;
+
+/* HW2/Point_light.h:5-8 */
+typedef struct rt_point_light {
+  float position[3];
+  float intensity[3];
+} rt_point_light;
+
+/* A camera after HW2/Camera.h:10-29's precompute: primary ray for pixel (x, y) is
+ *   o = e,  d = normalize((top_left + (x+0.5)*s_u) - (y+0.5)*s_v - e).          Camera.h:30-35
+ * num_samples is the per-axis sample count n = (int)sqrt(<NumSamples>) (Scene.cpp:275-276). */
+typedef struct rt_camera {
+  float e[3];
+  float top_left[3];
+  float s_u[3];
+  float s_v[3];
+  int width, height;
+  int num_samples;
+} rt_camera;
+
+/* Scene description, flattened, 0-based, host-owned (copied by rt_scene_create).
+ * Objects enter the top-level BVH in the reference's parse order: meshes, then loose
+ * triangles, then spheres (HW2/Scene.cpp:380-449). */
+typedef struct rt_scene_desc {
+  float background[3];          /* <BackgroundColor>, default 0 0 0      */
+  float shadow_ray_epsilon;     /* <ShadowRayEpsilon>, default 0.001     */
+  int max_recursion_depth;      /* <MaxRecursionDepth>, default 0        */
+  float ambient_light[3];       /* <Lights><AmbientLight>                */
+
+  const float* vertices;        /* fp32[3*num_vertices]  <VertexData>    */
+  int num_vertices;
+  const rt_material* materials;
+  int num_materials;
+  const rt_point_light* lights;
+  int num_lights;
+  const rt_camera* cameras;
+  int num_cameras;
+
+  int num_meshes;               /* <Mesh>: material + faces              */
+  const int* mesh_material;     /* int32[num_meshes]                     */
+  const int* mesh_face_count;   /* int32[num_meshes]                     */
+  const int* mesh_faces;        /* int32[3*sum(face_count)], vertex ids  */
+
+  int num_triangles;            /* <Triangle>                            */
+  const int* triangle_indices;  /* int32[3*num_triangles]                */
+  const int* triangle_material; /* int32[num_triangles]                  */
+
+  int num_spheres;              /* <Sphere>                              */
+  const int* sphere_center;     /* int32[num_spheres], vertex id         */
+  const float* sphere_radius;   /* fp32[num_spheres]                     */
+  const int* sphere_material;   /* int32[num_spheres]                    */
+} rt_scene_desc;
+
+/* Work counters for one render call. */
+typedef struct rt_stats {
+  long long primary_rays;
+  long long shadow_rays;
+  long long secondary_rays;
+  long long primary_hits;
+  double kernel_ms;             /* HIP-event time of the render kernel(s)  */
+} rt_stats;
+
+/* Traversal modes.  Both give the reference's result; see DESIGN.md §Traversal. */
+enum {
+  RT_TRAVERSAL_FAST = 0,        /* near-first order, distance culling (default) */
+  RT_TRAVERSAL_REFERENCE = 1    /* visits every box the reference visits       */
+};
+
+typedef struct rt_scene rt_scene;
+
+/* Replaces Scene::Scene's object + BVH construction (HW2/Scene.cpp:378-449 and
+ * Bounding_volume_hierarchy.cpp:3-29).  `device` < 0 = the calling thread's current HIP
+ * device.  Uploads the flattened scene to that device. */
+int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out);
+void rt_scene_destroy(rt_scene* scene);
+
+/* Host convenience: HW2/Scene.cpp:198-451's XML ingest, then rt_scene_create. */
+int rt_scene_load_xml(const char* xml_path, int device, rt_scene** out);
+
+int rt_scene_num_cameras(const rt_scene* scene);
+int rt_scene_camera(const rt_scene* scene, int camera_index, rt_camera* out);
+/* Output file name of a camera's <ImageName> (loaded scenes only; "" otherwise). */
+const char* rt_scene_image_name(const rt_scene* scene, int camera_index);
+int rt_scene_num_lights(const rt_scene* scene);
+/* Preorder BVH dump (oracle/ref/ref_harness.cpp `bvh` format) for topology parity. */
+int rt_scene_dump_bvh(const rt_scene* scene, const char* path);
+/* Host-only variant for tests without a GPU: XML ingest + BVH build + flatten, then the
+ * same dump.  Touches no HIP API. */
+int rt_host_dump_bvh_xml(const char* xml_path, const char* out_path);
+/* Height of the flattened BVH (levels of internal nodes). */
+int rt_scene_bvh_depth(const rt_scene* scene);
+
+int rt_set_traversal(rt_scene* scene, int mode);
+
+/* Scene::render_image(camera_index, result, starting_row, row_stride) with NumSamples == 1
+ * (HW2/Scene.cpp:24-31).  Writes fp32 RGB radiance — exactly Pixel::color after the
+ * reference's add_color(color, 1) — for rows j = starting_row + k*row_stride into
+ * out_rgb[3*(j*width + i)] (w*h*3 floats, row-major, top row first).  Other rows are left
+ * untouched.  Synchronous; safe to call concurrently on one scene from several threads. */
+int rt_render(rt_scene* scene, int camera_index, int starting_row, int row_stride,
+              float* out_rgb, rt_stats* stats);
+
+/* Device-resident variant for multi-GPU image tiling.  The image (rows starting_row +
+ * k*row_stride) is cut into 8x8 tiles numbered row-major; this call renders tiles
+ * tile_begin, tile_begin + tile_step, ... into d_out (device memory):
+ *   tile_major == 0: d_out is a full w*h*3 frame, written in place;
+ *   tile_major == 1: d_out holds the selected tiles back to back, 8*8*3 floats each
+ *                    (pixels outside the image are written as 0).
+ * Asynchronous on `hip_stream` (a hipStream_t, NULL = default stream).  stats may be NULL;
+ * when given, ray counts are filled after the caller synchronises the stream and calls
+ * rt_collect_stats. */
+int rt_render_device(rt_scene* scene, int camera_index, int starting_row, int row_stride,
+                     int tile_begin, int tile_step, int tile_major, float* d_out,
+                     void* hip_stream);
+int rt_num_tiles(const rt_scene* scene, int camera_index, int starting_row, int row_stride);
+/* Reads (and resets) the device ray counters accumulated by rt_render_device calls. */
+int rt_collect_stats(rt_scene* scene, rt_stats* stats);
+
+/* PNG output as HW2/main.cpp:43-57: per channel clamp(int(c), 0, 255), alpha 255. */
+int rt_write_png(const char* path, const float* rgb, int width, int height);
+
+/* Camera precompute of HW2/Camera.h:10-29 in the reference's fp32 operation order. */
+int rt_camera_from_view(const float position[3], const float gaze[3], const float up[3],
+                        const float near_plane[4] /* l r b t */, float near_distance,
+                        int width, int height, int num_samples, rt_camera* out);
+
+const char* rt_last_error(void);
+int rt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

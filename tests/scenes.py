@@ -1,0 +1,61 @@
+"""Scene catalogue for the tests: deterministic XML from tools/gen_scene.py.
+
+Each entry names what it covers from SURVEY.md appendix A (parity hazards)."""
+from __future__ import annotations
+
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import gen_scene as G  # noqa: E402
+
+# name -> (factory, what it exercises)
+CATALOGUE = {
+    # C1: 3 triangles + 1 sphere, Phong exponent 10 on one material (double pow)
+    "c1": (lambda: G.simple_scene(400, 400), "C1 plumbing scene; misses -> background"),
+    "hf_small": (lambda: G.heightfield_scene(32, 64, 48), "shared mesh edges (equal-t ties)"),
+    "hf_side": (lambda: G.heightfield_scene(48, 96, 64, view="side"),
+                "partial coverage, oblique + grazing rays, silhouettes"),
+    "soup1": (lambda: G.soup_scene(1, 96, 96),
+              "meshes + loose tris + spheres, 4 lights, back-lit faces, grazing camera"),
+    "soup2": (lambda: G.soup_scene(2, 80, 64), "second seed"),
+    "soup3": (lambda: G.soup_scene(3, 64, 72, n_mesh_tris=2000), "bigger mesh"),
+    "single_sphere": (lambda: G.single_sphere_scene(64, 64),
+                      "root is a sphere: negative-t hits shaded (Sphere.h:43-45)"),
+    "single_triangle": (lambda: G.single_triangle_scene(64, 64), "root is a triangle"),
+    "c2": (lambda: G.heightfield_scene(187, 800, 800, name="c2.png"), "C2 69k tris 800x800"),
+}
+
+# Scenes whose MaxRecursionDepth > 0 with mirror / dielectric materials.
+RECURSIVE = {
+    "soup_depth3": (lambda: G.soup_scene(4, 96, 96, depth=3, mirror=True, glass=True),
+                    "mirror + dielectric recursion depth 3"),
+}
+
+SMALL = ["c1", "hf_small", "hf_side", "soup1", "soup2", "soup3", "single_sphere",
+         "single_triangle"]
+
+
+def write(name: str, directory: str) -> str:
+    table = {**CATALOGUE, **RECURSIVE}
+    path = os.path.join(directory, f"{name}.xml")
+    if not os.path.exists(path):
+        text = table[name][0]().to_xml()
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(text)
+        os.replace(tmp, path)
+    return path
+
+
+def write_c3(directory: str, cameras: int = 1) -> str:
+    path = os.path.join(directory, f"c3_{cameras}.xml")
+    if not os.path.exists(path):
+        spec = G.heightfield_scene(708, 1920, 1080, name="c3.png", cameras=cameras)
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(spec.to_xml())
+        os.replace(tmp, path)
+    return path

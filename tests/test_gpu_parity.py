@@ -1,0 +1,105 @@
+"""GPU parity: the HIP render path against the CPU oracle (oracle/cpu_ref, which
+tests/test_oracle_golden.py pins bit for bit to the reference's own output).
+
+Run on the GPU box: ``python -m pytest tests -m gpu``.  Everything goes through the C ABI
+(libceng795_rt.so) via ceng795_amd.Scene."""
+import os
+
+import numpy as np
+import pytest
+
+import scenes
+from conftest import assert_parity
+from oracle.cpu_ref import OracleScene
+
+pytestmark = pytest.mark.gpu
+
+THREADS = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope="module")
+def rt():
+    import ceng795_amd
+    return ceng795_amd
+
+
+_ORACLE_CACHE = {}
+
+
+def oracle_frame(xml, cam):
+    key = (xml, cam)
+    if key not in _ORACLE_CACHE:
+        o = OracleScene(xml)
+        _ORACLE_CACHE[key] = o.render(cam, threads=THREADS)
+    return _ORACLE_CACHE[key]
+
+
+@pytest.mark.parametrize("mode", ["fast", "reference"])
+@pytest.mark.parametrize("name", scenes.SMALL + ["c2"])
+def test_render_matches_oracle(rt, scene_dir, name, mode):
+    xml = scenes.write(name, scene_dir)
+    with rt.Scene(xml, traversal=mode) as s:
+        for cam in range(s.num_cameras):
+            ref, st = oracle_frame(xml, cam)
+            got, gst = s.render_image(cam)
+            nbad = assert_parity(got, ref, f"{name}/cam{cam}/{mode}")
+            assert nbad == 0, f"{name}/cam{cam}/{mode}: {nbad} channels within 1 ulp but not identical"
+            assert gst.primary_rays == st.primary_rays
+            assert gst.primary_hits == st.primary_hits
+            assert gst.shadow_rays == st.shadow_rays
+
+
+@pytest.mark.parametrize("start,stride", [(0, 1), (3, 5), (7, 8), (0, 64), (47, 1)])
+def test_row_subset_like_render_image(rt, scene_dir, start, stride):
+    """render_image(cam, px, starting_row, height_increase) writes exactly those rows."""
+    xml = scenes.write("soup1", scene_dir)
+    ref, _ = oracle_frame(xml, 0)
+    with rt.Scene(xml) as s:
+        sentinel = np.full(ref.shape, -7.0, np.float32)
+        got, _ = s.render_image(0, sentinel, start, stride)
+        rows = np.arange(ref.shape[0])
+        sel = (rows >= start) & ((rows - start) % stride == 0)
+        assert np.array_equal(got[sel].view(np.uint32), ref[sel].view(np.uint32))
+        assert np.all(got[~sel] == -7.0)
+
+
+def test_tile_major_device_render(rt, scene_dir):
+    """Multi-GPU building block: tiles tile_begin + k*tile_step, tile-major, in HBM."""
+    import torch
+    xml = scenes.write("hf_side", scene_dir)
+    ref, _ = oracle_frame(xml, 0)
+    h, w, _ = ref.shape
+    with rt.Scene(xml) as s:
+        total = s.num_tiles(0)
+        for begin, step in [(0, 1), (1, 3), (2, 4)]:
+            sel = list(range(begin, total, step))
+            out = torch.full((len(sel) * 64 * 3,), -1.0, dtype=torch.float32, device="cuda")
+            s.render_device(0, out.data_ptr(), tile_begin=begin, tile_step=step, tile_major=True,
+                            stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            tiles = out.cpu().numpy().reshape(len(sel), 8, 8, 3)
+            tx = (w + 7) // 8
+            for k, t in enumerate(sel):
+                y0, x0 = (t // tx) * 8, (t % tx) * 8
+                exp = np.zeros((8, 8, 3), np.float32)
+                blk = ref[y0:y0 + 8, x0:x0 + 8]
+                exp[:blk.shape[0], :blk.shape[1]] = blk
+                assert np.array_equal(tiles[k].view(np.uint32), exp.view(np.uint32)), (begin, step, t)
+
+
+def test_recursive_scene_reports_unsupported(rt, scene_dir):
+    xml = scenes.write("soup_depth3", scene_dir)
+    with rt.Scene(xml) as s:
+        with pytest.raises(rt.RTError) as e:
+            s.render_image(0)
+        assert e.value.code == -5
+
+
+@pytest.mark.slow
+def test_c3_full_resolution_matches_oracle(rt, scene_dir):
+    xml = scenes.write_c3(scene_dir)
+    ref, st = oracle_frame(xml, 0)
+    with rt.Scene(xml) as s:
+        got, gst = s.render_image(0)
+        assert assert_parity(got, ref, "c3") == 0
+        assert gst.rays() == st.primary_rays + st.shadow_rays
