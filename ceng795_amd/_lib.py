@@ -9,7 +9,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libceng795_rt.so")
+# CENG795_LIB=diag selects the RT_DIAG build (packet-level work counters, slower).
+LIB_PATH = os.path.join(_HERE, "lib", "libceng795_rt_diag.so"
+                        if os.environ.get("CENG795_LIB") == "diag" else "libceng795_rt.so")
 
 RT_OK = 0
 RT_E_INVALID = -1
@@ -90,6 +92,7 @@ SIGNATURES = {
     "rt_last_error": (C.c_char_p, []),
     "rt_abi_version": (C.c_int, []),
     "rt_host_dump_bvh_xml": (C.c_int, [C.c_char_p, C.c_char_p]),
+    "rt_debug_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong)]),
 }
 
 _lib = None

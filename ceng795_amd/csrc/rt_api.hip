@@ -20,6 +20,8 @@ hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevP
                          const float* normals, const DevMaterial* mats, const DevLight* lights,
                          bool fast, bool deep, hipStream_t stream);
 int max_supported_depth();
+unsigned long long read_reset_exact_fallbacks();
+bool diag_build();
 void write_png(const std::string& path, const float* rgb, int w, int h);
 }  // namespace rt
 
@@ -37,6 +39,9 @@ struct rt_scene {
   DevMaterial* d_mats = nullptr;
   DevLight* d_lights = nullptr;
   unsigned long long* d_counters = nullptr;
+  int2_t* d_hits = nullptr;  // rt_render_device's primary-hit records (largest camera)
+  unsigned* d_occ = nullptr; // rt_render_device's occlusion bits
+  size_t hits_capacity = 0;  // records
 };
 
 namespace {
@@ -96,6 +101,8 @@ void free_device(rt_scene* s) {
   (void)hipFree(s->d_mats);
   (void)hipFree(s->d_lights);
   (void)hipFree(s->d_counters);
+  (void)hipFree(s->d_hits);
+  (void)hipFree(s->d_occ);
   if (cur != s->device) (void)hipSetDevice(cur);
 }
 
@@ -110,6 +117,8 @@ struct DeviceGuard {
     if (hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
 };
+
+int occ_words(const HostScene& h) { return std::max(1, ((int)h.lights.size() + 31) / 32); }
 
 int create_from_host(rt_scene* s, int device) {
   if (device < 0) hip_check(hipGetDevice(&device), "hipGetDevice");
@@ -130,10 +139,18 @@ int create_from_host(rt_scene* s, int device) {
   s->d_normals = upload(h.normals, "upload normals");
   s->d_mats = upload(h.materials, "upload materials");
   s->d_lights = upload(h.lights, "upload lights");
-  hip_check(hipMalloc(&s->d_counters, sizeof(unsigned long long) * 4 * kCounterRows),
+  hip_check(hipMalloc(&s->d_counters, sizeof(unsigned long long) * kCounterWidth * kCounterRows),
             "alloc counters");
-  hip_check(hipMemset(s->d_counters, 0, sizeof(unsigned long long) * 4 * kCounterRows),
+  hip_check(hipMemset(s->d_counters, 0, sizeof(unsigned long long) * kCounterWidth * kCounterRows),
             "zero counters");
+  size_t most = 1;
+  for (const rt_camera& c : h.cameras) {
+    const size_t tiles = (size_t)((c.width + kTile - 1) / kTile) * ((c.height + kTile - 1) / kTile);
+    most = std::max(most, tiles * kTile * kTile);
+  }
+  hip_check(hipMalloc(&s->d_hits, most * sizeof(int2_t)), "alloc hit records");
+  hip_check(hipMalloc(&s->d_occ, most * sizeof(unsigned) * occ_words(h)), "alloc occlusion bits");
+  s->hits_capacity = most;
   return RT_OK;
 }
 
@@ -186,6 +203,9 @@ RenderParams make_params(const rt_scene* s, int cam, int row0, int row_stride, i
       tile_begin < tp.tiles_total ? (tp.tiles_total - tile_begin + tile_step - 1) / tile_step : 0;
   P.tile_major = tile_major;
   P.out = out;
+  P.hits = s->d_hits;
+  P.occ = s->d_occ;
+  P.occ_words = occ_words(h);
   P.counters = counters ? s->d_counters : nullptr;
   return P;
 }
@@ -336,18 +356,36 @@ int rt_collect_stats(rt_scene* s, rt_stats* stats) {
   if (!s || !stats) return set_error(RT_E_INVALID, "rt_collect_stats: NULL argument");
   return guarded([&] {
     DeviceGuard g(s->device);
-    std::vector<unsigned long long> c(4 * kCounterRows);
+    std::vector<unsigned long long> c(kCounterWidth * kCounterRows);
     hip_check(hipMemcpy(c.data(), s->d_counters, c.size() * sizeof c[0], hipMemcpyDeviceToHost),
               "read counters");
     hip_check(hipMemset(s->d_counters, 0, c.size() * sizeof c[0]), "reset counters");
     std::memset(stats, 0, sizeof *stats);
     for (int r = 0; r < kCounterRows; r++) {
-      stats->primary_rays += (long long)c[4 * r];
-      stats->shadow_rays += (long long)c[4 * r + 1];
-      stats->secondary_rays += (long long)c[4 * r + 2];
-      stats->primary_hits += (long long)c[4 * r + 3];
+      stats->primary_rays += (long long)c[kCounterWidth * r + kCntPrimary];
+      stats->shadow_rays += (long long)c[kCounterWidth * r + kCntShadow];
+      stats->secondary_rays += (long long)c[kCounterWidth * r + kCntSecondary];
+      stats->primary_hits += (long long)c[kCounterWidth * r + kCntHits];
     }
     return RT_OK;
+  });
+}
+
+int rt_debug_counters(rt_scene* s, long long* out16) {
+  if (!s || !out16) return set_error(RT_E_INVALID, "rt_debug_counters: NULL argument");
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    std::vector<unsigned long long> c(kCounterWidth * kCounterRows);
+    hip_check(hipMemcpy(c.data(), s->d_counters, c.size() * sizeof c[0], hipMemcpyDeviceToHost),
+              "read counters");
+    hip_check(hipMemset(s->d_counters, 0, c.size() * sizeof c[0]), "reset counters");
+    for (int k = 0; k < kCounterWidth; k++) {
+      unsigned long long sum = 0;
+      for (int r = 0; r < kCounterRows; r++) sum += c[kCounterWidth * r + k];
+      out16[k] = (long long)sum;
+    }
+    out16[kCntExactBox] = (long long)read_reset_exact_fallbacks();
+    return diag_build() ? 1 : 0;
   });
 }
 
@@ -361,10 +399,14 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
       if (tp.rows == 0) return RT_OK;
       const size_t frame = (size_t)c.width * c.height * 3;
       float* d_out = nullptr;
+      int2_t* d_hits = nullptr;
+      unsigned* d_occ = nullptr;
       hipStream_t stream = nullptr;
       hipEvent_t e0 = nullptr, e1 = nullptr;
       auto cleanup = [&] {
         if (d_out) (void)hipFree(d_out);
+        if (d_hits) (void)hipFree(d_hits);
+        if (d_occ) (void)hipFree(d_occ);
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         if (stream) (void)hipStreamDestroy(stream);
@@ -376,11 +418,18 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
         hip_check(hipEventCreate(&e1), "event");
         // Counters are per scene; this call reports its own deltas via a private buffer.
         unsigned long long* d_cnt = nullptr;
-        hip_check(hipMalloc(&d_cnt, sizeof(unsigned long long) * 4 * kCounterRows), "alloc counters");
-        hip_check(hipMemsetAsync(d_cnt, 0, sizeof(unsigned long long) * 4 * kCounterRows, stream),
+        hip_check(hipMalloc(&d_cnt, sizeof(unsigned long long) * kCounterWidth * kCounterRows), "alloc counters");
+        hip_check(hipMemsetAsync(d_cnt, 0, sizeof(unsigned long long) * kCounterWidth * kCounterRows, stream),
                   "zero counters");
         RenderParams P = make_params(s, cam, row0, row_stride, 0, 1, 0, d_out, true);
         P.counters = d_cnt;
+        hip_check(hipMalloc(&d_hits, sizeof(int2_t) * kTile * kTile * (size_t)std::max(1, P.num_sel_tiles)),
+                  "alloc hit records");
+        P.hits = d_hits;
+        hip_check(hipMalloc(&d_occ, sizeof(unsigned) * P.occ_words * kTile * kTile *
+                                        (size_t)std::max(1, P.num_sel_tiles)),
+                  "alloc occlusion bits");
+        P.occ = d_occ;
         hip_check(hipEventRecord(e0, stream), "event record");
         hipError_t le = launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats,
                                       s->d_lights, s->mode == RT_TRAVERSAL_FAST, s->deep, stream);
@@ -395,7 +444,7 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
                                    d_out + (size_t)row0 * c.width * 3, row_bytes * row_stride,
                                    row_bytes, tp.rows, hipMemcpyDeviceToHost, stream),
                   "copy rows");
-        std::vector<unsigned long long> cnt(4 * kCounterRows);
+        std::vector<unsigned long long> cnt(kCounterWidth * kCounterRows);
         hip_check(hipMemcpyAsync(cnt.data(), d_cnt, cnt.size() * sizeof cnt[0],
                                  hipMemcpyDeviceToHost, stream),
                   "copy counters");
@@ -404,10 +453,10 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
         if (stats) {
           std::memset(stats, 0, sizeof *stats);
           for (int r = 0; r < kCounterRows; r++) {
-            stats->primary_rays += (long long)cnt[4 * r];
-            stats->shadow_rays += (long long)cnt[4 * r + 1];
-            stats->secondary_rays += (long long)cnt[4 * r + 2];
-            stats->primary_hits += (long long)cnt[4 * r + 3];
+            stats->primary_rays += (long long)cnt[kCounterWidth * r + kCntPrimary];
+            stats->shadow_rays += (long long)cnt[kCounterWidth * r + kCntShadow];
+            stats->secondary_rays += (long long)cnt[kCounterWidth * r + kCntSecondary];
+            stats->primary_hits += (long long)cnt[kCounterWidth * r + kCntHits];
           }
           float ms = 0;
           hip_check(hipEventElapsedTime(&ms, e0, e1), "elapsed");

@@ -20,6 +20,15 @@ constexpr int kTile = 8;          // one wavefront = one 8x8 pixel packet
 constexpr int kWavesPerBlock = 4; // 256-thread workgroups
 constexpr int kLaneStack = 64;    // per-wave traversal stack held one entry per VGPR lane
 constexpr int kCounterRows = 64;  // ray-counter rows (spread atomics)
+constexpr int kCounterWidth = 16; // u64 counters per row
+// counter columns
+enum : int {
+  kCntPrimary = 0, kCntShadow = 1, kCntSecondary = 2, kCntHits = 3,
+  // RT_DIAG builds only: packet-level traversal work
+  kCntPrimNodes = 4, kCntPrimNodeLanes = 5, kCntPrimLeaves = 6, kCntPrimLeafLanes = 7,
+  kCntShadNodes = 8, kCntShadNodeLanes = 9, kCntShadLeaves = 10, kCntShadLeafLanes = 11,
+  kCntExactBox = 12
+};
 
 struct alignas(16) DevNode {
   float b0[6];   // child 0 box: lo.xyz, hi.xyz (unused if child 0 is a leaf)
@@ -57,6 +66,10 @@ struct DevLight {
   float pad[2];
 };
 
+struct alignas(8) int2_t {
+  int32_t x, y;
+};
+
 enum RootKind : int32_t { kRootNode = 0, kRootTriangle = 1, kRootSphere = 2 };
 
 struct RenderParams {
@@ -82,7 +95,10 @@ struct RenderParams {
   int tiles_x, tiles_total, tile_begin, tile_step, num_sel_tiles;
   int tile_major;
   float* out;
-  // kCounterSlots rows of 4: primary rays, shadow rays, secondary rays, primary hits
+  int2_t* hits;   // num_sel_tiles * 64 records {t bits, leaf}: trace_primary -> shadow, shade
+  unsigned* occ;  // num_sel_tiles * 64 * occ_words light-occlusion bits: trace_shadow -> shade
+  int occ_words;  // ceil(num_lights / 32)
+  // kCounterRows rows of kCounterWidth u64 (columns: kCnt*)
   unsigned long long* counters;
 };
 

@@ -32,6 +32,15 @@ namespace rt {
 constexpr float kEps = 0.000001f;  // HW2/Vector3.h:7 kEpsilon
 constexpr int kCounterSlots = kCounterRows;
 
+#ifdef RT_DIAG
+#define DIAG(stmt) stmt
+#else
+#define DIAG(stmt)
+#endif
+struct Diag {  // per-wave traversal work (RT_DIAG builds)
+  unsigned long long nodes = 0, node_lanes = 0, leaves = 0, leaf_lanes = 0, exact = 0;
+};
+
 // ------------------------------------------------------------------ vector helpers
 struct V3 {
   float x, y, z;
@@ -94,6 +103,10 @@ __device__ __forceinline__ bool box_exact(const float* b, const LaneRay& r) {
   return !(bt < 0.0f || bt == RT_INF);
 }
 
+#ifdef RT_DIAG
+__device__ unsigned long long g_exact_fallbacks;  // lanes that needed box_exact
+#endif
+
 // Fast slab test.  With q = RN(RN(m - o) / d) the reference's quotient and q' = RN(RN(m - o)
 // * rcp(d)) ours, |q' - q| <= 2^-22 |q| and sign(q') == sign(q) exactly.  The reference
 // accepts iff tmin <= tmax and tmax >= 0 (tmin, tmax finite here); the sign test is exact and
@@ -121,6 +134,9 @@ __device__ __forceinline__ bool box_hit(const float* b, const LaneRay& r, float&
   const float band = (__builtin_fabsf(tn) + __builtin_fabsf(tf)) * 0x1p-20f + 0x1p-120f;
   if (tn < tf - band) return tf >= 0.0f;
   if (tn > tf + band) return false;
+#ifdef RT_DIAG
+  atomicAdd(&g_exact_fallbacks, 1ull);
+#endif
   return box_exact(b, r);
 }
 
@@ -223,7 +239,7 @@ __device__ __forceinline__ float cull_limit(float t) { return t + t * 0x1p-8f; }
 template <bool SKIP, bool FAST, bool DEEP>
 __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode* __restrict__ nodes,
                             const DevPrim* __restrict__ prims, int* spill, const LaneRay& r,
-                            bool active, float& best_t, int& best_leaf) {
+                            bool active, float& best_t, int& best_leaf, Diag& dg) {
   best_t = RT_INF;
   best_leaf = -1;
   if (P.root_kind != kRootNode) {  // the root IS the primitive (BVH.h:13-14): its own rule
@@ -244,6 +260,9 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
   for (;;) {
     const DevNode& N = nodes[node];
     const bool in = (m >> lane) & 1;
+    DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m);
+         dg.leaves += (N.child[0] < 0) + (N.child[1] < 0);
+         dg.leaf_lanes += ((N.child[0] < 0) + (N.child[1] < 0)) * __builtin_popcountll(m));
     const int c0 = N.child[0], c1 = N.child[1];
     uint64_t m0 = 0, m1 = 0;
     float t0 = RT_INF, t1 = RT_INF;
@@ -304,7 +323,7 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
 template <bool SKIP, bool FAST, bool DEEP>
 __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* __restrict__ nodes,
                          const DevPrim* __restrict__ prims, int* spill, const LaneRay& r,
-                         bool active, float thr) {
+                         bool active, float thr, Diag& dg) {
   if (P.root_kind != kRootNode) {
     float t;
     return active && leaf_test(prims, P.root_ref, r, t) && t < thr && t > 0.0f;
@@ -322,6 +341,9 @@ __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* _
   for (;;) {
     const DevNode& N = nodes[node];
     const bool in = (m >> lane) & 1;
+    DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m);
+         dg.leaves += (N.child[0] < 0) + (N.child[1] < 0);
+         dg.leaf_lanes += ((N.child[0] < 0) + (N.child[1] < 0)) * __builtin_popcountll(m));
     const int c0 = N.child[0], c1 = N.child[1];
     uint64_t m0 = 0, m1 = 0;
     float t0 = RT_INF, t1 = RT_INF;
@@ -376,117 +398,221 @@ __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* _
   return occ;
 }
 
-// ------------------------------------------------------------------ render kernel
-template <bool FAST, bool DEEP>
-__device__ __forceinline__ void render_packet(const RenderParams& P, const DevNode* __restrict__ nodes,
-                              const DevPrim* __restrict__ prims,
-                              const float* __restrict__ normals,
-                              const DevMaterial* __restrict__ mats,
-                              const DevLight* __restrict__ lights, int sel, int* spill) {
-  const int lane = lane_id();
+// ------------------------------------------------------------------ render kernels
+// Two launches per frame (wavefront style): `trace_primary` finds each pixel's closest hit and
+// writes an 8-byte {t, leaf} record; `shade` rebuilds the shading inputs from it and runs the
+// point-light loop with its shadow rays.  Splitting keeps each kernel's live state small
+// (occupancy is what hides the dependent node loads), at 16 B of HBM traffic per pixel.
+struct PacketPixel {
+  int lane, px, py;
+  bool valid;
+};
+
+__device__ __forceinline__ PacketPixel packet_pixel(const RenderParams& P, int sel) {
+  PacketPixel q;
+  q.lane = lane_id();
   const int tile = P.tile_begin + sel * P.tile_step;
   const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-  const int px = tx * kTile + (lane & 7);
-  const int lr = ty * kTile + (lane >> 3);  // logical row
-  const bool valid = px < P.width && lr < P.rows;
-  const int py = P.row0 + lr * P.row_stride;
+  q.px = tx * kTile + (q.lane & 7);
+  const int lr = ty * kTile + (q.lane >> 3);  // logical row
+  q.valid = q.px < P.width && lr < P.rows;
+  q.py = P.row0 + lr * P.row_stride;
+  return q;
+}
 
-  // Camera::calculate_ray_at (HW2/Camera.h:30-35); x + 0.5 is exact in fp32 for x < 2^23.
+// Camera::calculate_ray_at (HW2/Camera.h:30-35); x + 0.5 is exact in fp32 for x < 2^23.
+__device__ __forceinline__ V3 primary_dir(const RenderParams& P, int px, int py) {
   const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
-  const V3 e = ld3(P.cam_e);
   const V3 s = (ld3(P.cam_tl) + ld3(P.cam_su) * fx) - ld3(P.cam_sv) * fy;
-  const LaneRay ray = make_ray(e, normalize(s - e));
+  return normalize(s - ld3(P.cam_e));
+}
 
-  const bool skip = ballot(valid && (ray.skip0 || ray.skip1 || ray.skip2)) != 0;
+__device__ __forceinline__ unsigned long long* counter_row(const RenderParams& P, int sel) {
+  return P.counters + kCounterWidth * (sel % kCounterSlots);
+}
+
+template <bool FAST, bool DEEP>
+__device__ __forceinline__ void primary_packet(const RenderParams& P,
+                                               const DevNode* __restrict__ nodes,
+                                               const DevPrim* __restrict__ prims, int sel,
+                                               int* spill) {
+  const PacketPixel q = packet_pixel(P, sel);
+  const LaneRay ray = make_ray(ld3(P.cam_e), primary_dir(P, q.px, q.py));
+  Diag dg;
+  const bool skip = ballot(q.valid && (ray.skip0 || ray.skip1 || ray.skip2)) != 0;
   float t;
   int leaf;
   if (skip)
-    closest_hit<true, FAST, DEEP>(P, nodes, prims, spill, ray, valid, t, leaf);
+    closest_hit<true, FAST, DEEP>(P, nodes, prims, spill, ray, q.valid, t, leaf, dg);
   else
-    closest_hit<false, FAST, DEEP>(P, nodes, prims, spill, ray, valid, t, leaf);
-
-  const bool hit = valid && leaf >= 0;
-  V3 color = v3(0.0f, 0.0f, 0.0f);
-  V3 p = v3(0, 0, 0), n = v3(0, 0, 0), w0 = v3(0, 0, 0);
-  const DevMaterial* m = mats;
-  if (hit) {
-    p = ray.o + ray.d * t;  // Ray::point_at = o + t*d
-    const float* nr = normals + 4 * leaf;
-    const DevPrim& pr = prims[leaf];
-    m = mats + pr.material;
-    if (pr.kind == kPrimTriangle)
-      n = ld3(nr);
-    else
-      n = normalize(p - ld3(pr.v0));  // Sphere.h:42,50
-    w0 = normalize(ray.o - p);
-    color = color + ld3(m->ambient) * ld3(P.ambient);
-  } else if (valid) {
-    color = ld3(P.background);  // primary miss: max_recursion_depth == depth
-  }
-  const unsigned long long nhit = __builtin_popcountll(ballot(hit));
-  for (int li = 0; li < P.num_lights; li++) {
-    const DevLight& L = lights[li];
-    const V3 ld = ld3(L.position) - p;
-    const V3 wi = normalize(ld);
-    const float dist = length(ld);
-    const LaneRay sr = make_ray(p + wi * P.eps, wi);
-    const float thr = dist - P.eps;
-    const bool sskip = ballot(hit && (sr.skip0 || sr.skip1 || sr.skip2)) != 0;
-    bool occ;
-    if (sskip)
-      occ = occluded<true, FAST, DEEP>(P, nodes, prims, spill, sr, hit, thr);
-    else
-      occ = occluded<false, FAST, DEEP>(P, nodes, prims, spill, sr, hit, thr);
-    if (hit && !occ) {
-      const V3 I = ld3(L.intensity);
-      const float d2 = dist * dist;
-      const float cos_d = dot(n, wi);
-      color = color + ((ld3(m->diffuse) * I) * cos_d) / d2;
-      const float cos_s = __builtin_fmaxf(dot(n, normalize(w0 + wi)), 0.0f);
-      const float pw = (float)pow((double)cos_s, (double)m->phong_exponent);
-      color = color + ((ld3(m->specular) * I) * pw) / d2;
-    }
-  }
-  if (valid) {
-    float* o;
-    if (P.tile_major)
-      o = P.out + 3 * ((size_t)sel * (kTile * kTile) + lane);
-    else
-      o = P.out + 3 * ((size_t)py * P.width + px);
-    o[0] = 0.0f + color.x;  // Pixel::add_color(color, 1) onto a zeroed pixel
-    o[1] = 0.0f + color.y;
-    o[2] = 0.0f + color.z;
-  } else if (P.tile_major && sel < P.num_sel_tiles) {
-    float* o = P.out + 3 * ((size_t)sel * (kTile * kTile) + lane);
-    o[0] = o[1] = o[2] = 0.0f;
-  }
+    closest_hit<false, FAST, DEEP>(P, nodes, prims, spill, ray, q.valid, t, leaf, dg);
+  int2_t rec;
+  rec.x = __float_as_int(t);
+  rec.y = q.valid ? leaf : -2;  // -1 miss, -2 outside the image
+  P.hits[(size_t)sel * (kTile * kTile) + q.lane] = rec;
   if (P.counters) {  // spread over kCounterSlots rows: no single hot address
-    const unsigned long long nvalid = __builtin_popcountll(ballot(valid));
-    if (lane == 0) {
-      unsigned long long* c = P.counters + 4 * (sel % kCounterSlots);
-      atomicAdd(&c[0], nvalid);
-      atomicAdd(&c[1], nhit * (unsigned long long)P.num_lights);
-      atomicAdd(&c[3], nhit);
+    const unsigned long long nvalid = __builtin_popcountll(ballot(q.valid));
+    const unsigned long long nhit = __builtin_popcountll(ballot(q.valid && leaf >= 0));
+    if (q.lane == 0) {
+      unsigned long long* c = counter_row(P, sel);
+      atomicAdd(&c[kCntPrimary], nvalid);
+      atomicAdd(&c[kCntHits], nhit);
+#ifdef RT_DIAG
+      atomicAdd(&c[kCntPrimNodes], dg.nodes);
+      atomicAdd(&c[kCntPrimNodeLanes], dg.node_lanes);
+      atomicAdd(&c[kCntPrimLeaves], dg.leaves);
+      atomicAdd(&c[kCntPrimLeafLanes], dg.leaf_lanes);
+#endif
     }
   }
 }
 
+// Hit point and normal of a primary hit, rebuilt from its {t, leaf} record exactly as
+// trace_ray computes them (HW2/Scene.cpp:101-105; Sphere.h:42,50 for sphere normals).
+__device__ __forceinline__ V3 hit_point(const RenderParams& P, const PacketPixel& q, float t) {
+  return ld3(P.cam_e) + primary_dir(P, q.px, q.py) * t;  // Ray::point_at = o + t*d
+}
+
+// Shadow rays of HW2/Scene.cpp:113-127: one bit per point light, set when the light is
+// occluded for this pixel's primary hit.
 template <bool FAST, bool DEEP>
-__global__ __launch_bounds__(kWavesPerBlock * 64) void render_kernel(
-    RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims,
-    const float* __restrict__ normals, const DevMaterial* __restrict__ mats,
-    const DevLight* __restrict__ lights) {
-  extern __shared__ __attribute__((aligned(16))) int deep_stack[];
-  // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so hand each
-  // XCD a contiguous run of tiles — neighbouring packets share BVH nodes through its L2.
+__device__ __forceinline__ void shadow_packet(const RenderParams& P,
+                                              const DevNode* __restrict__ nodes,
+                                              const DevPrim* __restrict__ prims,
+                                              const DevLight* __restrict__ lights, int sel,
+                                              int* spill) {
+  const PacketPixel q = packet_pixel(P, sel);
+  const size_t pix = (size_t)sel * (kTile * kTile) + q.lane;
+  const int2_t rec = P.hits[pix];
+  const bool hit = rec.y >= 0;
+  const V3 p = hit ? hit_point(P, q, __int_as_float(rec.x)) : v3(0, 0, 0);
+  Diag dg;
+  for (int w = 0; w < P.occ_words; w++) {
+    unsigned bits = 0;
+    const int lend = min(P.num_lights, 32 * (w + 1));
+    for (int li = 32 * w; li < lend; li++) {
+      const DevLight& L = lights[li];
+      const V3 ld = ld3(L.position) - p;
+      const V3 wi = normalize(ld);
+      const float dist = length(ld);
+      const LaneRay sr = make_ray(p + wi * P.eps, wi);  // p + eps * w_i
+      const float thr = dist - P.eps;
+      const bool sskip = ballot(hit && (sr.skip0 || sr.skip1 || sr.skip2)) != 0;
+      bool occ;
+      if (sskip)
+        occ = occluded<true, FAST, DEEP>(P, nodes, prims, spill, sr, hit, thr, dg);
+      else
+        occ = occluded<false, FAST, DEEP>(P, nodes, prims, spill, sr, hit, thr, dg);
+      bits |= (occ ? 1u : 0u) << (li - 32 * w);
+    }
+    P.occ[pix * P.occ_words + w] = bits;
+  }
+  if (P.counters) {
+    const unsigned long long nhit = __builtin_popcountll(ballot(hit));
+    if (q.lane == 0) {
+      unsigned long long* c = counter_row(P, sel);
+      atomicAdd(&c[kCntShadow], nhit * (unsigned long long)P.num_lights);
+#ifdef RT_DIAG
+      atomicAdd(&c[kCntShadNodes], dg.nodes);
+      atomicAdd(&c[kCntShadNodeLanes], dg.node_lanes);
+      atomicAdd(&c[kCntShadLeaves], dg.leaves);
+      atomicAdd(&c[kCntShadLeafLanes], dg.leaf_lanes);
+#endif
+    }
+  }
+}
+
+// Local shading of HW2/Scene.cpp:101-138 given the occlusion bits, in the reference's
+// accumulation order: ambient, then per light diffuse then specular.  No traversal here, so
+// the fp64 pow (HW2 calls ::pow(double, double)) costs no occupancy in the traversal kernels.
+__device__ __forceinline__ void shade_pixel(const RenderParams& P,
+                                            const DevPrim* __restrict__ prims,
+                                            const float* __restrict__ normals,
+                                            const DevMaterial* __restrict__ mats,
+                                            const DevLight* __restrict__ lights, int sel) {
+  const PacketPixel q = packet_pixel(P, sel);
+  const size_t pix = (size_t)sel * (kTile * kTile) + q.lane;
+  const int2_t rec = P.hits[pix];
+  const bool valid = rec.y != -2;
+  const bool hit = rec.y >= 0;
+  V3 color = v3(0.0f, 0.0f, 0.0f);
+  if (hit) {
+    const int leaf = rec.y;
+    const V3 e = ld3(P.cam_e);
+    const V3 p = hit_point(P, q, __int_as_float(rec.x));
+    const DevPrim& pr = prims[leaf];
+    const V3 n = pr.kind == kPrimTriangle ? ld3(normals + 4 * leaf) : normalize(p - ld3(pr.v0));
+    const DevMaterial& m = mats[pr.material];
+    const V3 w0 = normalize(e - p);  // (ray.o - intersection_point).normalize()
+    color = color + ld3(m.ambient) * ld3(P.ambient);
+    for (int li = 0; li < P.num_lights; li++) {
+      if ((P.occ[pix * P.occ_words + (li >> 5)] >> (li & 31)) & 1u) continue;
+      const DevLight& L = lights[li];
+      const V3 ld = ld3(L.position) - p;
+      const V3 wi = normalize(ld);
+      const float dist = length(ld);
+      const V3 I = ld3(L.intensity);
+      const float d2 = dist * dist;
+      const float cos_d = dot(n, wi);
+      color = color + ((ld3(m.diffuse) * I) * cos_d) / d2;
+      const float cos_s = __builtin_fmaxf(dot(n, normalize(w0 + wi)), 0.0f);
+      const float pw = (float)pow((double)cos_s, (double)m.phong_exponent);
+      color = color + ((ld3(m.specular) * I) * pw) / d2;
+    }
+  } else if (valid) {
+    color = ld3(P.background);  // primary miss: max_recursion_depth == depth
+  }
+  if (valid) {
+    float* o;
+    if (P.tile_major)
+      o = P.out + 3 * pix;
+    else
+      o = P.out + 3 * ((size_t)q.py * P.width + q.px);
+    o[0] = 0.0f + color.x;  // Pixel::add_color(color, 1) onto a zeroed pixel
+    o[1] = 0.0f + color.y;
+    o[2] = 0.0f + color.z;
+  } else if (P.tile_major) {
+    float* o = P.out + 3 * pix;
+    o[0] = o[1] = o[2] = 0.0f;
+  }
+}
+
+// XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so hand each
+// XCD a contiguous run of tiles — neighbouring packets share BVH nodes through its L2.
+__device__ __forceinline__ int packet_index() {
   const int nb = (int)gridDim.x, b = (int)blockIdx.x;
   const int q = nb / 8, rem = nb % 8, x = b % 8;
   const int logical = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + b / 8;
-  const int wave = (int)threadIdx.x >> 6;
-  const int sel = uniform(logical * kWavesPerBlock + wave);
+  return uniform(logical * kWavesPerBlock + ((int)threadIdx.x >> 6));
+}
+
+template <bool FAST, bool DEEP>
+__global__ __launch_bounds__(kWavesPerBlock * 64) void trace_primary_kernel(
+    RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims) {
+  extern __shared__ __attribute__((aligned(16))) int deep_stack[];
+  const int sel = packet_index();
   if (sel >= P.num_sel_tiles) return;
-  int* spill = DEEP ? deep_stack + wave * 3 * kDeepStack : nullptr;
-  render_packet<FAST, DEEP>(P, nodes, prims, normals, mats, lights, sel, spill);
+  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * 3 * kDeepStack : nullptr;
+  primary_packet<FAST, DEEP>(P, nodes, prims, sel, spill);
+}
+
+template <bool FAST, bool DEEP>
+__global__ __launch_bounds__(kWavesPerBlock * 64) void trace_shadow_kernel(
+    RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims,
+    const DevLight* __restrict__ lights) {
+  extern __shared__ __attribute__((aligned(16))) int deep_stack[];
+  const int sel = packet_index();
+  if (sel >= P.num_sel_tiles) return;
+  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * 3 * kDeepStack : nullptr;
+  shadow_packet<FAST, DEEP>(P, nodes, prims, lights, sel, spill);
+}
+
+__global__ __launch_bounds__(kWavesPerBlock * 64) void shade_kernel(
+    RenderParams P, const DevPrim* __restrict__ prims, const float* __restrict__ normals,
+    const DevMaterial* __restrict__ mats, const DevLight* __restrict__ lights) {
+  const int sel = uniform((int)blockIdx.x * kWavesPerBlock + ((int)threadIdx.x >> 6));
+  if (sel >= P.num_sel_tiles) return;
+  shade_pixel(P, prims, normals, mats, lights, sel);
 }
 
 template <bool FAST, bool DEEP>
@@ -494,11 +620,35 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
                            const float* normals, const DevMaterial* mats,
                            const DevLight* lights, int blocks, hipStream_t stream) {
   const size_t lds = DEEP ? sizeof(int) * 3 * kDeepStack * kWavesPerBlock : 0;
-  hipLaunchKernelGGL((render_kernel<FAST, DEEP>), dim3(blocks), dim3(kWavesPerBlock * 64), lds,
-                     stream, P, nodes, prims, normals, mats, lights);
+  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP>), dim3(blocks),
+                     dim3(kWavesPerBlock * 64), lds, stream, P, nodes, prims);
+  if (P.num_lights > 0)
+    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP>), dim3(blocks),
+                       dim3(kWavesPerBlock * 64), lds, stream, P, nodes, prims, lights);
+  hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
+                     prims, normals, mats, lights);
 }
 
 int max_supported_depth() { return kDeepStack; }
+
+unsigned long long read_reset_exact_fallbacks() {
+#ifdef RT_DIAG
+  unsigned long long v = 0, z = 0;
+  (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_exact_fallbacks), sizeof v);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_exact_fallbacks), &z, sizeof z);
+  return v;
+#else
+  return 0;
+#endif
+}
+
+bool diag_build() {
+#ifdef RT_DIAG
+  return true;
+#else
+  return false;
+#endif
+}
 
 hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                          const float* normals, const DevMaterial* mats, const DevLight* lights,

@@ -124,6 +124,19 @@ class Scene:
                                      tile_begin, tile_step, int(tile_major),
                                      C.c_void_p(out_ptr), C.c_void_p(stream)))
 
+    DIAG_NAMES = ["primary_rays", "shadow_rays", "secondary_rays", "primary_hits",
+                  "prim_node_visits", "prim_node_lanes", "prim_leaf_visits", "prim_leaf_lanes",
+                  "shad_node_visits", "shad_node_lanes", "shad_leaf_visits", "shad_leaf_lanes",
+                  "exact_box_fallbacks", "c13", "c14", "c15"]
+
+    def debug_counters(self) -> dict:
+        """All device counters (diagnostic columns only in the CENG795_LIB=diag build)."""
+        arr = (C.c_longlong * 16)()
+        diag = check(lib().rt_debug_counters(self._h, arr))
+        d = dict(zip(self.DIAG_NAMES, list(arr)))
+        d["diag_build"] = bool(diag)
+        return d
+
     def collect_stats(self) -> "_lib.rt_stats":
         st = _lib.rt_stats()
         check(lib().rt_collect_stats(self._h, C.byref(st)))

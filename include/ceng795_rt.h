@@ -161,6 +161,13 @@ int rt_num_tiles(const rt_scene* scene, int camera_index, int starting_row, int 
 /* Reads (and resets) the device ray counters accumulated by rt_render_device calls. */
 int rt_collect_stats(rt_scene* scene, rt_stats* stats);
 
+/* Sums (and resets) all 16 device counter columns: [0] primary rays [1] shadow rays
+ * [2] secondary rays [3] primary hits; RT_DIAG builds (libceng795_rt_diag.so) add packet-level
+ * work: [4..7] primary node visits / active lanes summed over visits / leaf visits / leaf
+ * lane tests, [8..11] the same for shadow rays, [12] lanes that fell back to the exact slab
+ * test.  Returns 1 for a diagnostic build, 0 otherwise (columns 4..12 then read 0). */
+int rt_debug_counters(rt_scene* scene, long long* out16);
+
 /* PNG output as HW2/main.cpp:43-57: per channel clamp(int(c), 0, 255), alpha 255. */
 int rt_write_png(const char* path, const float* rgb, int width, int height);
 
