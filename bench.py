@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import subprocess
 import sys
@@ -121,9 +120,12 @@ def main() -> int:
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--traversal", default="fast", choices=["fast", "reference"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearsal of the N>1 path on one GPU (ranks share device 0)")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip rank 0's bit-for-bit check of the gathered frames")
     args = ap.parse_args()
 
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -132,10 +134,14 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
+    device = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
 
     import ceng795_amd
     from ceng795_amd import dist_tiles
@@ -147,13 +153,13 @@ def main() -> int:
         dist.barrier()
     xml = scene_path(args.workload, n_cams)
     t0 = time.perf_counter()
-    scene = ceng795_amd.Scene(xml, device=local, traversal=args.traversal)
+    scene = ceng795_amd.Scene(xml, device=device, traversal=args.traversal)
     log(f"[rank {rank}] scene loaded + uploaded in {time.perf_counter() - t0:.2f} s, "
         f"BVH depth {scene.bvh_depth}")
-    cam0 = scene.camera(0)
     plan = dist_tiles.TilePlan(scene, world, rank)
     stream = torch.cuda.current_stream()
-    renderer = dist_tiles.FrameRenderer(scene, plan, stream, gather=world > 1)
+    renderer = dist_tiles.FrameRenderer(scene, plan, stream, gather=world > 1,
+                                        host_staging=args.dist_backend == "gloo")
 
     # warmup (also yields the per-step ray count from the device counters)
     for _ in range(args.warmup):
@@ -161,7 +167,8 @@ def main() -> int:
     torch.cuda.synchronize()
     st = scene.collect_stats()
     rays_local = (st.primary_rays + st.shadow_rays + st.secondary_rays) / max(1, args.warmup)
-    rays_step = torch.tensor([rays_local], dtype=torch.float64, device="cuda")
+    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+    rays_step = torch.tensor([rays_local], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(rays_step)
     rays_step = float(rays_step.item())
@@ -178,13 +185,24 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    el = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     kernel_ms = [a.elapsed_time(b) for a, b in ev]
     kernel_ms_avg = sum(kernel_ms) / len(kernel_ms)
     scene.collect_stats()  # reset counters
+
+    verified = None
+    if world > 1 and rank == 0 and not args.no_verify:
+        # the gathered framebuffers must equal single-GPU renders of the same cameras, bit for bit
+        verified = True
+        for c, f in enumerate(renderer.frames):
+            ref = torch.empty_like(f)
+            scene.render_device(c, ref.data_ptr(), stream=stream.cuda_stream)
+            torch.cuda.synchronize()
+            verified &= bool(torch.equal(ref.view(torch.int32), f.view(torch.int32)))
+        log(f"[rank 0] gathered frames bit-identical to single-GPU renders: {verified}")
 
     if rank == 0:
         value = rays_step * args.steps / elapsed / 1e6
@@ -223,7 +241,8 @@ def main() -> int:
             "config": {"workload": desc, "frame": f"{w}x{h}", "frames_per_step": n_cams,
                        "triangles": 2 * (n - 1) ** 2, "rays_per_step": int(rays_step),
                        "traversal": args.traversal,
-                       "parallelism": f"tiles{world}" + ("+rccl_gather" if world > 1 else "")},
+                       "parallelism": f"tiles{world}" + (f"+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}_gather" if world > 1 else ""),
+                       "gather_verified": verified},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

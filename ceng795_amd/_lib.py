@@ -9,9 +9,11 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# CENG795_LIB=diag selects the RT_DIAG build (packet-level work counters, slower).
-LIB_PATH = os.path.join(_HERE, "lib", "libceng795_rt_diag.so"
-                        if os.environ.get("CENG795_LIB") == "diag" else "libceng795_rt.so")
+# CENG795_LIB=<variant> selects lib/libceng795_rt_<variant>.so: "diag" is the RT_DIAG build
+# (packet-level work counters); other variants are timing experiments (tools/experiments.sh).
+_VARIANT = os.environ.get("CENG795_LIB", "")
+LIB_PATH = os.path.join(_HERE, "lib", f"libceng795_rt_{_VARIANT}.so" if _VARIANT else
+                        "libceng795_rt.so")
 
 RT_OK = 0
 RT_E_INVALID = -1

@@ -18,7 +18,7 @@
 namespace rt {
 hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                          const float* normals, const DevMaterial* mats, const DevLight* lights,
-                         bool fast, bool deep, hipStream_t stream);
+                         bool fast, bool deep, bool spheres, hipStream_t stream);
 int max_supported_depth();
 unsigned long long read_reset_exact_fallbacks();
 bool diag_build();
@@ -33,6 +33,7 @@ struct rt_scene {
   int mode = RT_TRAVERSAL_FAST;
   bool deep = false;
   bool needs_recursion = false;
+  bool has_spheres = false;
   DevNode* d_nodes = nullptr;
   DevPrim* d_prims = nullptr;
   float* d_normals = nullptr;
@@ -129,6 +130,7 @@ int create_from_host(rt_scene* s, int device) {
     throw std::invalid_argument("BVH deeper than " + std::to_string(max_supported_depth()) +
                                 " levels is not supported");
   s->deep = h.depth > kLaneStack - 2;
+  for (const DevPrim& p : h.prims) s->has_spheres |= p.kind == kPrimSphere;
   for (const DevMaterial& m : h.materials) {
     const bool mirror = m.mirror[0] != 0 || m.mirror[1] != 0 || m.mirror[2] != 0;
     const bool glass = m.transparency[0] != 0 || m.transparency[1] != 0 || m.transparency[2] != 0;
@@ -346,7 +348,7 @@ int rt_render_device(rt_scene* s, int cam, int row0, int row_stride, int tile_be
       const RenderParams P =
           make_params(s, cam, row0, row_stride, tile_begin, tile_step, tile_major, d_out, true);
       hip_check(launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
-                              s->mode == RT_TRAVERSAL_FAST, s->deep, (hipStream_t)stream),
+                              s->mode == RT_TRAVERSAL_FAST, s->deep, s->has_spheres, (hipStream_t)stream),
                 "render launch");
       return RT_OK;
   });
@@ -432,7 +434,7 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
         P.occ = d_occ;
         hip_check(hipEventRecord(e0, stream), "event record");
         hipError_t le = launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats,
-                                      s->d_lights, s->mode == RT_TRAVERSAL_FAST, s->deep, stream);
+                                      s->d_lights, s->mode == RT_TRAVERSAL_FAST, s->deep, s->has_spheres, stream);
         if (le != hipSuccess) {
           (void)hipFree(d_cnt);
           hip_check(le, "render launch");

@@ -109,11 +109,13 @@ __device__ unsigned long long g_exact_fallbacks;  // lanes that needed box_exact
 
 // Fast slab test.  With q = RN(RN(m - o) / d) the reference's quotient and q' = RN(RN(m - o)
 // * rcp(d)) ours, |q' - q| <= 2^-22 |q| and sign(q') == sign(q) exactly.  The reference
-// accepts iff tmin <= tmax and tmax >= 0 (tmin, tmax finite here); the sign test is exact and
-// the order test is decided only outside a 2^-20 relative band — otherwise box_exact.
-// tnear (approximate entry distance) is only used for ordering / culling.
+// accepts iff tmin <= tmax and tmax >= 0 (tmin, tmax finite here): the sign test is exact, and
+// the order test is decided here only outside a 2^-20 relative band; inside it the lane is
+// flagged for box_exact.  Written branch-free: both children of a node are tested together.
+// tnear (approximate entry distance) only orders and culls.
 template <bool SKIP>
-__device__ __forceinline__ bool box_hit(const float* b, const LaneRay& r, float& tnear) {
+__device__ __forceinline__ void slab_fast(const float* b, const LaneRay& r, float& tn,
+                                          bool& accept, bool& undecided) {
   const float ax = (b[0] - r.o.x) * r.r.x, bx = (b[3] - r.o.x) * r.r.x;
   const float ay = (b[1] - r.o.y) * r.r.y, by = (b[4] - r.o.y) * r.r.y;
   const float az = (b[2] - r.o.z) * r.r.z, bz = (b[5] - r.o.z) * r.r.z;
@@ -128,16 +130,15 @@ __device__ __forceinline__ bool box_hit(const float* b, const LaneRay& r, float&
     nz = r.skip2 ? -RT_INF : nz;
     fz = r.skip2 ? RT_INF : fz;
   }
-  const float tn = __builtin_fmaxf(__builtin_fmaxf(nx, ny), nz);
+  tn = __builtin_fmaxf(__builtin_fmaxf(nx, ny), nz);
   const float tf = __builtin_fminf(__builtin_fminf(fx, fy), fz);
-  tnear = tn;
   const float band = (__builtin_fabsf(tn) + __builtin_fabsf(tf)) * 0x1p-20f + 0x1p-120f;
-  if (tn < tf - band) return tf >= 0.0f;
-  if (tn > tf + band) return false;
-#ifdef RT_DIAG
-  atomicAdd(&g_exact_fallbacks, 1ull);
-#endif
-  return box_exact(b, r);
+  const bool behind = !(tf >= 0.0f);  // exact sign (NaN -> undecided below)
+  const bool sure_in = tn < tf - band;
+  const bool sure_out = tn > tf + band;
+  accept = !behind & sure_in;
+  undecided = !(sure_in | sure_out) | (tf != tf);
+  undecided = undecided & !(tf < 0.0f);
 }
 
 // ------------------------------------------------------------------ primitives
@@ -183,11 +184,14 @@ __device__ __forceinline__ bool sphere_test(V3 c, float radius, const LaneRay& r
   return true;
 }
 
+// Shape::intersect of one leaf.  SPHERES == false: the scene has no spheres (host flag), so
+// the sphere code is not compiled into the traversal loop.
+template <bool SPHERES>
 __device__ __forceinline__ bool leaf_test(const DevPrim* __restrict__ prims, int leaf,
                                           const LaneRay& r, float& t) {
   const DevPrim& p = prims[leaf];
   const V3 v0 = ld3(p.v0);
-  if (p.kind == kPrimTriangle) return tri_test(v0, ld3(p.a1), ld3(p.a2), r, t);
+  if (!SPHERES || p.kind == kPrimTriangle) return tri_test(v0, ld3(p.a1), ld3(p.a2), r, t);
   return sphere_test(v0, p.a1[0], r, t);
 }
 
@@ -234,104 +238,169 @@ struct WaveStack {
 
 __device__ __forceinline__ float cull_limit(float t) { return t + t * 0x1p-8f; }
 
+// Node fetch.  Default: the wave-uniform address makes this a scalar (s_load) fetch.
+// RT_EXP_VNODE (experiment): four buffer_load_dwordx4 with the same address on every lane.
+__device__ __forceinline__ DevNode load_node(const DevNode* __restrict__ nodes, int node) {
+#ifdef RT_EXP_VNODE
+  DevNode N;
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const v4f* src = reinterpret_cast<const v4f*>(nodes + node);
+  const int zero = (int)__builtin_amdgcn_mbcnt_lo(0u, 0u);  // VGPR zero: keep it a vector load
+  const v4f q0 = src[0 + zero];
+  const v4f q1 = src[1 + zero];
+  const v4f q2 = src[2 + zero];
+  const v4f q3 = src[3 + zero];
+  N.b0[0] = q0.x; N.b0[1] = q0.y; N.b0[2] = q0.z; N.b0[3] = q0.w;
+  N.b0[4] = q1.x; N.b0[5] = q1.y; N.b1[0] = q1.z; N.b1[1] = q1.w;
+  N.b1[2] = q2.x; N.b1[3] = q2.y; N.b1[4] = q2.z; N.b1[5] = q2.w;
+  N.child[0] = uniform(__float_as_int(q3.x));
+  N.child[1] = uniform(__float_as_int(q3.y));
+  N.axis = 0;
+  N.pad = 0;
+  return N;
+#else
+  return nodes[node];
+#endif
+}
+
+// One packet visit of a BVH2 node: both child slab tests (computed unconditionally so the
+// 64-byte record arrives in one scalar load), the rare exact fallback behind one ballot, and
+// which lanes enter each child.  Leaf children are never entered (the caller tests them).
+template <bool SKIP>
+__device__ __forceinline__ void visit_boxes(const DevNode& N, const LaneRay& r, bool in,
+                                            bool& h0, bool& h1, float& t0, float& t1,
+                                            Diag& dg) {
+  bool u0, u1;
+  slab_fast<SKIP>(N.b0, r, t0, h0, u0);
+  slab_fast<SKIP>(N.b1, r, t1, h1, u1);
+  const bool live0 = in & (N.child[0] >= 0), live1 = in & (N.child[1] >= 0);
+  h0 &= live0;
+  h1 &= live1;
+  u0 &= live0;
+  u1 &= live1;
+  if (ballot(u0 | u1)) {
+    if (u0) h0 = box_exact(N.b0, r);
+    if (u1) h1 = box_exact(N.b1, r);
+    DIAG(if (u0 | u1) atomicAdd(&g_exact_fallbacks, 1ull));
+  }
+}
+
+// Pick the next node: near child first (judged by the first lane entering both), the far
+// one pushed; with neither, pop.  Returns false when the traversal is over.
+template <bool DEEP>
+__device__ __forceinline__ bool advance(WaveStack<DEEP>& st, int c0, int c1, uint64_t m0,
+                                        uint64_t m1, float t0, float t1, int& node,
+                                        uint64_t& m, uint64_t alive) {
+  if (m0 && m1) {
+    const int f = __builtin_ctzll((m0 & m1) ? (m0 & m1) : m0);
+    const float f0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t0), f));
+    const float f1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t1), f));
+    if (f1 < f0) {
+      st.push(c0, m0);
+      node = c1;
+      m = m1;
+    } else {
+      st.push(c1, m1);
+      node = c0;
+      m = m0;
+    }
+    return true;
+  }
+  if (m0 | m1) {
+    node = m0 ? c0 : c1;
+    m = m0 | m1;
+    return true;
+  }
+  for (;;) {
+    if (st.sp == 0) return false;
+    st.pop(node, m);
+    m &= alive;
+    if (m) return true;
+  }
+}
+
 // ------------------------------------------------------------------ closest hit
 // Returns the reference's (t, leaf) for every active lane: best_leaf < 0 = miss.
-template <bool SKIP, bool FAST, bool DEEP>
-__device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode* __restrict__ nodes,
-                            const DevPrim* __restrict__ prims, int* spill, const LaneRay& r,
-                            bool active, float& best_t, int& best_leaf, Diag& dg) {
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES>
+__device__ __forceinline__ void closest_hit(const RenderParams& P,
+                                            const DevNode* __restrict__ nodes,
+                                            const DevPrim* __restrict__ prims, int* spill,
+                                            const LaneRay& r, bool active, float& best_t,
+                                            int& best_leaf, Diag& dg) {
   best_t = RT_INF;
   best_leaf = -1;
   if (P.root_kind != kRootNode) {  // the root IS the primitive (BVH.h:13-14): its own rule
     float t;
-    if (active && leaf_test(prims, P.root_ref, r, t)) {
+    if (active && leaf_test<SPHERES>(prims, P.root_ref, r, t)) {
       best_t = t;
       best_leaf = P.root_ref;
     }
     return;
   }
   float tn;
-  uint64_t m = ballot(active && box_hit<SKIP>(P.root_box, r, tn));
+  bool acc, und;
+  slab_fast<SKIP>(P.root_box, r, tn, acc, und);
+  const bool h = active && (acc || (und && box_exact(P.root_box, r)));
+  uint64_t m = ballot(h);
   if (m == 0) return;
   const int lane = lane_id();
   WaveStack<DEEP> st;
   st.lds = spill;
   int node = P.root_ref;
   for (;;) {
-    const DevNode& N = nodes[node];
+    const DevNode N = load_node(nodes, node);
     const bool in = (m >> lane) & 1;
     DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m);
          dg.leaves += (N.child[0] < 0) + (N.child[1] < 0);
          dg.leaf_lanes += ((N.child[0] < 0) + (N.child[1] < 0)) * __builtin_popcountll(m));
-    const int c0 = N.child[0], c1 = N.child[1];
-    uint64_t m0 = 0, m1 = 0;
-    float t0 = RT_INF, t1 = RT_INF;
-    if (c0 >= 0) {
-      bool h = in && box_hit<SKIP>(N.b0, r, t0);
-      if (FAST) h = h && t0 <= cull_limit(best_t);
-      m0 = ballot(h);
-    } else if (in) {
-      float t;
-      if (leaf_test(prims, ~c0, r, t) && t > 0.0f && t < RT_INF &&
-          (t < best_t || (t == best_t && ~c0 < best_leaf))) {
-        best_t = t;
-        best_leaf = ~c0;
+    bool h0, h1;
+    float t0, t1;
+    visit_boxes<SKIP>(N, r, in, h0, h1, t0, t1, dg);
+#ifndef RT_EXP_NOLEAF
+#pragma unroll 1
+    for (int k = 0; k < 2; k++) {  // leaf children: Shape::intersect, accept 0 < t < best
+      const int c = k ? N.child[1] : N.child[0];
+      if (c < 0 && in) {
+        float t;
+        if (leaf_test<SPHERES>(prims, ~c, r, t) && t > 0.0f && t < RT_INF &&
+            (t < best_t || (t == best_t && ~c < best_leaf))) {
+          best_t = t;
+          best_leaf = ~c;
+        }
       }
     }
-    if (c1 >= 0) {
-      bool h = in && box_hit<SKIP>(N.b1, r, t1);
-      if (FAST) h = h && t1 <= cull_limit(best_t);
-      m1 = ballot(h);
-    } else if (in) {
-      float t;
-      if (leaf_test(prims, ~c1, r, t) && t > 0.0f && t < RT_INF &&
-          (t < best_t || (t == best_t && ~c1 < best_leaf))) {
-        best_t = t;
-        best_leaf = ~c1;
-      }
+#else
+    best_leaf -= in ? 1 : 0;  // timing experiment: keep the traversal observable
+#endif
+    if (FAST) {
+      const float lim = cull_limit(best_t);
+      h0 = h0 && t0 <= lim;
+      h1 = h1 && t1 <= lim;
     }
-    if (m0 && m1) {
-      // near child first, judged by the first lane that entered both
-      const int f = __builtin_ctzll(m0 & m1 ? (m0 & m1) : m0);
-      const float f0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t0), f));
-      const float f1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t1), f));
-      if (f1 < f0) {
-        st.push(c0, m0);
-        node = c1;
-        m = m1;
-      } else {
-        st.push(c1, m1);
-        node = c0;
-        m = m0;
-      }
-    } else if (m0) {
-      node = c0;
-      m = m0;
-    } else if (m1) {
-      node = c1;
-      m = m1;
-    } else {
-      if (st.sp == 0) break;
-      st.pop(node, m);
-    }
+    if (!advance(st, N.child[0], N.child[1], ballot(h0), ballot(h1), t0, t1, node, m, ~0ull))
+      break;
   }
 }
 
 // ------------------------------------------------------------------ shadow (any hit)
 // Occluded iff some leaf the ray may reach has 0 < t < thr — identical to the reference's
 // closest-hit shadow test `0 < t_closest < dist - eps` (HW2/Scene.cpp:123-127), appendix A.7.
-template <bool SKIP, bool FAST, bool DEEP>
-__device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* __restrict__ nodes,
-                         const DevPrim* __restrict__ prims, int* spill, const LaneRay& r,
-                         bool active, float thr, Diag& dg) {
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES>
+__device__ __forceinline__ bool occluded(const RenderParams& P,
+                                         const DevNode* __restrict__ nodes,
+                                         const DevPrim* __restrict__ prims, int* spill,
+                                         const LaneRay& r, bool active, float thr, Diag& dg) {
   if (P.root_kind != kRootNode) {
     float t;
-    return active && leaf_test(prims, P.root_ref, r, t) && t < thr && t > 0.0f;
+    return active && leaf_test<SPHERES>(prims, P.root_ref, r, t) && t < thr && t > 0.0f;
   }
   bool occ = false;
   float tn;
+  bool acc, und;
   // thr <= 0 (or NaN): nothing can satisfy 0 < t < thr
-  uint64_t m = ballot(active && thr > 0.0f && box_hit<SKIP>(P.root_box, r, tn));
+  slab_fast<SKIP>(P.root_box, r, tn, acc, und);
+  const bool h = active && thr > 0.0f && (acc || (und && box_exact(P.root_box, r)));
+  uint64_t m = ballot(h);
   if (m == 0) return false;
   const int lane = lane_id();
   WaveStack<DEEP> st;
@@ -339,61 +408,32 @@ __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* _
   int node = P.root_ref;
   uint64_t alive = m;
   for (;;) {
-    const DevNode& N = nodes[node];
+    const DevNode N = load_node(nodes, node);
     const bool in = (m >> lane) & 1;
     DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m);
          dg.leaves += (N.child[0] < 0) + (N.child[1] < 0);
          dg.leaf_lanes += ((N.child[0] < 0) + (N.child[1] < 0)) * __builtin_popcountll(m));
-    const int c0 = N.child[0], c1 = N.child[1];
-    uint64_t m0 = 0, m1 = 0;
-    float t0 = RT_INF, t1 = RT_INF;
-    if (c0 >= 0) {
-      bool h = in && box_hit<SKIP>(N.b0, r, t0);
-      if (FAST) h = h && t0 <= cull_limit(thr);
-      m0 = ballot(h);
-    } else if (in) {
-      float t;
-      if (leaf_test(prims, ~c0, r, t) && t > 0.0f && t < thr) occ = true;
-    }
-    if (c1 >= 0) {
-      bool h = in && box_hit<SKIP>(N.b1, r, t1);
-      if (FAST) h = h && t1 <= cull_limit(thr);
-      m1 = ballot(h);
-    } else if (in && !occ) {
-      float t;
-      if (leaf_test(prims, ~c1, r, t) && t > 0.0f && t < thr) occ = true;
+    bool h0, h1;
+    float t0, t1;
+    visit_boxes<SKIP>(N, r, in, h0, h1, t0, t1, dg);
+#pragma unroll 1
+    for (int k = 0; k < 2; k++) {
+      const int c = k ? N.child[1] : N.child[0];
+      if (c < 0 && in && !occ) {
+        float t;
+        if (leaf_test<SPHERES>(prims, ~c, r, t) && t > 0.0f && t < thr) occ = true;
+      }
     }
     alive &= ~ballot(occ);
     if (alive == 0) break;
-    m0 &= alive;
-    m1 &= alive;
-    if (m0 && m1) {
-      const int f = __builtin_ctzll(m0 & m1 ? (m0 & m1) : m0);
-      const float f0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t0), f));
-      const float f1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t1), f));
-      if (f1 < f0) {
-        st.push(c0, m0);
-        node = c1;
-        m = m1;
-      } else {
-        st.push(c1, m1);
-        node = c0;
-        m = m0;
-      }
-    } else if (m0) {
-      node = c0;
-      m = m0;
-    } else if (m1) {
-      node = c1;
-      m = m1;
-    } else {
-      m = 0;
-      while (m == 0 && st.sp > 0) {
-        st.pop(node, m);
-        m &= alive;
-      }
-      if (m == 0) break;
+    if (FAST) {
+      const float lim = cull_limit(thr);
+      h0 = h0 && t0 <= lim;
+      h1 = h1 && t1 <= lim;
     }
+    if (!advance(st, N.child[0], N.child[1], ballot(h0) & alive, ballot(h1) & alive, t0, t1,
+                 node, m, alive))
+      break;
   }
   return occ;
 }
@@ -431,7 +471,7 @@ __device__ __forceinline__ unsigned long long* counter_row(const RenderParams& P
   return P.counters + kCounterWidth * (sel % kCounterSlots);
 }
 
-template <bool FAST, bool DEEP>
+template <bool FAST, bool DEEP, bool SPHERES>
 __device__ __forceinline__ void primary_packet(const RenderParams& P,
                                                const DevNode* __restrict__ nodes,
                                                const DevPrim* __restrict__ prims, int sel,
@@ -443,9 +483,9 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
   float t;
   int leaf;
   if (skip)
-    closest_hit<true, FAST, DEEP>(P, nodes, prims, spill, ray, q.valid, t, leaf, dg);
+    closest_hit<true, FAST, DEEP, SPHERES>(P, nodes, prims, spill, ray, q.valid, t, leaf, dg);
   else
-    closest_hit<false, FAST, DEEP>(P, nodes, prims, spill, ray, q.valid, t, leaf, dg);
+    closest_hit<false, FAST, DEEP, SPHERES>(P, nodes, prims, spill, ray, q.valid, t, leaf, dg);
   int2_t rec;
   rec.x = __float_as_int(t);
   rec.y = q.valid ? leaf : -2;  // -1 miss, -2 outside the image
@@ -475,7 +515,7 @@ __device__ __forceinline__ V3 hit_point(const RenderParams& P, const PacketPixel
 
 // Shadow rays of HW2/Scene.cpp:113-127: one bit per point light, set when the light is
 // occluded for this pixel's primary hit.
-template <bool FAST, bool DEEP>
+template <bool FAST, bool DEEP, bool SPHERES>
 __device__ __forceinline__ void shadow_packet(const RenderParams& P,
                                               const DevNode* __restrict__ nodes,
                                               const DevPrim* __restrict__ prims,
@@ -500,9 +540,9 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P,
       const bool sskip = ballot(hit && (sr.skip0 || sr.skip1 || sr.skip2)) != 0;
       bool occ;
       if (sskip)
-        occ = occluded<true, FAST, DEEP>(P, nodes, prims, spill, sr, hit, thr, dg);
+        occ = occluded<true, FAST, DEEP, SPHERES>(P, nodes, prims, spill, sr, hit, thr, dg);
       else
-        occ = occluded<false, FAST, DEEP>(P, nodes, prims, spill, sr, hit, thr, dg);
+        occ = occluded<false, FAST, DEEP, SPHERES>(P, nodes, prims, spill, sr, hit, thr, dg);
       bits |= (occ ? 1u : 0u) << (li - 32 * w);
     }
     P.occ[pix * P.occ_words + w] = bits;
@@ -586,17 +626,17 @@ __device__ __forceinline__ int packet_index() {
   return uniform(logical * kWavesPerBlock + ((int)threadIdx.x >> 6));
 }
 
-template <bool FAST, bool DEEP>
+template <bool FAST, bool DEEP, bool SPHERES>
 __global__ __launch_bounds__(kWavesPerBlock * 64) void trace_primary_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
   const int sel = packet_index();
   if (sel >= P.num_sel_tiles) return;
   int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * 3 * kDeepStack : nullptr;
-  primary_packet<FAST, DEEP>(P, nodes, prims, sel, spill);
+  primary_packet<FAST, DEEP, SPHERES>(P, nodes, prims, sel, spill);
 }
 
-template <bool FAST, bool DEEP>
+template <bool FAST, bool DEEP, bool SPHERES>
 __global__ __launch_bounds__(kWavesPerBlock * 64) void trace_shadow_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims,
     const DevLight* __restrict__ lights) {
@@ -604,7 +644,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void trace_shadow_kernel(
   const int sel = packet_index();
   if (sel >= P.num_sel_tiles) return;
   int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * 3 * kDeepStack : nullptr;
-  shadow_packet<FAST, DEEP>(P, nodes, prims, lights, sel, spill);
+  shadow_packet<FAST, DEEP, SPHERES>(P, nodes, prims, lights, sel, spill);
 }
 
 __global__ __launch_bounds__(kWavesPerBlock * 64) void shade_kernel(
@@ -615,21 +655,45 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void shade_kernel(
   shade_pixel(P, prims, normals, mats, lights, sel);
 }
 
-template <bool FAST, bool DEEP>
+template <bool FAST, bool DEEP, bool SPHERES>
 static void launch_variant(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                            const float* normals, const DevMaterial* mats,
                            const DevLight* lights, int blocks, hipStream_t stream) {
   const size_t lds = DEEP ? sizeof(int) * 3 * kDeepStack * kWavesPerBlock : 0;
-  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP>), dim3(blocks),
+  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES>), dim3(blocks),
                      dim3(kWavesPerBlock * 64), lds, stream, P, nodes, prims);
   if (P.num_lights > 0)
-    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP>), dim3(blocks),
+    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES>), dim3(blocks),
                        dim3(kWavesPerBlock * 64), lds, stream, P, nodes, prims, lights);
   hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
                      prims, normals, mats, lights);
 }
 
 int max_supported_depth() { return kDeepStack; }
+
+hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
+                         const float* normals, const DevMaterial* mats, const DevLight* lights,
+                         bool fast, bool deep, bool spheres, hipStream_t stream) {
+  if (P.num_sel_tiles <= 0) return hipSuccess;
+  const int blocks = (P.num_sel_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int v = (fast ? 4 : 0) | (deep ? 2 : 0) | (spheres ? 1 : 0);
+  switch (v) {
+#define RT_CASE(F, D, S)                                                                  \
+  case (F ? 4 : 0) | (D ? 2 : 0) | (S ? 1 : 0):                                           \
+    launch_variant<F, D, S>(P, nodes, prims, normals, mats, lights, blocks, stream); \
+    break;
+    RT_CASE(true, false, false)
+    RT_CASE(true, false, true)
+    RT_CASE(true, true, false)
+    RT_CASE(true, true, true)
+    RT_CASE(false, false, false)
+    RT_CASE(false, false, true)
+    RT_CASE(false, true, false)
+    RT_CASE(false, true, true)
+#undef RT_CASE
+  }
+  return hipGetLastError();
+}
 
 unsigned long long read_reset_exact_fallbacks() {
 #ifdef RT_DIAG
@@ -648,18 +712,6 @@ bool diag_build() {
 #else
   return false;
 #endif
-}
-
-hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
-                         const float* normals, const DevMaterial* mats, const DevLight* lights,
-                         bool fast, bool deep, hipStream_t stream) {
-  if (P.num_sel_tiles <= 0) return hipSuccess;
-  const int blocks = (P.num_sel_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-  if (fast && !deep) launch_variant<true, false>(P, nodes, prims, normals, mats, lights, blocks, stream);
-  else if (fast) launch_variant<true, true>(P, nodes, prims, normals, mats, lights, blocks, stream);
-  else if (!deep) launch_variant<false, false>(P, nodes, prims, normals, mats, lights, blocks, stream);
-  else launch_variant<false, true>(P, nodes, prims, normals, mats, lights, blocks, stream);
-  return hipGetLastError();
 }
 
 }  // namespace rt

@@ -89,13 +89,15 @@ class FrameRenderer:
 
     world == 1 and gather == False renders each camera in place into a row-major frame."""
 
-    def __init__(self, scene, layout_or_none: Optional[TileLayout], stream, gather: bool):
+    def __init__(self, scene, layout_or_none: Optional[TileLayout], stream, gather: bool,
+                 host_staging: bool = False):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
         self.scene = scene
         self.stream = stream
         self.gather = gather
+        self.host_staging = host_staging  # gloo rehearsal: collectives on host copies
         self.sizes = [(scene.camera(c).width, scene.camera(c).height)
                       for c in range(scene.num_cameras)]
         self.layout = layout_or_none
@@ -131,7 +133,17 @@ class FrameRenderer:
                                          tile_major=True, stream=s)
         if events is not None:
             events[1].record(self.stream)
-        self.dist.gather(self.local, self.gather_list if self.rank == 0 else None, dst=0)
+        if self.host_staging:
+            torch = self.torch
+            self.stream.synchronize()
+            host = self.local.cpu()
+            glist = list(torch.empty((self.layout.world, self.layout.padded_tiles, TILE_FLOATS))) \
+                if self.rank == 0 else None
+            self.dist.gather(host, glist, dst=0)
+            if self.rank == 0:
+                self.gathered.copy_(torch.cat(glist))
+        else:
+            self.dist.gather(self.local, self.gather_list if self.rank == 0 else None, dst=0)
         if self.rank == 0:
             self.frames = [f.contiguous() for f in
                            untile(self.gathered, self.layout, self.sizes, self.index)]

@@ -1,0 +1,175 @@
+"""Host-side logic of the product library, CPU only (no HIP call is made):
+the C-ABI exports, the XML ingest + reference-identical BVH build + flattening (checked
+against the reference's own topology hashes in tests/golden/), the camera precompute, the PNG
+writer and the loader's error behaviour."""
+import ctypes as C
+import hashlib
+import json
+import os
+import re
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import scenes
+from ceng795_amd import _lib
+from ceng795_amd.scene import host_dump_bvh, write_png
+from oracle.cpu_ref import OracleScene
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+GOLDEN = json.load(open(os.path.join(HERE, "golden", "golden.json")))
+HEADER = os.path.join(ROOT, "include", "ceng795_rt.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\s*\*)\s*(rt_\w+)\s*\(", text, re.M)))
+
+
+def test_library_exports_every_declared_function():
+    L = _lib.lib()
+    names = declared_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(L, n), n
+        assert n in _lib.SIGNATURES, f"{n} missing from the ctypes table"
+    assert L.rt_abi_version() == 1
+
+
+def test_oracle_is_not_linked_into_the_product():
+    """The product must not route through the CPU oracle: no cpuref_* symbol, no libcpu_ref."""
+    path = _lib.LIB_PATH
+    data = open(path, "rb").read()
+    assert b"cpuref_" not in data and b"libcpu_ref" not in data
+
+
+@pytest.mark.parametrize("name", [n for n in GOLDEN if not n.startswith("_")])
+def test_bvh_topology_matches_reference(scene_dir, tmp_path, name):
+    """XML ingest + BVH build + DFS flattening reproduce the reference's tree exactly
+    (boxes as fp32 bits, leaf order, vertex ids, materials)."""
+    xml = scenes.write_c3(scene_dir) if name == "c3" else scenes.write(name, scene_dir)
+    out = tmp_path / "bvh.txt"
+    host_dump_bvh(xml, str(out))
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == GOLDEN[name]["bvh_sha256"]
+
+
+def primary_dirs(cam: _lib.rt_camera, w: int, h: int) -> np.ndarray:
+    """Camera::calculate_ray_at (HW2/Camera.h:30-35) replayed in numpy fp32 (one rounding
+    per operation, like the reference's SSE code)."""
+    f32 = np.float32
+    tl, su, sv, e = (np.array(list(v), f32) for v in (cam.top_left, cam.s_u, cam.s_v, cam.e))
+    xs = np.arange(w, dtype=f32) + f32(0.5)
+    ys = np.arange(h, dtype=f32) + f32(0.5)
+    s = (tl[None, None, :] + su[None, None, :] * xs[None, :, None]) - sv[None, None, :] * ys[:, None, None]
+    v = s - e
+    ln = np.sqrt((v[..., 0] * v[..., 0] + v[..., 1] * v[..., 1]) + v[..., 2] * v[..., 2])
+    return v / ln[..., None]
+
+
+@pytest.mark.parametrize("name", ["c1", "hf_small", "hf_side", "soup1", "single_sphere"])
+def test_camera_precompute_matches_reference(scene_dir, name):
+    spec = scenes.CATALOGUE[name][0]()
+    xml = scenes.write(name, scene_dir)
+    o = OracleScene(xml)
+    for k, c in enumerate(spec.cameras):
+        cam = _lib.rt_camera()
+        f3 = lambda v: (C.c_float * 3)(*[np.float32(x) for x in v])
+        np4 = (C.c_float * 4)(*[np.float32(x) for x in c.near_plane])
+        _lib.check(_lib.lib().rt_camera_from_view(f3(c.position), f3(c.gaze), f3(c.up), np4,
+                                                  np.float32(c.near_distance), c.width,
+                                                  c.height, 1, C.byref(cam)))
+        d = primary_dirs(cam, c.width, c.height)
+        ref = o.primary_records(k)[..., :3]
+        assert np.array_equal(d.view(np.uint32), ref.view(np.uint32)), (name, k)
+
+
+def decode_png_rgb(path):
+    data = open(path, "rb").read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat, w = 8, b"", None
+    while pos < len(data):
+        n = struct.unpack(">I", data[pos:pos + 4])[0]
+        typ = data[pos + 4:pos + 8]
+        body = data[pos + 8:pos + 8 + n]
+        assert struct.unpack(">I", data[pos + 8 + n:pos + 12 + n])[0] == zlib.crc32(typ + body)
+        if typ == b"IHDR":
+            w, h, depth, ctype = struct.unpack(">IIBB", body[:10])
+            assert depth == 8 and ctype == 2
+        elif typ == b"IDAT":
+            idat += body
+        pos += 12 + n
+    raw = zlib.decompress(idat)
+    rows = [raw[r * (1 + 3 * w) + 1:(r + 1) * (1 + 3 * w)] for r in range(h)]
+    assert all(raw[r * (1 + 3 * w)] == 0 for r in range(h))
+    return np.frombuffer(b"".join(rows), np.uint8).reshape(h, w, 3)
+
+
+def test_png_quantisation_like_pixel_get_color(tmp_path):
+    """HW2/Pixel.h:17-28 + main.cpp:43-54: clamp(int(c), 0, 255), truncation, NaN -> 0."""
+    vals = np.array([0.0, 0.99, 1.0, 254.99, 255.0, 300.0, -0.5, -3.0, np.nan, np.inf, -np.inf,
+                     127.5], np.float32)
+    img = np.tile(vals, (2, 1)).reshape(2, 4, 3)
+    path = tmp_path / "q.png"
+    write_png(str(path), img)
+    got = decode_png_rgb(str(path))
+    exp = np.array([0, 0, 1, 254, 255, 255, 0, 0, 0, 0, 0, 127], np.uint8)
+    assert np.array_equal(got.reshape(2, -1)[0], exp)
+
+
+# ---------------------------------------------------------------- loader error behaviour
+def _variant(scene_dir, tmp_path, transform, base="soup1"):
+    text = open(scenes.write(base, scene_dir)).read()
+    p = tmp_path / "v.xml"
+    p.write_text(transform(text))
+    return str(p)
+
+
+def _dump_rc(xml, tmp_path):
+    return _lib.lib().rt_host_dump_bvh_xml(xml.encode(), str(tmp_path / "o.txt").encode())
+
+
+def test_xml_declaration_and_comments_are_accepted(scene_dir, tmp_path):
+    """The reference takes file.FirstChild() as root and would crash on a prolog (appendix B);
+    ours skips it — a superset — and builds the identical tree."""
+    plain = scenes.write("soup1", scene_dir)
+    host_dump_bvh(plain, str(tmp_path / "a.txt"))
+    v = _variant(scene_dir, tmp_path,
+                 lambda t: '<?xml version="1.0"?>\n<!-- scene -->\n' +
+                 t.replace("<Objects>", "<Objects><!-- objects -->"))
+    host_dump_bvh(v, str(tmp_path / "b.txt"))
+    assert (tmp_path / "a.txt").read_text() == (tmp_path / "b.txt").read_text()
+
+
+@pytest.mark.parametrize("mutate,code", [
+    (lambda t: t.replace("<Cameras>", "<CamerasX>").replace("</Cameras>", "</CamerasX>"),
+     _lib.RT_E_PARSE),
+    (lambda t: t.replace("</Scene>", ""), _lib.RT_E_PARSE),
+    (lambda t: re.sub(r"<Faces>.*?</Faces>", "<Faces> </Faces>", t, count=1, flags=re.S),
+     _lib.RT_E_INVALID),
+    (lambda t: re.sub(r"<Material>1</Material>", "<Material>99</Material>", t, count=1),
+     _lib.RT_E_INVALID),
+    (lambda t: re.sub(r"<Indices>\d+", "<Indices>999999", t, count=1), _lib.RT_E_INVALID),
+    (lambda t: re.sub(r"<Objects>.*</Objects>", "<Objects></Objects>", t, flags=re.S),
+     _lib.RT_E_INVALID),
+])
+def test_loader_errors(scene_dir, tmp_path, mutate, code):
+    rc = _dump_rc(_variant(scene_dir, tmp_path, mutate), tmp_path)
+    assert rc == code, (rc, _lib.lib().rt_last_error())
+    assert _lib.lib().rt_last_error()
+
+
+def test_missing_file_is_io_error(tmp_path):
+    assert _dump_rc(str(tmp_path / "nope.xml"), tmp_path) == _lib.RT_E_IO
+
+
+def test_defaults_match_reference(scene_dir, tmp_path):
+    """Optional tags fall back to the reference's defaults (HW2/Scene.cpp:211-236, 312-353):
+    stripping BackgroundColor / ShadowRayEpsilon / MaxRecursionDepth and the optional
+    material fields must not change the tree."""
+    v = _variant(scene_dir, tmp_path,
+                 lambda t: re.sub(r"\s*<(BackgroundColor|ShadowRayEpsilon|MaxRecursionDepth)>.*?</\1>",
+                                  "", t))
+    assert _dump_rc(v, tmp_path) == 0
