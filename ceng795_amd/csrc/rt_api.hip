@@ -42,6 +42,8 @@ struct rt_scene {
   unsigned long long* d_counters = nullptr;
   int2_t* d_hits = nullptr;  // rt_render_device's primary-hit records (largest camera)
   unsigned* d_occ = nullptr; // rt_render_device's occlusion bits
+  float* d_frames = nullptr; // rt_render_device's ray-tree frames (recursive scenes)
+  size_t frames_capacity = 0;
   size_t hits_capacity = 0;  // records
 };
 
@@ -104,6 +106,7 @@ void free_device(rt_scene* s) {
   (void)hipFree(s->d_counters);
   (void)hipFree(s->d_hits);
   (void)hipFree(s->d_occ);
+  (void)hipFree(s->d_frames);
   if (cur != s->device) (void)hipSetDevice(cur);
 }
 
@@ -118,6 +121,12 @@ struct DeviceGuard {
     if (hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
 };
+
+constexpr int kFrameFloats = 28;  // rt_kernels.hip kFrFields
+
+size_t frame_floats(const HostScene& h, int sel_tiles) {
+  return (size_t)(h.max_depth + 1) * kFrameFloats * kTile * kTile * (size_t)std::max(1, sel_tiles);
+}
 
 int occ_words(const HostScene& h) { return std::max(1, ((int)h.lights.size() + 31) / 32); }
 
@@ -219,8 +228,6 @@ void check_render_args(const rt_scene* s, int cam, int row0, int row_stride) {
   if (row0 < 0 || row_stride < 1) throw std::invalid_argument("bad row selection");
   if (s->host.cameras[cam].num_samples != 1)
     throw std::domain_error("NumSamples > 1 (jittered MSAA, HW2/Scene.cpp:32-69) is not supported yet");
-  if (s->needs_recursion)
-    throw std::domain_error("mirror / dielectric recursion (HW2/Scene.cpp:141-194) is not supported yet");
 }
 
 }  // namespace
@@ -345,8 +352,19 @@ int rt_render_device(rt_scene* s, int cam, int row0, int row_stride, int tile_be
       if (tile_begin < 0 || tile_step < 1 || !d_out)
         throw std::invalid_argument("rt_render_device: bad tile selection / output");
       DeviceGuard g(s->device);
-      const RenderParams P =
+      RenderParams P =
           make_params(s, cam, row0, row_stride, tile_begin, tile_step, tile_major, d_out, true);
+      if (s->needs_recursion) {
+        const size_t need = frame_floats(s->host, P.num_sel_tiles);
+        if (need > s->frames_capacity) {
+          (void)hipFree(s->d_frames);
+          s->d_frames = nullptr;
+          s->frames_capacity = 0;
+          hip_check(hipMalloc(&s->d_frames, need * sizeof(float)), "alloc ray-tree frames");
+          s->frames_capacity = need;
+        }
+        P.frames = s->d_frames;
+      }
       hip_check(launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
                               s->mode == RT_TRAVERSAL_FAST, s->deep, s->has_spheres, (hipStream_t)stream),
                 "render launch");
@@ -403,12 +421,14 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
       float* d_out = nullptr;
       int2_t* d_hits = nullptr;
       unsigned* d_occ = nullptr;
+      float* d_frames = nullptr;
       hipStream_t stream = nullptr;
       hipEvent_t e0 = nullptr, e1 = nullptr;
       auto cleanup = [&] {
         if (d_out) (void)hipFree(d_out);
         if (d_hits) (void)hipFree(d_hits);
         if (d_occ) (void)hipFree(d_occ);
+        if (d_frames) (void)hipFree(d_frames);
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         if (stream) (void)hipStreamDestroy(stream);
@@ -432,6 +452,11 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
                                         (size_t)std::max(1, P.num_sel_tiles)),
                   "alloc occlusion bits");
         P.occ = d_occ;
+        if (s->needs_recursion) {
+          hip_check(hipMalloc(&d_frames, frame_floats(s->host, P.num_sel_tiles) * sizeof(float)),
+                    "alloc ray-tree frames");
+          P.frames = d_frames;
+        }
         hip_check(hipEventRecord(e0, stream), "event record");
         hipError_t le = launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats,
                                       s->d_lights, s->mode == RT_TRAVERSAL_FAST, s->deep, s->has_spheres, stream);

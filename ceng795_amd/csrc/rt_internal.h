@@ -98,6 +98,7 @@ struct RenderParams {
   int2_t* hits;   // num_sel_tiles * 64 records {t bits, leaf}: trace_primary -> shadow, shade
   unsigned* occ;  // num_sel_tiles * 64 * occ_words light-occlusion bits: trace_shadow -> shade
   int occ_words;  // ceil(num_lights / 32)
+  float* frames;  // recursive scenes only: (max_depth+1) * 28 * lanes ray-tree frames, else null
   // kCounterRows rows of kCounterWidth u64 (columns: kCnt*)
   unsigned long long* counters;
 };

@@ -617,6 +617,277 @@ __device__ __forceinline__ void shade_pixel(const RenderParams& P,
   }
 }
 
+// ------------------------------------------------------------------ recursion (f1)
+// HW2/Scene.cpp:88-196 with MaxRecursionDepth > 0: mirror rays (:141-146) and dielectrics
+// (:149-194, refract_ray :72-86).  Each lane walks its ray tree in the reference's post order
+// with an explicit stack of frames in HBM (layout [level][field][lane]); traversal calls stay
+// wave-uniform packet calls over the lanes' current rays.  The parent's colour is combined
+// with each child result in the source's order: color += km (x) child; and for a dielectric
+// color += k (x) (r*refl + (1-r)*trans), with r*refl held in the frame until trans returns.
+enum : int {
+  kFrColor = 0, kFrStage = 3, kFrP = 4, kFrN = 7, kFrW0 = 10, kFrD = 13, kFrT = 16,
+  kFrMat = 17, kFrDepth = 18, kFrMedium = 19, kFrK = 20, kFrR = 23, kFrA = 24, kFrFields = 28
+};
+enum : int {
+  kStStart = 0, kStMirrorWait = 1, kStRefr = 2, kStTirWait = 3, kStReflWait = 4,
+  kStTransWait = 5, kStDone = 6
+};
+
+struct FrameRef {
+  float* base;
+  size_t stride;  // floats between fields (= lanes in the launch)
+  __device__ __forceinline__ float& f(int field) const { return base[(size_t)field * stride]; }
+  __device__ __forceinline__ V3 v(int field) const { return v3(f(field), f(field + 1), f(field + 2)); }
+  __device__ __forceinline__ void put(int field, V3 a) const {
+    f(field) = a.x;
+    f(field + 1) = a.y;
+    f(field + 2) = a.z;
+  }
+  __device__ __forceinline__ int i(int field) const { return __float_as_int(f(field)); }
+  __device__ __forceinline__ void put_i(int field, int x) const { f(field) = __int_as_float(x); }
+};
+
+// HW2/Scene.cpp:72-86
+__device__ __forceinline__ bool refract_ray(V3 dir, V3 n, float idx, V3& out) {
+  const float n_ratio = 1 / idx;
+  const float cos_t = dot(v3(-dir.x, -dir.y, -dir.z), n);
+  const float delta = 1 - (n_ratio) * (n_ratio) * (1 - (cos_t * cos_t));
+  if (delta < 0.0f) return false;
+  out = normalize((dir + n * cos_t) * n_ratio - n * __builtin_sqrtf(delta));
+  return true;
+}
+
+// Local shading of one hit (ambient + point lights with shadow rays), Scene.cpp:107-139.
+// Wave-uniform: every lane calls it; `shade` selects the lanes that shade (hit, !in_medium).
+template <bool FAST, bool DEEP, bool SPHERES>
+__device__ __forceinline__ V3 local_color(const RenderParams& P, const DevNode* __restrict__ nodes,
+                                          const DevPrim* __restrict__ prims,
+                                          const DevMaterial* __restrict__ mats,
+                                          const DevLight* __restrict__ lights, int* spill,
+                                          bool shade, V3 o, V3 p, V3 n, int mat, Diag& dg,
+                                          unsigned long long& shadow_rays) {
+  V3 color = v3(0.0f, 0.0f, 0.0f);
+  const DevMaterial& m = mats[shade ? mat : 0];
+  if (shade) color = color + ld3(m.ambient) * ld3(P.ambient);
+  const V3 w0 = shade ? normalize(o - p) : v3(0, 0, 0);
+  for (int li = 0; li < P.num_lights; li++) {
+    const DevLight& L = lights[li];
+    const V3 ld = ld3(L.position) - p;
+    const V3 wi = normalize(ld);
+    const float dist = length(ld);
+    const LaneRay sr = make_ray(p + wi * P.eps, wi);
+    const float thr = dist - P.eps;
+    const bool sskip = ballot(shade && (sr.skip0 || sr.skip1 || sr.skip2)) != 0;
+    bool occ;
+    if (sskip)
+      occ = occluded<true, FAST, DEEP, SPHERES>(P, nodes, prims, spill, sr, shade, thr, dg);
+    else
+      occ = occluded<false, FAST, DEEP, SPHERES>(P, nodes, prims, spill, sr, shade, thr, dg);
+    shadow_rays += __builtin_popcountll(ballot(shade));
+    if (shade && !occ) {
+      const V3 I = ld3(L.intensity);
+      const float d2 = dist * dist;
+      color = color + ((ld3(m.diffuse) * I) * dot(n, wi)) / d2;
+      const float cos_s = __builtin_fmaxf(dot(n, normalize(w0 + wi)), 0.0f);
+      const float pw = (float)pow((double)cos_s, (double)m.phong_exponent);
+      color = color + ((ld3(m.specular) * I) * pw) / d2;
+    }
+  }
+  return color;
+}
+
+template <bool FAST, bool DEEP, bool SPHERES>
+__device__ __forceinline__ void recursive_packet(const RenderParams& P,
+                                                 const DevNode* __restrict__ nodes,
+                                                 const DevPrim* __restrict__ prims,
+                                                 const float* __restrict__ normals,
+                                                 const DevMaterial* __restrict__ mats,
+                                                 const DevLight* __restrict__ lights, int sel,
+                                                 int* spill) {
+  const PacketPixel q = packet_pixel(P, sel);
+  const size_t lanes_total = (size_t)P.num_sel_tiles * (kTile * kTile);
+  const size_t g = (size_t)sel * (kTile * kTile) + q.lane;
+  auto frame = [&](int level) {
+    return FrameRef{P.frames + (size_t)level * kFrFields * lanes_total + g, lanes_total};
+  };
+  // current ray of this lane
+  V3 ro = ld3(P.cam_e), rd = primary_dir(P, q.px, q.py);
+  bool medium = false;
+  int depth = P.max_depth;
+  bool active = q.valid;  // has a ray to trace
+  int sp = 0;             // frames on this lane's stack
+  V3 res = v3(0, 0, 0), out = v3(0, 0, 0);
+  Diag dg;
+  unsigned long long n_primary = __builtin_popcountll(ballot(q.valid)), n_hits = 0;
+  unsigned long long n_shadow = 0, n_secondary = 0;
+  bool first = true;
+  while (ballot(active)) {
+    const LaneRay ray = make_ray(ro, rd);
+    const bool skip = ballot(active && (ray.skip0 || ray.skip1 || ray.skip2)) != 0;
+    float t;
+    int leaf;
+    if (skip)
+      closest_hit<true, FAST, DEEP, SPHERES>(P, nodes, prims, spill, ray, active, t, leaf, dg);
+    else
+      closest_hit<false, FAST, DEEP, SPHERES>(P, nodes, prims, spill, ray, active, t, leaf, dg);
+    const bool hit = active && leaf >= 0;
+    if (first) n_hits = __builtin_popcountll(ballot(hit));
+    first = false;
+    V3 p = v3(0, 0, 0), n = v3(0, 0, 0);
+    int mat = 0;
+    if (hit) {
+      p = ray.o + ray.d * t;
+      const DevPrim& pr = prims[leaf];
+      n = pr.kind == kPrimTriangle ? ld3(normals + 4 * leaf) : normalize(p - ld3(pr.v0));
+      mat = pr.material;
+    }
+    const V3 local = local_color<FAST, DEEP, SPHERES>(P, nodes, prims, mats, lights, spill,
+                                                      hit && !medium, ray.o, p, n, mat, dg,
+                                                      n_shadow);
+    if (active) {
+      bool spawned = false;
+      if (hit) {  // open a frame for this hit
+        const FrameRef F = frame(sp++);
+        F.put(kFrColor, local);
+        F.put_i(kFrStage, kStStart);
+        F.put(kFrP, p);
+        F.put(kFrN, n);
+        F.put(kFrW0, normalize(ray.o - p));
+        F.put(kFrD, ray.d);
+        F.f(kFrT) = t;
+        F.put_i(kFrMat, mat);
+        F.put_i(kFrDepth, depth);
+        F.put_i(kFrMedium, medium ? 1 : 0);
+      } else {  // a miss returns background only at the primary depth (Scene.cpp:96-99)
+        res = depth == P.max_depth ? ld3(P.background) : v3(0.0f, 0.0f, 0.0f);
+      }
+      // run the post-order state machine until a new ray is spawned or the tree is done
+      while (sp > 0 && !spawned) {
+        const FrameRef F = frame(sp - 1);
+        const int stage = F.i(kFrStage);
+        const DevMaterial& m = mats[F.i(kFrMat)];
+        const int fdepth = F.i(kFrDepth);
+        V3 color = F.v(kFrColor);
+        const V3 fn = F.v(kFrN), fp = F.v(kFrP), fw0 = F.v(kFrW0);
+        const V3 wr = normalize(fn * (2 * dot(fn, fw0)) - fw0);  // (2 n.w0) n - w0
+        int next = stage;
+        if (stage == kStStart) {
+          const bool mirror = m.mirror[0] != 0.0f || m.mirror[1] != 0.0f || m.mirror[2] != 0.0f;
+          if (mirror && fdepth > 0) {
+            ro = fp + wr * P.eps;
+            rd = wr;
+            medium = false;
+            spawned = true;
+            next = kStMirrorWait;
+          } else {
+            next = kStRefr;
+          }
+        } else if (stage == kStMirrorWait) {
+          color = color + ld3(m.mirror) * res;
+          next = kStRefr;
+        } else if (stage == kStRefr) {
+          const bool glass = m.transparency[0] != 0.0f || m.transparency[1] != 0.0f ||
+                             m.transparency[2] != 0.0f;
+          if (glass && fdepth > 0) {
+            V3 td = v3(0.0f, 0.0f, 0.0f), k = v3(0.0f, 0.0f, 0.0f);
+            float cos_t = 0.0f;
+            const V3 dn = normalize(F.v(kFrD));
+            const float idx = m.refraction_index;
+            bool tir = false, entering;
+            if (dot(dn, fn) < 0.0f) {
+              refract_ray(dn, fn, idx, td);
+              cos_t = dot(v3(-dn.x, -dn.y, -dn.z), fn);
+              k = v3(1.0f, 1.0f, 1.0f);
+              entering = true;
+            } else {
+              const double tt = (double)F.f(kFrT);
+              k.x = (float)exp(-log((double)m.transparency[0]) * tt);
+              k.y = (float)exp(-log((double)m.transparency[1]) * tt);
+              k.z = (float)exp(-log((double)m.transparency[2]) * tt);
+              entering = false;
+              if (refract_ray(dn, v3(-fn.x, -fn.y, -fn.z), 1.0f / idx, td))
+                cos_t = dot(td, fn);
+              else
+                tir = true;
+            }
+            F.put(kFrK, k);
+            ro = fp + wr * P.eps;
+            rd = wr;
+            spawned = true;
+            if (tir) {
+              medium = true;
+              next = kStTirWait;
+            } else {
+              const float r0 = (idx - 1) * (idx - 1) / ((idx + 1) * (idx + 1));
+              const float r =
+                  (float)((double)r0 + (double)(1 - r0) * pow((double)(1 - cos_t), 5.0));
+              F.f(kFrR) = r;
+              F.put(kFrA, td);  // transmission direction until the reflection returns
+              medium = !entering;
+              F.put_i(kFrMedium, entering ? 1 : 0);  // medium flag of the transmission ray
+              next = kStReflWait;
+            }
+          } else {
+            next = kStDone;
+          }
+        } else if (stage == kStTirWait) {
+          color = color + F.v(kFrK) * res;
+          next = kStDone;
+        } else if (stage == kStReflWait) {
+          const V3 td = F.v(kFrA);
+          F.put(kFrA, res * F.f(kFrR));  // r * trace(reflection)
+          ro = fp + td * P.eps;
+          rd = td;
+          medium = F.i(kFrMedium) != 0;
+          spawned = true;
+          next = kStTransWait;
+        } else if (stage == kStTransWait) {
+          color = color + F.v(kFrK) * (F.v(kFrA) + res * (1 - F.f(kFrR)));
+          next = kStDone;
+        }
+        if (next == kStDone) {
+          res = color;
+          sp--;
+          continue;
+        }
+        F.put(kFrColor, color);
+        F.put_i(kFrStage, next);
+        if (spawned) {
+          depth = fdepth - 1;
+          n_secondary++;
+        }
+      }
+      if (!spawned) {  // the whole tree of this pixel is done
+        out = res;
+        active = false;
+      }
+    }
+  }
+  if (q.valid) {
+    float* o;
+    if (P.tile_major)
+      o = P.out + 3 * g;
+    else
+      o = P.out + 3 * ((size_t)q.py * P.width + q.px);
+    o[0] = 0.0f + out.x;  // Pixel::add_color(color, 1) onto a zeroed pixel
+    o[1] = 0.0f + out.y;
+    o[2] = 0.0f + out.z;
+  } else if (P.tile_major) {
+    float* o = P.out + 3 * g;
+    o[0] = o[1] = o[2] = 0.0f;
+  }
+  if (P.counters) {
+    // n_secondary is per lane: reduce over the wave with atomics from every lane that spawned
+    unsigned long long* c = counter_row(P, sel);
+    if (n_secondary) atomicAdd(&c[kCntSecondary], n_secondary);
+    if (q.lane == 0) {
+      atomicAdd(&c[kCntPrimary], n_primary);
+      atomicAdd(&c[kCntHits], n_hits);
+      atomicAdd(&c[kCntShadow], n_shadow);
+    }
+  }
+}
+
 // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so hand each
 // XCD a contiguous run of tiles — neighbouring packets share BVH nodes through its L2.
 __device__ __forceinline__ int packet_index() {
@@ -647,6 +918,18 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void trace_shadow_kernel(
   shadow_packet<FAST, DEEP, SPHERES>(P, nodes, prims, lights, sel, spill);
 }
 
+template <bool FAST, bool DEEP, bool SPHERES>
+__global__ __launch_bounds__(kWavesPerBlock * 64) void recursive_kernel(
+    RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims,
+    const float* __restrict__ normals, const DevMaterial* __restrict__ mats,
+    const DevLight* __restrict__ lights) {
+  extern __shared__ __attribute__((aligned(16))) int deep_stack[];
+  const int sel = packet_index();
+  if (sel >= P.num_sel_tiles) return;
+  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * 3 * kDeepStack : nullptr;
+  recursive_packet<FAST, DEEP, SPHERES>(P, nodes, prims, normals, mats, lights, sel, spill);
+}
+
 __global__ __launch_bounds__(kWavesPerBlock * 64) void shade_kernel(
     RenderParams P, const DevPrim* __restrict__ prims, const float* __restrict__ normals,
     const DevMaterial* __restrict__ mats, const DevLight* __restrict__ lights) {
@@ -660,6 +943,12 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
                            const float* normals, const DevMaterial* mats,
                            const DevLight* lights, int blocks, hipStream_t stream) {
   const size_t lds = DEEP ? sizeof(int) * 3 * kDeepStack * kWavesPerBlock : 0;
+  if (P.frames) {  // recursive scenes: one kernel walks each pixel's ray tree
+    hipLaunchKernelGGL((recursive_kernel<FAST, DEEP, SPHERES>), dim3(blocks),
+                       dim3(kWavesPerBlock * 64), lds, stream, P, nodes, prims, normals, mats,
+                       lights);
+    return;
+  }
   hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES>), dim3(blocks),
                      dim3(kWavesPerBlock * 64), lds, stream, P, nodes, prims);
   if (P.num_lights > 0)

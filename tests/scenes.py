@@ -32,6 +32,13 @@ CATALOGUE = {
 RECURSIVE = {
     "soup_depth3": (lambda: G.soup_scene(4, 96, 96, depth=3, mirror=True, glass=True),
                     "mirror + dielectric recursion depth 3"),
+    "soup_depth1": (lambda: G.soup_scene(5, 64, 64, depth=1, mirror=True, glass=True),
+                    "depth 1: one bounce, misses below max depth return black"),
+    "soup_depth6": (lambda: G.soup_scene(6, 48, 40, depth=6, mirror=True, glass=True,
+                                         n_spheres=10),
+                    "depth 6: total internal reflection, exiting rays, Beer absorption"),
+    "mirror_only": (lambda: G.soup_scene(7, 64, 48, depth=4, mirror=True, glass=False),
+                    "mirrors only"),
 }
 
 SMALL = ["c1", "hf_small", "hf_side", "soup1", "soup2", "soup3", "single_sphere",
