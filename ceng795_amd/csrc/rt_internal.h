@@ -31,8 +31,10 @@ enum : int {
 };
 
 struct alignas(16) DevNode {
-  float b0[6];   // child 0 box: lo.xyz, hi.xyz (unused if child 0 is a leaf)
-  float b1[6];   // child 1 box
+  // Both CHILD boxes, interleaved per coordinate ([axis][child]) so one packed-fp32 op
+  // (v_pk_add_f32 / v_pk_mul_f32) works on both children.  Unused for a leaf child.
+  float lo[3][2];
+  float hi[3][2];
   int32_t child[2];  // >= 0: internal node index; < 0: leaf index ~child
   int32_t axis;      // split dimension of THIS node (Bounding_volume_hierarchy.cpp:8)
   int32_t pad;
@@ -49,7 +51,7 @@ struct alignas(16) DevPrim {
   float a2[3];
   int32_t kind;
   int32_t material;
-  int32_t pad;
+  float cx;  // triangle: a1.y*a2.z - a2.y*a1.z (the d-free minor of Triangle.h:35-37)
 };
 static_assert(sizeof(DevPrim) == 48, "prim record is three 16-byte loads");
 

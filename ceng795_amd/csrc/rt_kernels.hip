@@ -31,6 +31,10 @@ namespace rt {
 #define RT_INF __builtin_huge_valf()
 constexpr float kEps = 0.000001f;  // HW2/Vector3.h:7 kEpsilon
 constexpr int kCounterSlots = kCounterRows;
+#ifndef RT_RAYS_PER_LANE
+#define RT_RAYS_PER_LANE 1
+#endif
+constexpr int kRaysPerLane = RT_RAYS_PER_LANE;  // tiles per wave in the traversal kernels
 
 #ifdef RT_DIAG
 #define DIAG(stmt) stmt
@@ -149,15 +153,24 @@ __device__ __forceinline__ float det3(V3 c1, V3 c2, V3 c3) {
          c3.x * (c1.y * c2.z - c2.y * c1.z);
 }
 
-__device__ __forceinline__ bool tri_test(V3 v0, V3 a1, V3 a2, const LaneRay& r, float& t) {
-  const float det = det3(a1, a2, r.d);
+// det3(a1, a2, c3) with the c3-free minor `cx` = a1.y*a2.z - a2.y*a1.z precomputed (same bits)
+__device__ __forceinline__ float det3_cx(V3 c1, V3 c2, V3 c3, float cx) {
+  return c1.x * (c2.y * c3.z - c3.y * c2.z) + c2.x * (c3.y * c1.z - c1.y * c3.z) + c3.x * cx;
+}
+
+__device__ __forceinline__ bool tri_test(V3 v0, V3 a1, V3 a2, float cx, const LaneRay& r,
+                                         float& t) {
+#ifndef RT_EXP_CX
+#define det3_cx(c1, c2, c3, cx) det3(c1, c2, c3)
+#endif
+  const float det = det3_cx(a1, a2, r.d, cx);
   if (det == 0.0f) return false;
   const V3 b = (v0 - r.o) / det;
   const float beta = det3(b, a2, r.d);
   if (beta < 0.0f || beta > 1.0f) return false;
   const float gamma = det3(a1, b, r.d);
   if (gamma < 0.0f || beta + gamma > 1.0f) return false;
-  const float tt = det3(a1, a2, b);
+  const float tt = det3_cx(a1, a2, b, cx);
   if (tt > 0.0f) {
     t = tt;
     return true;
@@ -191,47 +204,58 @@ __device__ __forceinline__ bool leaf_test(const DevPrim* __restrict__ prims, int
                                           const LaneRay& r, float& t) {
   const DevPrim& p = prims[leaf];
   const V3 v0 = ld3(p.v0);
-  if (!SPHERES || p.kind == kPrimTriangle) return tri_test(v0, ld3(p.a1), ld3(p.a2), r, t);
+  if (!SPHERES || p.kind == kPrimTriangle) return tri_test(v0, ld3(p.a1), ld3(p.a2), p.cx, r, t);
   return sphere_test(v0, p.a1[0], r, t);
 }
 
 // ------------------------------------------------------------------ traversal stack
-// Wave-uniform (node, lane-mask) entries.  DEEP == false: entry i lives in VGPR lane i
-// (select-on-lane push / v_readlane pop, no memory traffic, 64 deep).  DEEP == true: a per-wave LDS
-// array of kDeepStack entries for trees deeper than 64 levels (lane 0 writes, all lanes
-// read the broadcast word; LDS ops of one wave complete in order).
+// Wave-uniform (node, R lane-masks) entries — R rays per lane.  DEEP == false: entry i lives
+// in VGPR lane i (select-on-lane push / v_readlane pop, no memory traffic, 64 deep).
+// DEEP == true: a per-wave LDS array of kDeepStack entries for trees deeper than 64 levels
+// (lane 0 writes, all lanes read the broadcast word; LDS ops of one wave complete in order).
 constexpr int kDeepStack = 1024;
 
-template <bool DEEP>
+template <bool DEEP, int R>
 struct WaveStack {
+  static constexpr int kWords = 1 + 2 * R;
   int node = 0;
-  unsigned mlo = 0, mhi = 0;
-  int sp = 0;       // wave-uniform
+  unsigned mlo[R] = {}, mhi[R] = {};
+  int sp = 0;  // wave-uniform
   int* lds = nullptr;
 
-  __device__ __forceinline__ void push(int n, uint64_t m) {
+  __device__ __forceinline__ void push(int n, const uint64_t (&m)[R]) {
     if (!DEEP) {
       const bool mine = lane_id() == sp;  // v_cmp + v_cndmask: lane sp takes the entry
       node = mine ? n : node;
-      mlo = mine ? (unsigned)m : mlo;
-      mhi = mine ? (unsigned)(m >> 32) : mhi;
+#pragma unroll
+      for (int k = 0; k < R; k++) {
+        mlo[k] = mine ? (unsigned)m[k] : mlo[k];
+        mhi[k] = mine ? (unsigned)(m[k] >> 32) : mhi[k];
+      }
     } else if (lane_id() == 0) {
-      lds[3 * sp] = n;
-      lds[3 * sp + 1] = (int)(unsigned)m;
-      lds[3 * sp + 2] = (int)(unsigned)(m >> 32);
+      lds[kWords * sp] = n;
+#pragma unroll
+      for (int k = 0; k < R; k++) {
+        lds[kWords * sp + 1 + 2 * k] = (int)(unsigned)m[k];
+        lds[kWords * sp + 2 + 2 * k] = (int)(unsigned)(m[k] >> 32);
+      }
     }
     sp++;
   }
-  __device__ __forceinline__ void pop(int& n, uint64_t& m) {
+  __device__ __forceinline__ void pop(int& n, uint64_t (&m)[R]) {
     sp--;
     if (!DEEP) {
       n = __builtin_amdgcn_readlane(node, sp);
-      m = (uint64_t)(unsigned)__builtin_amdgcn_readlane(mlo, sp) |
-          ((uint64_t)(unsigned)__builtin_amdgcn_readlane(mhi, sp) << 32);
+#pragma unroll
+      for (int k = 0; k < R; k++)
+        m[k] = (uint64_t)(unsigned)__builtin_amdgcn_readlane(mlo[k], sp) |
+               ((uint64_t)(unsigned)__builtin_amdgcn_readlane(mhi[k], sp) << 32);
     } else {
-      n = uniform(lds[3 * sp]);
-      m = (uint64_t)(unsigned)uniform(lds[3 * sp + 1]) |
-          ((uint64_t)(unsigned)uniform(lds[3 * sp + 2]) << 32);
+      n = uniform(lds[kWords * sp]);
+#pragma unroll
+      for (int k = 0; k < R; k++)
+        m[k] = (uint64_t)(unsigned)uniform(lds[kWords * sp + 1 + 2 * k]) |
+               ((uint64_t)(unsigned)uniform(lds[kWords * sp + 2 + 2 * k]) << 32);
     }
   }
 };
@@ -250,9 +274,12 @@ __device__ __forceinline__ DevNode load_node(const DevNode* __restrict__ nodes, 
   const v4f q1 = src[1 + zero];
   const v4f q2 = src[2 + zero];
   const v4f q3 = src[3 + zero];
-  N.b0[0] = q0.x; N.b0[1] = q0.y; N.b0[2] = q0.z; N.b0[3] = q0.w;
-  N.b0[4] = q1.x; N.b0[5] = q1.y; N.b1[0] = q1.z; N.b1[1] = q1.w;
-  N.b1[2] = q2.x; N.b1[3] = q2.y; N.b1[4] = q2.z; N.b1[5] = q2.w;
+  const float f[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+  for (int a = 0; a < 3; a++)
+    for (int c = 0; c < 2; c++) {
+      N.lo[a][c] = f[2 * a + c];
+      N.hi[a][c] = f[6 + 2 * a + c];
+    }
   N.child[0] = uniform(__float_as_int(q3.x));
   N.child[1] = uniform(__float_as_int(q3.y));
   N.axis = 0;
@@ -263,6 +290,11 @@ __device__ __forceinline__ DevNode load_node(const DevNode* __restrict__ nodes, 
 #endif
 }
 
+__device__ __forceinline__ bool child_box_exact(const DevNode& N, int c, const LaneRay& r) {
+  const float b[6] = {N.lo[0][c], N.lo[1][c], N.lo[2][c], N.hi[0][c], N.hi[1][c], N.hi[2][c]};
+  return box_exact(b, r);
+}
+
 // One packet visit of a BVH2 node: both child slab tests (computed unconditionally so the
 // 64-byte record arrives in one scalar load), the rare exact fallback behind one ballot, and
 // which lanes enter each child.  Leaf children are never entered (the caller tests them).
@@ -271,171 +303,249 @@ __device__ __forceinline__ void visit_boxes(const DevNode& N, const LaneRay& r, 
                                             bool& h0, bool& h1, float& t0, float& t1,
                                             Diag& dg) {
   bool u0, u1;
-  slab_fast<SKIP>(N.b0, r, t0, h0, u0);
-  slab_fast<SKIP>(N.b1, r, t1, h1, u1);
+  const float b0[6] = {N.lo[0][0], N.lo[1][0], N.lo[2][0], N.hi[0][0], N.hi[1][0], N.hi[2][0]};
+  const float b1[6] = {N.lo[0][1], N.lo[1][1], N.lo[2][1], N.hi[0][1], N.hi[1][1], N.hi[2][1]};
+  slab_fast<SKIP>(b0, r, t0, h0, u0);
+  slab_fast<SKIP>(b1, r, t1, h1, u1);
   const bool live0 = in & (N.child[0] >= 0), live1 = in & (N.child[1] >= 0);
   h0 &= live0;
   h1 &= live1;
   u0 &= live0;
   u1 &= live1;
   if (ballot(u0 | u1)) {
-    if (u0) h0 = box_exact(N.b0, r);
-    if (u1) h1 = box_exact(N.b1, r);
+    if (u0) h0 = child_box_exact(N, 0, r);
+    if (u1) h1 = child_box_exact(N, 1, r);
     DIAG(if (u0 | u1) atomicAdd(&g_exact_fallbacks, 1ull));
   }
 }
 
-// Pick the next node: near child first (judged by the first lane entering both), the far
-// one pushed; with neither, pop.  Returns false when the traversal is over.
-template <bool DEEP>
-__device__ __forceinline__ bool advance(WaveStack<DEEP>& st, int c0, int c1, uint64_t m0,
-                                        uint64_t m1, float t0, float t1, int& node,
-                                        uint64_t& m, uint64_t alive) {
-  if (m0 && m1) {
-    const int f = __builtin_ctzll((m0 & m1) ? (m0 & m1) : m0);
-    const float f0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t0), f));
-    const float f1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t1), f));
-    if (f1 < f0) {
+template <int R>
+__device__ __forceinline__ uint64_t any_of(const uint64_t (&m)[R]) {
+  uint64_t a = 0;
+#pragma unroll
+  for (int k = 0; k < R; k++) a |= m[k];
+  return a;
+}
+
+// Pick the next node: near child first (judged by the first lane of the first ray entering
+// both), the far one pushed; with neither, pop (masks restricted to `alive`).  Returns false
+// when the traversal is over.
+template <bool DEEP, int R>
+__device__ __forceinline__ bool advance(WaveStack<DEEP, R>& st, int c0, int c1,
+                                        const uint64_t (&m0)[R], const uint64_t (&m1)[R],
+                                        const float (&t0)[R], const float (&t1)[R], int& node,
+                                        uint64_t (&m)[R], const uint64_t (&alive)[R]) {
+  const bool e0 = any_of(m0) != 0, e1 = any_of(m1) != 0;
+  if (e0 && e1) {
+    int kk = 0;
+    uint64_t both = m0[0] & m1[0];
+#pragma unroll
+    for (int k = 1; k < R; k++)
+      if (!both && (m0[k] & m1[k])) {
+        both = m0[k] & m1[k];
+        kk = k;
+      }
+    bool near1 = false;
+    if (both) {
+      const int f = __builtin_ctzll(both);
+      float f0 = 0.0f, f1 = 0.0f;
+#pragma unroll
+      for (int k = 0; k < R; k++)
+        if (k == kk) {
+          f0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t0[k]), f));
+          f1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t1[k]), f));
+        }
+      near1 = f1 < f0;
+    }
+    if (near1) {
       st.push(c0, m0);
       node = c1;
-      m = m1;
+#pragma unroll
+      for (int k = 0; k < R; k++) m[k] = m1[k];
     } else {
       st.push(c1, m1);
       node = c0;
-      m = m0;
+#pragma unroll
+      for (int k = 0; k < R; k++) m[k] = m0[k];
     }
     return true;
   }
-  if (m0 | m1) {
-    node = m0 ? c0 : c1;
-    m = m0 | m1;
+  if (e0 || e1) {
+    node = e0 ? c0 : c1;
+#pragma unroll
+    for (int k = 0; k < R; k++) m[k] = e0 ? m0[k] : m1[k];
     return true;
   }
   for (;;) {
     if (st.sp == 0) return false;
     st.pop(node, m);
-    m &= alive;
-    if (m) return true;
+#pragma unroll
+    for (int k = 0; k < R; k++) m[k] &= alive[k];
+    if (any_of(m)) return true;
   }
 }
 
 // ------------------------------------------------------------------ closest hit
-// Returns the reference's (t, leaf) for every active lane: best_leaf < 0 = miss.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES>
+// R rays per lane.  Returns the reference's (t, leaf) for every active ray: leaf < 0 = miss.
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R>
 __device__ __forceinline__ void closest_hit(const RenderParams& P,
                                             const DevNode* __restrict__ nodes,
                                             const DevPrim* __restrict__ prims, int* spill,
-                                            const LaneRay& r, bool active, float& best_t,
-                                            int& best_leaf, Diag& dg) {
-  best_t = RT_INF;
-  best_leaf = -1;
+                                            const LaneRay (&r)[R], const bool (&active)[R],
+                                            float (&best_t)[R], int (&best_leaf)[R], Diag& dg) {
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    best_t[k] = RT_INF;
+    best_leaf[k] = -1;
+  }
   if (P.root_kind != kRootNode) {  // the root IS the primitive (BVH.h:13-14): its own rule
-    float t;
-    if (active && leaf_test<SPHERES>(prims, P.root_ref, r, t)) {
-      best_t = t;
-      best_leaf = P.root_ref;
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+      float t;
+      if (active[k] && leaf_test<SPHERES>(prims, P.root_ref, r[k], t)) {
+        best_t[k] = t;
+        best_leaf[k] = P.root_ref;
+      }
     }
     return;
   }
-  float tn;
-  bool acc, und;
-  slab_fast<SKIP>(P.root_box, r, tn, acc, und);
-  const bool h = active && (acc || (und && box_exact(P.root_box, r)));
-  uint64_t m = ballot(h);
-  if (m == 0) return;
+  uint64_t m[R];
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    float tn;
+    bool acc, und;
+    slab_fast<SKIP>(P.root_box, r[k], tn, acc, und);
+    m[k] = ballot(active[k] && (acc || (und && box_exact(P.root_box, r[k]))));
+  }
+  if (!any_of(m)) return;
   const int lane = lane_id();
-  WaveStack<DEEP> st;
+  WaveStack<DEEP, R> st;
   st.lds = spill;
+  uint64_t everyone[R];
+#pragma unroll
+  for (int k = 0; k < R; k++) everyone[k] = ~0ull;
   int node = P.root_ref;
   for (;;) {
     const DevNode N = load_node(nodes, node);
-    const bool in = (m >> lane) & 1;
-    DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m);
+    bool in[R], h0[R], h1[R];
+    float t0[R], t1[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+      in[k] = (m[k] >> lane) & 1;
+      visit_boxes<SKIP>(N, r[k], in[k], h0[k], h1[k], t0[k], t1[k], dg);
+    }
+    DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(any_of(m));
          dg.leaves += (N.child[0] < 0) + (N.child[1] < 0);
-         dg.leaf_lanes += ((N.child[0] < 0) + (N.child[1] < 0)) * __builtin_popcountll(m));
-    bool h0, h1;
-    float t0, t1;
-    visit_boxes<SKIP>(N, r, in, h0, h1, t0, t1, dg);
+         dg.leaf_lanes += ((N.child[0] < 0) + (N.child[1] < 0)) * __builtin_popcountll(any_of(m)));
 #ifndef RT_EXP_NOLEAF
 #pragma unroll 1
-    for (int k = 0; k < 2; k++) {  // leaf children: Shape::intersect, accept 0 < t < best
-      const int c = k ? N.child[1] : N.child[0];
-      if (c < 0 && in) {
-        float t;
-        if (leaf_test<SPHERES>(prims, ~c, r, t) && t > 0.0f && t < RT_INF &&
-            (t < best_t || (t == best_t && ~c < best_leaf))) {
-          best_t = t;
-          best_leaf = ~c;
+    for (int side = 0; side < 2; side++) {  // leaf children: Shape::intersect, 0 < t < best
+      const int c = side ? N.child[1] : N.child[0];
+      if (c < 0) {
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+          float t;
+          if (in[k] && leaf_test<SPHERES>(prims, ~c, r[k], t) && t > 0.0f && t < RT_INF &&
+              (t < best_t[k] || (t == best_t[k] && ~c < best_leaf[k]))) {
+            best_t[k] = t;
+            best_leaf[k] = ~c;
+          }
         }
       }
     }
 #else
-    best_leaf -= in ? 1 : 0;  // timing experiment: keep the traversal observable
+#pragma unroll
+    for (int k = 0; k < R; k++) best_leaf[k] -= in[k] ? 1 : 0;  // keep traversal observable
 #endif
-    if (FAST) {
-      const float lim = cull_limit(best_t);
-      h0 = h0 && t0 <= lim;
-      h1 = h1 && t1 <= lim;
+    uint64_t m0[R], m1[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+      if (FAST) {
+        const float lim = cull_limit(best_t[k]);
+        h0[k] = h0[k] && t0[k] <= lim;
+        h1[k] = h1[k] && t1[k] <= lim;
+      }
+      m0[k] = ballot(h0[k]);
+      m1[k] = ballot(h1[k]);
     }
-    if (!advance(st, N.child[0], N.child[1], ballot(h0), ballot(h1), t0, t1, node, m, ~0ull))
-      break;
+    if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, everyone)) break;
   }
 }
 
 // ------------------------------------------------------------------ shadow (any hit)
 // Occluded iff some leaf the ray may reach has 0 < t < thr — identical to the reference's
 // closest-hit shadow test `0 < t_closest < dist - eps` (HW2/Scene.cpp:123-127), appendix A.7.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES>
-__device__ __forceinline__ bool occluded(const RenderParams& P,
-                                         const DevNode* __restrict__ nodes,
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R>
+__device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* __restrict__ nodes,
                                          const DevPrim* __restrict__ prims, int* spill,
-                                         const LaneRay& r, bool active, float thr, Diag& dg) {
+                                         const LaneRay (&r)[R], const bool (&active)[R],
+                                         const float (&thr)[R], bool (&occ)[R], Diag& dg) {
+#pragma unroll
+  for (int k = 0; k < R; k++) occ[k] = false;
   if (P.root_kind != kRootNode) {
-    float t;
-    return active && leaf_test<SPHERES>(prims, P.root_ref, r, t) && t < thr && t > 0.0f;
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+      float t;
+      occ[k] = active[k] && leaf_test<SPHERES>(prims, P.root_ref, r[k], t) && t < thr[k] &&
+               t > 0.0f;
+    }
+    return;
   }
-  bool occ = false;
-  float tn;
-  bool acc, und;
-  // thr <= 0 (or NaN): nothing can satisfy 0 < t < thr
-  slab_fast<SKIP>(P.root_box, r, tn, acc, und);
-  const bool h = active && thr > 0.0f && (acc || (und && box_exact(P.root_box, r)));
-  uint64_t m = ballot(h);
-  if (m == 0) return false;
+  uint64_t m[R], alive[R];
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    float tn;
+    bool acc, und;
+    // thr <= 0 (or NaN): nothing can satisfy 0 < t < thr
+    slab_fast<SKIP>(P.root_box, r[k], tn, acc, und);
+    m[k] = ballot(active[k] && thr[k] > 0.0f && (acc || (und && box_exact(P.root_box, r[k]))));
+    alive[k] = m[k];
+  }
+  if (!any_of(m)) return;
   const int lane = lane_id();
-  WaveStack<DEEP> st;
+  WaveStack<DEEP, R> st;
   st.lds = spill;
   int node = P.root_ref;
-  uint64_t alive = m;
   for (;;) {
     const DevNode N = load_node(nodes, node);
-    const bool in = (m >> lane) & 1;
-    DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m);
+    bool in[R], h0[R], h1[R];
+    float t0[R], t1[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+      in[k] = (m[k] >> lane) & 1;
+      visit_boxes<SKIP>(N, r[k], in[k], h0[k], h1[k], t0[k], t1[k], dg);
+    }
+    DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(any_of(m));
          dg.leaves += (N.child[0] < 0) + (N.child[1] < 0);
-         dg.leaf_lanes += ((N.child[0] < 0) + (N.child[1] < 0)) * __builtin_popcountll(m));
-    bool h0, h1;
-    float t0, t1;
-    visit_boxes<SKIP>(N, r, in, h0, h1, t0, t1, dg);
+         dg.leaf_lanes += ((N.child[0] < 0) + (N.child[1] < 0)) * __builtin_popcountll(any_of(m)));
 #pragma unroll 1
-    for (int k = 0; k < 2; k++) {
-      const int c = k ? N.child[1] : N.child[0];
-      if (c < 0 && in && !occ) {
-        float t;
-        if (leaf_test<SPHERES>(prims, ~c, r, t) && t > 0.0f && t < thr) occ = true;
+    for (int side = 0; side < 2; side++) {
+      const int c = side ? N.child[1] : N.child[0];
+      if (c < 0) {
+#pragma unroll
+        for (int k = 0; k < R; k++) {
+          float t;
+          if (in[k] && !occ[k] && leaf_test<SPHERES>(prims, ~c, r[k], t) && t > 0.0f &&
+              t < thr[k])
+            occ[k] = true;
+        }
       }
     }
-    alive &= ~ballot(occ);
-    if (alive == 0) break;
-    if (FAST) {
-      const float lim = cull_limit(thr);
-      h0 = h0 && t0 <= lim;
-      h1 = h1 && t1 <= lim;
+    uint64_t m0[R], m1[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+      alive[k] &= ~ballot(occ[k]);
+      if (FAST) {
+        const float lim = cull_limit(thr[k]);
+        h0[k] = h0[k] && t0[k] <= lim;
+        h1[k] = h1[k] && t1[k] <= lim;
+      }
+      m0[k] = ballot(h0[k]) & alive[k];
+      m1[k] = ballot(h1[k]) & alive[k];
     }
-    if (!advance(st, N.child[0], N.child[1], ballot(h0) & alive, ballot(h1) & alive, t0, t1,
-                 node, m, alive))
-      break;
+    if (!any_of(alive)) break;
+    if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, alive)) break;
   }
-  return occ;
 }
 
 // ------------------------------------------------------------------ render kernels
@@ -471,39 +581,53 @@ __device__ __forceinline__ unsigned long long* counter_row(const RenderParams& P
   return P.counters + kCounterWidth * (sel % kCounterSlots);
 }
 
-template <bool FAST, bool DEEP, bool SPHERES>
+// R selected tiles per wave (tile sel0 + k is ray k of every lane): one packet traversal
+// serves 64*R rays, so the per-visit overhead (node fetch, masks, stack) is shared.
+template <bool FAST, bool DEEP, bool SPHERES, int R>
 __device__ __forceinline__ void primary_packet(const RenderParams& P,
                                                const DevNode* __restrict__ nodes,
-                                               const DevPrim* __restrict__ prims, int sel,
+                                               const DevPrim* __restrict__ prims, int sel0,
                                                int* spill) {
-  const PacketPixel q = packet_pixel(P, sel);
-  const LaneRay ray = make_ray(ld3(P.cam_e), primary_dir(P, q.px, q.py));
+  PacketPixel q[R];
+  LaneRay ray[R];
+  bool valid[R];
+  bool any_skip = false;
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    q[k] = packet_pixel(P, sel0 + k);
+    valid[k] = q[k].valid && sel0 + k < P.num_sel_tiles;
+    ray[k] = make_ray(ld3(P.cam_e), primary_dir(P, q[k].px, q[k].py));
+    any_skip |= valid[k] && (ray[k].skip0 || ray[k].skip1 || ray[k].skip2);
+  }
   Diag dg;
-  const bool skip = ballot(q.valid && (ray.skip0 || ray.skip1 || ray.skip2)) != 0;
-  float t;
-  int leaf;
-  if (skip)
-    closest_hit<true, FAST, DEEP, SPHERES>(P, nodes, prims, spill, ray, q.valid, t, leaf, dg);
+  float t[R];
+  int leaf[R];
+  if (ballot(any_skip))
+    closest_hit<true, FAST, DEEP, SPHERES, R>(P, nodes, prims, spill, ray, valid, t, leaf, dg);
   else
-    closest_hit<false, FAST, DEEP, SPHERES>(P, nodes, prims, spill, ray, q.valid, t, leaf, dg);
-  int2_t rec;
-  rec.x = __float_as_int(t);
-  rec.y = q.valid ? leaf : -2;  // -1 miss, -2 outside the image
-  P.hits[(size_t)sel * (kTile * kTile) + q.lane] = rec;
-  if (P.counters) {  // spread over kCounterSlots rows: no single hot address
-    const unsigned long long nvalid = __builtin_popcountll(ballot(q.valid));
-    const unsigned long long nhit = __builtin_popcountll(ballot(q.valid && leaf >= 0));
-    if (q.lane == 0) {
-      unsigned long long* c = counter_row(P, sel);
-      atomicAdd(&c[kCntPrimary], nvalid);
-      atomicAdd(&c[kCntHits], nhit);
-#ifdef RT_DIAG
-      atomicAdd(&c[kCntPrimNodes], dg.nodes);
-      atomicAdd(&c[kCntPrimNodeLanes], dg.node_lanes);
-      atomicAdd(&c[kCntPrimLeaves], dg.leaves);
-      atomicAdd(&c[kCntPrimLeafLanes], dg.leaf_lanes);
-#endif
+    closest_hit<false, FAST, DEEP, SPHERES, R>(P, nodes, prims, spill, ray, valid, t, leaf, dg);
+  unsigned long long nvalid = 0, nhit = 0;
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    if (sel0 + k < P.num_sel_tiles) {
+      int2_t rec;
+      rec.x = __float_as_int(t[k]);
+      rec.y = valid[k] ? leaf[k] : -2;  // -1 miss, -2 outside the image
+      P.hits[(size_t)(sel0 + k) * (kTile * kTile) + q[k].lane] = rec;
     }
+    nvalid += __builtin_popcountll(ballot(valid[k]));
+    nhit += __builtin_popcountll(ballot(valid[k] && leaf[k] >= 0));
+  }
+  if (P.counters && q[0].lane == 0) {  // spread over kCounterSlots rows: no hot address
+    unsigned long long* c = counter_row(P, sel0);
+    atomicAdd(&c[kCntPrimary], nvalid);
+    atomicAdd(&c[kCntHits], nhit);
+#ifdef RT_DIAG
+    atomicAdd(&c[kCntPrimNodes], dg.nodes);
+    atomicAdd(&c[kCntPrimNodeLanes], dg.node_lanes);
+    atomicAdd(&c[kCntPrimLeaves], dg.leaves);
+    atomicAdd(&c[kCntPrimLeafLanes], dg.leaf_lanes);
+#endif
   }
 }
 
@@ -514,51 +638,72 @@ __device__ __forceinline__ V3 hit_point(const RenderParams& P, const PacketPixel
 }
 
 // Shadow rays of HW2/Scene.cpp:113-127: one bit per point light, set when the light is
-// occluded for this pixel's primary hit.
-template <bool FAST, bool DEEP, bool SPHERES>
+// occluded for this pixel's primary hit.  R tiles per wave as in primary_packet.
+template <bool FAST, bool DEEP, bool SPHERES, int R>
 __device__ __forceinline__ void shadow_packet(const RenderParams& P,
                                               const DevNode* __restrict__ nodes,
                                               const DevPrim* __restrict__ prims,
-                                              const DevLight* __restrict__ lights, int sel,
+                                              const DevLight* __restrict__ lights, int sel0,
                                               int* spill) {
-  const PacketPixel q = packet_pixel(P, sel);
-  const size_t pix = (size_t)sel * (kTile * kTile) + q.lane;
-  const int2_t rec = P.hits[pix];
-  const bool hit = rec.y >= 0;
-  const V3 p = hit ? hit_point(P, q, __int_as_float(rec.x)) : v3(0, 0, 0);
+  PacketPixel q[R];
+  bool hit[R];
+  V3 p[R];
+  size_t pix[R];
+  unsigned long long nhit = 0;
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    q[k] = packet_pixel(P, sel0 + k);
+    const bool inside = sel0 + k < P.num_sel_tiles;
+    pix[k] = (size_t)(sel0 + k) * (kTile * kTile) + q[k].lane;
+    int2_t rec;
+    rec.x = 0;
+    rec.y = -2;
+    if (inside) rec = P.hits[pix[k]];
+    hit[k] = rec.y >= 0;
+    p[k] = hit[k] ? hit_point(P, q[k], __int_as_float(rec.x)) : v3(0, 0, 0);
+    nhit += __builtin_popcountll(ballot(hit[k]));
+  }
   Diag dg;
   for (int w = 0; w < P.occ_words; w++) {
-    unsigned bits = 0;
+    unsigned bits[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) bits[k] = 0;
     const int lend = min(P.num_lights, 32 * (w + 1));
     for (int li = 32 * w; li < lend; li++) {
       const DevLight& L = lights[li];
-      const V3 ld = ld3(L.position) - p;
-      const V3 wi = normalize(ld);
-      const float dist = length(ld);
-      const LaneRay sr = make_ray(p + wi * P.eps, wi);  // p + eps * w_i
-      const float thr = dist - P.eps;
-      const bool sskip = ballot(hit && (sr.skip0 || sr.skip1 || sr.skip2)) != 0;
-      bool occ;
-      if (sskip)
-        occ = occluded<true, FAST, DEEP, SPHERES>(P, nodes, prims, spill, sr, hit, thr, dg);
+      LaneRay sr[R];
+      float thr[R];
+      bool any_skip = false;
+#pragma unroll
+      for (int k = 0; k < R; k++) {
+        const V3 ld = ld3(L.position) - p[k];
+        const V3 wi = normalize(ld);
+        const float dist = length(ld);
+        sr[k] = make_ray(p[k] + wi * P.eps, wi);  // p + eps * w_i
+        thr[k] = dist - P.eps;
+        any_skip |= hit[k] && (sr[k].skip0 || sr[k].skip1 || sr[k].skip2);
+      }
+      bool occ[R];
+      if (ballot(any_skip))
+        occluded<true, FAST, DEEP, SPHERES, R>(P, nodes, prims, spill, sr, hit, thr, occ, dg);
       else
-        occ = occluded<false, FAST, DEEP, SPHERES>(P, nodes, prims, spill, sr, hit, thr, dg);
-      bits |= (occ ? 1u : 0u) << (li - 32 * w);
+        occluded<false, FAST, DEEP, SPHERES, R>(P, nodes, prims, spill, sr, hit, thr, occ, dg);
+#pragma unroll
+      for (int k = 0; k < R; k++) bits[k] |= (occ[k] ? 1u : 0u) << (li - 32 * w);
     }
-    P.occ[pix * P.occ_words + w] = bits;
+#pragma unroll
+    for (int k = 0; k < R; k++)
+      if (sel0 + k < P.num_sel_tiles) P.occ[pix[k] * P.occ_words + w] = bits[k];
   }
-  if (P.counters) {
-    const unsigned long long nhit = __builtin_popcountll(ballot(hit));
-    if (q.lane == 0) {
-      unsigned long long* c = counter_row(P, sel);
-      atomicAdd(&c[kCntShadow], nhit * (unsigned long long)P.num_lights);
+  if (P.counters && q[0].lane == 0) {
+    unsigned long long* c = counter_row(P, sel0);
+    atomicAdd(&c[kCntShadow], nhit * (unsigned long long)P.num_lights);
 #ifdef RT_DIAG
-      atomicAdd(&c[kCntShadNodes], dg.nodes);
-      atomicAdd(&c[kCntShadNodeLanes], dg.node_lanes);
-      atomicAdd(&c[kCntShadLeaves], dg.leaves);
-      atomicAdd(&c[kCntShadLeafLanes], dg.leaf_lanes);
+    atomicAdd(&c[kCntShadNodes], dg.nodes);
+    atomicAdd(&c[kCntShadNodeLanes], dg.node_lanes);
+    atomicAdd(&c[kCntShadLeaves], dg.leaves);
+    atomicAdd(&c[kCntShadLeafLanes], dg.leaf_lanes);
 #endif
-    }
   }
 }
 
@@ -675,16 +820,17 @@ __device__ __forceinline__ V3 local_color(const RenderParams& P, const DevNode* 
     const V3 ld = ld3(L.position) - p;
     const V3 wi = normalize(ld);
     const float dist = length(ld);
-    const LaneRay sr = make_ray(p + wi * P.eps, wi);
-    const float thr = dist - P.eps;
-    const bool sskip = ballot(shade && (sr.skip0 || sr.skip1 || sr.skip2)) != 0;
-    bool occ;
+    const LaneRay sr[1] = {make_ray(p + wi * P.eps, wi)};
+    const float thr[1] = {dist - P.eps};
+    const bool act[1] = {shade};
+    const bool sskip = ballot(shade && (sr[0].skip0 || sr[0].skip1 || sr[0].skip2)) != 0;
+    bool occ[1];
     if (sskip)
-      occ = occluded<true, FAST, DEEP, SPHERES>(P, nodes, prims, spill, sr, shade, thr, dg);
+      occluded<true, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, sr, act, thr, occ, dg);
     else
-      occ = occluded<false, FAST, DEEP, SPHERES>(P, nodes, prims, spill, sr, shade, thr, dg);
+      occluded<false, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, sr, act, thr, occ, dg);
     shadow_rays += __builtin_popcountll(ballot(shade));
-    if (shade && !occ) {
+    if (shade && !occ[0]) {
       const V3 I = ld3(L.intensity);
       const float d2 = dist * dist;
       color = color + ((ld3(m.diffuse) * I) * dot(n, wi)) / d2;
@@ -722,14 +868,18 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
   unsigned long long n_shadow = 0, n_secondary = 0;
   bool first = true;
   while (ballot(active)) {
-    const LaneRay ray = make_ray(ro, rd);
+    const LaneRay rays[1] = {make_ray(ro, rd)};
+    const LaneRay& ray = rays[0];
+    const bool act[1] = {active};
     const bool skip = ballot(active && (ray.skip0 || ray.skip1 || ray.skip2)) != 0;
-    float t;
-    int leaf;
+    float ts[1];
+    int leaves[1];
     if (skip)
-      closest_hit<true, FAST, DEEP, SPHERES>(P, nodes, prims, spill, ray, active, t, leaf, dg);
+      closest_hit<true, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, rays, act, ts, leaves, dg);
     else
-      closest_hit<false, FAST, DEEP, SPHERES>(P, nodes, prims, spill, ray, active, t, leaf, dg);
+      closest_hit<false, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, rays, act, ts, leaves, dg);
+    const float t = ts[0];
+    const int leaf = leaves[0];
     const bool hit = active && leaf >= 0;
     if (first) n_hits = __builtin_popcountll(ballot(hit));
     first = false;
@@ -897,25 +1047,25 @@ __device__ __forceinline__ int packet_index() {
   return uniform(logical * kWavesPerBlock + ((int)threadIdx.x >> 6));
 }
 
-template <bool FAST, bool DEEP, bool SPHERES>
+template <bool FAST, bool DEEP, bool SPHERES, int R>
 __global__ __launch_bounds__(kWavesPerBlock * 64) void trace_primary_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
-  const int sel = packet_index();
-  if (sel >= P.num_sel_tiles) return;
-  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * 3 * kDeepStack : nullptr;
-  primary_packet<FAST, DEEP, SPHERES>(P, nodes, prims, sel, spill);
+  const int sel0 = packet_index() * R;
+  if (sel0 >= P.num_sel_tiles) return;
+  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * (1 + 2 * R) * kDeepStack : nullptr;
+  primary_packet<FAST, DEEP, SPHERES, R>(P, nodes, prims, sel0, spill);
 }
 
-template <bool FAST, bool DEEP, bool SPHERES>
+template <bool FAST, bool DEEP, bool SPHERES, int R>
 __global__ __launch_bounds__(kWavesPerBlock * 64) void trace_shadow_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims,
     const DevLight* __restrict__ lights) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
-  const int sel = packet_index();
-  if (sel >= P.num_sel_tiles) return;
-  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * 3 * kDeepStack : nullptr;
-  shadow_packet<FAST, DEEP, SPHERES>(P, nodes, prims, lights, sel, spill);
+  const int sel0 = packet_index() * R;
+  if (sel0 >= P.num_sel_tiles) return;
+  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * (1 + 2 * R) * kDeepStack : nullptr;
+  shadow_packet<FAST, DEEP, SPHERES, R>(P, nodes, prims, lights, sel0, spill);
 }
 
 template <bool FAST, bool DEEP, bool SPHERES>
@@ -949,11 +1099,14 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
                        lights);
     return;
   }
-  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES>), dim3(blocks),
-                     dim3(kWavesPerBlock * 64), lds, stream, P, nodes, prims);
+  constexpr int R = kRaysPerLane;
+  const int tblocks = (P.num_sel_tiles + kWavesPerBlock * R - 1) / (kWavesPerBlock * R);
+  const size_t tlds = DEEP ? sizeof(int) * (1 + 2 * R) * kDeepStack * kWavesPerBlock : 0;
+  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, R>), dim3(tblocks),
+                     dim3(kWavesPerBlock * 64), tlds, stream, P, nodes, prims);
   if (P.num_lights > 0)
-    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES>), dim3(blocks),
-                       dim3(kWavesPerBlock * 64), lds, stream, P, nodes, prims, lights);
+    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, R>), dim3(tblocks),
+                       dim3(kWavesPerBlock * 64), tlds, stream, P, nodes, prims, lights);
   hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
                      prims, normals, mats, lights);
 }

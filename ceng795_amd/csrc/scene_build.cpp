@@ -272,6 +272,7 @@ void build_host_scene(const rt_scene_desc& d, HostScene& s) {
       const F3 a1 = v0 - v1, a2 = v0 - v2;
       const float rec[9] = {v0.x, v0.y, v0.z, a1.x, a1.y, a1.z, a2.x, a2.y, a2.z};
       std::memcpy(p.v0, rec, sizeof rec);
+      p.cx = a1.y * a2.z - a2.y * a1.z;  // c1.y*c2.z - c2.y*c1.z with c1 = a1, c2 = a2
     } else {
       std::memcpy(p.v0, ls.center, 12);
       p.a1[0] = ls.radius;
@@ -293,6 +294,12 @@ void build_host_scene(const rt_scene_desc& d, HostScene& s) {
     dst[3] = b.hi.x;
     dst[4] = b.hi.y;
     dst[5] = b.hi.z;
+  };
+  auto put_child_box = [](DevNode& n, int side, const Aabb& b) {
+    for (int a = 0; a < 3; a++) {
+      n.lo[a][side] = b.lo[a];
+      n.hi[a][side] = b.hi[a];
+    }
   };
   if (B.objs[root].kind != kObjBvh) {
     s.root_kind = B.objs[root].kind == kObjTri ? kRootTriangle : kRootSphere;
@@ -322,7 +329,7 @@ void build_host_scene(const rt_scene_desc& d, HostScene& s) {
       if (B.objs[child].kind == kObjBvh) {
         const int idx = (int)s.nodes.size();
         s.nodes.push_back(DevNode{});
-        put_box(side == 0 ? s.nodes[node].b0 : s.nodes[node].b1, B.objs[child].box);
+        put_child_box(s.nodes[node], side, B.objs[child].box);
         s.nodes[node].child[side] = idx;
         if (depth + 1 > s.depth) s.depth = depth + 1;
         st.push_back({child, idx, 0, depth + 1});  // invalidates f
@@ -357,9 +364,10 @@ std::string dump_bvh(const HostScene& s) {
   }
   struct Item {
     int ref;
-    const float* box;
+    float box[6];
   };
-  std::vector<Item> st{{0, s.root_box}};
+  std::vector<Item> st{{0, {s.root_box[0], s.root_box[1], s.root_box[2], s.root_box[3],
+                            s.root_box[4], s.root_box[5]}}};
   while (!st.empty()) {
     Item it = st.back();
     st.pop_back();
@@ -371,8 +379,9 @@ std::string dump_bvh(const HostScene& s) {
     for (int k = 0; k < 6; k++) os << " " << hex(it.box[k]);
     os << "\n";
     const DevNode& n = s.nodes[it.ref];
-    st.push_back({n.child[1], n.b1});
-    st.push_back({n.child[0], n.b0});
+    for (int side = 1; side >= 0; side--)
+      st.push_back({n.child[side], {n.lo[0][side], n.lo[1][side], n.lo[2][side], n.hi[0][side],
+                                    n.hi[1][side], n.hi[2][side]}});
   }
   return os.str();
 }

@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""A/B kernel timing on ONE box: each variant is a library build (lib/libceng795_rt_<v>.so,
+"" = the production build) timed by `tools/diag.py timing` in its own process; rounds are
+interleaved (A B C A B C ...) so device clock drift hits every variant alike.
+
+    python tools/ab.py base,nocx --rounds 3
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--workload", default="c3")
+    a = ap.parse_args()
+    res = defaultdict(lambda: defaultdict(list))
+    for _ in range(a.rounds):
+        for v in a.variants.split(","):
+            env = dict(os.environ)
+            env["CENG795_LIB"] = "" if v == "base" else v
+            out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "diag.py"), "timing",
+                                  "--workload", a.workload], env=env, capture_output=True,
+                                 text=True, timeout=300)
+            if out.returncode:
+                print(out.stderr[-2000:], file=sys.stderr)
+                sys.exit(1)
+            for k, t in json.loads(out.stdout).items():
+                res[v][k].append(t["median_ms"])
+    summary = {v: {k: round(sorted(x)[len(x) // 2], 4) for k, x in d.items()} for v, d in res.items()}
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()
