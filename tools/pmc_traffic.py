@@ -18,18 +18,27 @@ import json
 import os
 from collections import defaultdict
 
-KERNEL = "render_kernel"
+# the per-frame render step: every kernel of one rt_render_device call
+KERNELS = ("trace_primary_kernel", "trace_shadow_kernel", "shade_kernel", "recursive_kernel",
+           "render_kernel")
+FRAME_KERNEL = ("trace_primary_kernel", "recursive_kernel", "render_kernel")
 
 
 def per_launch(directory):
+    """Counter totals of the render kernels divided by the number of frames (one
+    trace_primary dispatch per frame): bytes per render step."""
     files = glob.glob(os.path.join(directory, "**", "*counter_collection.csv"), recursive=True)
-    vals = defaultdict(list)
+    vals = defaultdict(float)
+    frames = defaultdict(int)
     for path in files:
         with open(path) as f:
             for row in csv.DictReader(f):
-                if KERNEL in row["Kernel_Name"]:
-                    vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+                name = row["Kernel_Name"]
+                if any(k in name for k in KERNELS):
+                    vals[row["Counter_Name"]] += float(row["Counter_Value"])
+                if any(k in name for k in FRAME_KERNEL):
+                    frames[row["Counter_Name"]] += 1
+    return ({k: v / max(1, frames[k]) for k, v in vals.items()}, dict(frames))
 
 
 def main():
@@ -44,10 +53,10 @@ def main():
     fetch, nf = per_launch(a.fetch_dir)
     write, nw = per_launch(a.write_dir)
     out = {
-        "kernel": KERNEL,
+        "kernels": list(KERNELS),
         "workload": a.workload,
         "round": a.round,
-        "launches": {"fetch_pass": nf.get("FETCH_SIZE", 0), "write_pass": nw.get("WRITE_SIZE", 0)},
+        "frames": {"fetch_pass": nf.get("FETCH_SIZE", 0), "write_pass": nw.get("WRITE_SIZE", 0)},
         "fetch_size_kib_raw": fetch["FETCH_SIZE"],
         "write_size_kib": write["WRITE_SIZE"],
         "read_bytes_raw": fetch["FETCH_SIZE"] * 1024,
