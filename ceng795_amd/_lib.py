@@ -81,6 +81,7 @@ SIGNATURES = {
     "rt_scene_dump_bvh": (C.c_int, [C.c_void_p, C.c_char_p]),
     "rt_scene_bvh_depth": (C.c_int, [C.c_void_p]),
     "rt_set_traversal": (C.c_int, [C.c_void_p, C.c_int]),
+    "rt_set_msaa_seed": (C.c_int, [C.c_void_p, C.c_ulonglong]),
     "rt_render": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                             C.POINTER(rt_stats)]),
     "rt_render_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -118,6 +119,9 @@ def _share_torch_hip_runtime() -> None:
         pass
 
 
+ABI_VERSION = 2  # CENG795_RT_ABI_VERSION of include/ceng795_rt.h
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
@@ -131,6 +135,9 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if L.rt_abi_version() != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH}: C ABI version {L.rt_abi_version()}, this binding "
+                              f"expects {ABI_VERSION} (rebuild the library)")
         _lib = L
     return _lib
 

@@ -20,6 +20,7 @@ hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevP
                          const float* normals, const DevMaterial* mats, const DevLight* lights,
                          bool fast, bool deep, bool spheres, hipStream_t stream);
 int max_supported_depth();
+hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream);
 unsigned long long read_reset_exact_fallbacks();
 bool diag_build();
 void write_png(const std::string& path, const float* rgb, int w, int h);
@@ -45,6 +46,9 @@ struct rt_scene {
   float* d_frames = nullptr; // rt_render_device's ray-tree frames (recursive scenes)
   size_t frames_capacity = 0;
   size_t hits_capacity = 0;  // records
+  float* d_samples = nullptr;  // MSAA per-sample colours [s][h][w][3]
+  size_t samples_capacity = 0;
+  unsigned long long msaa_seed = 0;
 };
 
 namespace {
@@ -107,6 +111,7 @@ void free_device(rt_scene* s) {
   (void)hipFree(s->d_hits);
   (void)hipFree(s->d_occ);
   (void)hipFree(s->d_frames);
+  (void)hipFree(s->d_samples);
   if (cur != s->device) (void)hipSetDevice(cur);
 }
 
@@ -226,8 +231,60 @@ void check_render_args(const rt_scene* s, int cam, int row0, int row_stride) {
   if (cam < 0 || cam >= (int)s->host.cameras.size())
     throw std::invalid_argument("camera index out of range");
   if (row0 < 0 || row_stride < 1) throw std::invalid_argument("bad row selection");
-  if (s->host.cameras[cam].num_samples != 1)
-    throw std::domain_error("NumSamples > 1 (jittered MSAA, HW2/Scene.cpp:32-69) is not supported yet");
+  // MSAA splats every sample into the 3x3 neighbourhood (HW2/Scene.cpp:48-62), so a row subset
+  // is not a self-contained piece of the image: only whole frames are rendered.
+  if (s->host.cameras[cam].num_samples > 1 && (row0 != 0 || row_stride != 1))
+    throw std::domain_error("NumSamples > 1 renders whole frames only (starting_row 0, stride 1)");
+}
+
+unsigned powmod_minstd(unsigned a, unsigned e) {
+  unsigned long long r = 1, b = a;
+  while (e) {
+    if (e & 1) r = r * b % kMinstdM;
+    b = b * b % kMinstdM;
+    e >>= 1;
+  }
+  return (unsigned)r;
+}
+
+// One frame of camera `cam` into d_out.  Pixel-centre cameras: the render kernels write
+// d_out directly.  MSAA cameras (HW2/Scene.cpp:32-69): one render pass per sample index into
+// d_samples[s], then the resolve kernel's splat + colour / weight into d_out (row-major).
+void enqueue_frame(rt_scene* s, const RenderParams& P, int samples, float* d_samples,
+                   hipStream_t stream) {
+  const bool fast = s->mode == RT_TRAVERSAL_FAST;
+  if (samples <= 1) {
+    hip_check(launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
+                            fast, s->deep, s->has_spheres, stream),
+              "render launch");
+    return;
+  }
+  const size_t frame = (size_t)P.width * P.height * 3;
+  for (int k = 0; k < samples * samples; k++) {
+    RenderParams Q = P;
+    Q.msaa_n = samples;
+    Q.msaa_s = k;
+    Q.msaa_mul[0] = powmod_minstd(kMinstdA, 2 * k + 1);
+    Q.msaa_mul[1] = powmod_minstd(kMinstdA, 2 * k + 2);
+    Q.msaa_seed = s->msaa_seed;
+    Q.tile_major = 0;
+    Q.out = d_samples + (size_t)k * frame;
+    hip_check(launch_render(Q, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
+                            fast, s->deep, s->has_spheres, stream),
+              "render launch");
+  }
+  MsaaResolveParams M;
+  M.samples = d_samples;
+  M.out = P.out;
+  M.width = P.width;
+  M.height = P.height;
+  M.n = samples;
+  M.seed = s->msaa_seed;
+  hip_check(launch_msaa_resolve(M, stream), "msaa resolve launch");
+}
+
+size_t sample_floats(const rt_camera& c) {
+  return c.num_samples > 1 ? (size_t)c.num_samples * c.num_samples * c.width * c.height * 3 : 0;
 }
 
 }  // namespace
@@ -339,6 +396,12 @@ int rt_set_traversal(rt_scene* s, int mode) {
   return RT_OK;
 }
 
+int rt_set_msaa_seed(rt_scene* s, unsigned long long seed) {
+  if (!s) return set_error(RT_E_INVALID, "rt_set_msaa_seed: NULL scene");
+  s->msaa_seed = seed;
+  return RT_OK;
+}
+
 int rt_num_tiles(const rt_scene* s, int cam, int row0, int row_stride) {
   if (!s || cam < 0 || cam >= (int)s->host.cameras.size() || row0 < 0 || row_stride < 1)
     return set_error(RT_E_INVALID, "rt_num_tiles: bad argument");
@@ -365,9 +428,20 @@ int rt_render_device(rt_scene* s, int cam, int row0, int row_stride, int tile_be
         }
         P.frames = s->d_frames;
       }
-      hip_check(launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
-                              s->mode == RT_TRAVERSAL_FAST, s->deep, s->has_spheres, (hipStream_t)stream),
-                "render launch");
+      const rt_camera& c = s->host.cameras[cam];
+      if (c.num_samples > 1) {
+        if (tile_begin != 0 || tile_step != 1 || tile_major)
+          throw std::domain_error("NumSamples > 1 renders whole row-major frames only");
+        const size_t need = sample_floats(c);
+        if (need > s->samples_capacity) {
+          (void)hipFree(s->d_samples);
+          s->d_samples = nullptr;
+          s->samples_capacity = 0;
+          hip_check(hipMalloc(&s->d_samples, need * sizeof(float)), "alloc MSAA samples");
+          s->samples_capacity = need;
+        }
+      }
+      enqueue_frame(s, P, c.num_samples, s->d_samples, (hipStream_t)stream);
       return RT_OK;
   });
 }
@@ -422,6 +496,7 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
       int2_t* d_hits = nullptr;
       unsigned* d_occ = nullptr;
       float* d_frames = nullptr;
+      float* d_samples = nullptr;
       hipStream_t stream = nullptr;
       hipEvent_t e0 = nullptr, e1 = nullptr;
       auto cleanup = [&] {
@@ -429,6 +504,7 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
         if (d_hits) (void)hipFree(d_hits);
         if (d_occ) (void)hipFree(d_occ);
         if (d_frames) (void)hipFree(d_frames);
+        if (d_samples) (void)hipFree(d_samples);
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         if (stream) (void)hipStreamDestroy(stream);
@@ -457,12 +533,14 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
                     "alloc ray-tree frames");
           P.frames = d_frames;
         }
+        if (c.num_samples > 1)
+          hip_check(hipMalloc(&d_samples, sample_floats(c) * sizeof(float)), "alloc MSAA samples");
         hip_check(hipEventRecord(e0, stream), "event record");
-        hipError_t le = launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats,
-                                      s->d_lights, s->mode == RT_TRAVERSAL_FAST, s->deep, s->has_spheres, stream);
-        if (le != hipSuccess) {
+        try {
+          enqueue_frame(s, P, c.num_samples, d_samples, stream);
+        } catch (...) {
           (void)hipFree(d_cnt);
-          hip_check(le, "render launch");
+          throw;
         }
         hip_check(hipEventRecord(e1, stream), "event record");
         // rows j = row0 + k*row_stride only: a strided 2D copy leaves the others untouched

@@ -74,6 +74,17 @@ struct alignas(8) int2_t {
 
 enum RootKind : int32_t { kRootNode = 0, kRootTriangle = 1, kRootSphere = 2 };
 
+constexpr unsigned kMinstdM = 2147483647u;  // minstd_rand0 modulus (std::default_random_engine)
+constexpr unsigned kMinstdA = 16807u;
+
+// Resolve of the Gaussian MSAA splat: samples[s][h][w][3] -> out[h][w][3] = color / weight.
+struct MsaaResolveParams {
+  const float* samples;
+  float* out;
+  int width, height, n;
+  unsigned long long seed;
+};
+
 struct RenderParams {
   const DevNode* nodes;
   const DevPrim* prims;
@@ -96,6 +107,12 @@ struct RenderParams {
   // tiles over (rows x width), row-major; this launch does tile_begin + i*tile_step
   int tiles_x, tiles_total, tile_begin, tile_step, num_sel_tiles;
   int tile_major;
+  // jittered MSAA (HW2/Scene.cpp:32-69): 0 = pixel centres; else this launch traces sample
+  // msaa_s = x*n + y of every pixel, whose minstd_rand0 draws 2s+1, 2s+2 are
+  // u0 * msaa_mul[0], u0 * msaa_mul[1] (mod 2^31-1), u0 the pixel's seeded state.
+  int msaa_n, msaa_s;
+  unsigned msaa_mul[2];
+  unsigned long long msaa_seed;
   float* out;
   int2_t* hits;   // num_sel_tiles * 64 records {t bits, leaf}: trace_primary -> shadow, shade
   unsigned* occ;  // num_sel_tiles * 64 * occ_words light-occlusion bits: trace_shadow -> shade

@@ -570,9 +570,57 @@ __device__ __forceinline__ PacketPixel packet_pixel(const RenderParams& P, int s
   return q;
 }
 
+// ------------------------------------------------------------------ MSAA sample positions
+// HW2/Scene.cpp:35-44: a std::default_random_engine (libstdc++ minstd_rand0, x <- 16807 x mod
+// 2^31-1) per pixel, seeded here with splitmix64(seed, pixel) instead of the wall clock, and
+// uniform_real_distribution<float>(0, 1) = generate_canonical<float, 24>: one draw u,
+// float(u - 1) / 2^31, clamped below 1.  Sample s = x*n + y uses draws 2s+1 and 2s+2.
+__device__ __forceinline__ unsigned long long msaa_pixel_seed(unsigned long long base,
+                                                              unsigned long long pixel) {
+  unsigned long long z = base + 0x9E3779B97F4A7C15ull * (pixel + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ unsigned minstd_state0(unsigned long long seed) {
+  const unsigned x = (unsigned)(seed % kMinstdM);
+  return x == 0 ? 1u : x;
+}
+
+__device__ __forceinline__ unsigned minstd_mulmod(unsigned a, unsigned b) {
+  unsigned long long p = (unsigned long long)a * b;  // < 2^62; 2^31 = 1 (mod 2^31-1)
+  p = (p & kMinstdM) + (p >> 31);
+  p = (p & kMinstdM) + (p >> 31);
+  return (unsigned)(p >= kMinstdM ? p - kMinstdM : p);
+}
+
+__device__ __forceinline__ float minstd_uniform01(unsigned u) {
+  float r = (float)(u - 1u) / 2147483648.0f;  // exact: power-of-two divisor
+  return r >= 1.0f ? __uint_as_float(0x3f7fffffu) : r;
+}
+
+// sample_x, sample_y of HW2/Scene.cpp:43-44 for sample index s of pixel (px, py)
+__device__ __forceinline__ void msaa_offsets(const RenderParams& P, int px, int py, float& sx,
+                                             float& sy) {
+  const unsigned u0 = minstd_state0(
+      msaa_pixel_seed(P.msaa_seed, (unsigned long long)py * (unsigned)P.width + (unsigned)px));
+  const float n = (float)P.msaa_n;
+  sx = ((float)(P.msaa_s / P.msaa_n) + minstd_uniform01(minstd_mulmod(u0, P.msaa_mul[0]))) / n;
+  sy = ((float)(P.msaa_s % P.msaa_n) + minstd_uniform01(minstd_mulmod(u0, P.msaa_mul[1]))) / n;
+}
+
 // Camera::calculate_ray_at (HW2/Camera.h:30-35); x + 0.5 is exact in fp32 for x < 2^23.
+// MSAA passes x = i + sample_x - 0.5 (a double narrowed to the float parameter) and the
+// camera widens it again for x + 0.5 before the float multiply.
 __device__ __forceinline__ V3 primary_dir(const RenderParams& P, int px, int py) {
-  const float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+  float fx = (float)px + 0.5f, fy = (float)py + 0.5f;
+  if (P.msaa_n) {
+    float sx, sy;
+    msaa_offsets(P, px, py, sx, sy);
+    fx = (float)((double)(float)((double)((float)px + sx) - 0.5) + 0.5);
+    fy = (float)((double)(float)((double)((float)py + sy) - 0.5) + 0.5);
+  }
   const V3 s = (ld3(P.cam_tl) + ld3(P.cam_su) * fx) - ld3(P.cam_sv) * fy;
   return normalize(s - ld3(P.cam_e));
 }
@@ -1109,6 +1157,60 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
                        dim3(kWavesPerBlock * 64), tlds, stream, P, nodes, prims, lights);
   hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
                      prims, normals, mats, lights);
+}
+
+// Gaussian splat of HW2/Scene.cpp:46-62 turned inside out: one thread per destination pixel
+// gathers every contribution the reference adds to it, in the order a single-threaded
+// render_image adds them (source rows, source columns, samples x-major), so the fp32 sums of
+// Pixel::add_color are reproduced exactly; then Pixel::get_color's color / weight.
+__device__ __forceinline__ float gaussian_filter(float x, float y, float sigma) {
+  // HW2/Scene.cpp:12-14: double exp of a float argument, double division, narrowed
+  return (float)(exp((double)(-(x * x + y * y) / (2 * sigma * sigma))) /
+                 (2 * M_PI * (double)sigma));
+}
+
+__global__ __launch_bounds__(256) void msaa_resolve_kernel(MsaaResolveParams M) {
+  const int ai = (int)(blockIdx.x * 16 + (threadIdx.x & 15));
+  const int aj = (int)(blockIdx.y * 16 + (threadIdx.x >> 4));
+  if (ai >= M.width || aj >= M.height) return;
+  const int n = M.n, S = n * n;
+  const size_t frame = (size_t)M.width * M.height * 3;
+  float cr = 0.0f, cg = 0.0f, cb = 0.0f, wsum = 0.0f;
+  for (int j = aj - 1; j < aj + 2; j++) {
+    if (j < 0 || j >= M.height) continue;
+    for (int i = ai - 1; i < ai + 2; i++) {
+      if (i < 0 || i >= M.width) continue;
+      unsigned u = minstd_state0(
+          msaa_pixel_seed(M.seed, (unsigned long long)j * (unsigned)M.width + (unsigned)i));
+      const float* src = M.samples + 3 * ((size_t)j * M.width + i);
+      for (int k = 0; k < S; k++) {
+        u = minstd_mulmod(u, kMinstdA);
+        const float ex = minstd_uniform01(u);
+        u = minstd_mulmod(u, kMinstdA);
+        const float ey = minstd_uniform01(u);
+        const float sample_x = ((float)(k / n) + ex) / (float)n;
+        const float sample_y = ((float)(k % n) + ey) / (float)n;
+        const float s_x = ((float)i + sample_x) - ((float)ai + 0.5f);
+        const float s_y = ((float)j + sample_y) - ((float)aj + 0.5f);
+        const float w = gaussian_filter(s_x, s_y, 1.0f / 3.0f);
+        const float* c = src + (size_t)k * frame;
+        cr = cr + c[0] * w;
+        cg = cg + c[1] * w;
+        cb = cb + c[2] * w;
+        wsum = wsum + w;
+      }
+    }
+  }
+  float* o = M.out + 3 * ((size_t)aj * M.width + ai);
+  o[0] = cr / wsum;
+  o[1] = cg / wsum;
+  o[2] = cb / wsum;
+}
+
+hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream) {
+  const dim3 grid((M.width + 15) / 16, (M.height + 15) / 16);
+  hipLaunchKernelGGL(msaa_resolve_kernel, grid, dim3(256), 0, stream, M);
+  return hipGetLastError();
 }
 
 int max_supported_depth() { return kDeepStack; }

@@ -91,6 +91,10 @@ class Scene:
         m = {"fast": _lib.RT_TRAVERSAL_FAST, "reference": _lib.RT_TRAVERSAL_REFERENCE}[mode]
         check(lib().rt_set_traversal(self._h, m))
 
+    def set_msaa_seed(self, seed: int) -> None:
+        """Seed of the per-pixel MSAA generators (the reference uses the wall clock)."""
+        check(lib().rt_set_msaa_seed(self._h, int(seed)))
+
     def dump_bvh(self, path: str) -> None:
         check(lib().rt_scene_dump_bvh(self._h, str(path).encode()))
 
@@ -101,7 +105,9 @@ class Scene:
 
     def render_image(self, camera_index: int, result: Optional[np.ndarray] = None,
                      starting_row: int = 0, height_increase: int = 1):
-        """Scene::render_image (HW2/Scene.h:34-35).  Returns (result, rt_stats)."""
+        """Scene::render_image (HW2/Scene.h:34-35).  Returns (result, rt_stats).
+
+        NumSamples > 1: whole frames only; result is Pixel::color / Pixel::weight."""
         if result is None:
             result = self.new_image(camera_index)
         c = self.camera(camera_index)

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define CENG795_RT_ABI_VERSION 1
+#define CENG795_RT_ABI_VERSION 2  /* 2: MSAA cameras + rt_set_msaa_seed */
 
 enum {
   RT_OK = 0,
@@ -141,7 +141,15 @@ int rt_set_traversal(rt_scene* scene, int mode);
  * (HW2/Scene.cpp:24-31).  Writes fp32 RGB radiance — exactly Pixel::color after the
  * reference's add_color(color, 1) — for rows j = starting_row + k*row_stride into
  * out_rgb[3*(j*width + i)] (w*h*3 floats, row-major, top row first).  Other rows are left
- * untouched.  Synchronous; safe to call concurrently on one scene from several threads. */
+ * untouched.  Synchronous; safe to call concurrently on one scene from several threads.
+ *
+ * NumSamples > 1 (jittered MSAA + 3x3 Gaussian splat, HW2/Scene.cpp:32-69): whole frames
+ * only (starting_row 0, row_stride 1, else RT_E_UNSUPPORTED).  out_rgb is then
+ * Pixel::color / Pixel::weight, the value Pixel::get_color truncates (HW2/Pixel.h:17-27),
+ * with the splat summed in the single-threaded reference order.  The reference seeds each
+ * pixel's std::default_random_engine from the wall clock; here it is seeded with
+ * splitmix64(msaa_seed, j*width + i) (rt_set_msaa_seed, default 0), so frames are
+ * reproducible.  rt_stats counts every sample's rays. */
 int rt_render(rt_scene* scene, int camera_index, int starting_row, int row_stride,
               float* out_rgb, rt_stats* stats);
 
@@ -151,12 +159,16 @@ int rt_render(rt_scene* scene, int camera_index, int starting_row, int row_strid
  *   tile_major == 0: d_out is a full w*h*3 frame, written in place;
  *   tile_major == 1: d_out holds the selected tiles back to back, 8*8*3 floats each
  *                    (pixels outside the image are written as 0).
+ * MSAA cameras: only the whole frame, row-major (tile_begin 0, tile_step 1, tile_major 0).
  * Asynchronous on `hip_stream` (a hipStream_t, NULL = default stream).  stats may be NULL;
  * when given, ray counts are filled after the caller synchronises the stream and calls
  * rt_collect_stats. */
 int rt_render_device(rt_scene* scene, int camera_index, int starting_row, int row_stride,
                      int tile_begin, int tile_step, int tile_major, float* d_out,
                      void* hip_stream);
+/* Seed of the per-pixel MSAA generators (see rt_render).  Replaces the reference's
+ * system_clock seed (HW2/Scene.cpp:36-37) to make MSAA frames deterministic. */
+int rt_set_msaa_seed(rt_scene* scene, unsigned long long seed);
 int rt_num_tiles(const rt_scene* scene, int camera_index, int starting_row, int row_stride);
 /* Reads (and resets) the device ray counters accumulated by rt_render_device calls. */
 int rt_collect_stats(rt_scene* scene, rt_stats* stats);

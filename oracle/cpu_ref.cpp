@@ -10,6 +10,7 @@
 #include "cpu_ref.h"
 
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -303,6 +304,15 @@ struct Scene {
 
   // Camera::calculate_ray_at (HW2/Camera.h:30-35): (x + 0.5) is a double add, narrowed back
   // to float by Vector3 operator*(float, const Vector3&).
+  // calculate_ray_at(float x, float y) for an MSAA sample: the caller passes
+  // i + sample_x - 0.5 (a double narrowed to the float parameter, HW2/Scene.cpp:47-48).
+  Ray primary_f(const Camera& c, float x, float y) const {
+    const float fx = (float)((double)x + 0.5);
+    const float fy = (float)((double)y + 0.5);
+    const V3 s = sub(add(c.top_left, muls(c.s_u, fx)), muls(c.s_v, fy));
+    return Ray{c.e, normalize(sub(s, c.e)), false};
+  }
+
   Ray primary(const Camera& c, int x, int y) const {
     const float fx = (float)((double)(float)x + 0.5);
     const float fy = (float)((double)(float)y + 0.5);
@@ -711,6 +721,43 @@ void dump(const Scene& sc, int id, FILE* f) {
 
 }  // namespace
 
+// ------------------------------------------------------------------ MSAA (HW2/Scene.cpp:32-69)
+// std::default_random_engine is libstdc++'s minstd_rand0 (x <- 16807 x mod 2^31-1); the
+// reference seeds it per pixel from system_clock (non-deterministic), we from msaa_seed().
+// uniform_real_distribution<float>(0, 1) = generate_canonical<float, 24> with one draw:
+// float(u - 1) / float(2147483646.0L) (= 2^31), clamped below 1.
+constexpr uint64_t kMinstdM = 2147483647ull;
+
+uint64_t msaa_seed(uint64_t base, uint64_t pixel) {  // splitmix64 of (base, pixel)
+  uint64_t z = base + 0x9E3779B97F4A7C15ull * (pixel + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+struct Minstd {
+  uint64_t x;
+  explicit Minstd(uint64_t seed) {
+    x = seed % kMinstdM;
+    if (x == 0) x = 1;
+  }
+  uint64_t next() {
+    x = (x * 16807ull) % kMinstdM;
+    return x;
+  }
+  float uniform01() {
+    const float sum = (float)(next() - 1) * 1.0f;
+    const float tmp = (float)(1.0L * (2147483646.0L));
+    float r = sum / tmp;
+    if (r >= 1.0f) r = std::nextafter(1.0f, 0.0f);
+    return r * (1.0f - 0.0f) + 0.0f;
+  }
+};
+
+inline float gaussian_filter(float x, float y, float sigma) {  // HW2/Scene.cpp:12-14
+  return (float)(::exp((double)(-(x * x + y * y) / (2 * sigma * sigma))) / (2 * M_PI * sigma));
+}
+
 struct cpuref_scene {
   Scene sc;
 };
@@ -749,7 +796,7 @@ int cpuref_render(const cpuref_scene* s, int cam, int starting_row, int row_stri
     return -1;
   const Scene& sc = s->sc;
   const Camera& c = sc.cameras[cam];
-  if (c.samples != 1) return -2;
+  if (c.samples != 1) return -2;  // MSAA: cpuref_render_msaa
   if (threads < 1) threads = 1;
   if (c.height < threads) threads = 1;
   std::vector<cpuref_stats> st(threads);
@@ -791,6 +838,101 @@ int cpuref_render(const cpuref_scene* s, int cam, int starting_row, int row_stri
     }
   }
   return 0;
+}
+
+int cpuref_render_msaa(const cpuref_scene* s, int cam, unsigned long long seed, int threads,
+                       float* out, cpuref_stats* stats) {
+  if (cam < 0 || cam >= (int)s->sc.cameras.size()) return -1;
+  const Scene& sc = s->sc;
+  const Camera& c = sc.cameras[cam];
+  const int n = c.samples, W = c.width, H = c.height, S = n * n;
+  if (threads < 1) threads = 1;
+  // phase 1: every sample's colour (order-free), phase 2: the splat in the single-threaded
+  // reference order (source rows, source columns, samples x-major; neighbours j-1..j+1,
+  // i-1..i+1), so the per-pixel float sums are deterministic.
+  std::vector<float> col((size_t)W * H * S * 3), sx((size_t)W * H * S), sy((size_t)W * H * S);
+  std::vector<cpuref_stats> st(threads);
+  std::vector<Counters> ctr(threads * 3);
+  auto work = [&](int ti) {
+    cpuref_stats& St = st[ti];
+    std::memset(&St, 0, sizeof St);
+    Counters* C = &ctr[ti * 3];
+    for (int j = ti; j < H; j += threads)
+      for (int i = 0; i < W; i++) {
+        const size_t pix = (size_t)j * W + i;
+        Minstd gen(msaa_seed(seed, pix));
+        for (int x = 0; x < n; x++)
+          for (int y = 0; y < n; y++) {
+            const float ex = gen.uniform01();
+            const float ey = gen.uniform01();
+            const float smx = (x + ex) / n;
+            const float smy = (y + ey) / n;
+            const V3 color = sc.trace(sc.primary_f(c, (float)((double)(i + smx) - 0.5),
+                                                   (float)((double)(j + smy) - 0.5)),
+                                      sc.max_depth, C, &St);
+            St.primary_rays++;
+            const size_t k = pix * S + (size_t)(x * n + y);
+            col[3 * k] = color.x;
+            col[3 * k + 1] = color.y;
+            col[3 * k + 2] = color.z;
+            sx[k] = smx;
+            sy[k] = smy;
+          }
+      }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; t++) pool.emplace_back(work, t);
+  for (auto& t : pool) t.join();
+  std::vector<float> acc((size_t)W * H * 3, 0.0f), wsum((size_t)W * H, 0.0f);
+  for (int j = 0; j < H; j++)
+    for (int i = 0; i < W; i++)
+      for (int k = 0; k < S; k++) {
+        const size_t src = ((size_t)j * W + i) * S + k;
+        const V3 color{col[3 * src], col[3 * src + 1], col[3 * src + 2]};
+        for (int aj = j - 1; aj < j + 2; aj++) {
+          if (aj < 0 || aj >= H) continue;
+          for (int ai = i - 1; ai < i + 2; ai++) {
+            if (ai < 0 || ai >= W) continue;
+            const float dx = (i + sx[src]) - (ai + 0.5f);
+            const float dy = (j + sy[src]) - (aj + 0.5f);
+            const float w = gaussian_filter(dx, dy, 1.0f / 3.0f);
+            float* a = &acc[3 * ((size_t)aj * W + ai)];  // Pixel::add_color(color, w)
+            const V3 cw = muls(color, w);
+            a[0] += cw.x;
+            a[1] += cw.y;
+            a[2] += cw.z;
+            wsum[(size_t)aj * W + ai] += w;
+          }
+        }
+      }
+  for (size_t p = 0; p < (size_t)W * H; p++) {  // Pixel::get_color: color / weight
+    out[3 * p] = acc[3 * p] / wsum[p];
+    out[3 * p + 1] = acc[3 * p + 1] / wsum[p];
+    out[3 * p + 2] = acc[3 * p + 2] / wsum[p];
+  }
+  if (stats) {
+    std::memset(stats, 0, sizeof *stats);
+    for (int t = 0; t < threads; t++) {
+      stats->primary_rays += st[t].primary_rays;
+      stats->shadow_rays += st[t].shadow_rays;
+      stats->secondary_rays += st[t].secondary_rays;
+      stats->primary_hits += st[t].primary_hits;
+      for (int k = 0; k < 3; k++) {
+        stats->box_tests[k] += ctr[t * 3 + k].box;
+        stats->prim_tests[k] += ctr[t * 3 + k].prim;
+      }
+    }
+  }
+  return 0;
+}
+
+void cpuref_minstd_uniform(unsigned long long seed, int count, float* out) {
+  Minstd g(seed);
+  for (int k = 0; k < count; k++) out[k] = g.uniform01();
+}
+
+unsigned long long cpuref_msaa_seed(unsigned long long base, unsigned long long pixel) {
+  return msaa_seed(base, pixel);
 }
 
 int cpuref_dump_bvh(const cpuref_scene* s, const char* path) {

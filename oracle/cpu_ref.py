@@ -42,10 +42,23 @@ def lib():
                                          C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.cpuref_render.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.c_void_p, C.POINTER(Stats)]
+        L.cpuref_render_msaa.argtypes = [C.c_void_p, C.c_int, C.c_ulonglong, C.c_int,
+                                         C.c_void_p, C.POINTER(Stats)]
+        L.cpuref_minstd_uniform.argtypes = [C.c_ulonglong, C.c_int, C.c_void_p]
+        L.cpuref_msaa_seed.argtypes = [C.c_ulonglong, C.c_ulonglong]
+        L.cpuref_msaa_seed.restype = C.c_ulonglong
         L.cpuref_dump_bvh.argtypes = [C.c_void_p, C.c_char_p]
         L.cpuref_primary_records.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         _LIB = L
     return _LIB
+
+
+def minstd_uniform(seed: int, count: int) -> np.ndarray:
+    """The oracle's restatement of uniform_real_distribution<float>(0,1) over
+    std::default_random_engine(seed) (libstdc++)."""
+    out = np.zeros(count, np.float32)
+    lib().cpuref_minstd_uniform(seed, count, out.ctypes.data)
+    return out
 
 
 @dataclass
@@ -103,6 +116,16 @@ class OracleScene:
                                  out.ctypes.data, C.byref(st))
         if rc:
             raise RuntimeError(f"cpuref_render failed ({rc})")
+        return out, st
+
+    def render_msaa(self, cam: int = 0, seed: int = 0, threads: int = 0):
+        info = self.camera(cam)
+        out = np.zeros((info.height, info.width, 3), np.float32)
+        st = Stats()
+        rc = lib().cpuref_render_msaa(self._h, cam, seed, threads or (os.cpu_count() or 1),
+                                      out.ctypes.data, C.byref(st))
+        if rc:
+            raise RuntimeError(f"cpuref_render_msaa failed ({rc})")
         return out, st
 
     def dump_bvh(self, path: str):

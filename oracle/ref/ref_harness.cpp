@@ -12,6 +12,8 @@
 //
 // Commands:
 //   render <xml> <cam> <out.f32> [threads]          float RGB, w*h*3, row-major, top row first
+//   resolved <xml> <cam> <out.f32> [threads]        Pixel::color / Pixel::weight (what
+//                                                   get_color truncates; MSAA cameras)
 //   bvh    <xml> <out.txt>                          preorder BVH topology, floats as hex bits
 //   rays   <xml> <cam> <out.bin>                    per-pixel primary hit: t, normal (hex) + hit flag
 //   time   <xml> <cam> <threads> <reps> <row_step>  median wall time of render_image over rows
@@ -104,7 +106,7 @@ int main(int argc, char** argv) {
   }
   const std::string cmd = argv[1];
   Scene scene(argv[2]);
-  if (cmd == "render") {
+  if (cmd == "render" || cmd == "resolved") {
     const int cam = std::atoi(argv[3]);
     const int threads = argc > 5 ? std::atoi(argv[5]) : (int)std::thread::hardware_concurrency();
     const Image_plane& ip = scene.cameras[cam].get_image_plane();
@@ -113,9 +115,10 @@ int main(int argc, char** argv) {
     render_rows(scene, cam, px, 0, 1, threads);
     std::vector<float> out((size_t)w * h * 3);
     for (size_t i = 0; i < (size_t)w * h; i++) {
-      out[3 * i + 0] = px[i].color.x;
-      out[3 * i + 1] = px[i].color.y;
-      out[3 * i + 2] = px[i].color.z;
+      const float w = cmd == "resolved" ? px[i].weight : 1.0f;
+      out[3 * i + 0] = cmd == "resolved" ? px[i].color.x / w : px[i].color.x;
+      out[3 * i + 1] = cmd == "resolved" ? px[i].color.y / w : px[i].color.y;
+      out[3 * i + 2] = cmd == "resolved" ? px[i].color.z / w : px[i].color.z;
     }
     std::ofstream f(argv[4], std::ios::binary);
     f.write(reinterpret_cast<const char*>(out.data()), out.size() * sizeof(float));

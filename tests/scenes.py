@@ -41,12 +41,22 @@ RECURSIVE = {
                     "mirrors only"),
 }
 
+# Cameras with NumSamples > 1: jittered MSAA + Gaussian 3x3 splat.
+MSAA = {
+    "msaa4": (lambda: G.soup_scene(8, 48, 40, num_samples=4), "n = 2, depth 0"),
+    "msaa5": (lambda: G.soup_scene(9, 33, 27, num_samples=5),
+              "NumSamples 5 -> n = (int)sqrt(5) = 2; ragged tiles"),
+    "msaa9_depth2": (lambda: G.soup_scene(10, 40, 32, depth=2, mirror=True, glass=True,
+                                          num_samples=9), "n = 3 with mirror + dielectric"),
+    "msaa16": (lambda: G.soup_scene(11, 32, 24, num_samples=16), "n = 4"),
+}
+
 SMALL = ["c1", "hf_small", "hf_side", "soup1", "soup2", "soup3", "single_sphere",
          "single_triangle"]
 
 
 def write(name: str, directory: str) -> str:
-    table = {**CATALOGUE, **RECURSIVE}
+    table = {**CATALOGUE, **RECURSIVE, **MSAA}
     path = os.path.join(directory, f"{name}.xml")
     if not os.path.exists(path):
         text = table[name][0]().to_xml()

@@ -36,7 +36,7 @@ def test_library_exports_every_declared_function():
     for n in names:
         assert hasattr(L, n), n
         assert n in _lib.SIGNATURES, f"{n} missing from the ctypes table"
-    assert L.rt_abi_version() == 1
+    assert L.rt_abi_version() == 2
 
 
 def test_oracle_is_not_linked_into_the_product():
