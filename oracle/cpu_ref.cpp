@@ -8,6 +8,7 @@
 // islands of libm (pow, exp, log, sqrt) exactly where the reference calls the double
 // overloads.
 #include "cpu_ref.h"
+#include "xml_lite.h"
 
 #include <cmath>
 #include <cstdint>
@@ -23,6 +24,8 @@
 #include <vector>
 
 namespace {
+using oracle_xml::Elem;
+using oracle_xml::XmlParser;
 
 constexpr float kEps = 0.000001f;  // HW2/Vector3.h:7
 constexpr float kInf = std::numeric_limits<float>::infinity();
@@ -366,137 +369,7 @@ int build_bvh(Scene& sc, std::vector<int>& objs) {
 }
 
 // ------------------------------------------------------------------ XML (appendix B)
-struct Elem {
-  std::string name;
-  std::string text;
-  bool has_text = false;
-  std::vector<std::unique_ptr<Elem>> kids;
-  const Elem* child(const char* n) const {
-    for (auto& k : kids)
-      if (k->name == n) return k.get();
-    return nullptr;
-  }
-  std::vector<const Elem*> all(const char* n) const {
-    std::vector<const Elem*> v;
-    for (auto& k : kids)
-      if (k->name == n) v.push_back(k.get());
-    return v;
-  }
-};
-
-struct XmlParser {
-  const std::string& s;
-  size_t p = 0;
-  explicit XmlParser(const std::string& str) : s(str) {}
-  [[noreturn]] void fail(const char* m) { throw std::runtime_error(std::string("xml: ") + m); }
-  void skip_misc() {
-    for (;;) {
-      while (p < s.size() && isspace((unsigned char)s[p])) p++;
-      if (s.compare(p, 4, "<!--") == 0) {
-        size_t e = s.find("-->", p + 4);
-        if (e == std::string::npos) fail("unterminated comment");
-        p = e + 3;
-      } else if (s.compare(p, 2, "<?") == 0) {
-        size_t e = s.find("?>", p + 2);
-        if (e == std::string::npos) fail("unterminated declaration");
-        p = e + 2;
-      } else if (s.compare(p, 2, "<!") == 0) {
-        size_t e = s.find('>', p + 2);
-        if (e == std::string::npos) fail("unterminated doctype");
-        p = e + 1;
-      } else {
-        return;
-      }
-    }
-  }
-  static std::string decode(const std::string& t) {
-    std::string o;
-    for (size_t i = 0; i < t.size(); i++) {
-      if (t[i] != '&') {
-        o += t[i];
-        continue;
-      }
-      size_t e = t.find(';', i);
-      if (e == std::string::npos) {
-        o += t[i];
-        continue;
-      }
-      std::string ent = t.substr(i + 1, e - i - 1);
-      if (ent == "lt") o += '<';
-      else if (ent == "gt") o += '>';
-      else if (ent == "amp") o += '&';
-      else if (ent == "quot") o += '"';
-      else if (ent == "apos") o += '\'';
-      else if (!ent.empty() && ent[0] == '#') o += (char)std::strtol(ent.c_str() + 1 + (ent[1] == 'x'), nullptr, ent[1] == 'x' ? 16 : 10);
-      else o += "&" + ent + ";";
-      i = e;
-    }
-    return o;
-  }
-  std::unique_ptr<Elem> element() {
-    if (p >= s.size() || s[p] != '<') fail("expected element");
-    p++;
-    size_t b = p;
-    while (p < s.size() && !isspace((unsigned char)s[p]) && s[p] != '>' && s[p] != '/') p++;
-    auto e = std::make_unique<Elem>();
-    e->name = s.substr(b, p - b);
-    // attributes are ignored by the HW2 loader
-    while (p < s.size() && s[p] != '>' && !(s[p] == '/' && p + 1 < s.size() && s[p + 1] == '>')) {
-      if (s[p] == '"' || s[p] == '\'') {
-        char q = s[p++];
-        while (p < s.size() && s[p] != q) p++;
-      }
-      p++;
-    }
-    if (p >= s.size()) fail("unterminated tag");
-    if (s[p] == '/') {
-      p += 2;
-      return e;
-    }
-    p++;
-    bool first = true;
-    for (;;) {
-      if (p >= s.size()) fail("unterminated element");
-      if (s.compare(p, 2, "</") == 0) {
-        size_t c = s.find('>', p);
-        if (c == std::string::npos) fail("bad close tag");
-        p = c + 1;
-        return e;
-      }
-      if (s.compare(p, 4, "<!--") == 0) {
-        size_t c = s.find("-->", p);
-        if (c == std::string::npos) fail("unterminated comment");
-        p = c + 3;
-        first = false;
-        continue;
-      }
-      if (s.compare(p, 9, "<![CDATA[") == 0) {
-        size_t c = s.find("]]>", p);
-        if (c == std::string::npos) fail("unterminated CDATA");
-        if (first) {
-          e->text = s.substr(p + 9, c - p - 9);
-          e->has_text = true;
-        }
-        first = false;
-        p = c + 3;
-        continue;
-      }
-      if (s[p] == '<') {
-        e->kids.push_back(element());
-        first = false;
-        continue;
-      }
-      size_t c = s.find('<', p);
-      if (c == std::string::npos) fail("unterminated text");
-      if (first) {
-        e->text = decode(s.substr(p, c - p));
-        e->has_text = true;
-      }
-      first = false;
-      p = c;
-    }
-  }
-};
+// oracle/xml_lite.h: Elem + XmlParser (tinyxml2 GetText() semantics).
 
 const char* text_of(const Elem* e, const char* what) {
   if (!e || !e->has_text) throw std::runtime_error(std::string("missing text for ") + what);

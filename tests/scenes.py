@@ -76,3 +76,38 @@ def write_c3(directory: str, cameras: int = 1) -> str:
             f.write(spec.to_xml())
         os.replace(tmp, path)
     return path
+
+
+# PPM (photon mapping) scenes in the PPM XML dialect (tools/gen_ppm_scene.py).
+import gen_ppm_scene as GP  # noqa: E402
+
+PPM = {
+    "ppm_box": (lambda: GP.cornell(64, 64, photons=10000, iterations=10),
+                "C5 Cornell box at 64x64, 1e5 photons: mirror + glass spheres"),
+    "ppm_xform": (lambda: GP.cornell(64, 64, photons=10000, iterations=10, variant="transforms"),
+                  "scaled sphere, rotated smooth-shaded mesh + MeshInstance"),
+    "ppm_msaa": (lambda: GP.cornell(48, 40, photons=8000, iterations=10, num_samples=4),
+                 "NumSamples 4: 2x2 jittered eye samples per pixel"),
+    "ppm_shallow": (lambda: GP.cornell(40, 40, photons=6000, iterations=10, max_depth=3),
+                    "MaxRecursionDepth 3 cuts eye and photon paths"),
+}
+
+
+def write_ppm(name: str, directory: str) -> str:
+    path = os.path.join(directory, f"{name}.xml")
+    if not os.path.exists(path):
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(PPM[name][0]())
+        os.replace(tmp, path)
+    return path
+
+
+def write_c5(directory: str) -> str:
+    path = os.path.join(directory, "c5.xml")
+    if not os.path.exists(path):
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(GP.cornell(256, 256, photons=10000, iterations=1000))
+        os.replace(tmp, path)
+    return path
