@@ -1,0 +1,550 @@
+// C-ABI implementation of the photon-mapping path (include/ceng795_ppm.h): scene upload, the
+// eye / grid / photon / density passes and their device buffers.  One HIP stream per scene.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/ceng795_ppm.h"
+#include "ppm_host.h"
+#include "ppm_internal.h"
+
+namespace ppm {  // ppm_kernels.hip
+hipError_t launch_eye(const PScene&, const PCamera&, unsigned long long, int*, const int*,
+                      PHitPoint*, unsigned long long*, hipStream_t);
+hipError_t launch_grid(const PHitPoint*, int, int, int, PGrid*, float4*, unsigned*, hipStream_t);
+hipError_t launch_photons(const PScene&, unsigned long long, long long, int, int, PDeposit*, int*,
+                          unsigned long long*, hipStream_t);
+hipError_t launch_deposit_keys(const PDeposit*, const int*, const int*, int, int, const PGrid*,
+                               unsigned*, unsigned*, hipStream_t);
+hipError_t launch_bucket_bounds(const unsigned*, int, int*, int*, hipStream_t);
+hipError_t launch_hitpoint_update(const PScene&, const PHitPoint*, int, const PGrid*,
+                                  const PDeposit*, const unsigned*, const int*, const int*,
+                                  float4*, unsigned*, unsigned long long*, int*, hipStream_t);
+hipError_t launch_density(const PHitPoint*, const float4*, const int*, int, double, float*,
+                          hipStream_t);
+}  // namespace ppm
+namespace rt {
+void write_png(const std::string& path, const float* rgb, int w, int h);
+}
+
+using namespace ppm;
+
+namespace {
+
+thread_local std::string g_error;
+
+struct HipFailure {
+  hipError_t err;
+  const char* what;
+};
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw HipFailure{e, what};
+}
+int set_error(int code, const std::string& msg) {
+  g_error = msg;
+  return code;
+}
+template <typename F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const HipFailure& h) {
+    return set_error(RT_E_HIP, std::string(h.what) + ": " + hipGetErrorString(h.err));
+  } catch (const std::domain_error& e) {
+    return set_error(RT_E_UNSUPPORTED, e.what());
+  } catch (const std::invalid_argument& e) {
+    return set_error(RT_E_INVALID, e.what());
+  } catch (const std::ios_base::failure& e) {
+    return set_error(RT_E_IO, e.what());
+  } catch (const std::runtime_error& e) {
+    return set_error(RT_E_PARSE, e.what());
+  } catch (const std::exception& e) {
+    return set_error(RT_E_INVALID, e.what());
+  }
+}
+
+template <typename T>
+struct DevBuf {  // grow-only device array
+  T* p = nullptr;
+  size_t cap = 0;
+  void reserve(size_t n, const char* what) {
+    if (n <= cap) return;
+    (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hip_check(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)), what);
+    cap = n;
+  }
+  void release() {
+    (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+template <typename T>
+T* upload(const std::vector<T>& v, const char* what) {
+  T* p = nullptr;
+  hip_check(hipMalloc(&p, std::max<size_t>(v.size() * sizeof(T), 16)), what);
+  if (!v.empty()) hip_check(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice), what);
+  return p;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) hip_check(hipSetDevice(dev), "hipSetDevice");
+  }
+  ~DeviceGuard() {
+    int cur;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+constexpr size_t kSlotBytesPerBatch = size_t(1536) << 20;  // deposit slot rows per batch
+
+}  // namespace
+
+struct ppm_scene {
+  HostPPM host;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  unsigned long long seed = 0;
+  PScene S{};
+  std::vector<void*> owned;  // scene arrays
+  // eye pass / hash grid
+  int eye_cam = -1;
+  int n_hp = 0;
+  bool grid_ready = false;
+  DevBuf<PHitPoint> hp;
+  DevBuf<float4> state;
+  DevBuf<unsigned> nupd;
+  DevBuf<int> pix_cnt, pix_off;
+  DevBuf<PGrid> grid;
+  DevBuf<int> bstart, bend;
+  // photon batches
+  DevBuf<PDeposit> slots;
+  DevBuf<int> ndep, dep_off;
+  DevBuf<unsigned> keys, vals, keys2, vals2;
+  DevBuf<unsigned char> temp;
+  DevBuf<unsigned long long> stats;  // [photons, photon_rays, deposits, updates, eye_rays]
+  DevBuf<int> error;
+  DevBuf<float> image;
+  long long photons = 0;
+
+  void free_all() {
+    for (void* p : owned) (void)hipFree(p);
+    owned.clear();
+    hp.release(), state.release(), nupd.release(), pix_cnt.release(), pix_off.release();
+    grid.release(), bstart.release(), bend.release(), slots.release(), ndep.release();
+    dep_off.release(), keys.release(), vals.release(), keys2.release(), vals2.release();
+    temp.release(), stats.release(), error.release(), image.release();
+    if (stream) (void)hipStreamDestroy(stream);
+    stream = nullptr;
+  }
+};
+
+namespace {
+
+template <typename T>
+const T* own(ppm_scene* s, const std::vector<T>& v, const char* what) {
+  T* p = upload(v, what);
+  s->owned.push_back(p);
+  return p;
+}
+
+void create_device(ppm_scene* s, int device) {
+  s->device = device;
+  DeviceGuard g(device);
+  hip_check(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking), "stream");
+  const HostPPM& h = s->host;
+  PScene& S = s->S;
+  S.top_nodes = own(s, h.top_nodes, "upload top nodes");
+  S.objects = own(s, h.objects, "upload objects");
+  S.mesh_nodes = own(s, h.mesh_nodes, "upload mesh nodes");
+  S.triangles = own(s, h.triangles, "upload triangles");
+  S.meshes = own(s, h.meshes, "upload meshes");
+  S.vpos = own(s, h.vpos, "upload vertices");
+  S.vnormal = own(s, h.vnormal, "upload vertex normals");
+  S.materials = own(s, h.materials, "upload materials");
+  S.top_root = h.top_root;
+  S.max_depth = h.max_depth;
+  S.eps = h.eps;
+  std::memcpy(S.light_pos, h.lights.data(), 12);  // lights[0] (Scene.cpp:97)
+  std::memcpy(S.light_intensity, h.lights.data() + 3, 12);
+  s->stats.reserve(8, "alloc counters");
+  hip_check(hipMemset(s->stats.p, 0, 8 * sizeof(unsigned long long)), "zero counters");
+  s->error.reserve(1, "alloc error flag");
+  hip_check(hipMemset(s->error.p, 0, sizeof(int)), "zero error flag");
+  s->grid.reserve(1, "alloc grid");
+}
+
+void check_scene(const ppm_scene* s) {
+  if (!s) throw std::invalid_argument("scene is NULL");
+}
+
+void eye_pass(ppm_scene* s, int cam) {
+  if (cam < 0 || cam >= (int)s->host.cameras.size())
+    throw std::invalid_argument("camera index out of range");
+  const PCamera C = s->host.cameras[cam].cam;
+  const int npix = C.width * C.height;
+  s->pix_cnt.reserve(npix + 1, "alloc pixel counts");
+  s->pix_off.reserve(npix + 1, "alloc pixel offsets");
+  hip_check(hipMemsetAsync(s->pix_cnt.p, 0, (npix + 1) * sizeof(int), s->stream), "zero counts");
+  hip_check(launch_eye(s->S, C, s->seed, s->pix_cnt.p, nullptr, nullptr, s->stats.p, s->stream),
+            "eye pass (count)");
+  size_t bytes = 0;
+  hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, s->pix_cnt.p, s->pix_off.p, npix + 1,
+                                             s->stream), "scan size");
+  s->temp.reserve(bytes, "alloc scan temp");
+  hip_check(hipcub::DeviceScan::ExclusiveSum(s->temp.p, bytes, s->pix_cnt.p, s->pix_off.p,
+                                             npix + 1, s->stream), "scan hit points");
+  int total = 0;
+  hip_check(hipMemcpyAsync(&total, s->pix_off.p + npix, sizeof(int), hipMemcpyDeviceToHost,
+                           s->stream), "read hit-point count");
+  hip_check(hipStreamSynchronize(s->stream), "eye pass");
+  s->hp.reserve(total, "alloc hit points");
+  s->state.reserve(total, "alloc hit-point state");
+  s->nupd.reserve(total, "alloc hit-point counts");
+  hip_check(launch_eye(s->S, C, s->seed, nullptr, s->pix_off.p, s->hp.p, nullptr, s->stream),
+            "eye pass (write)");
+  s->n_hp = total;
+  s->eye_cam = cam;
+  s->grid_ready = false;
+}
+
+void build_grid(ppm_scene* s, int width, int height) {
+  if (s->eye_cam < 0) throw std::invalid_argument("build_hash_grid before the eye pass");
+  hip_check(launch_grid(s->hp.p, s->n_hp, width, height, s->grid.p, s->state.p, s->nupd.p,
+                        s->stream), "build hash grid");
+  s->bstart.reserve(std::max(1, s->n_hp), "alloc bucket starts");
+  s->bend.reserve(std::max(1, s->n_hp), "alloc bucket ends");
+  s->grid_ready = true;
+}
+
+void trace_photons(ppm_scene* s, long long first, long long count) {
+  if (count < 0 || first < 0) throw std::invalid_argument("bad photon range");
+  if (!s->grid_ready) throw std::invalid_argument("trace_photons before build_hash_grid");
+  const int K = std::max(1, s->host.max_depth - 1);
+  const long long batch_max = std::max<long long>(1, (long long)(kSlotBytesPerBatch / (sizeof(PDeposit) * K)));
+  const int H = s->n_hp;
+  int bits = 1;
+  while (bits < 32 && (1ull << bits) < (unsigned long long)std::max(H, 1)) bits++;
+  for (long long done = 0; done < count;) {
+    const int b = (int)std::min(count - done, batch_max);
+    s->slots.reserve((size_t)b * K, "alloc deposit slots");
+    s->ndep.reserve(b + 1, "alloc deposit counts");
+    s->dep_off.reserve(b + 1, "alloc deposit offsets");
+    hip_check(hipMemsetAsync(s->ndep.p + b, 0, sizeof(int), s->stream), "zero sentinel");
+    hip_check(launch_photons(s->S, s->seed, first + done, b, K, s->slots.p, s->ndep.p, s->stats.p,
+                             s->stream), "photon pass");
+    if (H > 0) {
+      size_t bytes = 0;
+      hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, s->ndep.p, s->dep_off.p, b + 1,
+                                                 s->stream), "scan size");
+      s->temp.reserve(bytes, "alloc scan temp");
+      hip_check(hipcub::DeviceScan::ExclusiveSum(s->temp.p, bytes, s->ndep.p, s->dep_off.p, b + 1,
+                                                 s->stream), "scan deposits");
+      int D = 0;
+      hip_check(hipMemcpyAsync(&D, s->dep_off.p + b, sizeof(int), hipMemcpyDeviceToHost,
+                               s->stream), "read deposit count");
+      hip_check(hipStreamSynchronize(s->stream), "photon batch");
+      if (D > 0) {
+        s->keys.reserve(D, "alloc keys");
+        s->vals.reserve(D, "alloc values");
+        s->keys2.reserve(D, "alloc keys");
+        s->vals2.reserve(D, "alloc values");
+        hip_check(launch_deposit_keys(s->slots.p, s->ndep.p, s->dep_off.p, b, K, s->grid.p,
+                                      s->keys.p, s->vals.p, s->stream), "deposit keys");
+        bytes = 0;
+        hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, s->keys.p, s->keys2.p,
+                                                     s->vals.p, s->vals2.p, D, 0, bits, s->stream),
+                  "sort size");
+        s->temp.reserve(bytes, "alloc sort temp");
+        hip_check(hipcub::DeviceRadixSort::SortPairs(s->temp.p, bytes, s->keys.p, s->keys2.p,
+                                                     s->vals.p, s->vals2.p, D, 0, bits, s->stream),
+                  "sort deposits by bucket");
+        hip_check(hipMemsetAsync(s->bstart.p, 0, H * sizeof(int), s->stream), "zero buckets");
+        hip_check(hipMemsetAsync(s->bend.p, 0, H * sizeof(int), s->stream), "zero buckets");
+        hip_check(launch_bucket_bounds(s->keys2.p, D, s->bstart.p, s->bend.p, s->stream),
+                  "bucket bounds");
+        hip_check(launch_hitpoint_update(s->S, s->hp.p, H, s->grid.p, s->slots.p, s->vals2.p,
+                                         s->bstart.p, s->bend.p, s->state.p, s->nupd.p,
+                                         s->stats.p, s->error.p, s->stream),
+                  "hit-point updates");
+      }
+    }
+    done += b;
+  }
+  s->photons += count;
+  int err = 0;
+  hip_check(hipMemcpyAsync(&err, s->error.p, sizeof(int), hipMemcpyDeviceToHost, s->stream),
+            "read error flag");
+  hip_check(hipStreamSynchronize(s->stream), "photon pass");
+  if (err) throw std::domain_error("a hit point's radius box spans more than 27 hash cells");
+}
+
+void density(ppm_scene* s, long long total, float* out) {
+  if (s->eye_cam < 0) throw std::invalid_argument("density_estimation before the eye pass");
+  const PCamera& C = s->host.cameras[s->eye_cam].cam;
+  const int npix = C.width * C.height;
+  s->image.reserve((size_t)npix * 3, "alloc image");
+  hip_check(launch_density(s->hp.p, s->state.p, s->pix_off.p, npix, (double)total, s->image.p,
+                           s->stream), "density estimation");
+  hip_check(hipMemcpyAsync(out, s->image.p, (size_t)npix * 3 * sizeof(float),
+                           hipMemcpyDeviceToHost, s->stream), "copy image");
+  hip_check(hipStreamSynchronize(s->stream), "density estimation");
+}
+
+}  // namespace
+
+extern "C" {
+
+int ppm_abi_version(void) { return CENG795_PPM_ABI_VERSION; }
+const char* ppm_last_error(void) { return g_error.c_str(); }
+
+int ppm_scene_load_xml(const char* xml_path, int device, ppm_scene** out) {
+  if (!xml_path || !out) return set_error(RT_E_INVALID, "ppm_scene_load_xml: NULL argument");
+  *out = nullptr;
+  auto s = std::make_unique<ppm_scene>();
+  const int rc = guarded([&] {
+    load_ppm_xml(xml_path, s->host);
+    create_device(s.get(), device);
+    return RT_OK;
+  });
+  if (rc != RT_OK) {
+    s->free_all();
+    return rc;
+  }
+  *out = s.release();
+  return RT_OK;
+}
+
+void ppm_scene_destroy(ppm_scene* s) {
+  if (!s) return;
+  int cur = -1;
+  if (hipGetDevice(&cur) == hipSuccess && cur != s->device) (void)hipSetDevice(s->device);
+  s->free_all();
+  if (cur >= 0 && cur != s->device) (void)hipSetDevice(cur);
+  delete s;
+}
+
+int ppm_num_cameras(const ppm_scene* s) { return s ? (int)s->host.cameras.size() : 0; }
+
+int ppm_camera_info(const ppm_scene* s, int cam, int* w, int* h, int* n) {
+  if (!s || cam < 0 || cam >= (int)s->host.cameras.size() || !w || !h || !n)
+    return set_error(RT_E_INVALID, "ppm_camera_info: bad argument");
+  const PCamera& c = s->host.cameras[cam].cam;
+  *w = c.width, *h = c.height, *n = c.samples;
+  return RT_OK;
+}
+
+const char* ppm_image_name(const ppm_scene* s, int cam) {
+  if (!s || cam < 0 || cam >= (int)s->host.cameras.size()) return "";
+  return s->host.cameras[cam].image_name.c_str();
+}
+
+int ppm_settings(const ppm_scene* s, int* per_iteration, int* iterations, int* max_depth) {
+  if (!s || !per_iteration || !iterations || !max_depth)
+    return set_error(RT_E_INVALID, "ppm_settings: NULL argument");
+  *per_iteration = s->host.per_iteration;
+  *iterations = s->host.iterations;
+  *max_depth = s->host.max_depth;
+  return RT_OK;
+}
+
+int ppm_set_seed(ppm_scene* s, unsigned long long seed) {
+  if (!s) return set_error(RT_E_INVALID, "ppm_set_seed: NULL scene");
+  s->seed = seed;
+  return RT_OK;
+}
+
+int ppm_eye_pass(ppm_scene* s, int cam) {
+  return guarded([&] {
+    check_scene(s);
+    DeviceGuard g(s->device);
+    eye_pass(s, cam);
+    hip_check(hipStreamSynchronize(s->stream), "eye pass");
+    return RT_OK;
+  });
+}
+
+int ppm_build_hash_grid(ppm_scene* s, int width, int height, double* info) {
+  return guarded([&] {
+    check_scene(s);
+    if (width <= 0 || height <= 0) throw std::invalid_argument("bad image size");
+    DeviceGuard g(s->device);
+    build_grid(s, width, height);
+    PGrid G;
+    hip_check(hipMemcpyAsync(&G, s->grid.p, sizeof G, hipMemcpyDeviceToHost, s->stream), "read grid");
+    hip_check(hipStreamSynchronize(s->stream), "build hash grid");
+    if (info) {
+      const double v[8] = {G.radius, G.hash_scale, G.bmin[0], G.bmin[1], G.bmin[2],
+                           G.bmax[0], G.bmax[1], G.bmax[2]};
+      std::memcpy(info, v, sizeof v);
+    }
+    return RT_OK;
+  });
+}
+
+int ppm_num_hit_points(const ppm_scene* s) { return s ? s->n_hp : 0; }
+
+int ppm_read_hit_points(ppm_scene* s, float* out) {
+  return guarded([&] {
+    check_scene(s);
+    if (!out) throw std::invalid_argument("ppm_read_hit_points: NULL output");
+    DeviceGuard g(s->device);
+    std::vector<PHitPoint> hp(s->n_hp);
+    std::vector<float4> st(s->n_hp);
+    if (s->n_hp) {
+      hip_check(hipMemcpyAsync(hp.data(), s->hp.p, hp.size() * sizeof(PHitPoint),
+                               hipMemcpyDeviceToHost, s->stream), "read hit points");
+      if (s->grid_ready)
+        hip_check(hipMemcpyAsync(st.data(), s->state.p, st.size() * sizeof(float4),
+                                 hipMemcpyDeviceToHost, s->stream), "read hit-point state");
+      hip_check(hipStreamSynchronize(s->stream), "read hit points");
+    }
+    for (int k = 0; k < s->n_hp; k++) {
+      const PHitPoint& h = hp[k];
+      float* r = out + 16 * (size_t)k;
+      std::memcpy(r, h.pos, 12);
+      std::memcpy(r + 3, h.normal, 12);
+      std::memcpy(r + 6, h.w_o, 12);
+      std::memcpy(r + 9, h.att, 12);
+      r[12] = (float)h.pixel;
+      r[13] = h.weight;
+      r[14] = s->grid_ready ? st[k].w : 0.0f;
+      r[15] = (float)s->host.materials[h.material].type;
+    }
+    return RT_OK;
+  });
+}
+
+int ppm_read_hit_state(ppm_scene* s, float* out) {
+  return guarded([&] {
+    check_scene(s);
+    if (!out) throw std::invalid_argument("ppm_read_hit_state: NULL output");
+    if (!s->grid_ready) throw std::invalid_argument("no hash grid yet");
+    DeviceGuard g(s->device);
+    std::vector<float4> st(s->n_hp);
+    std::vector<unsigned> n(s->n_hp);
+    if (s->n_hp) {
+      hip_check(hipMemcpyAsync(st.data(), s->state.p, st.size() * sizeof(float4),
+                               hipMemcpyDeviceToHost, s->stream), "read state");
+      hip_check(hipMemcpyAsync(n.data(), s->nupd.p, n.size() * sizeof(unsigned),
+                               hipMemcpyDeviceToHost, s->stream), "read counts");
+      hip_check(hipStreamSynchronize(s->stream), "read state");
+    }
+    for (int k = 0; k < s->n_hp; k++) {
+      float* r = out + 5 * (size_t)k;
+      r[0] = st[k].x, r[1] = st[k].y, r[2] = st[k].z, r[3] = st[k].w, r[4] = (float)n[k];
+    }
+    return RT_OK;
+  });
+}
+
+int ppm_trace_photons(ppm_scene* s, long long first, long long count) {
+  return guarded([&] {
+    check_scene(s);
+    DeviceGuard g(s->device);
+    trace_photons(s, first, count);
+    return RT_OK;
+  });
+}
+
+int ppm_density_estimation(ppm_scene* s, long long total, float* out) {
+  return guarded([&] {
+    check_scene(s);
+    if (!out) throw std::invalid_argument("ppm_density_estimation: NULL output");
+    DeviceGuard g(s->device);
+    density(s, total, out);
+    return RT_OK;
+  });
+}
+
+int ppm_collect_stats(ppm_scene* s, ppm_stats* st) {
+  return guarded([&] {
+    check_scene(s);
+    if (!st) throw std::invalid_argument("ppm_collect_stats: NULL output");
+    DeviceGuard g(s->device);
+    unsigned long long c[8];
+    hip_check(hipMemcpyAsync(c, s->stats.p, sizeof c, hipMemcpyDeviceToHost, s->stream), "read counters");
+    hip_check(hipMemsetAsync(s->stats.p, 0, sizeof c, s->stream), "reset counters");
+    hip_check(hipStreamSynchronize(s->stream), "counters");
+    std::memset(st, 0, sizeof *st);
+    st->photons = s->photons;
+    st->photon_rays = (long long)c[1];
+    st->deposits = (long long)c[2];
+    st->updates = (long long)c[3];
+    st->eye_rays = (long long)c[4];
+    st->hit_points = s->n_hp;
+    s->photons = 0;
+    return RT_OK;
+  });
+}
+
+int ppm_render(ppm_scene* s, int cam, int threads, float* out, ppm_stats* stats) {
+  return guarded([&] {
+    check_scene(s);
+    if (threads < 1 || !out) throw std::invalid_argument("ppm_render: bad argument");
+    if (cam < 0 || cam >= (int)s->host.cameras.size())
+      throw std::invalid_argument("camera index out of range");
+    DeviceGuard g(s->device);
+    const PCamera& C = s->host.cameras[cam].cam;
+    hipEvent_t ev[5];
+    for (auto& e : ev) hip_check(hipEventCreate(&e), "event");
+    struct Events {
+      hipEvent_t* e;
+      ~Events() {
+        for (int k = 0; k < 5; k++) (void)hipEventDestroy(e[k]);
+      }
+    } guard{ev};
+    hip_check(hipMemsetAsync(s->stats.p, 0, 8 * sizeof(unsigned long long), s->stream), "zero counters");
+    s->photons = 0;
+    hip_check(hipEventRecord(ev[0], s->stream), "event");
+    eye_pass(s, cam);
+    hip_check(hipEventRecord(ev[1], s->stream), "event");
+    build_grid(s, C.width, C.height);
+    hip_check(hipEventRecord(ev[2], s->stream), "event");
+    const long long P = s->host.per_iteration, I = s->host.iterations;
+    const long long per_thread = P / threads;
+    const long long traced = C.height < threads ? P * I : per_thread * I * threads;
+    trace_photons(s, 0, traced);
+    hip_check(hipEventRecord(ev[3], s->stream), "event");
+    const int normalizer = (int)(P * per_thread * threads);  // main.cpp:94, int arithmetic
+    density(s, normalizer, out);
+    hip_check(hipEventRecord(ev[4], s->stream), "event");
+    hip_check(hipEventSynchronize(ev[4]), "render");
+    if (stats) {
+      const long long photons = s->photons;
+      ppm_collect_stats(s, stats);
+      stats->photons = photons;
+      float ms[4];
+      for (int k = 0; k < 4; k++) hip_check(hipEventElapsedTime(&ms[k], ev[k], ev[k + 1]), "elapsed");
+      stats->eye_ms = ms[0], stats->grid_ms = ms[1], stats->photon_ms = ms[2], stats->density_ms = ms[3];
+    }
+    return RT_OK;
+  });
+}
+
+int ppm_write_png(const char* path, const float* rgb, int w, int h) {
+  if (!path || !rgb || w <= 0 || h <= 0) return set_error(RT_E_INVALID, "ppm_write_png: bad argument");
+  return guarded([&] {
+    std::vector<float> v((size_t)w * h * 3);
+    for (size_t k = 0; k < v.size(); k++)  // main.cpp:148-154: double exp / pow
+      v[k] = (float)(int)(std::pow(1 - std::exp(-(double)rgb[k]), (double)(1 / 2.2f)) * 255 + 0.5f);
+    rt::write_png(path, v.data(), w, h);
+    return RT_OK;
+  });
+}
+
+}  // extern "C"

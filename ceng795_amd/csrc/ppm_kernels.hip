@@ -1,0 +1,750 @@
+// Photon-mapping (PPM) kernels for gfx950 — the reference's PPM/src/Scene.cpp passes:
+//
+//   eye_kernel<COUNT|WRITE>  eye_trace_lines + eye_trace (Scene.cpp:250-361): one lane per
+//                            pixel walks its eye-ray tree depth first; pass 1 counts hit
+//                            points per pixel, a scan gives offsets, pass 2 writes them, so the
+//                            hit-point array is in the single-threaded reference order.
+//   grid_kernel              build_hash_grid (Scene.cpp:53-93): one block reduces the hit-point
+//                            bounding box, derives the initial radius / hash scale and resets
+//                            every hit point's (flux, radius^2, n).
+//   photon_kernel            generate_photon + photon_trace (Point_light.cpp:7-30,
+//                            Scene.cpp:106-249): one lane per photon; every diffuse hit leaves a
+//                            deposit {x, n, w_i, flux} in the photon's slot row.
+//   deposit_keys_kernel      compacts the deposits in (photon, bounce) order and keys each by
+//                            the hash bucket of its cell (Scene.cpp:125-130).
+//   (hipcub stable radix sort by bucket -> per-bucket deposit runs in photon order)
+//   hitpoint_update_kernel   the radius / flux updates of Scene.cpp:131-168, turned inside out:
+//                            one lane per hit point merges the deposit runs of the buckets its
+//                            radius box was filed under and applies them in photon order.
+//   density_kernel           density_estimation + Pixel::get_color (Scene.cpp:363-371).
+//
+// Why the update pass is exact: a photon's path never reads hit-point state, so the reference's
+// per-photon updates (under a per-hit-point mutex) are, for each hit point, a sequential
+// recurrence over the photons that reach one of its buckets.  Applying that recurrence in
+// photon order reproduces a single-threaded reference run exactly (the oracle,
+// oracle/ppm_ref.cpp, does literally that), without atomics or locks.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "ppm_internal.h"
+#include "ppm_math.h"
+
+#pragma clang fp contract(off)
+
+namespace ppm {
+namespace {
+
+constexpr float kTestEps = 0.0001f;  // intersection_test_epsilon (PPM/include/Vector3.h:10)
+constexpr float kInf = __builtin_huge_valf();
+constexpr float kAlpha = 0.7f;       // ALPHA (Scene.cpp:13)
+
+struct V {
+  float x, y, z;
+};
+__device__ __forceinline__ V mk(float x, float y, float z) { return V{x, y, z}; }
+__device__ __forceinline__ V ld(const float* p) { return V{p[0], p[1], p[2]}; }
+__device__ __forceinline__ V operator+(V a, V b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V operator-(V a, V b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V operator*(V a, V b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V operator*(V a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V operator/(V a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ V operator-(V a, float s) { return mk(a.x - s, a.y - s, a.z - s); }
+__device__ __forceinline__ V operator+(V a, float s) { return mk(a.x + s, a.y + s, a.z + s); }
+__device__ __forceinline__ V neg(V a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(V a, V b) { return (a.x * b.x) + (a.y * b.y) + (a.z * b.z); }
+__device__ __forceinline__ V cross(V a, V b) {
+  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ V normalize(V a) {
+  return a / __builtin_sqrtf(a.x * a.x + a.y * a.y + a.z * a.z);
+}
+__device__ __forceinline__ float fmax0(float v) { return (0.0f < v) ? v : 0.0f; }  // std::max(0,v)
+__device__ __forceinline__ float comp(V v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+
+struct Ray {
+  V o, d;
+};
+__device__ __forceinline__ V point_at(const Ray& r, float t) { return r.o + r.d * t; }
+
+// Matrix4x4::multiply (Matrix4x4.cpp:27-45): rows accumulate from 0 (vector) or m[i][3] (point).
+__device__ __forceinline__ V mul_vector(const float* m, int stride, V v) {
+  float r[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    r[i] = 0.0f;
+    r[i] += m[stride * i] * v.x;
+    r[i] += m[stride * i + 1] * v.y;
+    r[i] += m[stride * i + 2] * v.z;
+  }
+  return mk(r[0], r[1], r[2]);
+}
+__device__ __forceinline__ V mul_point(const float* m, V v) {  // 3x4 rows
+  float r[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    r[i] = m[4 * i + 3];
+    r[i] += m[4 * i] * v.x;
+    r[i] += m[4 * i + 1] * v.y;
+    r[i] += m[4 * i + 2] * v.z;
+  }
+  return mk(r[0], r[1], r[2]);
+}
+
+// Bounding_box::intersect + the caller's `t < 0 || t == inf` rejection (Bounding_box.cpp:32-54,
+// BVH.cpp:33-35, Mesh.h:72-75), literally: true division, axes with |d| < 1e-4 skipped.
+__device__ __forceinline__ bool box_accept(const float* lo, const float* hi, const Ray& r) {
+  float tmin = -kInf, tmax = kInf;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const float d = comp(r.d, i), o = comp(r.o, i);
+    if (__builtin_fabsf(d) < kTestEps) continue;
+    float t0 = (lo[i] - o) / d;
+    float t1 = (hi[i] - o) / d;
+    if (d < 0) {
+      const float s = t0;
+      t0 = t1;
+      t1 = s;
+    }
+    if (t0 > tmin) tmin = t0;
+    if (t1 < tmax) tmax = t1;
+    if (tmin > tmax) return false;  // returns kInf
+  }
+  const float v = tmin > 0.0f ? tmin : tmax;
+  return !(v < 0.0f || v == kInf);
+}
+
+__device__ __forceinline__ float det3(V c1, V c2, V c3) {  // Mesh_triangle.h:44-49
+  return c1.x * (c2.y * c3.z - c3.y * c2.z) + c2.x * (c3.y * c1.z - c1.y * c3.z) +
+         c3.x * (c1.y * c2.z - c2.y * c1.z);
+}
+
+// Mesh_triangle::intersect (Mesh_triangle.cpp:57-111) without the normal (computed for the
+// winner only).  Returns the raw acceptance (t > -1e-4).
+__device__ __forceinline__ bool tri_test(const PScene& S, const PTriangle& tr, const Ray& r,
+                                         bool culling, float& t, float& beta, float& gamma) {
+  const V p0 = ld(S.vpos + 3 * tr.v[0]), p1 = ld(S.vpos + 3 * tr.v[1]),
+          p2 = ld(S.vpos + 3 * tr.v[2]);
+  const V a1 = p0 - p1, a2 = p0 - p2;
+  if (culling && dot(r.d, ld(tr.normal)) > 0.0f) return false;
+  const float det_a = det3(a1, a2, r.d);
+  if (det_a == 0.0f) return false;
+  const V b = (p0 - r.o) / det_a;
+  beta = det3(b, a2, r.d);
+  if (beta < -kTestEps) return false;
+  gamma = det3(a1, b, r.d);
+  if (gamma < -kTestEps || beta + gamma > 1.0f + kTestEps) return false;
+  t = det3(a1, a2, b);
+  return t > -kTestEps;
+}
+
+// Sphere::intersect (Sphere.cpp:26-64): true for any root, the caller filters t > 0.
+__device__ __forceinline__ bool sphere_test(const PObject& o, const Ray& r, float& t) {
+  const Ray rl{mul_point(o.inv, r.o), mul_vector(o.inv, 4, r.d)};
+  const V co = rl.o - ld(o.center);
+  const float a = dot(rl.d, rl.d);
+  const float b = 2 * dot(rl.d, co);
+  const float c = dot(co, co) - o.radius * o.radius;
+  const float disc = b * b - 4 * a * c;
+  if (disc < -kTestEps) return false;
+  if (disc < kTestEps) {
+    t = -b / (2 * a);
+  } else {
+    const float sq = __builtin_sqrtf(disc);
+    const float t1 = (-b + sq) / (2 * a);
+    const float t2 = (-b - sq) / (2 * a);
+    t = t2 < 0.0f ? t1 : t2;
+  }
+  return true;
+}
+
+struct Hit {
+  float t;
+  int obj;  // top-level object
+  int tri;  // triangle (instances), -1 for spheres
+  float beta, gamma;
+};
+
+// Mesh::intersect -> the mesh's BVH with the local ray (Mesh.h:21-27, BVH.cpp:30-52): the
+// first triangle in DFS order with the smallest t > 0.  A one-triangle mesh (create_bvh
+// returns the triangle itself) gives the raw test, t > -1e-4 included.
+__device__ bool mesh_closest(const PScene& S, int root, const Ray& rl, bool culling, Hit& h) {
+  float t, b, g;
+  if (root < 0) {
+    if (!tri_test(S, S.triangles[~root], rl, culling, t, b, g)) return false;
+    h.t = t, h.tri = ~root, h.beta = b, h.gamma = g;
+    return true;
+  }
+  int stack[kMeshStack];
+  int sp = 0;
+  stack[sp++] = root;
+  bool any = false;
+  h.t = kInf;
+  while (sp > 0) {
+    const int e = stack[--sp];
+    if (e >= 0) {
+      const PNode& n = S.mesh_nodes[e];
+      if (!box_accept(n.lo, n.hi, rl)) continue;
+      stack[sp++] = n.child[1];  // left child popped (visited) first
+      stack[sp++] = n.child[0];
+    } else if (tri_test(S, S.triangles[~e], rl, culling, t, b, g) && t > 0.0f && t < h.t) {
+      h.t = t, h.tri = ~e, h.beta = b, h.gamma = g;
+      any = true;
+    }
+  }
+  return any;
+}
+
+// Shape::intersect of a top-level object, unfiltered (the parent BVH node filters t > 0).
+__device__ __forceinline__ bool object_test(const PScene& S, int obj, const Ray& r,
+                                            bool culling, Hit& h) {
+  const PObject& o = S.objects[obj];
+  h.obj = obj;
+  if (o.kind == kObjSphere) {
+    h.tri = -1;
+    return sphere_test(o, r, h.t);
+  }
+  // Mesh_instance::intersect (Mesh.h:70-93): world box, then the mesh with the local ray;
+  // refractive instances are never culled.
+  if (!box_accept(o.lo, o.hi, r)) return false;
+  const Ray rl{mul_point(o.inv, r.o), mul_vector(o.inv, 4, r.d)};
+  return mesh_closest(S, S.meshes[o.mesh].root, rl, o.refractive ? false : culling, h);
+}
+
+// bvh->intersect(ray, intersection, true) at the top level (BVH.cpp:30-52).
+__device__ bool closest(const PScene& S, const Ray& r, Hit& best) {
+  if (S.top_root == INT_MIN) return false;
+  if (S.top_root < 0) return object_test(S, ~S.top_root, r, true, best);  // root = one object
+  int stack[kTopStack];
+  int sp = 0;
+  stack[sp++] = S.top_root;
+  bool any = false;
+  best.t = kInf;
+  while (sp > 0) {
+    const int e = stack[--sp];
+    if (e >= 0) {
+      const PNode& n = S.top_nodes[e];
+      if (!box_accept(n.lo, n.hi, r)) continue;
+      stack[sp++] = n.child[1];
+      stack[sp++] = n.child[0];
+      continue;
+    }
+    Hit h;
+    if (object_test(S, ~e, r, true, h) && h.t > 0.0f && h.t < best.t) {
+      best = h;
+      any = true;
+    }
+  }
+  return any;
+}
+
+// The winner's shading normal, as the winning intersect call computed it: sphere normal from
+// the local hit point (Sphere.cpp:55-60), flat or smooth triangle normal (Mesh_triangle.cpp:
+// 91-103), then Mesh_instance's normal transform (Mesh.h:84-87).
+__device__ V hit_normal(const PScene& S, const Ray& r, const Hit& h) {
+  const PObject& o = S.objects[h.obj];
+  if (o.kind == kObjSphere) {
+    const Ray rl{mul_point(o.inv, r.o), mul_vector(o.inv, 4, r.d)};
+    const V local = point_at(rl, h.t) - ld(o.center);
+    return normalize(mul_vector(o.nrm, 3, normalize(local)));
+  }
+  const PTriangle& tr = S.triangles[h.tri];
+  V n;
+  if (tr.smooth) {
+    const float w0 = (1 - h.beta) - h.gamma;
+    n = normalize((ld(S.vnormal + 3 * tr.v[0]) * w0 + ld(S.vnormal + 3 * tr.v[1]) * h.beta) +
+                  ld(S.vnormal + 3 * tr.v[2]) * h.gamma);
+  } else {
+    n = ld(tr.normal);
+  }
+  return normalize(mul_vector(o.nrm, 3, n));
+}
+
+// Shared refraction set-up of eye_trace / photon_trace (Scene.cpp:225-245, 330-352).
+struct Refraction {
+  bool tir, into;
+  Ray reflection, refraction;
+  float fresnel;
+};
+__device__ Refraction refract_setup(const PScene& S, const Ray& ray, V x, V normal,
+                                    const PMaterial& m) {
+  Refraction R;
+  const V nl = dot(normal, ray.d) < 0.0f ? normal : normal * -1;
+  const V w_o = normalize(ray.o - x);
+  const V w_r = normalize((normal * (2.0f * dot(normal, w_o))) - w_o);
+  R.reflection = Ray{x + (w_r * S.eps), w_r};
+  R.into = dot(normal, nl) > 0.0f;
+  const float air = 1.0f;
+  const float nnt = R.into ? air / m.refraction_index : m.refraction_index / air;
+  const float ddn = dot(ray.d, nl);
+  const float cos2t = 1 - nnt * nnt * (1 - ddn * ddn);
+  R.tir = cos2t < 0.0f;
+  R.fresnel = 0.0f;
+  if (R.tir) {
+    R.refraction = R.reflection;
+    return R;
+  }
+  const V dir = normalize(ray.d * nnt -
+                          normal * ((float)(R.into ? 1 : -1) * (ddn * nnt + __builtin_sqrtf(cos2t))));
+  const float a = m.refraction_index - air, b = m.refraction_index + air;
+  const float r0 = a * a / (b * b);
+  const float cosa = R.into ? -ddn : dot(dir, normal);
+  const float c = 1 - cosa;
+  R.fresnel = r0 + (1 - r0) * c * c * c * c * c;
+  R.refraction = Ray{x + (dir * S.eps), dir};
+  return R;
+}
+
+__device__ __forceinline__ Ray camera_ray(const PCamera& c, float x, float y) {
+  // Camera::calculate_ray_at (PPM/include/Camera.h:76-84): (tl + x*s_u) - y*s_v
+  const V s = (ld(c.top_left) + ld(c.s_u) * x) - ld(c.s_v) * y;
+  const V e = ld(c.e);
+  return Ray{e, normalize(s - e)};
+}
+
+struct EyeItem {
+  Ray ray;
+  V att;
+  int depth;
+};
+
+// eye_trace (Scene.cpp:286-361) of one primary ray, depth first (reflection subtree before
+// the refraction one).  WRITE: store the hit points at out[k++]; always counts them.
+template <bool WRITE>
+__device__ int eye_trace(const PScene& S, const Ray& primary, int pixel, PHitPoint* out, int k,
+                         unsigned long long& rays) {
+  EyeItem stack[kEyeStack];
+  int sp = 0;
+  stack[sp++] = EyeItem{primary, mk(1.0f, 1.0f, 1.0f), 0};
+  while (sp > 0) {
+    const EyeItem it = stack[--sp];
+    Hit h;
+    rays++;
+    if (!closest(S, it.ray, h)) continue;
+    const V x = point_at(it.ray, h.t);
+    const V normal = hit_normal(S, it.ray, h);
+    const int mid = S.objects[h.obj].material;
+    const PMaterial& m = S.materials[mid];
+    if (m.type == kMatDiffuse) {
+      if (WRITE) {
+        PHitPoint hp;
+        const V w_o = normalize(it.ray.o - x);
+        hp.pos[0] = x.x, hp.pos[1] = x.y, hp.pos[2] = x.z;
+        hp.normal[0] = normal.x, hp.normal[1] = normal.y, hp.normal[2] = normal.z;
+        hp.w_o[0] = w_o.x, hp.w_o[1] = w_o.y, hp.w_o[2] = w_o.z;
+        hp.att[0] = it.att.x, hp.att[1] = it.att.y, hp.att[2] = it.att.z;
+        hp.material = mid;
+        hp.pixel = pixel;
+        hp.weight = 1.0f;
+        hp.pad = 0.0f;
+        out[k] = hp;
+      }
+      k++;
+    } else if (it.depth >= S.max_depth) {
+      continue;
+    } else if (m.type == kMatMirror) {
+      const V w_o = normalize(it.ray.o - x);
+      const V w_r = normalize((normal * (2.0f * dot(normal, w_o))) - w_o);
+      stack[sp++] = EyeItem{Ray{x + (w_r * S.eps), w_r}, ld(m.mirror) * it.att, it.depth + 1};
+    } else {
+      const Refraction R = refract_setup(S, it.ray, x, normal, m);
+      if (R.tir) {
+        stack[sp++] = EyeItem{R.reflection, ld(m.transparency) * it.att, it.depth + 1};
+        continue;
+      }
+      const V attenuated = ld(m.transparency) * it.att;
+      if (R.into) {
+        stack[sp++] = EyeItem{R.refraction, attenuated * (1.0f - R.fresnel), it.depth + 1};
+        stack[sp++] = EyeItem{R.reflection, it.att * R.fresnel, it.depth + 1};
+      } else {
+        stack[sp++] = EyeItem{R.refraction, attenuated, it.depth + 1};
+      }
+    }
+  }
+  return k;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ unsigned bucket_of(const PGrid& G, int ix, int iy, int iz) {
+  // Scene::hash (PPM/include/Scene.h:65-68): int products wrap, xor, unsigned % num_hash
+  const unsigned a = (unsigned)ix * 73856093u, b = (unsigned)iy * 19349663u,
+                 c = (unsigned)iz * 83492791u;
+  return (a ^ b ^ c) % G.num_hash;
+}
+__device__ __forceinline__ int cell(float v) { const int i = (int)v; return i < 0 ? -i : i; }
+
+}  // namespace
+
+// ------------------------------------------------------------------ eye pass
+// counts != null: pass 1 (hit points per pixel); else pass 2 writes at offsets[pixel].
+__global__ __launch_bounds__(256) void eye_kernel(PScene S, PCamera C, unsigned long long seed,
+                                                  int* counts, const int* offsets,
+                                                  PHitPoint* out, unsigned long long* stats) {
+  const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const bool active = p < C.width * C.height;
+  unsigned long long rays = 0;
+  if (active) {
+    const int i = p % C.width, j = p / C.width;
+    const bool write = counts == nullptr;
+    int k = write ? offsets[p] : 0;
+    if (C.samples == 1) {  // Scene.cpp:257-263
+      const Ray r = camera_ray(C, i + 0.5f, j + 0.5f);
+      k = write ? eye_trace<true>(S, r, p, out, k, rays) : eye_trace<false>(S, r, p, out, k, rays);
+    } else {  // Scene.cpp:264-284: at most 2x2 jittered samples
+      const int n = C.samples < 2 ? C.samples : 2;
+      ppm_math::Rng rng(seed, ppm_math::kEyeStream | (unsigned long long)p);
+      for (int x = 0; x < n; x++)
+        for (int y = 0; y < n; y++) {
+          const float ex = rng.uniform01();
+          const float ey = rng.uniform01();
+          const float sx = (x + ex) / n;
+          const float sy = (y + ey) / n;
+          const Ray r = camera_ray(C, i + sx, j + sy);
+          k = write ? eye_trace<true>(S, r, p, out, k, rays)
+                    : eye_trace<false>(S, r, p, out, k, rays);
+        }
+    }
+    if (!write) counts[p] = k;
+  }
+  const unsigned long long tot = wave_sum(rays);
+  if (stats && (threadIdx.x & 63) == 0 && tot) atomicAdd(&stats[4], tot);
+}
+
+// ------------------------------------------------------------------ hash grid
+__global__ __launch_bounds__(1024) void grid_kernel(const PHitPoint* hps, int n, int width,
+                                                    int height, PGrid* grid, float4* state,
+                                                    unsigned* counts) {
+  __shared__ float red[6][1024];
+  const int t = (int)threadIdx.x;
+  float lo[3] = {kInf, kInf, kInf}, hi[3] = {-kInf, -kInf, -kInf};
+  for (int k = t; k < n; k += 1024)
+    for (int a = 0; a < 3; a++) {  // Bounding_box::fit: std::min / std::max
+      const float v = hps[k].pos[a];
+      lo[a] = (v < lo[a]) ? v : lo[a];
+      hi[a] = (hi[a] < v) ? v : hi[a];
+    }
+  for (int a = 0; a < 3; a++) red[a][t] = lo[a], red[3 + a][t] = hi[a];
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if (t < s)
+      for (int a = 0; a < 3; a++) {
+        const float l = red[a][t + s], h = red[3 + a][t + s];
+        red[a][t] = (l < red[a][t]) ? l : red[a][t];
+        red[3 + a][t] = (red[3 + a][t] < h) ? h : red[3 + a][t];
+      }
+    __syncthreads();
+  }
+  // Scene.cpp:59-61: initial radius from the mean bounding-box extent and image size
+  const float dx = red[3][0] - red[0][0], dy = red[4][0] - red[1][0], dz = red[5][0] - red[2][0];
+  const float r = ((dx + dy + dz) / 3.0f) / ((width + height) / 2.0f) * 2.0f * 4.0f;
+  __syncthreads();
+  for (int a = 0; a < 3; a++) lo[a] = kInf, hi[a] = -kInf;
+  const float r2 = r * r;
+  for (int k = t; k < n; k += 1024) {
+    for (int a = 0; a < 3; a++) {  // fit(position - r), fit(position + r)
+      const float m = hps[k].pos[a] - r, p = hps[k].pos[a] + r;
+      lo[a] = (m < lo[a]) ? m : lo[a];
+      hi[a] = (hi[a] < m) ? m : hi[a];
+      lo[a] = (p < lo[a]) ? p : lo[a];
+      hi[a] = (hi[a] < p) ? p : hi[a];
+    }
+    state[k] = make_float4(0.0f, 0.0f, 0.0f, r2);  // flux = 0, radius^2 (Scene.cpp:64-67)
+    counts[k] = 0u;
+  }
+  for (int a = 0; a < 3; a++) red[a][t] = lo[a], red[3 + a][t] = hi[a];
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if (t < s)
+      for (int a = 0; a < 3; a++) {
+        const float l = red[a][t + s], h = red[3 + a][t + s];
+        red[a][t] = (l < red[a][t]) ? l : red[a][t];
+        red[3 + a][t] = (red[3 + a][t] < h) ? h : red[3 + a][t];
+      }
+    __syncthreads();
+  }
+  if (t == 0) {
+    PGrid G;
+    for (int a = 0; a < 3; a++) G.bmin[a] = red[a][0], G.bmax[a] = red[3 + a][0];
+    G.radius = r;
+    G.hash_scale = (float)(1.0 / ((double)r * 2.0));
+    G.num_hash = (unsigned)n;
+    G.pad = 0;
+    *grid = G;
+  }
+}
+
+// ------------------------------------------------------------------ photon pass
+// Photon first + i traces its chain (photon_trace's recursion never branches) and leaves
+// one deposit per diffuse hit in slots[i * K + k], k < K = max(1, MaxRecursionDepth - 1).
+__global__ __launch_bounds__(256) void photon_kernel(PScene S, unsigned long long seed,
+                                                     long long first, int count, int K,
+                                                     PDeposit* slots, int* ndep,
+                                                     unsigned long long* stats) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  unsigned long long rays = 0, deps = 0;
+  if (i < count) {
+    ppm_math::Rng rng(seed, (unsigned long long)(first + i));
+    // Point_light::generate_photon (Point_light.cpp:7-30): theta = 2 pi e2 on purpose
+    V flux = ld(S.light_intensity) * (float)(M_PI * 4.0f);
+    const float e1 = rng.uniform01();
+    const float e2 = rng.uniform01();
+    const V w = mk(0.0f, 1.0f, 0.0f);
+    const V u = normalize((w.x != 0.0f || w.y != 0.0f) ? mk(-w.y, w.x, 0.0f) : mk(0.0f, 1.0f, 0.0f));
+    const V v = cross(w, u);
+    const float phi = (float)(2 * M_PI * (double)e1);
+    const float theta = (float)(2 * M_PI * (double)e2);
+    float st, ct, sp, cp;
+    ppm_math::sincosf_ieee(theta, st, ct);
+    ppm_math::sincosf_ieee(phi, sp, cp);
+    Ray ray{ld(S.light_pos), normalize((w * ct + (v * st) * cp) + (u * st) * sp)};
+    int depth = 0, k = 0;
+    for (;;) {
+      depth++;
+      if (depth >= S.max_depth) break;
+      Hit h;
+      rays++;
+      if (!closest(S, ray, h)) break;
+      const V x = point_at(ray, h.t);
+      const V normal = hit_normal(S, ray, h);
+      const PMaterial& m = S.materials[S.objects[h.obj].material];
+      if (m.type == kMatDiffuse) {
+        const V w_i = neg(normalize(ray.d));
+        PDeposit& d = slots[(size_t)i * K + k];
+        d.x[0] = x.x, d.x[1] = x.y, d.x[2] = x.z;
+        d.normal[0] = normal.x, d.normal[1] = normal.y, d.normal[2] = normal.z;
+        d.w_i[0] = w_i.x, d.w_i[1] = w_i.y, d.w_i[2] = w_i.z;
+        d.flux[0] = flux.x, d.flux[1] = flux.y, d.flux[2] = flux.z;
+        k++;
+        deps++;
+        // sample_hemisphere(normal) (Scene.cpp:15-44), cosine weighted
+        const float h1 = rng.uniform01();
+        const float h2 = rng.uniform01();
+        const V hu = normalize((normal.x != 0.0f || normal.y != 0.0f) ? mk(-normal.y, normal.x, 0.0f)
+                                                                      : mk(0.0f, 1.0f, 0.0f));
+        const V hv = cross(normal, hu);
+        const float hphi = (float)(2 * M_PI * (double)h1);
+        const float htheta = ppm_math::asinf_ieee(__builtin_sqrtf(h2));
+        float hst, hct, hsp, hcp;
+        ppm_math::sincosf_ieee(htheta, hst, hct);
+        ppm_math::sincosf_ieee(hphi, hsp, hcp);
+        const V dir = normalize((normal * hct + (hv * hst) * hcp) + (hu * hst) * hsp);
+        const float prob = (float)((double)fmax0(dot(normal, dir)) / M_PI);
+        // BRDF weight (Scene.cpp:173-194): nl from the incoming ray, as the reference
+        const V nl = dot(normal, ray.d) < 0 ? normal : normal * -1;
+        V base = mk(0.0f, 0.0f, 0.0f);
+        const float cos_i = fmax0(dot(normal, w_i));
+        if (m.brdf_id == -1 && !(cos_i > 1.0f || cos_i <= 0.0f)) {
+          const float sc = fmax0(dot(nl, normalize(dir + w_i)));
+          base = ld(m.diffuse) + (ld(m.specular) * ppm_math::powf_ieee(sc, m.phong)) / cos_i;
+        }
+        base = base * fmax0(dot(normal, dir));
+        if (!(rng.uniform01() < prob)) break;  // Russian roulette (Scene.cpp:196-199)
+        ray = Ray{x + (dir * S.eps), dir};
+        flux = (base * flux) / prob;
+      } else if (m.type == kMatMirror) {
+        const V w_o = normalize(ray.o - x);
+        const V w_r = normalize((normal * (2.0f * dot(normal, w_o))) - w_o);
+        ray = Ray{x + (w_r * S.eps), w_r};
+        flux = ld(m.mirror) * flux;
+      } else {
+        const Refraction R = refract_setup(S, ray, x, normal, m);
+        if (R.tir) ray = R.reflection;
+        else if (R.into) ray = rng.uniform01() < R.fresnel ? R.reflection : R.refraction;
+        else ray = R.refraction;
+      }
+    }
+    ndep[i] = k;
+  }
+  const unsigned long long tr = wave_sum(rays), td = wave_sum(deps);
+  if (stats && (threadIdx.x & 63) == 0) {
+    if (tr) atomicAdd(&stats[1], tr);
+    if (td) atomicAdd(&stats[2], td);
+  }
+}
+
+// Deposit d of photon i -> dense position offsets[i] + d, keyed by the bucket of its cell
+// (Scene.cpp:125-130); values are slot indices, increasing in photon order.
+__global__ __launch_bounds__(256) void deposit_keys_kernel(const PDeposit* slots,
+                                                           const int* ndep, const int* offsets,
+                                                           int count, int K,
+                                                           const PGrid* grid, unsigned* keys,
+                                                           unsigned* vals) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= count) return;
+  const PGrid G = *grid;
+  const int n = ndep[i], o = offsets[i];
+  for (int k = 0; k < n; k++) {
+    const unsigned s = (unsigned)((size_t)i * K + k);
+    const PDeposit& d = slots[s];
+    const V hh = (ld(d.x) - ld(G.bmin)) * G.hash_scale;
+    keys[o + k] = bucket_of(G, cell(hh.x), cell(hh.y), cell(hh.z));
+    vals[o + k] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void bucket_bounds_kernel(const unsigned* keys, int n,
+                                                            int* start, int* end) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= n) return;
+  const unsigned k = keys[i];
+  if (i == 0 || keys[i - 1] != k) start[k] = i;
+  if (i == n - 1 || keys[i + 1] != k) end[k] = i + 1;
+}
+
+// One lane per hit point: the buckets its (initial-radius) box was filed under
+// (Scene.cpp:79-91, with multiplicity when two cells share a bucket), their deposit runs
+// merged in photon order, each applied as Scene.cpp:131-168 does.
+__global__ __launch_bounds__(256) void hitpoint_update_kernel(
+    PScene S, const PHitPoint* hps, int n, const PGrid* grid, const PDeposit* slots,
+    const unsigned* vals, const int* start, const int* end, float4* state, unsigned* nupd,
+    unsigned long long* stats, int* error) {
+  const int h = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  unsigned long long applied = 0;
+  if (h < n) {
+    const PGrid G = *grid;
+    const PHitPoint hp = hps[h];
+    const V pos = ld(hp.pos), hn = ld(hp.normal), w_o = ld(hp.w_o), att = ld(hp.att);
+    const PMaterial m = S.materials[hp.material];
+    const V bmin = ((pos - G.radius) - ld(G.bmin)) * G.hash_scale;
+    const V bmax = ((pos + G.radius) - ld(G.bmin)) * G.hash_scale;
+    unsigned bucket[kMaxCells];
+    int mult[kMaxCells], cur[kMaxCells], stop[kMaxCells];
+    int nb = 0;
+    bool overflow = false;
+    for (int iz = cell(bmin.z); iz <= cell(bmax.z); iz++)
+      for (int iy = cell(bmin.y); iy <= cell(bmax.y); iy++)
+        for (int ix = cell(bmin.x); ix <= cell(bmax.x); ix++) {
+          const unsigned b = bucket_of(G, ix, iy, iz);
+          int u = 0;
+          while (u < nb && bucket[u] != b) u++;
+          if (u < nb) {
+            mult[u]++;
+          } else if (nb < kMaxCells) {
+            bucket[nb] = b;
+            mult[nb] = 1;
+            cur[nb] = start[b];
+            stop[nb] = end[b];
+            nb++;
+          } else {
+            overflow = true;
+          }
+        }
+    if (overflow) atomicExch(error, 1);
+    float4 st = state[h];
+    V flux = mk(st.x, st.y, st.z);
+    float r2 = st.w;
+    unsigned cnt = nupd[h];
+    for (;;) {
+      int best = -1;
+      unsigned bv = 0xffffffffu;
+      for (int u = 0; u < nb; u++)
+        if (cur[u] < stop[u] && vals[cur[u]] < bv) bv = vals[cur[u]], best = u;
+      if (best < 0) break;
+      cur[best]++;
+      const PDeposit d = slots[bv];
+      const V x = ld(d.x), dn = ld(d.normal), w_i = ld(d.w_i), pf = ld(d.flux);
+      for (int rep = 0; rep < mult[best]; rep++) {
+        const V v = pos - x;
+        if (!((dot(hn, dn) > 1e-3f) && (dot(v, v) <= r2))) continue;
+        const float nf = (float)cnt * kAlpha;
+        const float rr = (float)((double)(nf + kAlpha) / ((double)nf + 1.0));
+        r2 = r2 * rr;
+        cnt++;
+        applied++;
+        V color = mk(0.0f, 0.0f, 0.0f);
+        if (m.brdf_id == -1) {
+          const float cos_i = dot(hn, w_i);
+          if (!(cos_i > 1.0f || cos_i <= 0.0f)) {
+            const float sc = fmax0(dot(hn, normalize(w_o + w_i)));
+            color = (ld(m.diffuse) + (ld(m.specular) * ppm_math::powf_ieee(sc, m.phong)) / cos_i) *
+                    att;
+          }
+        }
+        flux = (flux + color * pf) * rr;
+      }
+    }
+    state[h] = make_float4(flux.x, flux.y, flux.z, r2);
+    nupd[h] = cnt;
+  }
+  const unsigned long long tot = wave_sum(applied);
+  if (stats && (threadIdx.x & 63) == 0 && tot) atomicAdd(&stats[3], tot);
+}
+
+// density_estimation + Pixel::get_color: a pixel's hit points are contiguous, in order.
+__global__ __launch_bounds__(256) void density_kernel(const PHitPoint* hps, const float4* state,
+                                                      const int* pix_offsets, int npix,
+                                                      double total, float* out) {
+  const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (p >= npix) return;
+  V col = mk(0.0f, 0.0f, 0.0f);
+  float wsum = 0.0f;
+  for (int k = pix_offsets[p]; k < pix_offsets[p + 1]; k++) {
+    const float4 st = state[k];
+    const float s = (float)(1.0f / ((M_PI * (double)st.w) * total));
+    const float w = hps[k].weight;
+    col = col + (mk(st.x, st.y, st.z) * s) * w;
+    wsum = wsum + w;
+  }
+  const V c = wsum == 0 ? mk(0.0f, 0.0f, 0.0f) : col / wsum;
+  out[3 * p] = c.x;
+  out[3 * p + 1] = c.y;
+  out[3 * p + 2] = c.z;
+}
+
+// ------------------------------------------------------------------ launchers (ppm_api.hip)
+constexpr int kThreads = 256;
+static int blocks_for(long long n) { return (int)((n + kThreads - 1) / kThreads); }
+
+hipError_t launch_eye(const PScene& S, const PCamera& C, unsigned long long seed, int* counts,
+                      const int* offsets, PHitPoint* out, unsigned long long* stats,
+                      hipStream_t st) {
+  hipLaunchKernelGGL(eye_kernel, dim3(blocks_for((long long)C.width * C.height)), dim3(kThreads),
+                     0, st, S, C, seed, counts, offsets, out, stats);
+  return hipGetLastError();
+}
+hipError_t launch_grid(const PHitPoint* hps, int n, int w, int h, PGrid* grid, float4* state,
+                       unsigned* counts, hipStream_t st) {
+  hipLaunchKernelGGL(grid_kernel, dim3(1), dim3(1024), 0, st, hps, n, w, h, grid, state, counts);
+  return hipGetLastError();
+}
+hipError_t launch_photons(const PScene& S, unsigned long long seed, long long first, int count,
+                          int K, PDeposit* slots, int* ndep, unsigned long long* stats,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(photon_kernel, dim3(blocks_for(count)), dim3(kThreads), 0, st, S, seed,
+                     first, count, K, slots, ndep, stats);
+  return hipGetLastError();
+}
+hipError_t launch_deposit_keys(const PDeposit* slots, const int* ndep, const int* offsets,
+                               int count, int K, const PGrid* grid, unsigned* keys,
+                               unsigned* vals, hipStream_t st) {
+  hipLaunchKernelGGL(deposit_keys_kernel, dim3(blocks_for(count)), dim3(kThreads), 0, st, slots,
+                     ndep, offsets, count, K, grid, keys, vals);
+  return hipGetLastError();
+}
+hipError_t launch_bucket_bounds(const unsigned* keys, int n, int* start, int* end,
+                                hipStream_t st) {
+  hipLaunchKernelGGL(bucket_bounds_kernel, dim3(blocks_for(n)), dim3(kThreads), 0, st, keys, n,
+                     start, end);
+  return hipGetLastError();
+}
+hipError_t launch_hitpoint_update(const PScene& S, const PHitPoint* hps, int n, const PGrid* grid,
+                                  const PDeposit* slots, const unsigned* vals, const int* start,
+                                  const int* end, float4* state, unsigned* nupd,
+                                  unsigned long long* stats, int* error, hipStream_t st) {
+  hipLaunchKernelGGL(hitpoint_update_kernel, dim3(blocks_for(n)), dim3(kThreads), 0, st, S, hps,
+                     n, grid, slots, vals, start, end, state, nupd, stats, error);
+  return hipGetLastError();
+}
+hipError_t launch_density(const PHitPoint* hps, const float4* state, const int* pix_offsets,
+                          int npix, double total, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(density_kernel, dim3(blocks_for(npix)), dim3(kThreads), 0, st, hps, state,
+                     pix_offsets, npix, total, out);
+  return hipGetLastError();
+}
+
+}  // namespace ppm

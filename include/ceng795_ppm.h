@@ -1,0 +1,89 @@
+/* ceng795_ppm.h — C ABI of the MI355X progressive-photon-mapping path (BASELINE config C5).
+ *
+ * Replaces the reference's PPM Scene passes (PPM/include/Scene.h:44-56, PPM/src/Scene.cpp):
+ *   Scene::Scene(xml)                       -> ppm_scene_load_xml             (Scene.cpp:373)
+ *   reset_hash_grid + eye_trace_lines       -> ppm_eye_pass                   (Scene.cpp:46, 250)
+ *   build_hash_grid(width, height)          -> ppm_build_hash_grid            (Scene.cpp:53)
+ *   trace_n_photons(n, iterations)          -> ppm_trace_photons              (Scene.cpp:95)
+ *   density_estimation(pixels, total)       -> ppm_density_estimation         (Scene.cpp:363)
+ *   main.cpp:30-104 for one camera          -> ppm_render
+ * The reference runs these on T host threads (main.cpp:36-90); here each is one or a few HIP
+ * launches.  Hit points, the hash grid and the photon deposits stay in device memory.
+ *
+ * Results are those of the reference run on ONE thread (pixels row-major, photons in order,
+ * each photon's hit-point updates applied before the next photon's), with two documented
+ * substitutions for the reference's non-reproducible parts: random numbers come from a
+ * per-photon SplitMix64 stream (seed, photon index) instead of random_device-seeded mt19937,
+ * and sinf/cosf/asinf/powf are correctly rounded (ceng795_amd/csrc/ppm_math.h).  The photon
+ * sequence is therefore a pure function of (scene, seed, photon index range).
+ *
+ * Error codes are the RT_E* values of ceng795_rt.h; messages via ppm_last_error().
+ */
+#ifndef CENG795_PPM_H_
+#define CENG795_PPM_H_
+#include "ceng795_rt.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CENG795_PPM_ABI_VERSION 1
+
+typedef struct ppm_scene ppm_scene;
+
+typedef struct ppm_stats {
+  long long photons;      /* photons emitted                                     */
+  long long photon_rays;  /* photon segments traced (closest-hit queries)        */
+  long long deposits;     /* diffuse photon hits (hash-cell lookups)             */
+  long long updates;      /* hit-point radius / flux updates applied             */
+  long long eye_rays;     /* eye-pass closest-hit queries                        */
+  long long hit_points;
+  double eye_ms, grid_ms, photon_ms, density_ms;  /* device time of each pass (ppm_render) */
+} ppm_stats;
+
+int ppm_abi_version(void);
+const char* ppm_last_error(void);
+
+/* PPM/src/Scene.cpp:373-505 (+ Camera / Material / Transformation / Point_light / Sphere /
+ * Mesh loaders) and the BVH builds; uploads to HIP device `device`. */
+int ppm_scene_load_xml(const char* xml_path, int device, ppm_scene** out);
+void ppm_scene_destroy(ppm_scene* scene);
+int ppm_num_cameras(const ppm_scene* scene);
+int ppm_camera_info(const ppm_scene* scene, int camera, int* width, int* height,
+                    int* num_samples);
+const char* ppm_image_name(const ppm_scene* scene, int camera);
+/* PhotonCountPerIteration, NumberOfIterations, MaxRecursionDepth (Scene.cpp:388-430). */
+int ppm_settings(const ppm_scene* scene, int* per_iteration, int* iterations, int* max_depth);
+int ppm_set_seed(ppm_scene* scene, unsigned long long seed);
+
+/* reset_hash_grid + eye_trace_lines over all rows: builds the hit points. */
+int ppm_eye_pass(ppm_scene* scene, int camera);
+/* build_hash_grid; info8 (nullable) receives {initial radius, hash scale, grid bbox min xyz,
+ * max xyz}. */
+int ppm_build_hash_grid(ppm_scene* scene, int width, int height, double* info8);
+int ppm_num_hit_points(const ppm_scene* scene);
+/* 16 floats per hit point: position, normal, w_o, attenuation, pixel, pixel_weight,
+ * radius_squared, material type (the layout oracle/_ref/ppm_harness `hitpoints` writes). */
+int ppm_read_hit_points(ppm_scene* scene, float* out16);
+/* 5 floats per hit point: flux xyz, radius_squared, n. */
+int ppm_read_hit_state(ppm_scene* scene, float* out5);
+/* Photons [first, first + count) of the scene's photon sequence (trace_n_photons). */
+int ppm_trace_photons(ppm_scene* scene, long long first, long long count);
+/* density_estimation(pixels, total) + Pixel::get_color into out_rgb (w*h*3, host memory). */
+int ppm_density_estimation(ppm_scene* scene, long long total_num_of_photons, float* out_rgb);
+
+/* main.cpp:30-104 for one camera with the photon budget and normaliser the reference uses on
+ * `reference_threads` host threads: traces T*(P/T)*I photons (P*I when height < T) and
+ * normalises by P*(P/T)*T (main.cpp:74, 94).  Synchronous; stats nullable. */
+int ppm_render(ppm_scene* scene, int camera, int reference_threads, float* out_rgb,
+               ppm_stats* stats);
+/* Reads (and resets) the device counters of the passes run since the last call. */
+int ppm_collect_stats(ppm_scene* scene, ppm_stats* stats);
+
+/* main.cpp:142-156 (no tone-mapping operator): c -> int(pow(1 - exp(-c), 1/2.2f)*255 + 0.5f),
+ * clamped to [0, 255], RGBA8 PNG. */
+int ppm_write_png(const char* path, const float* rgb, int width, int height);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

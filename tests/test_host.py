@@ -173,3 +173,17 @@ def test_defaults_match_reference(scene_dir, tmp_path):
                  lambda t: re.sub(r"\s*<(BackgroundColor|ShadowRayEpsilon|MaxRecursionDepth)>.*?</\1>",
                                   "", t))
     assert _dump_rc(v, tmp_path) == 0
+
+
+def test_ppm_library_exports_every_declared_function():
+    from ceng795_amd import ppm
+    text = open(os.path.join(ROOT, "include", "ceng795_ppm.h")).read()
+    names = sorted(set(re.findall(r"^\s*(?:int|void|const char\s*\*)\s*(ppm_\w+)\s*\(", text, re.M)))
+    assert len(names) >= 18
+    L = ppm.lib()
+    for n in names:
+        assert hasattr(L, n), n
+        assert n in ppm.SIGNATURES, f"{n} missing from the ctypes table"
+    assert L.ppm_abi_version() == ppm.ABI_VERSION
+    data = open(ppm.LIB_PATH, "rb").read()
+    assert b"ppmref_" not in data and b"libppm_ref" not in data and b"cpuref_" not in data
