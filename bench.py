@@ -4,6 +4,7 @@ the ~1M-triangle height field (BASELINE.json configs[2], "C3"), plus the HBM-roo
 of the render kernel and the reference CPU path timed on this box's host cores.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py --workload c5        (photon mapping, tools/bench_ppm.py)
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
 One step = one full render of every camera in the job: N frames of 1920x1080 for N ranks.
@@ -117,7 +118,8 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS) + ["c5"],
+                    help="c5: the photon-mapping Cornell box (tools/bench_ppm.py), 1 GPU")
     ap.add_argument("--traversal", default="fast", choices=["fast", "reference"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -125,6 +127,13 @@ def main() -> int:
     ap.add_argument("--no-verify", action="store_true",
                     help="skip rank 0's bit-for-bit check of the gathered frames")
     args = ap.parse_args()
+    if args.workload == "c5":
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            log("c5 (photon mapping) is a one-GPU configuration (BASELINE.json configs[4])")
+            return 2
+        import bench_ppm
+        print(json.dumps(bench_ppm.run(args.steps, args.warmup, not args.no_cpu_baseline)))
+        return 0
 
     import torch
     import torch.distributed as dist

@@ -25,9 +25,16 @@ hipError_t launch_photons(const PScene&, unsigned long long, long long, int, int
 hipError_t launch_deposit_keys(const PDeposit*, const int*, const int*, int, int, const PGrid*,
                                unsigned*, unsigned*, hipStream_t);
 hipError_t launch_bucket_bounds(const unsigned*, int, int*, int*, hipStream_t);
-hipError_t launch_hitpoint_update(const PScene&, const PHitPoint*, int, const PGrid*,
-                                  const PDeposit*, const unsigned*, const int*, const int*,
-                                  float4*, unsigned*, unsigned long long*, int*, hipStream_t);
+hipError_t launch_group_keys(const PHitPoint*, int, const PGrid*, unsigned long long*, int*, int*,
+                            hipStream_t);
+hipError_t launch_group_flags(const unsigned long long*, int, int*, hipStream_t);
+hipError_t launch_group_starts(const int*, const int*, int, int*, hipStream_t);
+hipError_t launch_group_tiles(const int*, int, int*, hipStream_t);
+hipError_t launch_tile_table(const int*, const int*, int, int2*, hipStream_t);
+hipError_t launch_group_update(const PScene&, const PHitPoint*, const int*, const int*,
+                               const int2*, int, const PGrid*, const PDeposit*, const unsigned*,
+                               const int*, const int*, float4*, unsigned*, unsigned long long*,
+                               hipStream_t);
 hipError_t launch_density(const PHitPoint*, const float4*, const int*, int, double, float*,
                           hipStream_t);
 }  // namespace ppm
@@ -110,7 +117,9 @@ struct DeviceGuard {
   }
 };
 
-constexpr size_t kSlotBytesPerBatch = size_t(1536) << 20;  // deposit slot rows per batch
+// Deposit slot rows per photon batch: 8 GiB holds C5's 1e7 photons x 19 slots in one batch
+// (one sort, one update launch); HBM is 288 GB.
+constexpr size_t kSlotBytesPerBatch = size_t(8) << 30;
 
 }  // namespace
 
@@ -131,6 +140,10 @@ struct ppm_scene {
   DevBuf<int> pix_cnt, pix_off;
   DevBuf<PGrid> grid;
   DevBuf<int> bstart, bend;
+  DevBuf<unsigned long long> gkeys, gkeys2;  // hit-point groups (same hash-cell range)
+  DevBuf<int> gidx, perm, gflags, gid, gstart, ntile, tile_off;
+  DevBuf<int2> tiles;
+  int n_groups = 0, n_tiles = 0;
   // photon batches
   DevBuf<PDeposit> slots;
   DevBuf<int> ndep, dep_off;
@@ -146,6 +159,8 @@ struct ppm_scene {
     owned.clear();
     hp.release(), state.release(), nupd.release(), pix_cnt.release(), pix_off.release();
     grid.release(), bstart.release(), bend.release(), slots.release(), ndep.release();
+    gkeys.release(), gkeys2.release(), gidx.release(), perm.release(), gflags.release();
+    gid.release(), gstart.release(), ntile.release(), tile_off.release(), tiles.release();
     dep_off.release(), keys.release(), vals.release(), keys2.release(), vals2.release();
     temp.release(), stats.release(), error.release(), image.release();
     if (stream) (void)hipStreamDestroy(stream);
@@ -224,10 +239,64 @@ void eye_pass(ppm_scene* s, int cam) {
 
 void build_grid(ppm_scene* s, int width, int height) {
   if (s->eye_cam < 0) throw std::invalid_argument("build_hash_grid before the eye pass");
-  hip_check(launch_grid(s->hp.p, s->n_hp, width, height, s->grid.p, s->state.p, s->nupd.p,
-                        s->stream), "build hash grid");
-  s->bstart.reserve(std::max(1, s->n_hp), "alloc bucket starts");
-  s->bend.reserve(std::max(1, s->n_hp), "alloc bucket ends");
+  const int n = s->n_hp;
+  hip_check(launch_grid(s->hp.p, n, width, height, s->grid.p, s->state.p, s->nupd.p, s->stream),
+            "build hash grid");
+  s->bstart.reserve(std::max(1, n), "alloc bucket starts");
+  s->bend.reserve(std::max(1, n), "alloc bucket ends");
+  s->n_groups = 0;
+  if (n > 0) {  // group the hit points by hash-cell range (group_update_kernel)
+    s->gkeys.reserve(n, "alloc group keys");
+    s->gkeys2.reserve(n, "alloc group keys");
+    s->gidx.reserve(n, "alloc group index");
+    s->perm.reserve(n, "alloc group permutation");
+    s->gflags.reserve(n + 1, "alloc group flags");
+    s->gid.reserve(n + 1, "alloc group ids");
+    s->gstart.reserve(n + 1, "alloc group starts");
+    hip_check(launch_group_keys(s->hp.p, n, s->grid.p, s->gkeys.p, s->gidx.p, s->error.p,
+                                s->stream), "group keys");
+    size_t bytes = 0;
+    hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, s->gkeys.p, s->gkeys2.p, s->gidx.p,
+                                                 s->perm.p, n, 0, 64, s->stream), "sort size");
+    s->temp.reserve(bytes, "alloc sort temp");
+    hip_check(hipcub::DeviceRadixSort::SortPairs(s->temp.p, bytes, s->gkeys.p, s->gkeys2.p,
+                                                 s->gidx.p, s->perm.p, n, 0, 64, s->stream),
+              "sort hit points by cell range");
+    hip_check(launch_group_flags(s->gkeys2.p, n, s->gflags.p, s->stream), "group flags");
+    bytes = 0;
+    hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, s->gflags.p, s->gid.p, n + 1,
+                                               s->stream), "scan size");
+    s->temp.reserve(bytes, "alloc scan temp");
+    hip_check(hipcub::DeviceScan::ExclusiveSum(s->temp.p, bytes, s->gflags.p, s->gid.p, n + 1,
+                                               s->stream), "scan groups");
+    hip_check(launch_group_starts(s->gflags.p, s->gid.p, n, s->gstart.p, s->stream), "group starts");
+    int groups = 0, err = 0;
+    hip_check(hipMemcpyAsync(&groups, s->gid.p + n, sizeof(int), hipMemcpyDeviceToHost, s->stream),
+              "read group count");
+    hip_check(hipMemcpyAsync(&err, s->error.p, sizeof(int), hipMemcpyDeviceToHost, s->stream),
+              "read error flag");
+    hip_check(hipStreamSynchronize(s->stream), "group hit points");
+    if (err) throw std::domain_error("a hit point's radius box spans more hash cells than supported");
+    s->n_groups = groups;
+    // tiles of <= 16 hit points per group (group_update_kernel)
+    s->ntile.reserve(groups + 1, "alloc tile counts");
+    s->tile_off.reserve(groups + 1, "alloc tile offsets");
+    hip_check(launch_group_tiles(s->gstart.p, groups, s->ntile.p, s->stream), "group tiles");
+    bytes = 0;
+    hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, s->ntile.p, s->tile_off.p, groups + 1,
+                                               s->stream), "scan size");
+    s->temp.reserve(bytes, "alloc scan temp");
+    hip_check(hipcub::DeviceScan::ExclusiveSum(s->temp.p, bytes, s->ntile.p, s->tile_off.p,
+                                               groups + 1, s->stream), "scan tiles");
+    int ntiles = 0;
+    hip_check(hipMemcpyAsync(&ntiles, s->tile_off.p + groups, sizeof(int), hipMemcpyDeviceToHost,
+                             s->stream), "read tile count");
+    hip_check(hipStreamSynchronize(s->stream), "tile count");
+    s->tiles.reserve(std::max(1, ntiles), "alloc tiles");
+    hip_check(launch_tile_table(s->gstart.p, s->tile_off.p, groups, s->tiles.p, s->stream),
+              "tile table");
+    s->n_tiles = ntiles;
+  }
   s->grid_ready = true;
 }
 
@@ -277,9 +346,10 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
         hip_check(hipMemsetAsync(s->bend.p, 0, H * sizeof(int), s->stream), "zero buckets");
         hip_check(launch_bucket_bounds(s->keys2.p, D, s->bstart.p, s->bend.p, s->stream),
                   "bucket bounds");
-        hip_check(launch_hitpoint_update(s->S, s->hp.p, H, s->grid.p, s->slots.p, s->vals2.p,
-                                         s->bstart.p, s->bend.p, s->state.p, s->nupd.p,
-                                         s->stats.p, s->error.p, s->stream),
+        hip_check(launch_group_update(s->S, s->hp.p, s->perm.p, s->gstart.p, s->tiles.p, s->n_tiles,
+                                      s->grid.p,
+                                      s->slots.p, s->vals2.p, s->bstart.p, s->bend.p, s->state.p,
+                                      s->nupd.p, s->stats.p, s->stream),
                   "hit-point updates");
       }
     }
@@ -290,7 +360,7 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
   hip_check(hipMemcpyAsync(&err, s->error.p, sizeof(int), hipMemcpyDeviceToHost, s->stream),
             "read error flag");
   hip_check(hipStreamSynchronize(s->stream), "photon pass");
-  if (err) throw std::domain_error("a hit point's radius box spans more than 27 hash cells");
+  if (err) throw std::domain_error("photon pass: device error flag set");
 }
 
 void density(ppm_scene* s, long long total, float* out) {

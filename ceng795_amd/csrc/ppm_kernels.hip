@@ -13,9 +13,10 @@
 //   deposit_keys_kernel      compacts the deposits in (photon, bounce) order and keys each by
 //                            the hash bucket of its cell (Scene.cpp:125-130).
 //   (hipcub stable radix sort by bucket -> per-bucket deposit runs in photon order)
-//   hitpoint_update_kernel   the radius / flux updates of Scene.cpp:131-168, turned inside out:
-//                            one lane per hit point merges the deposit runs of the buckets its
-//                            radius box was filed under and applies them in photon order.
+//   group_update_kernel      the radius / flux updates of Scene.cpp:131-168, turned inside out:
+//                            hit points filed under the same buckets form a group; one wave per
+//                            group merges those buckets' deposit runs in photon order through
+//                            LDS and each lane applies them to its own hit point.
 //   density_kernel           density_estimation + Pixel::get_color (Scene.cpp:363-371).
 //
 // Why the update pass is exact: a photon's path never reads hit-point state, so the reference's
@@ -596,83 +597,271 @@ __global__ __launch_bounds__(256) void bucket_bounds_kernel(const unsigned* keys
   if (i == n - 1 || keys[i + 1] != k) end[k] = i + 1;
 }
 
-// One lane per hit point: the buckets its (initial-radius) box was filed under
-// (Scene.cpp:79-91, with multiplicity when two cells share a bucket), their deposit runs
-// merged in photon order, each applied as Scene.cpp:131-168 does.
-__global__ __launch_bounds__(256) void hitpoint_update_kernel(
-    PScene S, const PHitPoint* hps, int n, const PGrid* grid, const PDeposit* slots,
-    const unsigned* vals, const int* start, const int* end, float4* state, unsigned* nupd,
-    unsigned long long* stats, int* error) {
+// ------------------------------------------------------------------ grouped update pass
+// Hit points whose radius boxes cover the same cell range were filed under the same buckets,
+// so they see the same deposit stream.  group_key_kernel keys each hit point by its range
+// (lower cell corner + extent); a radix sort groups them; group_update_kernel then runs one
+// wave per group: it merges the group's bucket runs in photon order through LDS once and
+// every lane (hit point) applies the merged stream to its own state.
+__global__ __launch_bounds__(256) void group_key_kernel(const PHitPoint* hps, int n,
+                                                        const PGrid* grid,
+                                                        unsigned long long* keys, int* idx,
+                                                        int* error) {
   const int h = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  unsigned long long applied = 0;
-  if (h < n) {
-    const PGrid G = *grid;
-    const PHitPoint hp = hps[h];
-    const V pos = ld(hp.pos), hn = ld(hp.normal), w_o = ld(hp.w_o), att = ld(hp.att);
-    const PMaterial m = S.materials[hp.material];
+  if (h >= n) return;
+  const PGrid G = *grid;
+  const V pos = ld(hps[h].pos);
+  const V bmin = ((pos - G.radius) - ld(G.bmin)) * G.hash_scale;
+  const V bmax = ((pos + G.radius) - ld(G.bmin)) * G.hash_scale;
+  const int x0 = cell(bmin.x), y0 = cell(bmin.y), z0 = cell(bmin.z);
+  const int dx = cell(bmax.x) - x0, dy = cell(bmax.y) - y0, dz = cell(bmax.z) - z0;
+  if (x0 > 0xffff || y0 > 0xffff || z0 > 0xffff || dx < 0 || dy < 0 || dz < 0 || dx > 31 ||
+      dy > 31 || dz > 31 || (dx + 1) * (dy + 1) * (dz + 1) > kMaxCells)
+    atomicExch(error, 2);
+  keys[h] = (unsigned long long)(x0 & 0xffff) | (unsigned long long)(y0 & 0xffff) << 16 |
+            (unsigned long long)(z0 & 0xffff) << 32 | (unsigned long long)(dx & 31) << 48 |
+            (unsigned long long)(dy & 31) << 53 | (unsigned long long)(dz & 31) << 58;
+  idx[h] = h;
+}
+
+__global__ __launch_bounds__(256) void group_flags_kernel(const unsigned long long* keys, int n,
+                                                          int* flags) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i < n) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+  if (i == n) flags[n] = 0;
+}
+
+__global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, const int* gid,
+                                                           int n, int* gstart) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i < n && flags[i]) gstart[gid[i]] = i;
+  if (i == n) gstart[gid[n]] = n;  // gid[n] = number of groups
+}
+
+constexpr int kTileHP = 16;   // hit points per update workgroup
+constexpr int kWinMax = 1024; // merged deposits per window
+constexpr int kUpdThreads = 256;
+
+__global__ __launch_bounds__(256) void group_tiles_kernel(const int* gstart, int groups,
+                                                          int* ntile) {
+  const int g = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (g < groups) ntile[g] = (gstart[g + 1] - gstart[g] + kTileHP - 1) / kTileHP;
+  if (g == groups) ntile[groups] = 0;
+}
+
+__global__ __launch_bounds__(256) void tile_table_kernel(const int* gstart, const int* tile_off,
+                                                         int groups, int2* tiles) {
+  const int g = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (g >= groups) return;
+  for (int t = tile_off[g]; t < tile_off[g + 1]; t++)
+    tiles[t] = make_int2(g, gstart[g] + (t - tile_off[g]) * kTileHP);
+}
+
+__device__ __forceinline__ int lower_bound_lds(const unsigned* a, int n, unsigned v) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// One workgroup per (group, tile of <= 16 hit points).  The group's bucket runs are merged in
+// photon order in windows of <= 1024 deposits (each run contributes in proportion to what it
+// has left; every slot <= the smallest "last loaded" slot of a run that continues is final).
+// For each window: all 256 threads test (hit point, deposit) pairs against the radius^2 the
+// hit point had at the window start — a superset of the deposits that will pass, since the
+// radius only shrinks — into bitmasks; then one thread per hit point walks its bits in order
+// and applies Scene.cpp:136-168 exactly (radius re-tested with the running value).
+__global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
+    PScene S, const PHitPoint* hps, const int* perm, const int* gstart, const int2* tiles,
+    const PGrid* grid, const PDeposit* slots, const unsigned* vals, const int* bstart,
+    const int* bend, float4* state, unsigned* nupd, unsigned long long* stats) {
+  __shared__ unsigned s_bucket[kMaxCells];
+  __shared__ int s_mult[kMaxCells], s_cur[kMaxCells], s_stop[kMaxCells], s_take[kMaxCells];
+  __shared__ int s_off[kMaxCells + 1], s_emit[kMaxCells];
+  __shared__ int s_nb, s_total, s_loaded;
+  __shared__ unsigned s_limit;
+  __shared__ unsigned s_cat[kWinMax];
+  __shared__ unsigned char s_catrun[kWinMax];
+  __shared__ unsigned s_out[kWinMax];
+  __shared__ unsigned char s_run[kWinMax];
+  __shared__ float s_x[kWinMax][3], s_n[kWinMax][3];
+  __shared__ unsigned s_mask[kTileHP][kWinMax / 32];
+  __shared__ float s_pos[kTileHP][3], s_hn[kTileHP][3], s_r2[kTileHP];
+  const int tid = (int)threadIdx.x;
+  const int2 tile = tiles[blockIdx.x];
+  const int g = tile.x, first = tile.y;
+  const int nh = min(kTileHP, gstart[g + 1] - first);
+  const PGrid G = *grid;
+  if (tid == 0) {  // the group's buckets (Scene.cpp:79-91), deduplicated with multiplicity
+    const V pos = ld(hps[perm[gstart[g]]].pos);
     const V bmin = ((pos - G.radius) - ld(G.bmin)) * G.hash_scale;
     const V bmax = ((pos + G.radius) - ld(G.bmin)) * G.hash_scale;
-    unsigned bucket[kMaxCells];
-    int mult[kMaxCells], cur[kMaxCells], stop[kMaxCells];
     int nb = 0;
-    bool overflow = false;
     for (int iz = cell(bmin.z); iz <= cell(bmax.z); iz++)
       for (int iy = cell(bmin.y); iy <= cell(bmax.y); iy++)
         for (int ix = cell(bmin.x); ix <= cell(bmax.x); ix++) {
           const unsigned b = bucket_of(G, ix, iy, iz);
           int u = 0;
-          while (u < nb && bucket[u] != b) u++;
-          if (u < nb) {
-            mult[u]++;
-          } else if (nb < kMaxCells) {
-            bucket[nb] = b;
-            mult[nb] = 1;
-            cur[nb] = start[b];
-            stop[nb] = end[b];
-            nb++;
-          } else {
-            overflow = true;
-          }
+          while (u < nb && s_bucket[u] != b) u++;
+          if (u < nb) s_mult[u]++;
+          else if (nb < kMaxCells) s_bucket[nb] = b, s_mult[nb] = 1, nb++;
         }
-    if (overflow) atomicExch(error, 1);
-    float4 st = state[h];
-    V flux = mk(st.x, st.y, st.z);
-    float r2 = st.w;
-    unsigned cnt = nupd[h];
-    for (;;) {
-      int best = -1;
-      unsigned bv = 0xffffffffu;
-      for (int u = 0; u < nb; u++)
-        if (cur[u] < stop[u] && vals[cur[u]] < bv) bv = vals[cur[u]], best = u;
-      if (best < 0) break;
-      cur[best]++;
-      const PDeposit d = slots[bv];
-      const V x = ld(d.x), dn = ld(d.normal), w_i = ld(d.w_i), pf = ld(d.flux);
-      for (int rep = 0; rep < mult[best]; rep++) {
-        const V v = pos - x;
-        if (!((dot(hn, dn) > 1e-3f) && (dot(v, v) <= r2))) continue;
-        const float nf = (float)cnt * kAlpha;
-        const float rr = (float)((double)(nf + kAlpha) / ((double)nf + 1.0));
-        r2 = r2 * rr;
-        cnt++;
-        applied++;
-        V color = mk(0.0f, 0.0f, 0.0f);
-        if (m.brdf_id == -1) {
-          const float cos_i = dot(hn, w_i);
-          if (!(cos_i > 1.0f || cos_i <= 0.0f)) {
-            const float sc = fmax0(dot(hn, normalize(w_o + w_i)));
-            color = (ld(m.diffuse) + (ld(m.specular) * ppm_math::powf_ieee(sc, m.phong)) / cos_i) *
-                    att;
-          }
+    s_nb = nb;
+  }
+  __syncthreads();
+  const int nb = s_nb;
+  if (tid < nb) s_cur[tid] = bstart[s_bucket[tid]], s_stop[tid] = bend[s_bucket[tid]];
+  // the gate threads own their hit point's state
+  const int h = tid < nh ? perm[first + tid] : -1;
+  V w_o = mk(0, 0, 0), att = w_o, flux = w_o, pos = w_o, hn = w_o;
+  float r2 = 0.0f;
+  unsigned cnt = 0;
+  PMaterial m{};
+  if (h >= 0) {
+    const PHitPoint hp = hps[h];
+    pos = ld(hp.pos), hn = ld(hp.normal), w_o = ld(hp.w_o), att = ld(hp.att);
+    m = S.materials[hp.material];
+    const float4 st = state[h];
+    flux = mk(st.x, st.y, st.z);
+    r2 = st.w;
+    cnt = nupd[h];
+    for (int a = 0; a < 3; a++) s_pos[tid][a] = hp.pos[a], s_hn[tid][a] = hp.normal[a];
+    s_r2[tid] = r2;
+  }
+  unsigned long long applied = 0;
+  __syncthreads();
+  for (;;) {
+    // (1) plan the window: each run contributes in proportion to what it has left
+    if (tid == 0) {
+      long long rem_total = 0;
+      for (int u = 0; u < nb; u++) rem_total += s_stop[u] - s_cur[u];
+      int off = 0;
+      for (int u = 0; u < nb; u++) {
+        const int rem = s_stop[u] - s_cur[u];
+        int take = rem;
+        if (rem_total > kWinMax) {
+          take = (int)((long long)(kWinMax - nb) * rem / rem_total);
+          if (take < 1 && rem > 0) take = 1;
         }
-        flux = (flux + color * pf) * rr;
+        s_take[u] = take;
+        s_off[u] = off;
+        off += take;
       }
+      s_off[nb] = off;
+      s_loaded = off;
     }
+    __syncthreads();
+    if (s_loaded == 0) break;
+    // (2) load the slices
+    for (int u = 0; u < nb; u++)
+      for (int i = tid; i < s_take[u]; i += kUpdThreads) {
+        s_cat[s_off[u] + i] = vals[s_cur[u] + i];
+        s_catrun[s_off[u] + i] = (unsigned char)u;
+      }
+    __syncthreads();
+    // (3) everything <= limit is final
+    if (tid == 0) {
+      unsigned limit = 0xffffffffu;
+      for (int u = 0; u < nb; u++)
+        if (s_take[u] > 0 && s_cur[u] + s_take[u] < s_stop[u])
+          limit = min(limit, s_cat[s_off[u] + s_take[u] - 1]);
+      int total = 0;
+      for (int u = 0; u < nb; u++) {
+        const int k = limit == 0xffffffffu ? s_take[u]
+                                           : lower_bound_lds(s_cat + s_off[u], s_take[u], limit + 1);
+        s_emit[u] = k;
+        total += k;
+      }
+      s_limit = limit;
+      s_total = total;
+    }
+    __syncthreads();
+    const unsigned limit = s_limit;
+    const int total = s_total;
+    // (4) merge by rank (slots are distinct across runs: one bucket per deposit)
+    for (int i = tid; i < s_loaded; i += kUpdThreads) {
+      const unsigned e = s_cat[i];
+      if (e > limit) continue;
+      const int u = s_catrun[i];
+      int rank = i - s_off[u];
+      for (int v = 0; v < nb; v++)
+        if (v != u) rank += lower_bound_lds(s_cat + s_off[v], s_take[v], e);
+      s_out[rank] = e;
+      s_run[rank] = (unsigned char)u;
+    }
+    __syncthreads();
+    // (5) positions and normals of the window's deposits
+    for (int k = tid; k < total; k += kUpdThreads) {
+      const PDeposit& d = slots[s_out[k]];
+      for (int a = 0; a < 3; a++) s_x[k][a] = d.x[a], s_n[k][a] = d.normal[a];
+    }
+    __syncthreads();
+    // (6) superset filter with the window-start radius
+    const int nwords = (total + 31) >> 5;
+    for (int p = tid; p < nh * nwords; p += kUpdThreads) {
+      const int j = p / nwords, w = p % nwords;
+      const V hp_pos = mk(s_pos[j][0], s_pos[j][1], s_pos[j][2]);
+      const V hp_n = mk(s_hn[j][0], s_hn[j][1], s_hn[j][2]);
+      const float rr2 = s_r2[j];
+      unsigned bits = 0;
+      const int kend = min(32, total - w * 32);
+      for (int b = 0; b < kend; b++) {
+        const int k = w * 32 + b;
+        const V v = hp_pos - mk(s_x[k][0], s_x[k][1], s_x[k][2]);
+        const V dn = mk(s_n[k][0], s_n[k][1], s_n[k][2]);
+        if ((dot(hp_n, dn) > 1e-3f) && (dot(v, v) <= rr2)) bits |= 1u << b;
+      }
+      s_mask[j][w] = bits;
+    }
+    __syncthreads();
+    // (7) exact, in-order application per hit point
+    if (h >= 0) {
+      for (int w = 0; w < nwords; w++) {
+        unsigned bits = s_mask[tid][w];
+        while (bits) {
+          const int b = __builtin_ctz(bits);
+          bits &= bits - 1;
+          const int k = w * 32 + b;
+          const V x = mk(s_x[k][0], s_x[k][1], s_x[k][2]), dn = mk(s_n[k][0], s_n[k][1], s_n[k][2]);
+          const int reps = s_mult[s_run[k]];
+          const PDeposit& d = slots[s_out[k]];
+          for (int rep = 0; rep < reps; rep++) {
+            const V v = pos - x;
+            if (!((dot(hn, dn) > 1e-3f) && (dot(v, v) <= r2))) continue;
+            const V w_i = ld(d.w_i), pf = ld(d.flux);
+            const float nf = (float)cnt * kAlpha;
+            const float rr = (float)((double)(nf + kAlpha) / ((double)nf + 1.0));
+            r2 = r2 * rr;
+            cnt++;
+            applied++;
+            V color = mk(0.0f, 0.0f, 0.0f);
+            if (m.brdf_id == -1) {
+              const float cos_i = dot(hn, w_i);
+              if (!(cos_i > 1.0f || cos_i <= 0.0f)) {
+                const float sc = fmax0(dot(hn, normalize(w_o + w_i)));
+                color = (ld(m.diffuse) + (ld(m.specular) * ppm_math::powf_ieee(sc, m.phong)) / cos_i) *
+                        att;
+              }
+            }
+            flux = (flux + color * pf) * rr;
+          }
+        }
+      }
+      s_r2[tid] = r2;
+    }
+    // (8) advance the runs
+    if (tid < nb) s_cur[tid] += s_emit[tid];
+    __syncthreads();
+  }
+  if (h >= 0) {
     state[h] = make_float4(flux.x, flux.y, flux.z, r2);
     nupd[h] = cnt;
   }
   const unsigned long long tot = wave_sum(applied);
-  if (stats && (threadIdx.x & 63) == 0 && tot) atomicAdd(&stats[3], tot);
+  if (stats && (tid & 63) == 0 && tot) atomicAdd(&stats[3], tot);
 }
 
 // density_estimation + Pixel::get_color: a pixel's hit points are contiguous, in order.
@@ -732,12 +921,42 @@ hipError_t launch_bucket_bounds(const unsigned* keys, int n, int* start, int* en
                      start, end);
   return hipGetLastError();
 }
-hipError_t launch_hitpoint_update(const PScene& S, const PHitPoint* hps, int n, const PGrid* grid,
-                                  const PDeposit* slots, const unsigned* vals, const int* start,
-                                  const int* end, float4* state, unsigned* nupd,
-                                  unsigned long long* stats, int* error, hipStream_t st) {
-  hipLaunchKernelGGL(hitpoint_update_kernel, dim3(blocks_for(n)), dim3(kThreads), 0, st, S, hps,
-                     n, grid, slots, vals, start, end, state, nupd, stats, error);
+hipError_t launch_group_keys(const PHitPoint* hps, int n, const PGrid* grid,
+                            unsigned long long* keys, int* idx, int* error, hipStream_t st) {
+  hipLaunchKernelGGL(group_key_kernel, dim3(blocks_for(n)), dim3(kThreads), 0, st, hps, n, grid,
+                     keys, idx, error);
+  return hipGetLastError();
+}
+hipError_t launch_group_flags(const unsigned long long* keys, int n, int* flags, hipStream_t st) {
+  hipLaunchKernelGGL(group_flags_kernel, dim3(blocks_for(n + 1)), dim3(kThreads), 0, st, keys, n,
+                     flags);
+  return hipGetLastError();
+}
+hipError_t launch_group_starts(const int* flags, const int* gid, int n, int* gstart,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(group_starts_kernel, dim3(blocks_for(n + 1)), dim3(kThreads), 0, st, flags,
+                     gid, n, gstart);
+  return hipGetLastError();
+}
+hipError_t launch_group_tiles(const int* gstart, int groups, int* ntile, hipStream_t st) {
+  hipLaunchKernelGGL(group_tiles_kernel, dim3(blocks_for(groups + 1)), dim3(kThreads), 0, st,
+                     gstart, groups, ntile);
+  return hipGetLastError();
+}
+hipError_t launch_tile_table(const int* gstart, const int* tile_off, int groups, int2* tiles,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(tile_table_kernel, dim3(blocks_for(groups)), dim3(kThreads), 0, st, gstart,
+                     tile_off, groups, tiles);
+  return hipGetLastError();
+}
+hipError_t launch_group_update(const PScene& S, const PHitPoint* hps, const int* perm,
+                               const int* gstart, const int2* tiles, int ntiles,
+                               const PGrid* grid, const PDeposit* slots, const unsigned* vals,
+                               const int* start, const int* end, float4* state, unsigned* nupd,
+                               unsigned long long* stats, hipStream_t st) {
+  if (ntiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(group_update_kernel, dim3(ntiles), dim3(kUpdThreads), 0, st, S, hps, perm,
+                     gstart, tiles, grid, slots, vals, start, end, state, nupd, stats);
   return hipGetLastError();
 }
 hipError_t launch_density(const PHitPoint* hps, const float4* state, const int* pix_offsets,
