@@ -23,7 +23,14 @@ hipError_t launch_grid(const PHitPoint*, int, int, int, PGrid*, float4*, unsigne
 hipError_t launch_photons(const PScene&, unsigned long long, long long, int, int, PDeposit*, int*,
                           unsigned long long*, hipStream_t);
 hipError_t launch_deposit_keys(const PDeposit*, const int*, const int*, int, int, const PGrid*,
-                               unsigned*, unsigned*, hipStream_t);
+                               unsigned*, PDeposit*, hipStream_t);
+hipError_t launch_group_buckets(const PHitPoint*, const int*, const int*, int, const PGrid*,
+                                unsigned*, int*, int*, hipStream_t);
+hipError_t launch_bucket_group_pairs(const unsigned*, const int*, const int*, int, unsigned*,
+                                     unsigned*, hipStream_t);
+hipError_t launch_expand_count(const unsigned*, int, const int*, const int*, int*, hipStream_t);
+hipError_t launch_expand_write(const unsigned*, int, const int*, const int*, const unsigned*,
+                               const int*, unsigned*, unsigned*, hipStream_t);
 hipError_t launch_bucket_bounds(const unsigned*, int, int*, int*, hipStream_t);
 hipError_t launch_group_keys(const PHitPoint*, int, const PGrid*, unsigned long long*, int*, int*,
                             hipStream_t);
@@ -32,8 +39,9 @@ hipError_t launch_group_starts(const int*, const int*, int, int*, hipStream_t);
 hipError_t launch_group_tiles(const int*, int, int*, hipStream_t);
 hipError_t launch_tile_table(const int*, const int*, int, int2*, hipStream_t);
 hipError_t launch_group_update(const PScene&, const PHitPoint*, const int*, const int*,
-                               const int2*, int, const PGrid*, const PDeposit*, const unsigned*,
-                               const int*, const int*, float4*, unsigned*, unsigned long long*,
+                               const int2*, int, const unsigned*, const int*, const int*,
+                               const int*, const int*, const unsigned*, const PDeposit*,
+                               const unsigned*, float4*, unsigned*, unsigned long long*,
                                hipStream_t);
 hipError_t launch_density(const PHitPoint*, const float4*, const int*, int, double, float*,
                           hipStream_t);
@@ -147,7 +155,13 @@ struct ppm_scene {
   // photon batches
   DevBuf<PDeposit> slots;
   DevBuf<int> ndep, dep_off;
-  DevBuf<unsigned> keys, vals, keys2, vals2;
+  DevBuf<unsigned> dbucket;                      // per dense deposit: its bucket
+  DevBuf<PDeposit> dense;                        // deposits in photon order
+  DevBuf<int> pcount, poff, list_start, list_end;  // (group, deposit) expansion
+  DevBuf<unsigned> pkey, pval, pkey2, pval2;
+  DevBuf<unsigned> gb;                           // per group: buckets, multiplicity
+  DevBuf<int> gm, gnb, goff, bg_start, bg_end;
+  DevBuf<unsigned> bgkey, bgval, bgkey2, bgval2;  // bucket -> groups
   DevBuf<unsigned char> temp;
   DevBuf<unsigned long long> stats;  // [photons, photon_rays, deposits, updates, eye_rays]
   DevBuf<int> error;
@@ -161,7 +175,11 @@ struct ppm_scene {
     grid.release(), bstart.release(), bend.release(), slots.release(), ndep.release();
     gkeys.release(), gkeys2.release(), gidx.release(), perm.release(), gflags.release();
     gid.release(), gstart.release(), ntile.release(), tile_off.release(), tiles.release();
-    dep_off.release(), keys.release(), vals.release(), keys2.release(), vals2.release();
+    dep_off.release(), dbucket.release(), dense.release(), pcount.release(), poff.release();
+    list_start.release(), list_end.release(), pkey.release(), pval.release(), pkey2.release();
+    pval2.release(), gb.release(), gm.release(), gnb.release(), goff.release();
+    bg_start.release(), bg_end.release(), bgkey.release(), bgval.release(), bgkey2.release();
+    bgval2.release();
     temp.release(), stats.release(), error.release(), image.release();
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
@@ -278,7 +296,7 @@ void build_grid(ppm_scene* s, int width, int height) {
     hip_check(hipStreamSynchronize(s->stream), "group hit points");
     if (err) throw std::domain_error("a hit point's radius box spans more hash cells than supported");
     s->n_groups = groups;
-    // tiles of <= 16 hit points per group (group_update_kernel)
+    // tiles of <= 8 hit points per group (group_update_kernel)
     s->ntile.reserve(groups + 1, "alloc tile counts");
     s->tile_off.reserve(groups + 1, "alloc tile offsets");
     hip_check(launch_group_tiles(s->gstart.p, groups, s->ntile.p, s->stream), "group tiles");
@@ -296,6 +314,46 @@ void build_grid(ppm_scene* s, int width, int height) {
     hip_check(launch_tile_table(s->gstart.p, s->tile_off.p, groups, s->tiles.p, s->stream),
               "tile table");
     s->n_tiles = ntiles;
+    // each group's buckets, and the bucket -> groups map the expansion uses
+    s->gb.reserve((size_t)groups * kMaxCells, "alloc group buckets");
+    s->gm.reserve((size_t)groups * kMaxCells, "alloc group multiplicities");
+    s->gnb.reserve(groups + 1, "alloc group bucket counts");
+    s->goff.reserve(groups + 1, "alloc group bucket offsets");
+    hip_check(launch_group_buckets(s->hp.p, s->perm.p, s->gstart.p, groups, s->grid.p, s->gb.p,
+                                   s->gm.p, s->gnb.p, s->stream), "group buckets");
+    bytes = 0;
+    hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, s->gnb.p, s->goff.p, groups + 1,
+                                               s->stream), "scan size");
+    s->temp.reserve(bytes, "alloc scan temp");
+    hip_check(hipcub::DeviceScan::ExclusiveSum(s->temp.p, bytes, s->gnb.p, s->goff.p, groups + 1,
+                                               s->stream), "scan group buckets");
+    int npairs = 0;
+    hip_check(hipMemcpyAsync(&npairs, s->goff.p + groups, sizeof(int), hipMemcpyDeviceToHost,
+                             s->stream), "read pair count");
+    hip_check(hipStreamSynchronize(s->stream), "pair count");
+    s->bgkey.reserve(npairs, "alloc bucket-group keys");
+    s->bgval.reserve(npairs, "alloc bucket-group values");
+    s->bgkey2.reserve(npairs, "alloc bucket-group keys");
+    s->bgval2.reserve(npairs, "alloc bucket-group values");
+    hip_check(launch_bucket_group_pairs(s->gb.p, s->gnb.p, s->goff.p, groups, s->bgkey.p,
+                                        s->bgval.p, s->stream), "bucket-group pairs");
+    int hbits = 1;
+    while (hbits < 32 && (1ull << hbits) < (unsigned long long)n) hbits++;
+    bytes = 0;
+    hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, s->bgkey.p, s->bgkey2.p, s->bgval.p,
+                                                 s->bgval2.p, npairs, 0, hbits, s->stream), "sort size");
+    s->temp.reserve(bytes, "alloc sort temp");
+    hip_check(hipcub::DeviceRadixSort::SortPairs(s->temp.p, bytes, s->bgkey.p, s->bgkey2.p,
+                                                 s->bgval.p, s->bgval2.p, npairs, 0, hbits,
+                                                 s->stream), "sort bucket-group pairs");
+    s->bg_start.reserve(n, "alloc bucket-group starts");
+    s->bg_end.reserve(n, "alloc bucket-group ends");
+    hip_check(hipMemsetAsync(s->bg_start.p, 0, n * sizeof(int), s->stream), "zero");
+    hip_check(hipMemsetAsync(s->bg_end.p, 0, n * sizeof(int), s->stream), "zero");
+    hip_check(launch_bucket_bounds(s->bgkey2.p, npairs, s->bg_start.p, s->bg_end.p, s->stream),
+              "bucket-group bounds");
+    s->list_start.reserve(groups, "alloc list starts");
+    s->list_end.reserve(groups, "alloc list ends");
   }
   s->grid_ready = true;
 }
@@ -306,8 +364,6 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
   const int K = std::max(1, s->host.max_depth - 1);
   const long long batch_max = std::max<long long>(1, (long long)(kSlotBytesPerBatch / (sizeof(PDeposit) * K)));
   const int H = s->n_hp;
-  int bits = 1;
-  while (bits < 32 && (1ull << bits) < (unsigned long long)std::max(H, 1)) bits++;
   for (long long done = 0; done < count;) {
     const int b = (int)std::min(count - done, batch_max);
     s->slots.reserve((size_t)b * K, "alloc deposit slots");
@@ -328,29 +384,55 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
                                s->stream), "read deposit count");
       hip_check(hipStreamSynchronize(s->stream), "photon batch");
       if (D > 0) {
-        s->keys.reserve(D, "alloc keys");
-        s->vals.reserve(D, "alloc values");
-        s->keys2.reserve(D, "alloc keys");
-        s->vals2.reserve(D, "alloc values");
+        // deposits in photon order, with their buckets
+        s->dense.reserve(D, "alloc dense deposits");
+        s->dbucket.reserve(D, "alloc deposit buckets");
         hip_check(launch_deposit_keys(s->slots.p, s->ndep.p, s->dep_off.p, b, K, s->grid.p,
-                                      s->keys.p, s->vals.p, s->stream), "deposit keys");
+                                      s->dbucket.p, s->dense.p, s->stream), "deposit keys");
+        // each deposit into every group filed under its bucket; a stable sort by group gives
+        // each group its deposit list in photon order
+        s->pcount.reserve(D + 1, "alloc expansion counts");
+        s->poff.reserve(D + 1, "alloc expansion offsets");
+        hip_check(launch_expand_count(s->dbucket.p, D, s->bg_start.p, s->bg_end.p, s->pcount.p,
+                                      s->stream), "expansion count");
         bytes = 0;
-        hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, s->keys.p, s->keys2.p,
-                                                     s->vals.p, s->vals2.p, D, 0, bits, s->stream),
-                  "sort size");
-        s->temp.reserve(bytes, "alloc sort temp");
-        hip_check(hipcub::DeviceRadixSort::SortPairs(s->temp.p, bytes, s->keys.p, s->keys2.p,
-                                                     s->vals.p, s->vals2.p, D, 0, bits, s->stream),
-                  "sort deposits by bucket");
-        hip_check(hipMemsetAsync(s->bstart.p, 0, H * sizeof(int), s->stream), "zero buckets");
-        hip_check(hipMemsetAsync(s->bend.p, 0, H * sizeof(int), s->stream), "zero buckets");
-        hip_check(launch_bucket_bounds(s->keys2.p, D, s->bstart.p, s->bend.p, s->stream),
-                  "bucket bounds");
-        hip_check(launch_group_update(s->S, s->hp.p, s->perm.p, s->gstart.p, s->tiles.p, s->n_tiles,
-                                      s->grid.p,
-                                      s->slots.p, s->vals2.p, s->bstart.p, s->bend.p, s->state.p,
-                                      s->nupd.p, s->stats.p, s->stream),
-                  "hit-point updates");
+        hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, s->pcount.p, s->poff.p, D + 1,
+                                                   s->stream), "scan size");
+        s->temp.reserve(bytes, "alloc scan temp");
+        hip_check(hipcub::DeviceScan::ExclusiveSum(s->temp.p, bytes, s->pcount.p, s->poff.p, D + 1,
+                                                   s->stream), "scan expansion");
+        int P = 0;
+        hip_check(hipMemcpyAsync(&P, s->poff.p + D, sizeof(int), hipMemcpyDeviceToHost, s->stream),
+                  "read expansion size");
+        hip_check(hipStreamSynchronize(s->stream), "expansion size");
+        hip_check(hipMemsetAsync(s->list_start.p, 0, s->n_groups * sizeof(int), s->stream), "zero");
+        hip_check(hipMemsetAsync(s->list_end.p, 0, s->n_groups * sizeof(int), s->stream), "zero");
+        if (P > 0) {
+          s->pkey.reserve(P, "alloc expansion keys");
+          s->pval.reserve(P, "alloc expansion values");
+          s->pkey2.reserve(P, "alloc expansion keys");
+          s->pval2.reserve(P, "alloc expansion values");
+          hip_check(launch_expand_write(s->dbucket.p, D, s->bg_start.p, s->bg_end.p, s->bgval2.p,
+                                        s->poff.p, s->pkey.p, s->pval.p, s->stream),
+                    "expansion write");
+          int gbits = 1;
+          while (gbits < 32 && (1ull << gbits) < (unsigned long long)s->n_groups) gbits++;
+          bytes = 0;
+          hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, s->pkey.p, s->pkey2.p,
+                                                       s->pval.p, s->pval2.p, P, 0, gbits,
+                                                       s->stream), "sort size");
+          s->temp.reserve(bytes, "alloc sort temp");
+          hip_check(hipcub::DeviceRadixSort::SortPairs(s->temp.p, bytes, s->pkey.p, s->pkey2.p,
+                                                       s->pval.p, s->pval2.p, P, 0, gbits,
+                                                       s->stream), "sort expansion by group");
+          hip_check(launch_bucket_bounds(s->pkey2.p, P, s->list_start.p, s->list_end.p, s->stream),
+                    "group list bounds");
+          hip_check(launch_group_update(s->S, s->hp.p, s->perm.p, s->gstart.p, s->tiles.p,
+                                        s->n_tiles, s->gb.p, s->gm.p, s->gnb.p, s->list_start.p,
+                                        s->list_end.p, s->pval2.p, s->dense.p, s->dbucket.p,
+                                        s->state.p, s->nupd.p, s->stats.p, s->stream),
+                    "hit-point updates");
+        }
       }
     }
     done += b;

@@ -568,23 +568,22 @@ __global__ __launch_bounds__(256) void photon_kernel(PScene S, unsigned long lon
   }
 }
 
-// Deposit d of photon i -> dense position offsets[i] + d, keyed by the bucket of its cell
-// (Scene.cpp:125-130); values are slot indices, increasing in photon order.
+// Deposit d of photon i -> dense position offsets[i] + d (photon order), with the bucket of
+// its cell (Scene.cpp:125-130).
 __global__ __launch_bounds__(256) void deposit_keys_kernel(const PDeposit* slots,
                                                            const int* ndep, const int* offsets,
                                                            int count, int K,
-                                                           const PGrid* grid, unsigned* keys,
-                                                           unsigned* vals) {
+                                                           const PGrid* grid, unsigned* bucket,
+                                                           PDeposit* dense) {
   const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (i >= count) return;
   const PGrid G = *grid;
   const int n = ndep[i], o = offsets[i];
   for (int k = 0; k < n; k++) {
-    const unsigned s = (unsigned)((size_t)i * K + k);
-    const PDeposit& d = slots[s];
+    const PDeposit d = slots[(size_t)i * K + k];
     const V hh = (ld(d.x) - ld(G.bmin)) * G.hash_scale;
-    keys[o + k] = bucket_of(G, cell(hh.x), cell(hh.y), cell(hh.z));
-    vals[o + k] = s;
+    bucket[o + k] = bucket_of(G, cell(hh.x), cell(hh.y), cell(hh.z));
+    dense[o + k] = d;
   }
 }
 
@@ -638,9 +637,77 @@ __global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, con
   if (i == n) gstart[gid[n]] = n;  // gid[n] = number of groups
 }
 
-constexpr int kTileHP = 16;   // hit points per update workgroup
+constexpr int kTileHP = 8;    // hit points per update workgroup (hot groups spread over CUs)
 constexpr int kWinMax = 1024; // merged deposits per window
 constexpr int kUpdThreads = 256;
+
+// Each group's buckets (Scene.cpp:79-91 for its first hit point; all members share them),
+// deduplicated, with multiplicity.
+__global__ __launch_bounds__(256) void group_buckets_kernel(const PHitPoint* hps, const int* perm,
+                                                            const int* gstart, int groups,
+                                                            const PGrid* grid, unsigned* gb,
+                                                            int* gm, int* gnb) {
+  const int g = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (g > groups) return;
+  if (g == groups) {
+    gnb[groups] = 0;
+    return;
+  }
+  const PGrid G = *grid;
+  const V pos = ld(hps[perm[gstart[g]]].pos);
+  const V bmin = ((pos - G.radius) - ld(G.bmin)) * G.hash_scale;
+  const V bmax = ((pos + G.radius) - ld(G.bmin)) * G.hash_scale;
+  unsigned* b_out = gb + (size_t)g * kMaxCells;
+  int* m_out = gm + (size_t)g * kMaxCells;
+  int nb = 0;
+  for (int iz = cell(bmin.z); iz <= cell(bmax.z); iz++)
+    for (int iy = cell(bmin.y); iy <= cell(bmax.y); iy++)
+      for (int ix = cell(bmin.x); ix <= cell(bmax.x); ix++) {
+        const unsigned b = bucket_of(G, ix, iy, iz);
+        int u = 0;
+        while (u < nb && b_out[u] != b) u++;
+        if (u < nb) m_out[u]++;
+        else if (nb < kMaxCells) b_out[nb] = b, m_out[nb] = 1, nb++;
+      }
+  gnb[g] = nb;
+}
+
+// (bucket, group) pairs in group order; a stable sort by bucket makes the bucket -> groups map.
+__global__ __launch_bounds__(256) void bucket_group_pairs_kernel(const unsigned* gb,
+                                                                 const int* gnb,
+                                                                 const int* goff, int groups,
+                                                                 unsigned* key, unsigned* val) {
+  const int g = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (g >= groups) return;
+  for (int u = 0; u < gnb[g]; u++) {
+    key[goff[g] + u] = gb[(size_t)g * kMaxCells + u];
+    val[goff[g] + u] = (unsigned)g;
+  }
+}
+
+// Expansion: every deposit (photon order) into each group filed under its bucket.
+__global__ __launch_bounds__(256) void expand_count_kernel(const unsigned* bucket, int n,
+                                                           const int* bg_start,
+                                                           const int* bg_end, int* count) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i < n) count[i] = bg_end[bucket[i]] - bg_start[bucket[i]];
+  if (i == n) count[n] = 0;
+}
+__global__ __launch_bounds__(256) void expand_write_kernel(const unsigned* bucket, int n,
+                                                           const int* bg_start,
+                                                           const int* bg_end,
+                                                           const unsigned* bg_group,
+                                                           const int* off, unsigned* key,
+                                                           unsigned* val) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= n) return;
+  const unsigned b = bucket[i];
+  int o = off[i];
+  for (int k = bg_start[b]; k < bg_end[b]; k++, o++) {
+    key[o] = bg_group[k];
+    val[o] = (unsigned)i;
+  }
+}
 
 __global__ __launch_bounds__(256) void group_tiles_kernel(const int* gstart, int groups,
                                                           int* ntile) {
@@ -657,64 +724,31 @@ __global__ __launch_bounds__(256) void tile_table_kernel(const int* gstart, cons
     tiles[t] = make_int2(g, gstart[g] + (t - tile_off[g]) * kTileHP);
 }
 
-__device__ __forceinline__ int lower_bound_lds(const unsigned* a, int n, unsigned v) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (a[mid] < v) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
 
-// One workgroup per (group, tile of <= 16 hit points).  The group's bucket runs are merged in
-// photon order in windows of <= 1024 deposits (each run contributes in proportion to what it
-// has left; every slot <= the smallest "last loaded" slot of a run that continues is final).
-// For each window: all 256 threads test (hit point, deposit) pairs against the radius^2 the
-// hit point had at the window start — a superset of the deposits that will pass, since the
-// radius only shrinks — into bitmasks; then one thread per hit point walks its bits in order
-// and applies Scene.cpp:136-168 exactly (radius re-tested with the running value).
+// One workgroup per (group, tile of <= kTileHP hit points).  The group's deposit list (every
+// deposit filed under one of its buckets, in photon order) is streamed in windows of
+// kWinMax.  For each window: all threads test (hit point, deposit) pairs against the
+// radius^2 the hit point had at the window start — a superset of the deposits that will
+// pass, since the radius only shrinks — into bitmasks; then one thread per hit point walks
+// its bits in order and applies Scene.cpp:136-168 exactly (radius re-tested with the running
+// value, twice when two of its cells share the deposit's bucket).
 __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
     PScene S, const PHitPoint* hps, const int* perm, const int* gstart, const int2* tiles,
-    const PGrid* grid, const PDeposit* slots, const unsigned* vals, const int* bstart,
-    const int* bend, float4* state, unsigned* nupd, unsigned long long* stats) {
+    const unsigned* gb, const int* gm, const int* gnb, const int* list_start,
+    const int* list_end, const unsigned* list, const PDeposit* dense, const unsigned* bucket,
+    float4* state, unsigned* nupd, unsigned long long* stats) {
   __shared__ unsigned s_bucket[kMaxCells];
-  __shared__ int s_mult[kMaxCells], s_cur[kMaxCells], s_stop[kMaxCells], s_take[kMaxCells];
-  __shared__ int s_off[kMaxCells + 1], s_emit[kMaxCells];
-  __shared__ int s_nb, s_total, s_loaded;
-  __shared__ unsigned s_limit;
-  __shared__ unsigned s_cat[kWinMax];
-  __shared__ unsigned char s_catrun[kWinMax];
-  __shared__ unsigned s_out[kWinMax];
-  __shared__ unsigned char s_run[kWinMax];
-  __shared__ float s_x[kWinMax][3], s_n[kWinMax][3];
+  __shared__ int s_mult[kMaxCells];
+  __shared__ float s_x[kWinMax][3], s_n[kWinMax][3], s_wi[kWinMax][3], s_f[kWinMax][3];
+  __shared__ unsigned char s_rep[kWinMax];
   __shared__ unsigned s_mask[kTileHP][kWinMax / 32];
   __shared__ float s_pos[kTileHP][3], s_hn[kTileHP][3], s_r2[kTileHP];
   const int tid = (int)threadIdx.x;
   const int2 tile = tiles[blockIdx.x];
   const int g = tile.x, first = tile.y;
   const int nh = min(kTileHP, gstart[g + 1] - first);
-  const PGrid G = *grid;
-  if (tid == 0) {  // the group's buckets (Scene.cpp:79-91), deduplicated with multiplicity
-    const V pos = ld(hps[perm[gstart[g]]].pos);
-    const V bmin = ((pos - G.radius) - ld(G.bmin)) * G.hash_scale;
-    const V bmax = ((pos + G.radius) - ld(G.bmin)) * G.hash_scale;
-    int nb = 0;
-    for (int iz = cell(bmin.z); iz <= cell(bmax.z); iz++)
-      for (int iy = cell(bmin.y); iy <= cell(bmax.y); iy++)
-        for (int ix = cell(bmin.x); ix <= cell(bmax.x); ix++) {
-          const unsigned b = bucket_of(G, ix, iy, iz);
-          int u = 0;
-          while (u < nb && s_bucket[u] != b) u++;
-          if (u < nb) s_mult[u]++;
-          else if (nb < kMaxCells) s_bucket[nb] = b, s_mult[nb] = 1, nb++;
-        }
-    s_nb = nb;
-  }
-  __syncthreads();
-  const int nb = s_nb;
-  if (tid < nb) s_cur[tid] = bstart[s_bucket[tid]], s_stop[tid] = bend[s_bucket[tid]];
-  // the gate threads own their hit point's state
+  const int nb = gnb[g];
+  if (tid < nb) s_bucket[tid] = gb[(size_t)g * kMaxCells + tid], s_mult[tid] = gm[(size_t)g * kMaxCells + tid];
   const int h = tid < nh ? perm[first + tid] : -1;
   V w_o = mk(0, 0, 0), att = w_o, flux = w_o, pos = w_o, hn = w_o;
   float r2 = 0.0f;
@@ -732,76 +766,25 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
     s_r2[tid] = r2;
   }
   unsigned long long applied = 0;
+  const int ls = list_start[g], le = list_end[g];
   __syncthreads();
-  for (;;) {
-    // (1) plan the window: each run contributes in proportion to what it has left
-    if (tid == 0) {
-      long long rem_total = 0;
-      for (int u = 0; u < nb; u++) rem_total += s_stop[u] - s_cur[u];
-      int off = 0;
-      for (int u = 0; u < nb; u++) {
-        const int rem = s_stop[u] - s_cur[u];
-        int take = rem;
-        if (rem_total > kWinMax) {
-          take = (int)((long long)(kWinMax - nb) * rem / rem_total);
-          if (take < 1 && rem > 0) take = 1;
-        }
-        s_take[u] = take;
-        s_off[u] = off;
-        off += take;
+  for (int base = ls; base < le; base += kWinMax) {
+    const int total = min(kWinMax, le - base);
+    for (int k = tid; k < total; k += kUpdThreads) {  // gather the window's deposits
+      const unsigned i = list[base + k];
+      const PDeposit d = dense[i];
+      for (int a = 0; a < 3; a++) {
+        s_x[k][a] = d.x[a], s_n[k][a] = d.normal[a];
+        s_wi[k][a] = d.w_i[a], s_f[k][a] = d.flux[a];
       }
-      s_off[nb] = off;
-      s_loaded = off;
+      const unsigned b = bucket[i];
+      int u = 0;
+      while (u < nb - 1 && s_bucket[u] != b) u++;
+      s_rep[k] = (unsigned char)s_mult[u];
     }
     __syncthreads();
-    if (s_loaded == 0) break;
-    // (2) load the slices
-    for (int u = 0; u < nb; u++)
-      for (int i = tid; i < s_take[u]; i += kUpdThreads) {
-        s_cat[s_off[u] + i] = vals[s_cur[u] + i];
-        s_catrun[s_off[u] + i] = (unsigned char)u;
-      }
-    __syncthreads();
-    // (3) everything <= limit is final
-    if (tid == 0) {
-      unsigned limit = 0xffffffffu;
-      for (int u = 0; u < nb; u++)
-        if (s_take[u] > 0 && s_cur[u] + s_take[u] < s_stop[u])
-          limit = min(limit, s_cat[s_off[u] + s_take[u] - 1]);
-      int total = 0;
-      for (int u = 0; u < nb; u++) {
-        const int k = limit == 0xffffffffu ? s_take[u]
-                                           : lower_bound_lds(s_cat + s_off[u], s_take[u], limit + 1);
-        s_emit[u] = k;
-        total += k;
-      }
-      s_limit = limit;
-      s_total = total;
-    }
-    __syncthreads();
-    const unsigned limit = s_limit;
-    const int total = s_total;
-    // (4) merge by rank (slots are distinct across runs: one bucket per deposit)
-    for (int i = tid; i < s_loaded; i += kUpdThreads) {
-      const unsigned e = s_cat[i];
-      if (e > limit) continue;
-      const int u = s_catrun[i];
-      int rank = i - s_off[u];
-      for (int v = 0; v < nb; v++)
-        if (v != u) rank += lower_bound_lds(s_cat + s_off[v], s_take[v], e);
-      s_out[rank] = e;
-      s_run[rank] = (unsigned char)u;
-    }
-    __syncthreads();
-    // (5) positions and normals of the window's deposits
-    for (int k = tid; k < total; k += kUpdThreads) {
-      const PDeposit& d = slots[s_out[k]];
-      for (int a = 0; a < 3; a++) s_x[k][a] = d.x[a], s_n[k][a] = d.normal[a];
-    }
-    __syncthreads();
-    // (6) superset filter with the window-start radius
     const int nwords = (total + 31) >> 5;
-    for (int p = tid; p < nh * nwords; p += kUpdThreads) {
+    for (int p = tid; p < nh * nwords; p += kUpdThreads) {  // superset filter
       const int j = p / nwords, w = p % nwords;
       const V hp_pos = mk(s_pos[j][0], s_pos[j][1], s_pos[j][2]);
       const V hp_n = mk(s_hn[j][0], s_hn[j][1], s_hn[j][2]);
@@ -817,8 +800,7 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
       s_mask[j][w] = bits;
     }
     __syncthreads();
-    // (7) exact, in-order application per hit point
-    if (h >= 0) {
+    if (h >= 0) {  // exact, in-order application per hit point
       for (int w = 0; w < nwords; w++) {
         unsigned bits = s_mask[tid][w];
         while (bits) {
@@ -826,12 +808,10 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
           bits &= bits - 1;
           const int k = w * 32 + b;
           const V x = mk(s_x[k][0], s_x[k][1], s_x[k][2]), dn = mk(s_n[k][0], s_n[k][1], s_n[k][2]);
-          const int reps = s_mult[s_run[k]];
-          const PDeposit& d = slots[s_out[k]];
-          for (int rep = 0; rep < reps; rep++) {
+          for (int rep = 0; rep < s_rep[k]; rep++) {
             const V v = pos - x;
             if (!((dot(hn, dn) > 1e-3f) && (dot(v, v) <= r2))) continue;
-            const V w_i = ld(d.w_i), pf = ld(d.flux);
+            const V w_i = ld(s_wi[k]), pf = ld(s_f[k]);
             const float nf = (float)cnt * kAlpha;
             const float rr = (float)((double)(nf + kAlpha) / ((double)nf + 1.0));
             r2 = r2 * rr;
@@ -852,8 +832,6 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
       }
       s_r2[tid] = r2;
     }
-    // (8) advance the runs
-    if (tid < nb) s_cur[tid] += s_emit[tid];
     __syncthreads();
   }
   if (h >= 0) {
@@ -909,10 +887,36 @@ hipError_t launch_photons(const PScene& S, unsigned long long seed, long long fi
   return hipGetLastError();
 }
 hipError_t launch_deposit_keys(const PDeposit* slots, const int* ndep, const int* offsets,
-                               int count, int K, const PGrid* grid, unsigned* keys,
-                               unsigned* vals, hipStream_t st) {
+                               int count, int K, const PGrid* grid, unsigned* bucket,
+                               PDeposit* dense, hipStream_t st) {
   hipLaunchKernelGGL(deposit_keys_kernel, dim3(blocks_for(count)), dim3(kThreads), 0, st, slots,
-                     ndep, offsets, count, K, grid, keys, vals);
+                     ndep, offsets, count, K, grid, bucket, dense);
+  return hipGetLastError();
+}
+hipError_t launch_group_buckets(const PHitPoint* hps, const int* perm, const int* gstart,
+                                int groups, const PGrid* grid, unsigned* gb, int* gm, int* gnb,
+                                hipStream_t st) {
+  hipLaunchKernelGGL(group_buckets_kernel, dim3(blocks_for(groups + 1)), dim3(kThreads), 0, st,
+                     hps, perm, gstart, groups, grid, gb, gm, gnb);
+  return hipGetLastError();
+}
+hipError_t launch_bucket_group_pairs(const unsigned* gb, const int* gnb, const int* goff,
+                                     int groups, unsigned* key, unsigned* val, hipStream_t st) {
+  hipLaunchKernelGGL(bucket_group_pairs_kernel, dim3(blocks_for(groups)), dim3(kThreads), 0, st,
+                     gb, gnb, goff, groups, key, val);
+  return hipGetLastError();
+}
+hipError_t launch_expand_count(const unsigned* bucket, int n, const int* bg_start,
+                               const int* bg_end, int* count, hipStream_t st) {
+  hipLaunchKernelGGL(expand_count_kernel, dim3(blocks_for(n + 1)), dim3(kThreads), 0, st, bucket,
+                     n, bg_start, bg_end, count);
+  return hipGetLastError();
+}
+hipError_t launch_expand_write(const unsigned* bucket, int n, const int* bg_start,
+                               const int* bg_end, const unsigned* bg_group, const int* off,
+                               unsigned* key, unsigned* val, hipStream_t st) {
+  hipLaunchKernelGGL(expand_write_kernel, dim3(blocks_for(n)), dim3(kThreads), 0, st, bucket, n,
+                     bg_start, bg_end, bg_group, off, key, val);
   return hipGetLastError();
 }
 hipError_t launch_bucket_bounds(const unsigned* keys, int n, int* start, int* end,
@@ -951,12 +955,14 @@ hipError_t launch_tile_table(const int* gstart, const int* tile_off, int groups,
 }
 hipError_t launch_group_update(const PScene& S, const PHitPoint* hps, const int* perm,
                                const int* gstart, const int2* tiles, int ntiles,
-                               const PGrid* grid, const PDeposit* slots, const unsigned* vals,
-                               const int* start, const int* end, float4* state, unsigned* nupd,
-                               unsigned long long* stats, hipStream_t st) {
+                               const unsigned* gb, const int* gm, const int* gnb,
+                               const int* list_start, const int* list_end, const unsigned* list,
+                               const PDeposit* dense, const unsigned* bucket, float4* state,
+                               unsigned* nupd, unsigned long long* stats, hipStream_t st) {
   if (ntiles <= 0) return hipSuccess;
   hipLaunchKernelGGL(group_update_kernel, dim3(ntiles), dim3(kUpdThreads), 0, st, S, hps, perm,
-                     gstart, tiles, grid, slots, vals, start, end, state, nupd, stats);
+                     gstart, tiles, gb, gm, gnb, list_start, list_end, list, dense, bucket, state,
+                     nupd, stats);
   return hipGetLastError();
 }
 hipError_t launch_density(const PHitPoint* hps, const float4* state, const int* pix_offsets,

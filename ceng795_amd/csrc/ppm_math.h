@@ -259,6 +259,7 @@ PPM_HD float powf_ieee(float xf, float yf) {
   const double x = (double)xf, y = (double)yf;
   if (y == 0.0 || x == 1.0) return 1.0f;
   if (x != x || y != y) return (float)(x + y);
+  if (y == 1.0) return xf;  // exact (the default PhongExponent)
   if (x == 0.0) return y > 0.0 ? 0.0f : (float)(1.0 / x);
   if (x < 0.0) return (float)((x - x) / (x - x));  // not used by the path (documented)
   if (x - x != 0.0) return y > 0.0 ? xf : 0.0f;    // +inf
