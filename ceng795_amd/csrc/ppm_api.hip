@@ -6,6 +6,8 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -38,11 +40,14 @@ hipError_t launch_group_flags(const unsigned long long*, int, int*, hipStream_t)
 hipError_t launch_group_starts(const int*, const int*, int, int*, hipStream_t);
 hipError_t launch_group_tiles(const int*, int, int*, hipStream_t);
 hipError_t launch_tile_table(const int*, const int*, int, int2*, hipStream_t);
+hipError_t launch_rr_table(float*, int, hipStream_t);
+hipError_t launch_materialize(const unsigned*, const unsigned*, int, const PDeposit*,
+                              const unsigned*, const unsigned*, const int*, const int*, PDeposit*,
+                              unsigned char*, hipStream_t);
 hipError_t launch_group_update(const PScene&, const PHitPoint*, const int*, const int*,
-                               const int2*, int, const unsigned*, const int*, const int*,
-                               const int*, const int*, const unsigned*, const PDeposit*,
-                               const unsigned*, float4*, unsigned*, unsigned long long*,
-                               hipStream_t);
+                               const int2*, int, const int*, const int*, const PDeposit*,
+                               const unsigned char*, const float*, int, float4*, unsigned*,
+                               unsigned long long*, hipStream_t);
 hipError_t launch_density(const PHitPoint*, const float4*, const int*, int, double, float*,
                           hipStream_t);
 }  // namespace ppm
@@ -127,6 +132,7 @@ struct DeviceGuard {
 
 // Deposit slot rows per photon batch: 8 GiB holds C5's 1e7 photons x 19 slots in one batch
 // (one sort, one update launch); HBM is 288 GB.
+constexpr int kRRTable = 1 << 20;  // rr(n) tabulated for n < 2^20 (larger n computed inline)
 constexpr size_t kSlotBytesPerBatch = size_t(8) << 30;
 
 }  // namespace
@@ -162,6 +168,9 @@ struct ppm_scene {
   DevBuf<unsigned> gb;                           // per group: buckets, multiplicity
   DevBuf<int> gm, gnb, goff, bg_start, bg_end;
   DevBuf<unsigned> bgkey, bgval, bgkey2, bgval2;  // bucket -> groups
+  DevBuf<PDeposit> grec;                         // per-group deposit lists, materialised
+  DevBuf<unsigned char> grep;
+  DevBuf<float> rrtab;                           // rr(n), n < kRRTable
   DevBuf<unsigned char> temp;
   DevBuf<unsigned long long> stats;  // [photons, photon_rays, deposits, updates, eye_rays]
   DevBuf<int> error;
@@ -179,7 +188,7 @@ struct ppm_scene {
     list_start.release(), list_end.release(), pkey.release(), pval.release(), pkey2.release();
     pval2.release(), gb.release(), gm.release(), gnb.release(), goff.release();
     bg_start.release(), bg_end.release(), bgkey.release(), bgval.release(), bgkey2.release();
-    bgval2.release();
+    bgval2.release(), grec.release(), grep.release(), rrtab.release();
     temp.release(), stats.release(), error.release(), image.release();
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
@@ -212,6 +221,7 @@ void create_device(ppm_scene* s, int device) {
   S.top_root = h.top_root;
   S.max_depth = h.max_depth;
   S.eps = h.eps;
+  if (const char* d = std::getenv("CENG795_PPM_DIAG")) S.diag = std::atoi(d);  // experiments
   std::memcpy(S.light_pos, h.lights.data(), 12);  // lights[0] (Scene.cpp:97)
   std::memcpy(S.light_intensity, h.lights.data() + 3, 12);
   s->stats.reserve(8, "alloc counters");
@@ -219,6 +229,8 @@ void create_device(ppm_scene* s, int device) {
   s->error.reserve(1, "alloc error flag");
   hip_check(hipMemset(s->error.p, 0, sizeof(int)), "zero error flag");
   s->grid.reserve(1, "alloc grid");
+  s->rrtab.reserve(kRRTable, "alloc radius-reduction table");
+  hip_check(launch_rr_table(s->rrtab.p, kRRTable, s->stream), "radius-reduction table");
 }
 
 void check_scene(const ppm_scene* s) {
@@ -427,10 +439,15 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
                                                        s->stream), "sort expansion by group");
           hip_check(launch_bucket_bounds(s->pkey2.p, P, s->list_start.p, s->list_end.p, s->stream),
                     "group list bounds");
+          s->grec.reserve(P, "alloc group deposit lists");
+          s->grep.reserve(P, "alloc group multiplicities");
+          hip_check(launch_materialize(s->pkey2.p, s->pval2.p, P, s->dense.p, s->dbucket.p, s->gb.p,
+                                       s->gm.p, s->gnb.p, s->grec.p, s->grep.p, s->stream),
+                    "materialise group lists");
           hip_check(launch_group_update(s->S, s->hp.p, s->perm.p, s->gstart.p, s->tiles.p,
-                                        s->n_tiles, s->gb.p, s->gm.p, s->gnb.p, s->list_start.p,
-                                        s->list_end.p, s->pval2.p, s->dense.p, s->dbucket.p,
-                                        s->state.p, s->nupd.p, s->stats.p, s->stream),
+                                        s->n_tiles, s->list_start.p, s->list_end.p, s->grec.p,
+                                        s->grep.p, s->rrtab.p, kRRTable, s->state.p, s->nupd.p,
+                                        s->stats.p, s->stream),
                     "hit-point updates");
         }
       }
@@ -639,6 +656,9 @@ int ppm_collect_stats(ppm_scene* s, ppm_stats* st) {
     st->updates = (long long)c[3];
     st->eye_rays = (long long)c[4];
     st->hit_points = s->n_hp;
+    if (s->S.diag == 2) std::fprintf(stderr, "ppm diag: windows %llu deposit-visits %llu tiles %d groups %d "
+                                     "longest tile %llu ticks\n", c[5], c[6], s->n_tiles,
+                                     s->n_groups, c[7]);
     s->photons = 0;
     return RT_OK;
   });

@@ -84,6 +84,7 @@ struct PScene {  // device pointers + scalars, passed by value to every kernel
   int max_depth;
   float eps;
   float light_pos[3], light_intensity[3];
+  int diag;  // timing experiments only (CENG795_PPM_DIAG): 1 = skip the update recurrence
 };
 
 struct PCamera {

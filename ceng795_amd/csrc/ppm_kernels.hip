@@ -637,9 +637,18 @@ __global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, con
   if (i == n) gstart[gid[n]] = n;  // gid[n] = number of groups
 }
 
-constexpr int kTileHP = 8;    // hit points per update workgroup (hot groups spread over CUs)
-constexpr int kWinMax = 1024; // merged deposits per window
-constexpr int kUpdThreads = 256;
+#ifndef PPM_TILE
+#define PPM_TILE 8
+#endif
+#ifndef PPM_WIN
+#define PPM_WIN 512
+#endif
+#ifndef PPM_THREADS
+#define PPM_THREADS 256
+#endif
+constexpr int kTileHP = PPM_TILE;       // hit points per update workgroup
+constexpr int kWinMax = PPM_WIN;        // deposits per window
+constexpr int kUpdThreads = PPM_THREADS;
 
 // Each group's buckets (Scene.cpp:79-91 for its first hit point; all members share them),
 // deduplicated, with multiplicity.
@@ -725,113 +734,227 @@ __global__ __launch_bounds__(256) void tile_table_kernel(const int* gstart, cons
 }
 
 
-// One workgroup per (group, tile of <= kTileHP hit points).  The group's deposit list (every
-// deposit filed under one of its buckets, in photon order) is streamed in windows of
-// kWinMax.  For each window: all threads test (hit point, deposit) pairs against the
-// radius^2 the hit point had at the window start — a superset of the deposits that will
-// pass, since the radius only shrinks — into bitmasks; then one thread per hit point walks
-// its bits in order and applies Scene.cpp:136-168 exactly (radius re-tested with the running
-// value, twice when two of its cells share the deposit's bucket).
+// rr(n) of Scene.cpp:139-140, the radius reduction of a hit point's (n+1)-th update:
+// (n*ALPHA + ALPHA) / (n*ALPHA + 1.0), a double division rounded to float.  It depends on n
+// only, so it is tabulated once (rr_table_kernel) and staged in LDS per window.
+__device__ __forceinline__ float radius_reduction(unsigned n) {
+  const float nf = (float)n * kAlpha;
+  return (float)((double)(nf + kAlpha) / ((double)nf + 1.0));
+}
+
+__global__ __launch_bounds__(256) void rr_table_kernel(float* rr, int n) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i < n) rr[i] = radius_reduction((unsigned)i);
+}
+
+// The expanded (group, deposit) pairs, sorted by group, materialised contiguously: the
+// deposit record and its multiplicity in that group (how many of the group's cells share the
+// deposit's bucket).
+__global__ __launch_bounds__(256) void materialize_kernel(const unsigned* pkey, const unsigned* pval,
+                                                         int n, const PDeposit* dense,
+                                                         const unsigned* bucket, const unsigned* gb,
+                                                         const int* gm, const int* gnb,
+                                                         PDeposit* rec, unsigned char* rep) {
+  const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (p >= n) return;
+  const unsigned g = pkey[p], i = pval[p];
+  rec[p] = dense[i];
+  const unsigned b = bucket[i];
+  const unsigned* gbb = gb + (size_t)g * kMaxCells;
+  const int nb = gnb[g];
+  int u = 0;
+  while (u < nb - 1 && gbb[u] != b) u++;
+  rep[p] = (unsigned char)gm[(size_t)g * kMaxCells + u];
+}
+
+// One workgroup per (group, tile of <= kTileHP hit points), streaming the group's deposits
+// (photon order) in windows of kWinMax.  Per window:
+//  (1) every thread tests its deposits against every hit point of the tile with the radius^2
+//      the hit point had at the window start — a superset of the deposits that will pass,
+//      since the radius only shrinks (normal test and |v|^2 of Scene.cpp:136-137);
+//  (2) the candidates are listed per hit point, in photon order;
+//  (3) the state-independent term color * photon_flux (Scene.cpp:142-166) is computed for
+//      the candidates by all threads;
+//  (4) one thread per hit point applies the recurrence exactly, in order: r^2 re-tested with
+//      the running value, r^2 *= rr(n), n++, flux = (flux + color * photon_flux) * rr(n) —
+//      repeated when two of its cells share the deposit's bucket.
+// The next window is fetched (coalesced) while the current one is processed.
 __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
     PScene S, const PHitPoint* hps, const int* perm, const int* gstart, const int2* tiles,
-    const unsigned* gb, const int* gm, const int* gnb, const int* list_start,
-    const int* list_end, const unsigned* list, const PDeposit* dense, const unsigned* bucket,
-    float4* state, unsigned* nupd, unsigned long long* stats) {
-  __shared__ unsigned s_bucket[kMaxCells];
-  __shared__ int s_mult[kMaxCells];
-  __shared__ float s_x[kWinMax][3], s_n[kWinMax][3], s_wi[kWinMax][3], s_f[kWinMax][3];
+    const int* list_start, const int* list_end, const PDeposit* rec,
+    const unsigned char* rep, const float* rrtab, int nrr, float4* state, unsigned* nupd,
+    unsigned long long* stats) {
+  constexpr int kPer = kWinMax / kUpdThreads;
+  constexpr int kWords = kWinMax / 32;
+  constexpr int kChunk = 1024;  // candidates per color / apply round
+  __shared__ float s_hp[kTileHP][12];  // pos, normal, w_o, attenuation
+  __shared__ int s_mat[kTileHP];
+  __shared__ float s_r2[kTileHP];
+  __shared__ unsigned s_cnt[kTileHP];
+  __shared__ unsigned s_mask[kTileHP][kWords];
+  __shared__ int s_wc[kTileHP * kWords + 1];
+  __shared__ unsigned short s_ck[kTileHP * kWinMax];
+  __shared__ float s_cd2[kTileHP * kWinMax];
+  __shared__ float s_ccf[kChunk][3];
+  constexpr int kRRStage = 64;  // rr(n) staged per hit point per window (more: computed inline)
+  __shared__ float s_rr[kTileHP][kRRStage];
   __shared__ unsigned char s_rep[kWinMax];
-  __shared__ unsigned s_mask[kTileHP][kWinMax / 32];
-  __shared__ float s_pos[kTileHP][3], s_hn[kTileHP][3], s_r2[kTileHP];
-  const int tid = (int)threadIdx.x;
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const unsigned long long t_start = S.diag == 2 ? wall_clock64() : 0;
   const int2 tile = tiles[blockIdx.x];
   const int g = tile.x, first = tile.y;
   const int nh = min(kTileHP, gstart[g + 1] - first);
-  const int nb = gnb[g];
-  if (tid < nb) s_bucket[tid] = gb[(size_t)g * kMaxCells + tid], s_mult[tid] = gm[(size_t)g * kMaxCells + tid];
   const int h = tid < nh ? perm[first + tid] : -1;
-  V w_o = mk(0, 0, 0), att = w_o, flux = w_o, pos = w_o, hn = w_o;
+  V flux = mk(0, 0, 0);
   float r2 = 0.0f;
   unsigned cnt = 0;
-  PMaterial m{};
   if (h >= 0) {
     const PHitPoint hp = hps[h];
-    pos = ld(hp.pos), hn = ld(hp.normal), w_o = ld(hp.w_o), att = ld(hp.att);
-    m = S.materials[hp.material];
+    for (int a = 0; a < 3; a++) {
+      s_hp[tid][a] = hp.pos[a], s_hp[tid][3 + a] = hp.normal[a];
+      s_hp[tid][6 + a] = hp.w_o[a], s_hp[tid][9 + a] = hp.att[a];
+    }
+    s_mat[tid] = hp.material;
     const float4 st = state[h];
     flux = mk(st.x, st.y, st.z);
     r2 = st.w;
     cnt = nupd[h];
-    for (int a = 0; a < 3; a++) s_pos[tid][a] = hp.pos[a], s_hn[tid][a] = hp.normal[a];
     s_r2[tid] = r2;
+    s_cnt[tid] = cnt;
   }
   unsigned long long applied = 0;
   const int ls = list_start[g], le = list_end[g];
+  PDeposit dep[kPer];
+  unsigned char drep[kPer];
+  auto fetch = [&](int base) {
+#pragma unroll
+    for (int q = 0; q < kPer; q++) {
+      const int k = base + tid + q * kUpdThreads;
+      if (k < le) dep[q] = rec[k], drep[q] = rep[k];
+    }
+  };
+  fetch(ls);
   __syncthreads();
+  V tp[kTileHP], tn[kTileHP];
+#pragma unroll
+  for (int j = 0; j < kTileHP; j++) {
+    tp[j] = mk(s_hp[j][0], s_hp[j][1], s_hp[j][2]);
+    tn[j] = mk(s_hp[j][3], s_hp[j][4], s_hp[j][5]);
+  }
   for (int base = ls; base < le; base += kWinMax) {
     const int total = min(kWinMax, le - base);
-    for (int k = tid; k < total; k += kUpdThreads) {  // gather the window's deposits
-      const unsigned i = list[base + k];
-      const PDeposit d = dense[i];
-      for (int a = 0; a < 3; a++) {
-        s_x[k][a] = d.x[a], s_n[k][a] = d.normal[a];
-        s_wi[k][a] = d.w_i[a], s_f[k][a] = d.flux[a];
-      }
-      const unsigned b = bucket[i];
-      int u = 0;
-      while (u < nb - 1 && s_bucket[u] != b) u++;
-      s_rep[k] = (unsigned char)s_mult[u];
-    }
-    __syncthreads();
     const int nwords = (total + 31) >> 5;
-    for (int p = tid; p < nh * nwords; p += kUpdThreads) {  // superset filter
-      const int j = p / nwords, w = p % nwords;
-      const V hp_pos = mk(s_pos[j][0], s_pos[j][1], s_pos[j][2]);
-      const V hp_n = mk(s_hn[j][0], s_hn[j][1], s_hn[j][2]);
-      const float rr2 = s_r2[j];
-      unsigned bits = 0;
-      const int kend = min(32, total - w * 32);
-      for (int b = 0; b < kend; b++) {
-        const int k = w * 32 + b;
-        const V v = hp_pos - mk(s_x[k][0], s_x[k][1], s_x[k][2]);
-        const V dn = mk(s_n[k][0], s_n[k][1], s_n[k][2]);
-        if ((dot(hp_n, dn) > 1e-3f) && (dot(v, v) <= rr2)) bits |= 1u << b;
+    // stage rr(n) for the updates this window can make
+    for (int e = tid; e < nh * kRRStage; e += kUpdThreads) {
+      const int j = e / kRRStage, t = e % kRRStage;
+      const unsigned n = s_cnt[j] + (unsigned)t;
+      s_rr[j][t] = n < (unsigned)nrr ? rrtab[n] : radius_reduction(n);
+    }
+    // (1) superset filter
+    float r2w[kTileHP];
+#pragma unroll
+    for (int j = 0; j < kTileHP; j++) r2w[j] = s_r2[j];
+    float d2r[kPer][kTileHP];
+    bool cr[kPer][kTileHP];
+#pragma unroll
+    for (int q = 0; q < kPer; q++) {
+      const int k = tid + q * kUpdThreads;  // a wave covers 64 consecutive deposits
+      const bool live = k < total;
+      const V x = ld(dep[q].x), dn = ld(dep[q].normal);
+      if (live) s_rep[k] = drep[q];
+#pragma unroll
+      for (int j = 0; j < kTileHP; j++) {
+        const V v = tp[j] - x;
+        d2r[q][j] = dot(v, v);
+        cr[q][j] = live && j < nh && (dot(tn[j], dn) > 1e-3f) && (d2r[q][j] <= r2w[j]);
+        const unsigned long long bal = __ballot(cr[q][j]);
+        if (lane == 0) {
+          s_mask[j][(k - lane) >> 5] = (unsigned)bal;
+          s_mask[j][((k - lane) >> 5) + 1] = (unsigned)(bal >> 32);
+        }
       }
-      s_mask[j][w] = bits;
+    }
+    fetch(base + kWinMax);  // next window in flight
+    __syncthreads();
+    // (2) candidates per hit point, in photon order
+    for (int e = tid; e < nh * nwords; e += kUpdThreads)
+      s_wc[e] = __builtin_popcount(s_mask[e / nwords][e % nwords]);
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the word counts (one wave)
+      const int n = nh * nwords;
+      int carry = 0;
+      for (int c0 = 0; c0 < n; c0 += 64) {
+        const int v = c0 + lane < n ? s_wc[c0 + lane] : 0;
+        int x = v;
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(x, o, 64);
+          if (lane >= o) x += y;
+        }
+        if (c0 + lane < n) s_wc[c0 + lane] = carry + x - v;
+        carry += __shfl(x, 63, 64);
+      }
+      if (lane == 0) s_wc[n] = carry;
     }
     __syncthreads();
-    if (h >= 0) {  // exact, in-order application per hit point
-      for (int w = 0; w < nwords; w++) {
-        unsigned bits = s_mask[tid][w];
-        while (bits) {
-          const int b = __builtin_ctz(bits);
-          bits &= bits - 1;
-          const int k = w * 32 + b;
-          const V x = mk(s_x[k][0], s_x[k][1], s_x[k][2]), dn = mk(s_n[k][0], s_n[k][1], s_n[k][2]);
-          for (int rep = 0; rep < s_rep[k]; rep++) {
-            const V v = pos - x;
-            if (!((dot(hn, dn) > 1e-3f) && (dot(v, v) <= r2))) continue;
-            const V w_i = ld(s_wi[k]), pf = ld(s_f[k]);
-            const float nf = (float)cnt * kAlpha;
-            const float rr = (float)((double)(nf + kAlpha) / ((double)nf + 1.0));
+#pragma unroll
+    for (int q = 0; q < kPer; q++) {
+      const int k = tid + q * kUpdThreads;
+#pragma unroll
+      for (int j = 0; j < kTileHP; j++) {
+        if (!cr[q][j]) continue;
+        const int w = k >> 5;
+        const int idx = s_wc[j * nwords + w] + __builtin_popcount(s_mask[j][w] & ((1u << (k & 31)) - 1u));
+        s_ck[idx] = (unsigned short)k;
+        s_cd2[idx] = d2r[q][j];
+      }
+    }
+    __syncthreads();
+    const int ncand = s_wc[nh * nwords];
+    const int my_beg = h >= 0 ? s_wc[tid * nwords] : 0;
+    const int my_end = h >= 0 ? (tid + 1 < nh ? s_wc[(tid + 1) * nwords] : ncand) : 0;
+    int t_rr = 0;  // updates made by this hit point in this window
+    for (int c0 = 0; c0 < ncand; c0 += kChunk) {
+      // (3) color * photon_flux for candidates [c0, c0 + kChunk)
+      for (int e = c0 + tid; e < min(ncand, c0 + kChunk); e += kUpdThreads) {
+        int j = 0;
+        while (j + 1 < nh && s_wc[(j + 1) * nwords] <= e) j++;
+        const PDeposit d = rec[base + s_ck[e]];
+        const V hn = tn[j], w_i = ld(d.w_i), pf = ld(d.flux);
+        const PMaterial& m = S.materials[s_mat[j]];
+        V color = mk(0.0f, 0.0f, 0.0f);
+        if (m.brdf_id == -1) {
+          const float cos_i = dot(hn, w_i);
+          if (!(cos_i > 1.0f || cos_i <= 0.0f)) {
+            const V w_o = mk(s_hp[j][6], s_hp[j][7], s_hp[j][8]);
+            const float sc = fmax0(dot(hn, normalize(w_o + w_i)));
+            color = (ld(m.diffuse) + (ld(m.specular) * ppm_math::powf_ieee(sc, m.phong)) / cos_i) *
+                    mk(s_hp[j][9], s_hp[j][10], s_hp[j][11]);
+          }
+        }
+        const V cf = color * pf;
+        s_ccf[e - c0][0] = cf.x, s_ccf[e - c0][1] = cf.y, s_ccf[e - c0][2] = cf.z;
+      }
+      __syncthreads();
+      // (4) the exact recurrence, in photon order
+      if (h >= 0 && S.diag != 1) {
+        const int e1 = min(my_end, c0 + kChunk);
+        for (int e = max(my_beg, c0); e < e1; e++) {
+          const float d2 = s_cd2[e];
+          const int reps = s_rep[s_ck[e]];
+          for (int r = 0; r < reps; r++) {
+            if (!(d2 <= r2)) break;
+            const float rr = t_rr < kRRStage ? s_rr[tid][t_rr] : radius_reduction(cnt);
+            t_rr++;
             r2 = r2 * rr;
             cnt++;
             applied++;
-            V color = mk(0.0f, 0.0f, 0.0f);
-            if (m.brdf_id == -1) {
-              const float cos_i = dot(hn, w_i);
-              if (!(cos_i > 1.0f || cos_i <= 0.0f)) {
-                const float sc = fmax0(dot(hn, normalize(w_o + w_i)));
-                color = (ld(m.diffuse) + (ld(m.specular) * ppm_math::powf_ieee(sc, m.phong)) / cos_i) *
-                        att;
-              }
-            }
-            flux = (flux + color * pf) * rr;
+            flux = (flux + mk(s_ccf[e - c0][0], s_ccf[e - c0][1], s_ccf[e - c0][2])) * rr;
           }
         }
       }
-      s_r2[tid] = r2;
+      __syncthreads();
     }
+    if (h >= 0) s_r2[tid] = r2, s_cnt[tid] = cnt;
     __syncthreads();
   }
   if (h >= 0) {
@@ -840,6 +963,11 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
   }
   const unsigned long long tot = wave_sum(applied);
   if (stats && (tid & 63) == 0 && tot) atomicAdd(&stats[3], tot);
+  if (stats && S.diag == 2 && tid == 0) {  // experiment counters: windows, deposit-visits
+    atomicAdd(&stats[5], (unsigned long long)((le - ls + kWinMax - 1) / kWinMax));
+    atomicAdd(&stats[6], (unsigned long long)(le - ls));
+    atomicMax(&stats[7], wall_clock64() - t_start);  // longest tile, in wall-clock ticks
+  }
 }
 
 // density_estimation + Pixel::get_color: a pixel's hit points are contiguous, in order.
@@ -953,16 +1081,28 @@ hipError_t launch_tile_table(const int* gstart, const int* tile_off, int groups,
                      tile_off, groups, tiles);
   return hipGetLastError();
 }
+hipError_t launch_rr_table(float* rr, int n, hipStream_t st) {
+  hipLaunchKernelGGL(rr_table_kernel, dim3(blocks_for(n)), dim3(kThreads), 0, st, rr, n);
+  return hipGetLastError();
+}
+hipError_t launch_materialize(const unsigned* pkey, const unsigned* pval, int n,
+                              const PDeposit* dense, const unsigned* bucket, const unsigned* gb,
+                              const int* gm, const int* gnb, PDeposit* rec, unsigned char* rep,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(materialize_kernel, dim3(blocks_for(n)), dim3(kThreads), 0, st, pkey, pval,
+                     n, dense, bucket, gb, gm, gnb, rec, rep);
+  return hipGetLastError();
+}
 hipError_t launch_group_update(const PScene& S, const PHitPoint* hps, const int* perm,
                                const int* gstart, const int2* tiles, int ntiles,
-                               const unsigned* gb, const int* gm, const int* gnb,
-                               const int* list_start, const int* list_end, const unsigned* list,
-                               const PDeposit* dense, const unsigned* bucket, float4* state,
-                               unsigned* nupd, unsigned long long* stats, hipStream_t st) {
+                               const int* list_start, const int* list_end, const PDeposit* rec,
+                               const unsigned char* rep, const float* rrtab, int nrr,
+                               float4* state, unsigned* nupd, unsigned long long* stats,
+                               hipStream_t st) {
   if (ntiles <= 0) return hipSuccess;
   hipLaunchKernelGGL(group_update_kernel, dim3(ntiles), dim3(kUpdThreads), 0, st, S, hps, perm,
-                     gstart, tiles, gb, gm, gnb, list_start, list_end, list, dense, bucket, state,
-                     nupd, stats);
+                     gstart, tiles, list_start, list_end, rec, rep, rrtab, nrr, state, nupd,
+                     stats);
   return hipGetLastError();
 }
 hipError_t launch_density(const PHitPoint* hps, const float4* state, const int* pix_offsets,

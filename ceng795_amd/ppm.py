@@ -21,7 +21,10 @@ import numpy as np
 from ._lib import RTError, _share_torch_hip_runtime
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libceng795_ppm.so")
+# CENG795_PPM_LIB=<variant> picks lib/libceng795_ppm_<variant>.so (timing experiments only)
+_VARIANT = os.environ.get("CENG795_PPM_LIB", "")
+LIB_PATH = os.path.join(_HERE, "lib", f"libceng795_ppm_{_VARIANT}.so" if _VARIANT else
+                        "libceng795_ppm.so")
 ABI_VERSION = 1  # CENG795_PPM_ABI_VERSION
 
 _lib = None
