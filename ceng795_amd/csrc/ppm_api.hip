@@ -224,8 +224,8 @@ void create_device(ppm_scene* s, int device) {
   if (const char* d = std::getenv("CENG795_PPM_DIAG")) S.diag = std::atoi(d);  // experiments
   std::memcpy(S.light_pos, h.lights.data(), 12);  // lights[0] (Scene.cpp:97)
   std::memcpy(S.light_intensity, h.lights.data() + 3, 12);
-  s->stats.reserve(8, "alloc counters");
-  hip_check(hipMemset(s->stats.p, 0, 8 * sizeof(unsigned long long)), "zero counters");
+  s->stats.reserve(16, "alloc counters");
+  hip_check(hipMemset(s->stats.p, 0, 16 * sizeof(unsigned long long)), "zero counters");
   s->error.reserve(1, "alloc error flag");
   hip_check(hipMemset(s->error.p, 0, sizeof(int)), "zero error flag");
   s->grid.reserve(1, "alloc grid");
@@ -645,7 +645,7 @@ int ppm_collect_stats(ppm_scene* s, ppm_stats* st) {
     check_scene(s);
     if (!st) throw std::invalid_argument("ppm_collect_stats: NULL output");
     DeviceGuard g(s->device);
-    unsigned long long c[8];
+    unsigned long long c[16];
     hip_check(hipMemcpyAsync(c, s->stats.p, sizeof c, hipMemcpyDeviceToHost, s->stream), "read counters");
     hip_check(hipMemsetAsync(s->stats.p, 0, sizeof c, s->stream), "reset counters");
     hip_check(hipStreamSynchronize(s->stream), "counters");
@@ -657,8 +657,10 @@ int ppm_collect_stats(ppm_scene* s, ppm_stats* st) {
     st->eye_rays = (long long)c[4];
     st->hit_points = s->n_hp;
     if (s->S.diag == 2) std::fprintf(stderr, "ppm diag: windows %llu deposit-visits %llu tiles %d groups %d "
-                                     "longest tile %llu ticks\n", c[5], c[6], s->n_tiles,
-                                     s->n_groups, c[7]);
+                                     "longest tile %llu ticks phases(max) stage+filter %llu "
+                                     "counts %llu scan %llu scatter %llu color %llu gate %llu\n",
+                                     c[5], c[6], s->n_tiles, s->n_groups, c[7], c[8], c[9],
+                                     c[10], c[11], c[12], c[13]);
     s->photons = 0;
     return RT_OK;
   });
@@ -680,7 +682,7 @@ int ppm_render(ppm_scene* s, int cam, int threads, float* out, ppm_stats* stats)
         for (int k = 0; k < 5; k++) (void)hipEventDestroy(e[k]);
       }
     } guard{ev};
-    hip_check(hipMemsetAsync(s->stats.p, 0, 8 * sizeof(unsigned long long), s->stream), "zero counters");
+    hip_check(hipMemsetAsync(s->stats.p, 0, 16 * sizeof(unsigned long long), s->stream), "zero counters");
     s->photons = 0;
     hip_check(hipEventRecord(ev[0], s->stream), "event");
     eye_pass(s, cam);

@@ -641,10 +641,10 @@ __global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, con
 #define PPM_TILE 8
 #endif
 #ifndef PPM_WIN
-#define PPM_WIN 512
+#define PPM_WIN 1024
 #endif
 #ifndef PPM_THREADS
-#define PPM_THREADS 256
+#define PPM_THREADS 512
 #endif
 constexpr int kTileHP = PPM_TILE;       // hit points per update workgroup
 constexpr int kWinMax = PPM_WIN;        // deposits per window
@@ -841,6 +841,14 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
     tp[j] = mk(s_hp[j][0], s_hp[j][1], s_hp[j][2]);
     tn[j] = mk(s_hp[j][3], s_hp[j][4], s_hp[j][5]);
   }
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tp0 = 0;
+#define PPM_PHASE(i)                                              \
+  if (S.diag == 2 && tid == 0) {                                  \
+    const unsigned long long t1 = wall_clock64();                 \
+    ph[i] += t1 - tp0;                                            \
+    tp0 = t1;                                                     \
+  }
+  if (S.diag == 2 && tid == 0) tp0 = wall_clock64();
   for (int base = ls; base < le; base += kWinMax) {
     const int total = min(kWinMax, le - base);
     const int nwords = (total + 31) >> 5;
@@ -876,10 +884,12 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
     }
     fetch(base + kWinMax);  // next window in flight
     __syncthreads();
+    PPM_PHASE(0)
     // (2) candidates per hit point, in photon order
     for (int e = tid; e < nh * nwords; e += kUpdThreads)
       s_wc[e] = __builtin_popcount(s_mask[e / nwords][e % nwords]);
     __syncthreads();
+    PPM_PHASE(1)
     if (tid < 64) {  // exclusive scan of the word counts (one wave)
       const int n = nh * nwords;
       int carry = 0;
@@ -896,6 +906,7 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
       if (lane == 0) s_wc[n] = carry;
     }
     __syncthreads();
+    PPM_PHASE(2)
 #pragma unroll
     for (int q = 0; q < kPer; q++) {
       const int k = tid + q * kUpdThreads;
@@ -909,6 +920,7 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
       }
     }
     __syncthreads();
+    PPM_PHASE(3)
     const int ncand = s_wc[nh * nwords];
     const int my_beg = h >= 0 ? s_wc[tid * nwords] : 0;
     const int my_end = h >= 0 ? (tid + 1 < nh ? s_wc[(tid + 1) * nwords] : ncand) : 0;
@@ -935,6 +947,7 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
         s_ccf[e - c0][0] = cf.x, s_ccf[e - c0][1] = cf.y, s_ccf[e - c0][2] = cf.z;
       }
       __syncthreads();
+      PPM_PHASE(4)
       // (4) the exact recurrence, in photon order
       if (h >= 0 && S.diag != 1) {
         const int e1 = min(my_end, c0 + kChunk);
@@ -953,9 +966,11 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
         }
       }
       __syncthreads();
+      PPM_PHASE(5)
     }
     if (h >= 0) s_r2[tid] = r2, s_cnt[tid] = cnt;
     __syncthreads();
+    PPM_PHASE(5)
   }
   if (h >= 0) {
     state[h] = make_float4(flux.x, flux.y, flux.z, r2);
@@ -967,7 +982,9 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
     atomicAdd(&stats[5], (unsigned long long)((le - ls + kWinMax - 1) / kWinMax));
     atomicAdd(&stats[6], (unsigned long long)(le - ls));
     atomicMax(&stats[7], wall_clock64() - t_start);  // longest tile, in wall-clock ticks
+    for (int i = 0; i < 6; i++) atomicMax(&stats[8 + i], ph[i]);
   }
+#undef PPM_PHASE
 }
 
 // density_estimation + Pixel::get_color: a pixel's hit points are contiguous, in order.
