@@ -10,12 +10,15 @@
 // the closest-hit tie-break order, and the set of boxes on each root-to-leaf path decides
 // which leaves a ray may test at all.  Compiled with -ffp-contract=off (no FMA) so every
 // fp32 expression rounds as on the reference's x86-64 SSE build.
+#include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <limits>
 #include <sstream>
 #include <stdexcept>
+#include <thread>
 #include <utility>
 
 #include "host_scene.h"
@@ -51,11 +54,13 @@ struct Aabb {
     b.mid = (hi + lo) / 2.0f;
     return b;
   }
-  void grow(const Aabb& o) {
+  void grow(const Aabb& o) {  // bounding_box.cpp:2-13 (center recomputed on every expand)
     lo = fmin3(lo, o.lo);
     hi = fmax3(hi, o.hi);
     mid = (hi + lo) / 2.0f;
   }
+  // n expands in a row: only the last center survives, so compute it once.
+  void grow_all(const std::vector<int>& ids, int b, int e, const std::vector<struct Obj>& objs);
 };
 
 // The reference's Shape hierarchy as a tagged list.
@@ -68,34 +73,42 @@ struct Obj {
   int leaf = -1;       // index into `leaves`
 };
 
+void Aabb::grow_all(const std::vector<int>& ids, int b, int e, const std::vector<Obj>& objs) {
+  for (int i = b; i < e; i++) {
+    lo = fmin3(lo, objs[ids[i]].box.lo);
+    hi = fmax3(hi, objs[ids[i]].box.hi);
+  }
+  if (e > b) mid = (hi + lo) / 2.0f;
+}
+
 struct Builder {
   std::vector<Obj> objs;
   std::vector<LeafSource> leaves;
   std::vector<F3> normals;
 
-  // create_bvh + BVH::BVH over the object ids in `ids` (permuted in place like the reference).
-  int build(std::vector<int>& ids) {
-    const int n = (int)ids.size();
-    if (n == 0) return -1;
-    if (n == 1) return ids[0];
+  // BVH::BVH over ids[begin, end) (HW2/Bounding_volume_hierarchy.cpp:3-29), iteratively,
+  // appending its nodes to `out`.  Leaf refs are object ids; refs to nodes of `out` are
+  // encoded as node_ref(local index) and resolved by the caller.  Reads only leaf boxes.
+  static int node_ref(int local) { return -2 - local; }
+  void build_range(std::vector<int>& ids, int begin, int end, int axis, std::vector<Obj>& out) const {
     struct Range {
       int begin, end, axis, node;
     };
     std::vector<Range> todo;
-    auto open = [&](int begin, int end, int axis) {
+    auto open = [&](int b, int e, int ax) {
       Obj o;
       o.kind = kObjBvh;
-      o.axis = axis;
-      for (int i = begin; i < end; i++) o.box.grow(objs[ids[i]].box);
-      objs.push_back(o);
-      todo.push_back({begin, end, axis, (int)objs.size() - 1});
-      return (int)objs.size() - 1;
+      o.axis = ax;
+      o.box.grow_all(ids, b, e, objs);
+      out.push_back(o);
+      todo.push_back({b, e, ax, (int)out.size() - 1});
+      return node_ref((int)out.size() - 1);
     };
-    const int root = open(0, n, 0);
+    open(begin, end, axis);
     while (!todo.empty()) {
       const Range r = todo.back();
       todo.pop_back();
-      const float split = objs[r.node].box.mid[r.axis];
+      const float split = out[r.node].box.mid[r.axis];
       int m = r.begin;
       for (int i = r.begin; i < r.end; i++)
         if (objs[ids[i]].box.mid[r.axis] < split) std::swap(ids[i], ids[m++]);
@@ -103,10 +116,93 @@ struct Builder {
       const int next = (r.axis + 1) % 3;
       const int left = (r.begin + 1 == m) ? ids[r.begin] : open(r.begin, m, next);
       const int right = (m + 1 == r.end) ? ids[m] : open(m, r.end, next);
-      objs[r.node].a = left;
-      objs[r.node].b = right;
+      out[r.node].a = left;
+      out[r.node].b = right;
     }
-    return root;
+  }
+
+  // create_bvh + BVH::BVH over the object ids in `ids` (permuted in place like the reference).
+  // The top levels are split on this thread; below them the independent subtrees are built
+  // on worker threads (each writes its own node list), then spliced in.  Same topology and
+  // boxes as a serial build: every node depends only on its own id range.
+  int build(std::vector<int>& ids) {
+    const int n = (int)ids.size();
+    if (n == 0) return -1;
+    if (n == 1) return ids[0];
+    constexpr int kParallelDepth = 5, kParallelMin = 1 << 12;
+    struct Task {
+      int begin, end, axis, parent, side;
+    };
+    std::vector<Task> tasks;
+    std::vector<Obj> top;
+    // top levels, serially, into `top` (local refs), deferring deep ranges to tasks
+    struct Range {
+      int begin, end, axis, node, depth;
+    };
+    std::vector<Range> todo;
+    auto open = [&](int b, int e, int ax, int depth) {
+      Obj o;
+      o.kind = kObjBvh;
+      o.axis = ax;
+      o.box.grow_all(ids, b, e, objs);
+      top.push_back(o);
+      todo.push_back({b, e, ax, (int)top.size() - 1, depth});
+      return node_ref((int)top.size() - 1);
+    };
+    open(0, n, 0, 0);
+    while (!todo.empty()) {
+      const Range r = todo.back();
+      todo.pop_back();
+      const float split = top[r.node].box.mid[r.axis];
+      int m = r.begin;
+      for (int i = r.begin; i < r.end; i++)
+        if (objs[ids[i]].box.mid[r.axis] < split) std::swap(ids[i], ids[m++]);
+      if (m == r.begin || m == r.end) m = r.begin + (r.end - r.begin) / 2;
+      const int next = (r.axis + 1) % 3;
+      const int bounds[2][2] = {{r.begin, m}, {m, r.end}};
+      for (int side = 0; side < 2; side++) {
+        const int b = bounds[side][0], e = bounds[side][1];
+        int ref;
+        if (b + 1 == e) {
+          ref = ids[b];
+        } else if (r.depth + 1 >= kParallelDepth || e - b < kParallelMin) {
+          tasks.push_back({b, e, next, r.node, side});
+          ref = -1;  // patched below
+        } else {
+          ref = open(b, e, next, r.depth + 1);
+        }
+        (side == 0 ? top[r.node].a : top[r.node].b) = ref;
+      }
+    }
+    std::vector<std::vector<Obj>> sub(tasks.size());
+    {
+      std::vector<std::thread> pool;
+      const unsigned workers = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+      std::atomic<size_t> next_task{0};
+      for (unsigned w = 0; w < workers && w < tasks.size(); w++)
+        pool.emplace_back([&] {
+          for (size_t t; (t = next_task++) < tasks.size();)
+            build_range(ids, tasks[t].begin, tasks[t].end, tasks[t].axis, sub[t]);
+        });
+      for (auto& t : pool) t.join();
+    }
+    // splice: top nodes, then each task's nodes; resolve local refs to object ids
+    auto splice = [&](std::vector<Obj>& nodes) {
+      const int base = (int)objs.size();
+      for (Obj& o : nodes) {
+        if (o.a <= -2) o.a = base + (-2 - o.a);
+        if (o.b <= -2) o.b = base + (-2 - o.b);
+        objs.push_back(o);
+      }
+      return base;
+    };
+    const int top_base = splice(top);
+    for (size_t t = 0; t < tasks.size(); t++) {
+      const int root = splice(sub[t]);  // a task's first node is its root
+      Obj& parent = objs[top_base + tasks[t].parent];
+      (tasks[t].side == 0 ? parent.a : parent.b) = root;
+    }
+    return top_base;
   }
 };
 

@@ -5,8 +5,14 @@
 //
 // The reference parses with tinyxml2 6.1.0 (vendored at HW2/tinyxml2.*); we use our own DOM
 // reader (xml_dom.h).
+#include <locale.h>
+
 #include <cctype>
+#include <cerrno>
+#include <climits>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <memory>
@@ -17,6 +23,122 @@
 #include "xml_dom.h"
 
 namespace rt {
+namespace {
+
+// ---- fast path for the two bulk lists (VertexData, Faces).  operator>> on a float is
+// libstdc++ num_get -> strtof in the "C" locale; on an int, strtol + range check.  For text
+// that is nothing but whitespace-separated plain decimal tokens (optional '-', digits, optional
+// fraction, optional exponent) in complete triples, the loop `while (!(ss >> x).eof())` reads
+// exactly those tokens, so calling strtof_l / strtol directly gives the same bits at a fraction
+// of the cost.  Anything else (a '+', "inf", a partial triple, a token strtof would stop
+// inside) takes the stream path unchanged.
+locale_t c_locale() {
+  static locale_t loc = newlocale(LC_ALL_MASK, "C", (locale_t)0);
+  return loc;
+}
+bool is_ws(char c) { return c == ' ' || c == '\n' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
+bool plain_number(const char* b, const char* e, bool integer) {
+  const char* p = b;
+  if (p < e && *p == '-') p++;
+  int digits = 0;
+  while (p < e && *p >= '0' && *p <= '9') p++, digits++;
+  if (integer) return digits > 0 && p == e;
+  if (p < e && *p == '.') {
+    p++;
+    while (p < e && *p >= '0' && *p <= '9') p++, digits++;
+  }
+  if (digits == 0) return false;
+  if (p < e && (*p == 'e' || *p == 'E')) {
+    p++;
+    if (p < e && (*p == '+' || *p == '-')) p++;
+    int ed = 0;
+    while (p < e && *p >= '0' && *p <= '9') p++, ed++;
+    if (ed == 0) return false;
+  }
+  return p == e;
+}
+// Parses `text` as whitespace-separated numbers; false = not eligible (use the stream).
+bool fast_floats(const std::string& text, std::vector<float>& out) {
+  std::vector<float> v;
+  const char* p = text.c_str();
+  const char* end = p + text.size();
+  while (true) {
+    while (p < end && is_ws(*p)) p++;
+    if (p == end) break;
+    const char* b = p;
+    while (p < end && !is_ws(*p)) p++;
+    if (!plain_number(b, p, false)) return false;
+    errno = 0;
+    char* stop = nullptr;
+    const float f = strtof_l(b, &stop, c_locale());
+    if (stop != p || errno == ERANGE) return false;
+    v.push_back(f);
+  }
+  if (v.size() % 3) return false;
+  out.insert(out.end(), v.begin(), v.end());
+  return true;
+}
+bool fast_ints(const std::string& text, std::vector<int>& out, int delta) {
+  std::vector<int> v;
+  const char* p = text.c_str();
+  const char* end = p + text.size();
+  while (true) {
+    while (p < end && is_ws(*p)) p++;
+    if (p == end) break;
+    const char* b = p;
+    while (p < end && !is_ws(*p)) p++;
+    if (!plain_number(b, p, true) || p - b > 11) return false;
+    errno = 0;
+    char* stop = nullptr;
+    const long x = std::strtol(b, &stop, 10);
+    if (stop != p || errno == ERANGE || x < INT_MIN || x > INT_MAX) return false;
+    v.push_back((int)x + delta);
+  }
+  if (v.size() % 3) return false;
+  out.insert(out.end(), v.begin(), v.end());
+  return true;
+}
+// The shared stream holds nothing but whitespace before its next read.
+bool stream_drained(std::stringstream& ss) {
+  const std::streampos g = ss.tellg();
+  if (g < 0) return false;
+  const std::string& all = ss.str();
+  for (size_t i = (size_t)g; i < all.size(); i++)
+    if (!is_ws(all[i])) return false;
+  return true;
+}
+
+// HW7's binary lists (HW7/src/Scene.cpp:1839-1904): int32 N, then N float triples (vertices)
+// or N int32 triples (faces).  The path is used as given (fopen, like the reference); a
+// relative path that does not open is retried next to the scene file.
+FILE* open_beside(const std::string& name, const std::string& scene_path) {
+  FILE* f = std::fopen(name.c_str(), "rb");
+  if (!f && !name.empty() && name[0] != '/') {
+    const size_t slash = scene_path.find_last_of('/');
+    if (slash != std::string::npos) f = std::fopen((scene_path.substr(0, slash + 1) + name).c_str(), "rb");
+  }
+  if (!f) throw std::ios_base::failure("cannot open binary list " + name);
+  return f;
+}
+template <typename T>
+void read_binary_triples(const std::string& name, const std::string& scene_path, std::vector<T>& out,
+                         T delta) {
+  FILE* f = open_beside(name, scene_path);
+  int n = 0;
+  if (std::fread(&n, sizeof n, 1, f) != 1 || n < 0) {
+    std::fclose(f);
+    throw std::runtime_error("scene xml: truncated binary list " + name);
+  }
+  const size_t base = out.size();
+  out.resize(base + 3 * (size_t)n);
+  const size_t got = std::fread(out.data() + base, sizeof(T), 3 * (size_t)n, f);
+  std::fclose(f);
+  if (got != 3 * (size_t)n) throw std::runtime_error("scene xml: truncated binary list " + name);
+  if (delta != T(0))
+    for (size_t i = base; i < out.size(); i++) out[i] += delta;
+}
+
+}  // namespace
 
 void load_scene_xml(const std::string& path, XmlSceneStorage& st, rt_scene_desc& d) {
   const std::unique_ptr<Node> root = parse_xml_file(path);
@@ -93,11 +215,23 @@ void load_scene_xml(const std::string& path, XmlSceneStorage& st, rt_scene_desc&
     st.materials.push_back(M);
   }
 
-  ss << node_text(root->first("VertexData"), "VertexData") << std::endl;
-  float x, y, z;
-  while (!(ss >> x).eof()) {  // HW2/Scene.cpp:372-375
-    ss >> y >> z;
-    st.vertices.insert(st.vertices.end(), {x, y, z});
+  // <ZeroBasedIndexing>true</ZeroBasedIndexing> applies to binary face lists (HW7 Scene.cpp:515-522)
+  bool zero_based = false;
+  if (const Node* z = root->first("ZeroBasedIndexing"))
+    zero_based = z->has_text && std::string(z->text) == "true";
+  const Node* vd = root->first("VertexData");
+  if (vd && vd->attr("binaryFile")) {  // HW7 format (f4)
+    read_binary_triples<float>(vd->attr("binaryFile"), path, st.vertices, 0.0f);
+  } else {
+    const char* vtext = node_text(vd, "VertexData");
+    if (!(stream_drained(ss) && fast_floats(vtext, st.vertices))) {
+      ss << vtext << std::endl;
+      float x, y, z;
+      while (!(ss >> x).eof()) {  // HW2/Scene.cpp:372-375
+        ss >> y >> z;
+        st.vertices.insert(st.vertices.end(), {x, y, z});
+      }
+    }
   }
   ss.clear();
 
@@ -107,12 +241,27 @@ void load_scene_xml(const std::string& path, XmlSceneStorage& st, rt_scene_desc&
     int mat;
     ss << node_text(m->first("Material"), "Material") << std::endl;
     ss >> mat;
-    ss << node_text(m->first("Faces"), "Faces") << std::endl;
-    int a, b, c, count = 0;
-    while (!(ss >> a).eof()) {  // HW2/Scene.cpp:394-398
-      ss >> b >> c;
-      st.mesh_faces.insert(st.mesh_faces.end(), {a - 1, b - 1, c - 1});
-      ++count;
+    const Node* faces = m->first("Faces");
+    int count = 0;
+    const size_t before = st.mesh_faces.size();
+    if (faces && faces->attr("binaryFile")) {  // HW7 format (f4), HW7 Scene.cpp:1866-1904
+      const int offset = faces->int_attr("vertexOffset", 0);
+      read_binary_triples<int>(faces->attr("binaryFile"), path, st.mesh_faces,
+                               (zero_based ? 0 : -1) + offset);
+      count = (int)((st.mesh_faces.size() - before) / 3);
+    } else {
+      const char* ftext = node_text(faces, "Faces");
+      if (stream_drained(ss) && fast_ints(ftext, st.mesh_faces, -1)) {
+        count = (int)((st.mesh_faces.size() - before) / 3);
+      } else {
+        ss << ftext << std::endl;
+        int a, b, c;
+        while (!(ss >> a).eof()) {  // HW2/Scene.cpp:394-398
+          ss >> b >> c;
+          st.mesh_faces.insert(st.mesh_faces.end(), {a - 1, b - 1, c - 1});
+          ++count;
+        }
+      }
     }
     ss.clear();
     st.mesh_material.push_back(mat - 1);
