@@ -1,0 +1,283 @@
+// Culling hierarchy over reference treelets.
+//
+// The reference BVH (midpoint split cycling x -> y -> z, HW2/Bounding_volume_hierarchy.cpp:
+// 3-29) decides WHICH leaves a ray may test: a leaf is reachable iff every ancestor box
+// accepts the ray (BVH.cpp:31-55).  Its shape, though, makes a ray test ~146 boxes on C3.
+// Here the reference tree is cut into treelets (maximal subtrees with <= K leaves; a lone leaf
+// child of a larger node is a treelet of its own) and a binned-SAH tree is built over the
+// treelets.  The kernels walk the SAH tree to find treelets, then walk each treelet with the
+// reference's own semantics.  Reachability is preserved by a per-treelet guard:
+//   * the guard box is the innermost reference ancestor box a ray must pass to enter the
+//     treelet (the treelet root's own box, or for a lone leaf its parent's box);
+//   * the fast slab test decides "accept" only with a 2^-20 relative margin, and an accept
+//     with that margin implies every enclosing reference box accepts too (the boxes are
+//     unions, so the exact t-intervals nest; each computed bound is within 2^-22 of its exact
+//     value) — no need to test the ancestors;
+//   * inside the margin band the kernel walks the ancestor chain with the literal reference
+//     test (ref_parent / ref_box below).
+// SAH inner boxes are only culling bounds: they contain every guard box below them, and the
+// kernel tests them conservatively (2^-18 relative slack), so a treelet the reference would
+// enter is never culled.  The SAH tree's nodes are appended to HostScene::nodes after the
+// reference nodes; DevNode::pad marks them (kAccelNode | guard bits per child).
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <stdexcept>
+#include <vector>
+
+#include "host_scene.h"
+
+namespace rt {
+namespace {
+
+struct Item {
+  int ref;        // treelet root: reference node index, or ~leaf
+  float box[6];   // guard box
+  float c[3];     // centroid (SAH binning)
+  int height;     // internal-node levels of the treelet (stack use inside it)
+};
+
+struct Box {
+  float lo[3] = {std::numeric_limits<float>::infinity(), std::numeric_limits<float>::infinity(),
+                 std::numeric_limits<float>::infinity()};
+  float hi[3] = {-std::numeric_limits<float>::infinity(), -std::numeric_limits<float>::infinity(),
+                 -std::numeric_limits<float>::infinity()};
+  void grow(const float* b) {
+    for (int a = 0; a < 3; a++) {
+      lo[a] = std::min(lo[a], b[a]);
+      hi[a] = std::max(hi[a], b[a + 3]);
+    }
+  }
+  void grow(const Box& b) {
+    for (int a = 0; a < 3; a++) {
+      lo[a] = std::min(lo[a], b.lo[a]);
+      hi[a] = std::max(hi[a], b.hi[a]);
+    }
+  }
+  double area() const {
+    const double dx = std::max(0.0, (double)hi[0] - lo[0]), dy = std::max(0.0, (double)hi[1] - lo[1]),
+                 dz = std::max(0.0, (double)hi[2] - lo[2]);
+    return dx * dy + dy * dz + dz * dx;
+  }
+};
+
+// outward by a few ulps: a culling bound only, never compared with the reference's boxes
+float widen_down(float x) { return x - std::fabs(x) * 0x1p-20f - 0x1p-100f; }
+float widen_up(float x) { return x + std::fabs(x) * 0x1p-20f + 0x1p-100f; }
+
+struct SahBuilder {
+  std::vector<Item>& items;
+  std::vector<DevNode>& nodes;
+  int depth = 0;  // max over leaves of (SAH levels + treelet height)
+
+  static constexpr int kBins = 32;
+
+  // Splits items[b, e) (e - b >= 2); returns the split point.
+  int split(int b, int e) {
+    Box cb;
+    for (int i = b; i < e; i++) {
+      const float p[6] = {items[i].c[0], items[i].c[1], items[i].c[2],
+                          items[i].c[0], items[i].c[1], items[i].c[2]};
+      cb.grow(p);
+    }
+    double best = std::numeric_limits<double>::infinity();
+    int best_axis = -1, best_bin = 0;
+    for (int a = 0; a < 3; a++) {
+      const float ext = cb.hi[a] - cb.lo[a];
+      if (!(ext > 0.0f)) continue;
+      Box bins[kBins];
+      int cnt[kBins] = {};
+      const float scale = kBins / ext;
+      for (int i = b; i < e; i++) {
+        int k = (int)((items[i].c[a] - cb.lo[a]) * scale);
+        k = std::min(std::max(k, 0), kBins - 1);
+        cnt[k]++;
+        bins[k].grow(items[i].box);
+      }
+      double right_area[kBins];
+      int right_cnt[kBins];
+      Box acc;
+      int n = 0;
+      for (int k = kBins - 1; k > 0; k--) {
+        acc.grow(bins[k]);
+        n += cnt[k];
+        right_area[k] = acc.area();
+        right_cnt[k] = n;
+      }
+      Box left;
+      int nl = 0;
+      for (int k = 1; k < kBins; k++) {  // split between bins k-1 and k
+        left.grow(bins[k - 1]);
+        nl += cnt[k - 1];
+        if (nl == 0 || right_cnt[k] == 0) continue;
+        const double cost = left.area() * nl + right_area[k] * right_cnt[k];
+        if (cost < best) {
+          best = cost;
+          best_axis = a;
+          best_bin = k;
+        }
+      }
+    }
+    if (best_axis < 0) return b + (e - b) / 2;  // coincident centroids: halve by position
+    const int a = best_axis;
+    const float scale = kBins / (cb.hi[a] - cb.lo[a]);
+    auto goes_left = [&](const Item& it) {
+      int k = (int)((it.c[a] - cb.lo[a]) * scale);
+      k = std::min(std::max(k, 0), kBins - 1);
+      return k < best_bin;
+    };
+    const int m = (int)(std::partition(items.begin() + b, items.begin() + e, goes_left) -
+                        items.begin());
+    return (m == b || m == e) ? b + (e - b) / 2 : m;
+  }
+
+  // Emits the SAH tree over items[b0, e0) (>= 2 items) in DFS preorder; returns its root.
+  int build(int b0, int e0) {
+    struct Task {
+      int b, e, parent, side, depth;
+    };
+    std::vector<Task> todo{{b0, e0, -1, 0, 0}};
+    int root = -1;
+    while (!todo.empty()) {
+      const Task t = todo.back();
+      todo.pop_back();
+      const int idx = (int)nodes.size();
+      nodes.push_back(DevNode{});
+      if (t.parent >= 0)
+        nodes[t.parent].child[t.side] = idx;
+      else
+        root = idx;
+      DevNode& N = nodes[idx];
+      N.pad = kAccelNode;
+      const int m = split(t.b, t.e);
+      const int ranges[2][2] = {{t.b, m}, {m, t.e}};
+      for (int side = 0; side < 2; side++) {
+        const int b = ranges[side][0], e = ranges[side][1];
+        if (e - b == 1) {
+          const Item& it = items[b];
+          N.child[side] = it.ref;
+          N.pad |= side ? kAccelGuard1 : kAccelGuard0;
+          for (int a = 0; a < 3; a++) {
+            N.lo[a][side] = it.box[a];
+            N.hi[a][side] = it.box[a + 3];
+          }
+          depth = std::max(depth, t.depth + 1 + it.height);
+        } else {
+          Box u;
+          for (int i = b; i < e; i++) u.grow(items[i].box);
+          for (int a = 0; a < 3; a++) {
+            N.lo[a][side] = widen_down(u.lo[a]);
+            N.hi[a][side] = widen_up(u.hi[a]);
+          }
+        }
+      }
+      // right pushed first: the left subtree is emitted first (preorder)
+      for (int side = 1; side >= 0; side--)
+        if (ranges[side][1] - ranges[side][0] >= 2)
+          todo.push_back({ranges[side][0], ranges[side][1], idx, side, t.depth + 1});
+    }
+    return root;
+  }
+};
+
+}  // namespace
+
+void build_accel(HostScene& s, int K) {
+  if (s.accel_root >= 0) s.nodes.resize(s.accel_root);  // drop an earlier culling tree
+  s.accel_root = -1;
+  s.accel_depth = 0;
+  s.accel_items = 0;
+  s.ancestry.clear();
+  if (K <= 0 || s.root_kind != kRootNode) return;
+  const int nn = (int)s.nodes.size();
+  std::vector<int> leaves(nn, 0), height(nn, 1);
+  std::vector<int> parent(nn, -1), leaf_parent(s.prims.size(), -1);
+  std::vector<float> ref_box((size_t)nn * 6, 0.0f);
+  std::memcpy(&ref_box[0], s.root_box, sizeof s.root_box);
+  for (int n = 0; n < nn; n++) {  // preorder: a parent precedes its children
+    const DevNode& N = s.nodes[n];
+    for (int side = 0; side < 2; side++) {
+      const int c = N.child[side];
+      if (c >= 0) {
+        parent[c] = n;
+        float* b = &ref_box[(size_t)c * 6];
+        for (int a = 0; a < 3; a++) {
+          b[a] = N.lo[a][side];
+          b[a + 3] = N.hi[a][side];
+        }
+      } else {
+        leaf_parent[~c] = n;
+      }
+    }
+  }
+  for (int n = nn - 1; n >= 0; n--) {
+    const DevNode& N = s.nodes[n];
+    int h = 0;
+    for (int side = 0; side < 2; side++) {
+      const int c = N.child[side];
+      if (c >= 0) {
+        leaves[n] += leaves[c];
+        h = std::max(h, height[c]);
+      } else {
+        leaves[n] += 1;
+      }
+    }
+    height[n] = h + 1;
+  }
+  if (leaves[0] <= K) return;  // the whole tree is one treelet: nothing to cull
+  s.ancestry.assign(std::max<size_t>(nn, leaf_parent.size()), DevAncestry{});
+  for (size_t i = 0; i < s.ancestry.size(); i++) {
+    DevAncestry& A = s.ancestry[i];
+    if (i < (size_t)nn) {
+      std::memcpy(A.box, &ref_box[i * 6], sizeof A.box);
+      A.parent = parent[i];
+    }
+    A.leaf_parent = i < leaf_parent.size() ? leaf_parent[i] : -1;
+  }
+  std::vector<Item> items;
+  std::vector<int> todo{0};
+  auto push_item = [&](int ref, const float* box, int h) {
+    Item it;
+    it.ref = ref;
+    std::memcpy(it.box, box, sizeof it.box);
+    for (int a = 0; a < 3; a++) it.c[a] = 0.5f * (box[a] + box[a + 3]);
+    it.height = h;
+    items.push_back(it);
+  };
+  while (!todo.empty()) {
+    const int n = todo.back();
+    todo.pop_back();
+    const DevNode& N = s.nodes[n];
+    for (int side = 0; side < 2; side++) {
+      const int c = N.child[side];
+      if (c < 0)
+        push_item(c, &ref_box[(size_t)n * 6], 0);  // lone leaf: guarded by the parent's box
+      else if (leaves[c] <= K)
+        push_item(c, &ref_box[(size_t)c * 6], height[c]);
+      else
+        todo.push_back(c);
+    }
+  }
+  // The node array is appended to; nothing else refers to the indices past the reference's.
+  SahBuilder B{items, s.nodes};
+  const int root = B.build(0, (int)items.size());
+  Box u;
+  for (const Item& it : items) u.grow(it.box);
+  for (int a = 0; a < 3; a++) {
+    s.accel_box[a] = widen_down(u.lo[a]);
+    s.accel_box[a + 3] = widen_up(u.hi[a]);
+  }
+  s.accel_root = root;
+  s.accel_depth = B.depth + 1;
+  s.accel_items = (int)items.size();
+}
+
+int accel_treelet_leaves() {
+  const char* e = std::getenv("CENG795_RT_TREELET");
+  if (e && *e) return std::atoi(e);
+  return kDefaultTreeletLeaves;
+}
+
+}  // namespace rt

@@ -37,7 +37,18 @@ struct HostScene {
   int root_ref = 0;
   float root_box[6] = {0, 0, 0, 0, 0, 0};
   int depth = 0;  // internal-node levels
+  // culling tree over reference treelets (accel_build.cpp), FAST traversal only
+  int accel_root = -1;   // index into nodes (SAH nodes follow the reference's), -1 = none
+  int accel_depth = 0;   // stack levels a traversal from accel_root can need
+  int accel_items = 0;   // treelets
+  float accel_box[6] = {0, 0, 0, 0, 0, 0};
+  std::vector<DevAncestry> ancestry;  // max(nodes, leaves) entries, see DevAncestry
 };
+
+// Cuts the reference tree into treelets of <= K leaves and appends a SAH tree over them
+// (K <= 0: none).  Leaves the reference nodes, leaves and tie-break order untouched.
+void build_accel(HostScene& s, int K);
+int accel_treelet_leaves();  // CENG795_RT_TREELET, else kDefaultTreeletLeaves
 
 // Builds `out` from `desc`; throws std::invalid_argument on a bad description.
 void build_host_scene(const rt_scene_desc& desc, HostScene& out);

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <memory>
@@ -38,6 +39,7 @@ struct rt_scene {
   DevNode* d_nodes = nullptr;
   DevPrim* d_prims = nullptr;
   float* d_normals = nullptr;
+  DevAncestry* d_anc = nullptr;
   DevMaterial* d_mats = nullptr;
   DevLight* d_lights = nullptr;
   unsigned long long* d_counters = nullptr;
@@ -105,6 +107,7 @@ void free_device(rt_scene* s) {
   (void)hipFree(s->d_nodes);
   (void)hipFree(s->d_prims);
   (void)hipFree(s->d_normals);
+  (void)hipFree(s->d_anc);
   (void)hipFree(s->d_mats);
   (void)hipFree(s->d_lights);
   (void)hipFree(s->d_counters);
@@ -139,11 +142,17 @@ int create_from_host(rt_scene* s, int device) {
   if (device < 0) hip_check(hipGetDevice(&device), "hipGetDevice");
   s->device = device;
   DeviceGuard g(device);
+  build_accel(s->host, accel_treelet_leaves());
+  if (s->host.accel_depth > max_supported_depth()) build_accel(s->host, 0);
+  if (std::getenv("CENG795_RT_VERBOSE"))
+    std::fprintf(stderr, "ceng795_rt: %zu nodes (reference depth %d), culling tree root %d over "
+                 "%d treelets, depth %d\n", s->host.nodes.size(), s->host.depth,
+                 s->host.accel_root, s->host.accel_items, s->host.accel_depth);
   const HostScene& h = s->host;
   if (h.depth > max_supported_depth())
     throw std::invalid_argument("BVH deeper than " + std::to_string(max_supported_depth()) +
                                 " levels is not supported");
-  s->deep = h.depth > kLaneStack - 2;
+  s->deep = std::max(h.depth, h.accel_depth) > kLaneStack - 2;
   for (const DevPrim& p : h.prims) s->has_spheres |= p.kind == kPrimSphere;
   for (const DevMaterial& m : h.materials) {
     const bool mirror = m.mirror[0] != 0 || m.mirror[1] != 0 || m.mirror[2] != 0;
@@ -153,6 +162,7 @@ int create_from_host(rt_scene* s, int device) {
   s->d_nodes = upload(h.nodes, "upload nodes");
   s->d_prims = upload(h.prims, "upload prims");
   s->d_normals = upload(h.normals, "upload normals");
+  s->d_anc = upload(h.ancestry, "upload ancestry");
   s->d_mats = upload(h.materials, "upload materials");
   s->d_lights = upload(h.lights, "upload lights");
   hip_check(hipMalloc(&s->d_counters, sizeof(unsigned long long) * kCounterWidth * kCounterRows),
@@ -201,6 +211,9 @@ RenderParams make_params(const rt_scene* s, int cam, int row0, int row_stride, i
   P.root_kind = h.root_kind;
   P.root_ref = h.root_ref;
   std::memcpy(P.root_box, h.root_box, sizeof P.root_box);
+  P.accel_root = h.accel_root;
+  std::memcpy(P.accel_box, h.accel_box, sizeof P.accel_box);
+  P.anc = s->d_anc;
   std::memcpy(P.cam_e, c.e, 12);
   std::memcpy(P.cam_tl, c.top_left, 12);
   std::memcpy(P.cam_su, c.s_u, 12);

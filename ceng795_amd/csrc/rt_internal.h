@@ -30,6 +30,12 @@ enum : int {
   kCntExactBox = 12
 };
 
+// DevNode::pad of the culling-tree nodes (accel_build.cpp); reference nodes have pad == 0.
+// Guard bit set: that child is a treelet root (node index or ~leaf) behind a reachability
+// guard; clear: an inner culling node tested conservatively.
+enum : int32_t { kAccelGuard0 = 1, kAccelGuard1 = 2, kAccelNode = 4 };
+constexpr int kDefaultTreeletLeaves = 2;
+
 struct alignas(16) DevNode {
   // Both CHILD boxes, interleaved per coordinate ([axis][child]) so one packed-fp32 op
   // (v_pk_add_f32 / v_pk_mul_f32) works on both children.  Unused for a leaf child.
@@ -37,7 +43,7 @@ struct alignas(16) DevNode {
   float hi[3][2];
   int32_t child[2];  // >= 0: internal node index; < 0: leaf index ~child
   int32_t axis;      // split dimension of THIS node (Bounding_volume_hierarchy.cpp:8)
-  int32_t pad;
+  int32_t pad;       // 0: reference node; else kAccelNode | guard bits
 };
 static_assert(sizeof(DevNode) == 64, "node must be one 64-byte scalar load");
 
@@ -54,6 +60,15 @@ struct alignas(16) DevPrim {
   float cx;  // triangle: a1.y*a2.z - a2.y*a1.z (the d-free minor of Triangle.h:35-37)
 };
 static_assert(sizeof(DevPrim) == 48, "prim record is three 16-byte loads");
+
+// Reference ancestry for the culling tree's exact guard (accel_build.cpp): entry i holds
+// reference node i's own box and parent (-1 at the root), and the node holding leaf i.
+struct alignas(16) DevAncestry {
+  float box[6];
+  int32_t parent;
+  int32_t leaf_parent;
+};
+static_assert(sizeof(DevAncestry) == 32, "");
 
 struct DevMaterial {  // HW2/Material.h
   float ambient[3], diffuse[3], specular[3], mirror[3], transparency[3];
@@ -99,6 +114,11 @@ struct RenderParams {
   int root_kind;
   int root_ref;           // kRootNode: node index; else leaf index
   float root_box[6];
+  // culling tree (FAST traversal): root node index or -1, its conservative box, and the
+  // reference ancestry a guard walks when its fast test cannot decide
+  int accel_root;
+  float accel_box[6];
+  const struct DevAncestry* anc;
   // camera (rt_camera)
   float cam_e[3], cam_tl[3], cam_su[3], cam_sv[3];
   int width, height;

@@ -118,8 +118,7 @@ __device__ unsigned long long g_exact_fallbacks;  // lanes that needed box_exact
 // flagged for box_exact.  Written branch-free: both children of a node are tested together.
 // tnear (approximate entry distance) only orders and culls.
 template <bool SKIP>
-__device__ __forceinline__ void slab_fast(const float* b, const LaneRay& r, float& tn,
-                                          bool& accept, bool& undecided) {
+__device__ __forceinline__ void slab_span(const float* b, const LaneRay& r, float& tn, float& tf) {
   const float ax = (b[0] - r.o.x) * r.r.x, bx = (b[3] - r.o.x) * r.r.x;
   const float ay = (b[1] - r.o.y) * r.r.y, by = (b[4] - r.o.y) * r.r.y;
   const float az = (b[2] - r.o.z) * r.r.z, bz = (b[5] - r.o.z) * r.r.z;
@@ -135,14 +134,40 @@ __device__ __forceinline__ void slab_fast(const float* b, const LaneRay& r, floa
     fz = r.skip2 ? RT_INF : fz;
   }
   tn = __builtin_fmaxf(__builtin_fmaxf(nx, ny), nz);
-  const float tf = __builtin_fminf(__builtin_fminf(fx, fy), fz);
+  tf = __builtin_fminf(__builtin_fminf(fx, fy), fz);
+}
+
+// sure_in: the reference accepts (tf >= 0, and tn <= tf decided outside a 2^-20 relative
+// band); sure_out: it rejects.  Neither: box_exact decides (NaN lands here too).
+__device__ __forceinline__ void decide_sure(float tn, float tf, bool& sure_in, bool& sure_out) {
   const float band = (__builtin_fabsf(tn) + __builtin_fabsf(tf)) * 0x1p-20f + 0x1p-120f;
-  const bool behind = !(tf >= 0.0f);  // exact sign (NaN -> undecided below)
-  const bool sure_in = tn < tf - band;
-  const bool sure_out = tn > tf + band;
-  accept = !behind & sure_in;
-  undecided = !(sure_in | sure_out) | (tf != tf);
-  undecided = undecided & !(tf < 0.0f);
+  sure_in = (tn < tf - band) & (tf >= 0.0f);
+  sure_out = (tf < 0.0f) | (tn > tf + band);
+}
+
+__device__ __forceinline__ void decide_fast(float tn, float tf, bool& accept, bool& undecided) {
+  bool out;
+  decide_sure(tn, tf, accept, out);
+  undecided = !(accept | out);
+}
+
+template <bool SKIP>
+__device__ __forceinline__ void slab_fast(const float* b, const LaneRay& r, float& tn,
+                                          bool& accept, bool& undecided) {
+  float tf;
+  slab_span<SKIP>(b, r, tn, tf);
+  decide_fast(tn, tf, accept, undecided);
+}
+
+// Culling-tree boxes (accel_build.cpp) contain every reference box below them.  If the
+// reference test accepts a contained box, the exact t-intervals nest and every computed
+// bound is within 2^-22 relative of its exact value, so the container is never `sure_out`
+// (2^-20 band, same skipped axes): a culling node never drops a treelet the reference would
+// enter.  Its test is therefore just !sure_out.
+__device__ __forceinline__ bool decide_cull(float tn, float tf) {
+  bool in, out;
+  decide_sure(tn, tf, in, out);
+  return !out;
 }
 
 // ------------------------------------------------------------------ primitives
@@ -295,26 +320,49 @@ __device__ __forceinline__ bool child_box_exact(const DevNode& N, int c, const L
   return box_exact(b, r);
 }
 
-// One packet visit of a BVH2 node: both child slab tests (computed unconditionally so the
-// 64-byte record arrives in one scalar load), the rare exact fallback behind one ballot, and
-// which lanes enter each child.  Leaf children are never entered (the caller tests them).
+// Treelet guard that the fast test could not decide: the reference's literal test on the
+// guard box and on every enclosing reference box (the ancestry of BVH.cpp:31-55).
+__device__ bool guard_exact(const RenderParams& P, int child, const LaneRay& r) {
+  int v = child >= 0 ? child : P.anc[~child].leaf_parent;
+  while (v >= 0) {
+    if (!box_exact(P.anc[v].box, r)) return false;
+    v = P.anc[v].parent;
+  }
+  return true;
+}
+
+// One packet visit of a node of either tree, per child:
+//   * leaf of a reference node: every lane in the node tests it (leaves have no box);
+//   * inner child of a reference node: the reference's box test (fast, else box_exact);
+//   * guarded child of a culling node (treelet root or lone leaf): the reference's acceptance
+//     of its guard box, decided with margin — which implies every enclosing reference box
+//     accepts too (accel_build.cpp) — else guard_exact over the whole ancestry;
+//   * inner child of a culling node: the conservative cull test.
+// h0/h1: lanes that enter (inner) or test (leaf) each child.
 template <bool SKIP>
-__device__ __forceinline__ void visit_boxes(const DevNode& N, const LaneRay& r, bool in,
-                                            bool& h0, bool& h1, float& t0, float& t1,
-                                            Diag& dg) {
-  bool u0, u1;
+__device__ __forceinline__ void visit_node(const RenderParams& P, const DevNode& N,
+                                           const LaneRay& r, bool in, bool& h0, bool& h1,
+                                           float& t0, float& t1) {
   const float b0[6] = {N.lo[0][0], N.lo[1][0], N.lo[2][0], N.hi[0][0], N.hi[1][0], N.hi[2][0]};
   const float b1[6] = {N.lo[0][1], N.lo[1][1], N.lo[2][1], N.hi[0][1], N.hi[1][1], N.hi[2][1]};
-  slab_fast<SKIP>(b0, r, t0, h0, u0);
-  slab_fast<SKIP>(b1, r, t1, h1, u1);
-  const bool live0 = in & (N.child[0] >= 0), live1 = in & (N.child[1] >= 0);
-  h0 &= live0;
-  h1 &= live1;
-  u0 &= live0;
-  u1 &= live1;
+  float f0, f1;
+  slab_span<SKIP>(b0, r, t0, f0);
+  slab_span<SKIP>(b1, r, t1, f1);
+  bool in0, out0, in1, out1;
+  decide_sure(t0, f0, in0, out0);
+  decide_sure(t1, f1, in1, out1);
+  const int pad = N.pad;  // wave-uniform
+  const bool an = (pad & kAccelNode) != 0;
+  const bool g0 = (pad & kAccelGuard0) != 0, g1 = (pad & kAccelGuard1) != 0;
+  const bool rleaf0 = !an & (N.child[0] < 0), rleaf1 = !an & (N.child[1] < 0);
+  const bool cull0 = an & !g0, cull1 = an & !g1;
+  h0 = in & (rleaf0 | in0 | (cull0 & !out0));
+  h1 = in & (rleaf1 | in1 | (cull1 & !out1));
+  const bool u0 = in & !(rleaf0 | cull0) & !(in0 | out0);
+  const bool u1 = in & !(rleaf1 | cull1) & !(in1 | out1);
   if (ballot(u0 | u1)) {
-    if (u0) h0 = child_box_exact(N, 0, r);
-    if (u1) h1 = child_box_exact(N, 1, r);
+    if (u0) h0 = g0 ? guard_exact(P, N.child[0], r) : child_box_exact(N, 0, r);
+    if (u1) h1 = g1 ? guard_exact(P, N.child[1], r) : child_box_exact(N, 1, r);
     DIAG(if (u0 | u1) atomicAdd(&g_exact_fallbacks, 1ull));
   }
 }
@@ -409,13 +457,19 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
     }
     return;
   }
+  const bool accel = FAST && P.accel_root >= 0;  // culling tree over treelets (§4.4)
   uint64_t m[R];
 #pragma unroll
   for (int k = 0; k < R; k++) {
-    float tn;
+    float tn, tf;
     bool acc, und;
-    slab_fast<SKIP>(P.root_box, r[k], tn, acc, und);
-    m[k] = ballot(active[k] && (acc || (und && box_exact(P.root_box, r[k]))));
+    if (accel) {
+      slab_span<SKIP>(P.accel_box, r[k], tn, tf);
+      m[k] = ballot(active[k] && decide_cull(tn, tf));
+    } else {
+      slab_fast<SKIP>(P.root_box, r[k], tn, acc, und);
+      m[k] = ballot(active[k] && (acc || (und && box_exact(P.root_box, r[k]))));
+    }
   }
   if (!any_of(m)) return;
   const int lane = lane_id();
@@ -424,19 +478,18 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
   uint64_t everyone[R];
 #pragma unroll
   for (int k = 0; k < R; k++) everyone[k] = ~0ull;
-  int node = P.root_ref;
+  int node = accel ? P.accel_root : P.root_ref;
   for (;;) {
     const DevNode N = load_node(nodes, node);
-    bool in[R], h0[R], h1[R];
+    bool h0[R], h1[R];
     float t0[R], t1[R];
 #pragma unroll
-    for (int k = 0; k < R; k++) {
-      in[k] = (m[k] >> lane) & 1;
-      visit_boxes<SKIP>(N, r[k], in[k], h0[k], h1[k], t0[k], t1[k], dg);
-    }
+    for (int k = 0; k < R; k++)
+      visit_node<SKIP>(P, N, r[k], (m[k] >> lane) & 1, h0[k], h1[k], t0[k], t1[k]);
     DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(any_of(m));
          dg.leaves += (N.child[0] < 0) + (N.child[1] < 0);
-         dg.leaf_lanes += ((N.child[0] < 0) + (N.child[1] < 0)) * __builtin_popcountll(any_of(m)));
+         dg.leaf_lanes += (N.child[0] < 0 ? __builtin_popcountll(ballot(h0[0])) : 0) +
+                          (N.child[1] < 0 ? __builtin_popcountll(ballot(h1[0])) : 0));
 #ifndef RT_EXP_NOLEAF
 #pragma unroll 1
     for (int side = 0; side < 2; side++) {  // leaf children: Shape::intersect, 0 < t < best
@@ -444,8 +497,9 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
       if (c < 0) {
 #pragma unroll
         for (int k = 0; k < R; k++) {
+          const bool tests = side ? h1[k] : h0[k];
           float t;
-          if (in[k] && leaf_test<SPHERES>(prims, ~c, r[k], t) && t > 0.0f && t < RT_INF &&
+          if (tests && leaf_test<SPHERES>(prims, ~c, r[k], t) && t > 0.0f && t < RT_INF &&
               (t < best_t[k] || (t == best_t[k] && ~c < best_leaf[k]))) {
             best_t[k] = t;
             best_leaf[k] = ~c;
@@ -455,11 +509,13 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
     }
 #else
 #pragma unroll
-    for (int k = 0; k < R; k++) best_leaf[k] -= in[k] ? 1 : 0;  // keep traversal observable
+    for (int k = 0; k < R; k++) best_leaf[k] -= (int)((m[k] >> lane) & 1);  // keep it observable
 #endif
     uint64_t m0[R], m1[R];
 #pragma unroll
-    for (int k = 0; k < R; k++) {
+    for (int k = 0; k < R; k++) {  // leaves are done; only inner children are entered
+      h0[k] &= N.child[0] >= 0;
+      h1[k] &= N.child[1] >= 0;
       if (FAST) {
         const float lim = cull_limit(best_t[k]);
         h0[k] = h0[k] && t0[k] <= lim;
@@ -491,41 +547,48 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
     }
     return;
   }
+  const bool accel = FAST && P.accel_root >= 0;
   uint64_t m[R], alive[R];
 #pragma unroll
   for (int k = 0; k < R; k++) {
-    float tn;
+    float tn, tf;
     bool acc, und;
     // thr <= 0 (or NaN): nothing can satisfy 0 < t < thr
-    slab_fast<SKIP>(P.root_box, r[k], tn, acc, und);
-    m[k] = ballot(active[k] && thr[k] > 0.0f && (acc || (und && box_exact(P.root_box, r[k]))));
+    if (accel) {
+      slab_span<SKIP>(P.accel_box, r[k], tn, tf);
+      m[k] = ballot(active[k] && thr[k] > 0.0f && decide_cull(tn, tf));
+    } else {
+      slab_fast<SKIP>(P.root_box, r[k], tn, acc, und);
+      m[k] = ballot(active[k] && thr[k] > 0.0f &&
+                    (acc || (und && box_exact(P.root_box, r[k]))));
+    }
     alive[k] = m[k];
   }
   if (!any_of(m)) return;
   const int lane = lane_id();
   WaveStack<DEEP, R> st;
   st.lds = spill;
-  int node = P.root_ref;
+  int node = accel ? P.accel_root : P.root_ref;
   for (;;) {
     const DevNode N = load_node(nodes, node);
-    bool in[R], h0[R], h1[R];
+    bool h0[R], h1[R];
     float t0[R], t1[R];
 #pragma unroll
-    for (int k = 0; k < R; k++) {
-      in[k] = (m[k] >> lane) & 1;
-      visit_boxes<SKIP>(N, r[k], in[k], h0[k], h1[k], t0[k], t1[k], dg);
-    }
+    for (int k = 0; k < R; k++)
+      visit_node<SKIP>(P, N, r[k], (m[k] >> lane) & 1, h0[k], h1[k], t0[k], t1[k]);
     DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(any_of(m));
          dg.leaves += (N.child[0] < 0) + (N.child[1] < 0);
-         dg.leaf_lanes += ((N.child[0] < 0) + (N.child[1] < 0)) * __builtin_popcountll(any_of(m)));
+         dg.leaf_lanes += (N.child[0] < 0 ? __builtin_popcountll(ballot(h0[0])) : 0) +
+                          (N.child[1] < 0 ? __builtin_popcountll(ballot(h1[0])) : 0));
 #pragma unroll 1
     for (int side = 0; side < 2; side++) {
       const int c = side ? N.child[1] : N.child[0];
       if (c < 0) {
 #pragma unroll
         for (int k = 0; k < R; k++) {
+          const bool tests = side ? h1[k] : h0[k];
           float t;
-          if (in[k] && !occ[k] && leaf_test<SPHERES>(prims, ~c, r[k], t) && t > 0.0f &&
+          if (tests && !occ[k] && leaf_test<SPHERES>(prims, ~c, r[k], t) && t > 0.0f &&
               t < thr[k])
             occ[k] = true;
         }
@@ -535,6 +598,8 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
 #pragma unroll
     for (int k = 0; k < R; k++) {
       alive[k] &= ~ballot(occ[k]);
+      h0[k] &= N.child[0] >= 0;
+      h1[k] &= N.child[1] >= 0;
       if (FAST) {
         const float lim = cull_limit(thr[k]);
         h0[k] = h0[k] && t0[k] <= lim;
@@ -1086,6 +1151,12 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
   }
 }
 
+// Traversal kernels hide their dependent node loads with occupancy: hold them to 8 waves/SIMD
+// (<= 64 VGPRs, <= 100 SGPRs); the compiler otherwise settles at 7 on SGPR count.
+#ifndef RT_TRAVERSAL_OCCUPANCY
+#define RT_TRAVERSAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(8, 8)))
+#endif
+
 // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so hand each
 // XCD a contiguous run of tiles — neighbouring packets share BVH nodes through its L2.
 __device__ __forceinline__ int packet_index() {
@@ -1096,7 +1167,7 @@ __device__ __forceinline__ int packet_index() {
 }
 
 template <bool FAST, bool DEEP, bool SPHERES, int R>
-__global__ __launch_bounds__(kWavesPerBlock * 64) void trace_primary_kernel(
+__global__ __launch_bounds__(kWavesPerBlock * 64) RT_TRAVERSAL_OCCUPANCY void trace_primary_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
   const int sel0 = packet_index() * R;
@@ -1106,7 +1177,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void trace_primary_kernel(
 }
 
 template <bool FAST, bool DEEP, bool SPHERES, int R>
-__global__ __launch_bounds__(kWavesPerBlock * 64) void trace_shadow_kernel(
+__global__ __launch_bounds__(kWavesPerBlock * 64) RT_TRAVERSAL_OCCUPANCY void trace_shadow_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims,
     const DevLight* __restrict__ lights) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];

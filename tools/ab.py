@@ -4,6 +4,7 @@
 interleaved (A B C A B C ...) so device clock drift hits every variant alike.
 
     python tools/ab.py base,nocx --rounds 3
+    python tools/ab.py t0,t4,occ7@4     (tK / lib@K: treelet size K of the culling tree, 0 = none)
 """
 import argparse
 import json
@@ -25,7 +26,12 @@ def main():
     for _ in range(a.rounds):
         for v in a.variants.split(","):
             env = dict(os.environ)
-            env["CENG795_LIB"] = "" if v == "base" else v
+            lib, _, k = v.partition("@")  # <lib>@K: treelet size K of the culling tree
+            if lib[:1] == "t" and lib[1:].isdigit():  # tK: production lib
+                lib, k = "base", lib[1:]
+            env["CENG795_LIB"] = "" if lib == "base" else lib
+            if k:
+                env["CENG795_RT_TREELET"] = k
             out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "diag.py"), "timing",
                                   "--workload", a.workload], env=env, capture_output=True,
                                  text=True, timeout=300)
