@@ -138,11 +138,15 @@ __device__ __forceinline__ void slab_span(const float* b, const LaneRay& r, floa
 }
 
 // sure_in: the reference accepts (tf >= 0, and tn <= tf decided outside a 2^-20 relative
-// band); sure_out: it rejects.  Neither: box_exact decides (NaN lands here too).
+// band); sure_out: it rejects.  Neither: box_exact decides (NaN lands here too).  The sign of
+// each bound is exact (RN(b - o) * rcp(d) has the sign of the reference's quotient), and
+// d = RN(tn - tf) is within 2^-24 of tn - tf, so a decided case keeps a true margin above
+// 2^-21 relative.
 __device__ __forceinline__ void decide_sure(float tn, float tf, bool& sure_in, bool& sure_out) {
-  const float band = (__builtin_fabsf(tn) + __builtin_fabsf(tf)) * 0x1p-20f + 0x1p-120f;
-  sure_in = (tn < tf - band) & (tf >= 0.0f);
-  sure_out = (tf < 0.0f) | (tn > tf + band);
+  const float band = __builtin_fmaf(__builtin_fabsf(tn) + __builtin_fabsf(tf), 0x1p-20f, 0x1p-120f);
+  const float d = tn - tf;
+  sure_in = (d < -band) & (tf >= 0.0f);
+  sure_out = (tf < 0.0f) | (d > band);
 }
 
 __device__ __forceinline__ void decide_fast(float tn, float tf, bool& accept, bool& undecided) {
@@ -332,7 +336,8 @@ __device__ bool guard_exact(const RenderParams& P, int child, const LaneRay& r) 
 }
 
 // One packet visit of a node of either tree, per child:
-//   * leaf of a reference node: every lane in the node tests it (leaves have no box);
+//   * leaf of a reference node: every lane in the node tests it (leaves have no box; the slot
+//     holds a +-1e30 box that every normalised ray accepts, so no special case is needed);
 //   * inner child of a reference node: the reference's box test (fast, else box_exact);
 //   * guarded child of a culling node (treelet root or lone leaf): the reference's acceptance
 //     of its guard box, decided with margin — which implies every enclosing reference box
@@ -354,12 +359,12 @@ __device__ __forceinline__ void visit_node(const RenderParams& P, const DevNode&
   const int pad = N.pad;  // wave-uniform
   const bool an = (pad & kAccelNode) != 0;
   const bool g0 = (pad & kAccelGuard0) != 0, g1 = (pad & kAccelGuard1) != 0;
-  const bool rleaf0 = !an & (N.child[0] < 0), rleaf1 = !an & (N.child[1] < 0);
+  // (a reference node's leaf slot holds a +-1e30 box, scene_build.cpp: every lane accepts it)
   const bool cull0 = an & !g0, cull1 = an & !g1;
-  h0 = in & (rleaf0 | in0 | (cull0 & !out0));
-  h1 = in & (rleaf1 | in1 | (cull1 & !out1));
-  const bool u0 = in & !(rleaf0 | cull0) & !(in0 | out0);
-  const bool u1 = in & !(rleaf1 | cull1) & !(in1 | out1);
+  h0 = in & (in0 | (cull0 & !out0));
+  h1 = in & (in1 | (cull1 & !out1));
+  const bool u0 = in & !cull0 & !(in0 | out0);
+  const bool u1 = in & !cull1 & !(in1 | out1);
   if (ballot(u0 | u1)) {
     if (u0) h0 = g0 ? guard_exact(P, N.child[0], r) : child_box_exact(N, 0, r);
     if (u1) h1 = g1 ? guard_exact(P, N.child[1], r) : child_box_exact(N, 1, r);

@@ -432,6 +432,13 @@ void build_host_scene(const rt_scene_desc& d, HostScene& s) {
       } else {
         const int ref = emit_leaf(child);
         s.nodes[node].child[side] = ref;
+        // A leaf has no box in the reference (every ray in the node tests it).  Its slot gets
+        // a +-1e30 box that every ray with a normalised direction accepts by a wide margin in
+        // the kernels' slab test, so leaf and inner children share one decision path.
+        Aabb all;
+        all.lo = {-1e30f, -1e30f, -1e30f};
+        all.hi = {1e30f, 1e30f, 1e30f};
+        put_child_box(s.nodes[node], side, all);
       }
     }
   }
