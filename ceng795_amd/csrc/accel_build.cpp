@@ -1,4 +1,4 @@
-// Culling hierarchy over reference treelets (DESIGN.md §4.4).
+// Culling hierarchy over reference treelets (DESIGN.md §4.2).
 //
 // The reference BVH (midpoint split cycling x -> y -> z, HW2/Bounding_volume_hierarchy.cpp:
 // 3-29) decides WHICH leaves a ray may test: a leaf is reachable iff every ancestor box
@@ -16,7 +16,7 @@
 //   * inside the margin band the kernel walks the ancestor chain with the literal reference
 //     test (ref_parent / ref_box below).
 // SAH inner boxes are only culling bounds: they contain every guard box below them, and the
-// kernel tests them conservatively (2^-18 relative slack), so a treelet the reference would
+// kernel tests them conservatively (only a sure reject culls), so a treelet the reference would
 // enter is never culled.  The SAH tree's nodes are appended to HostScene::nodes after the
 // reference nodes; DevNode::pad marks them (kAccelNode | guard bits per child).
 #include <algorithm>
