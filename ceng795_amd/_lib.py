@@ -95,6 +95,7 @@ SIGNATURES = {
     "rt_last_error": (C.c_char_p, []),
     "rt_abi_version": (C.c_int, []),
     "rt_host_dump_bvh_xml": (C.c_int, [C.c_char_p, C.c_char_p]),
+    "rt_host_check_accel_xml": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_longlong)]),
     "rt_debug_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong)]),
 }
 

@@ -281,3 +281,120 @@ int accel_treelet_leaves() {
 }
 
 }  // namespace rt
+
+namespace rt {
+
+// Structural invariants of the culling tree the kernels' exactness argument relies on
+// (DESIGN.md §4.2).  Returns "" when they hold, else a description of the first violation.
+std::string check_accel(const HostScene& s, int K, long long stats[4]) {
+  for (int i = 0; i < 4; i++) stats[i] = 0;
+  if (s.accel_root < 0) return "";
+  const int nref = s.accel_root;  // culling nodes follow the reference's
+  const size_t nleaf = s.prims.size();
+  auto box_of = [&](int ref_node) { return s.ancestry[ref_node].box; };
+  // ancestry: each reference node's box is its parent's child slot; leaves point at holders
+  for (int n = 0; n < nref; n++) {
+    const DevNode& N = s.nodes[n];
+    if (N.pad != 0) return "reference node " + std::to_string(n) + " is flagged as culling";
+    for (int side = 0; side < 2; side++) {
+      const int c = N.child[side];
+      if (c >= 0) {
+        if (c >= nref || s.ancestry[c].parent != n) return "bad parent of node " + std::to_string(c);
+        for (int a = 0; a < 3; a++)
+          if (s.ancestry[c].box[a] != N.lo[a][side] || s.ancestry[c].box[a + 3] != N.hi[a][side])
+            return "ancestry box of node " + std::to_string(c) + " differs from its slot";
+      } else if ((size_t)~c >= nleaf || s.ancestry[~c].leaf_parent != n) {
+        return "bad holder of leaf " + std::to_string(~c);
+      }
+    }
+  }
+  for (int a = 0; a < 6; a++)
+    if (s.ancestry[0].box[a] != s.root_box[a]) return "root box differs from ancestry";
+  std::vector<int> seen(nleaf, 0);
+  long long lone = 0, items = 0;
+  struct Frame {
+    int node, depth;
+  };
+  std::vector<Frame> todo{{s.accel_root, 1}};
+  // leaves of a reference subtree, and the union of guard boxes under a culling node
+  auto ref_leaves = [&](int root, std::vector<int>& out) {
+    std::vector<int> st{root};
+    while (!st.empty()) {
+      const int n = st.back();
+      st.pop_back();
+      for (int side = 0; side < 2; side++) {
+        const int c = s.nodes[n].child[side];
+        if (c >= 0) st.push_back(c); else out.push_back(~c);
+      }
+    }
+  };
+  std::vector<float> lo(s.nodes.size() * 3), hi(s.nodes.size() * 3);
+  std::vector<int> order;  // culling nodes in preorder, for the bottom-up union pass
+  while (!todo.empty()) {
+    const Frame f = todo.back();
+    todo.pop_back();
+    const DevNode& N = s.nodes[f.node];
+    if (f.node < nref || !(N.pad & kAccelNode)) return "culling child is not a culling node";
+    order.push_back(f.node);
+    stats[2] = std::max<long long>(stats[2], f.depth);
+    for (int side = 0; side < 2; side++) {
+      const int c = N.child[side];
+      const bool guard = (N.pad & (side ? kAccelGuard1 : kAccelGuard0)) != 0;
+      if (!guard) {
+        if (c < nref) return "unguarded child is not a culling node";
+        todo.push_back({c, f.depth + 1});
+        continue;
+      }
+      items++;
+      const float* g = c >= 0 ? box_of(c) : box_of(s.ancestry[~c].leaf_parent);
+      for (int a = 0; a < 3; a++)
+        if (N.lo[a][side] != g[a] || N.hi[a][side] != g[a + 3])
+          return "guard box differs from the reference box it stands for";
+      std::vector<int> lv;
+      if (c >= 0) {
+        if (c >= nref) return "guarded child is not a reference node";
+        ref_leaves(c, lv);
+        if ((int)lv.size() > K) return "treelet larger than K";
+      } else {
+        lv.push_back(~c);
+        lone++;
+      }
+      for (int l : lv)
+        if (seen[l]++) return "leaf " + std::to_string(l) + " in two treelets";
+    }
+  }
+  for (size_t l = 0; l < nleaf; l++)
+    if (!seen[l]) return "leaf " + std::to_string(l) + " in no treelet";
+  // containment: every culling slot box contains every guard box below it
+  for (auto it = order.rbegin(); it != order.rend(); ++it) {
+    const DevNode& N = s.nodes[*it];
+    float ulo[3] = {INFINITY, INFINITY, INFINITY}, uhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int side = 0; side < 2; side++) {
+      const int c = N.child[side];
+      const bool guard = (N.pad & (side ? kAccelGuard1 : kAccelGuard0)) != 0;
+      const float* clo = guard ? nullptr : &lo[(size_t)c * 3];
+      const float* chi = guard ? nullptr : &hi[(size_t)c * 3];
+      for (int a = 0; a < 3; a++) {
+        const float l = guard ? N.lo[a][side] : clo[a], h = guard ? N.hi[a][side] : chi[a];
+        if (!guard && (N.lo[a][side] > l || N.hi[a][side] < h))
+          return "culling box does not contain the guard boxes below it";
+        ulo[a] = std::min(ulo[a], l);
+        uhi[a] = std::max(uhi[a], h);
+      }
+    }
+    for (int a = 0; a < 3; a++) {
+      lo[(size_t)*it * 3 + a] = ulo[a];
+      hi[(size_t)*it * 3 + a] = uhi[a];
+    }
+  }
+  for (int a = 0; a < 3; a++)
+    if (s.accel_box[a] > lo[(size_t)s.accel_root * 3 + a] ||
+        s.accel_box[a + 3] < hi[(size_t)s.accel_root * 3 + a])
+      return "culling root box does not contain the tree";
+  stats[0] = items;
+  stats[1] = (long long)order.size();
+  stats[3] = lone;
+  return "";
+}
+
+}  // namespace rt

@@ -49,6 +49,9 @@ struct HostScene {
 // (K <= 0: none).  Leaves the reference nodes, leaves and tie-break order untouched.
 void build_accel(HostScene& s, int K);
 int accel_treelet_leaves();  // CENG795_RT_TREELET, else kDefaultTreeletLeaves
+// Invariants of the culling tree (coverage, guard boxes, containment, ancestry); "" if they
+// hold.  stats: treelets, culling nodes, culling depth, lone-leaf treelets.
+std::string check_accel(const HostScene& s, int K, long long stats[4]);
 
 // Builds `out` from `desc`; throws std::invalid_argument on a bad description.
 void build_host_scene(const rt_scene_desc& desc, HostScene& out);

@@ -402,6 +402,21 @@ int rt_host_dump_bvh_xml(const char* xml_path, const char* out_path) {
   });
 }
 
+int rt_host_check_accel_xml(const char* xml_path, int treelet_leaves, long long* stats4) {
+  if (!xml_path || !stats4) return set_error(RT_E_INVALID, "rt_host_check_accel_xml: NULL argument");
+  return guarded([&] {
+    XmlSceneStorage st;
+    rt_scene_desc d;
+    load_scene_xml(xml_path, st, d);
+    HostScene h;
+    build_host_scene(d, h);
+    build_accel(h, treelet_leaves);
+    const std::string err = check_accel(h, treelet_leaves, stats4);
+    if (!err.empty()) throw std::invalid_argument("culling tree: " + err);
+    return RT_OK;
+  });
+}
+
 int rt_set_traversal(rt_scene* s, int mode) {
   if (!s || (mode != RT_TRAVERSAL_FAST && mode != RT_TRAVERSAL_REFERENCE))
     return set_error(RT_E_INVALID, "rt_set_traversal: bad argument");

@@ -132,6 +132,13 @@ int rt_scene_dump_bvh(const rt_scene* scene, const char* path);
 /* Host-only variant for tests without a GPU: XML ingest + BVH build + flatten, then the
  * same dump.  Touches no HIP API. */
 int rt_host_dump_bvh_xml(const char* xml_path, const char* out_path);
+/* Host-only, for tests: XML ingest + BVH build + the culling tree over reference treelets of
+ * <= treelet_leaves leaves, then a check of the invariants the kernels'
+ * exactness rests on (every leaf in exactly one treelet, guard boxes = the reference boxes
+ * they stand for, culling boxes contain every guard box below them, ancestry links).
+ * stats4: treelets, culling nodes, culling-tree depth, lone-leaf treelets (zeros when the
+ * tree is a single treelet).  RT_E_INVALID with the violation in rt_last_error(). */
+int rt_host_check_accel_xml(const char* xml_path, int treelet_leaves, long long* stats4);
 /* Height of the flattened BVH (levels of internal nodes). */
 int rt_scene_bvh_depth(const rt_scene* scene);
 

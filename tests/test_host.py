@@ -205,3 +205,30 @@ def test_binary_mesh_lists_load_to_the_same_scene(scene_dir, tmp_path, name, zer
     host_dump_bvh(xml, str(a))
     host_dump_bvh(binxml, str(b))
     assert a.read_bytes() == b.read_bytes()
+
+
+@pytest.mark.parametrize("name", ["c1", "hf_small", "hf_side", "soup1", "single_sphere", "c2"])
+@pytest.mark.parametrize("k", [1, 2, 4, 8])
+def test_culling_tree_invariants(scene_dir, name, k):
+    """The culling tree over reference treelets keeps the invariants the
+    kernels' exactness rests on: every leaf in exactly one treelet of <= K leaves, each guard
+    box bit-equal to the reference box it stands for, every culling box containing the guard
+    boxes below it, ancestry links matching the reference tree."""
+    xml = scenes.write(name, scene_dir)
+    st = (C.c_longlong * 4)()
+    rc = _lib.lib().rt_host_check_accel_xml(xml.encode(), k, st)
+    assert rc == 0, _lib.lib().rt_last_error().decode()
+    treelets, culling_nodes, depth, lone = list(st)
+    if treelets:  # a scene whose whole tree is one treelet gets no culling tree
+        assert culling_nodes == treelets - 1
+        assert 1 <= depth <= treelets
+        assert 0 <= lone <= treelets
+
+
+def test_culling_tree_on_c3(scene_dir):
+    xml = scenes.write_c3(scene_dir)
+    st = (C.c_longlong * 4)()
+    rc = _lib.lib().rt_host_check_accel_xml(xml.encode(), 2, st)
+    assert rc == 0, _lib.lib().rt_last_error().decode()
+    treelets, culling_nodes, depth, lone = list(st)
+    assert treelets > 300000 and culling_nodes == treelets - 1 and depth < 64
