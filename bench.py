@@ -126,6 +126,9 @@ def main() -> int:
                     help="gloo: rehearsal of the N>1 path on one GPU (ranks share device 0)")
     ap.add_argument("--no-verify", action="store_true",
                     help="skip rank 0's bit-for-bit check of the gathered frames")
+    ap.add_argument("--gather-rehearsal", action="store_true",
+                    help="run the N>1 tile/gather pipeline even at WORLD_SIZE=1 (a one-rank "
+                         "process group; exercises the comm-stream gather on one GPU)")
     args = ap.parse_args()
     if args.workload == "c5":
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
@@ -145,8 +148,12 @@ def main() -> int:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
-    if world > 1:
+    use_pg = world > 1 or args.gather_rehearsal
+    if use_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29577")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
@@ -165,9 +172,9 @@ def main() -> int:
     scene = ceng795_amd.Scene(xml, device=device, traversal=args.traversal)
     log(f"[rank {rank}] scene loaded + uploaded in {time.perf_counter() - t0:.2f} s, "
         f"BVH depth {scene.bvh_depth}")
-    plan = dist_tiles.TilePlan(scene, world, rank)
+    plan = dist_tiles.TilePlan(scene, world, rank, force=use_pg)
     stream = torch.cuda.current_stream()
-    renderer = dist_tiles.FrameRenderer(scene, plan, stream, gather=world > 1,
+    renderer = dist_tiles.FrameRenderer(scene, plan, stream, gather=use_pg,
                                         host_staging=args.dist_backend == "gloo")
 
     # warmup (also yields the per-step ray count from the device counters)
@@ -203,7 +210,7 @@ def main() -> int:
     scene.collect_stats()  # reset counters
 
     verified = None
-    if world > 1 and rank == 0 and not args.no_verify:
+    if use_pg and rank == 0 and not args.no_verify:
         # the gathered framebuffers must equal single-GPU renders of the same cameras, bit for bit
         verified = True
         for c, f in enumerate(renderer.frames):
@@ -250,12 +257,12 @@ def main() -> int:
             "config": {"workload": desc, "frame": f"{w}x{h}", "frames_per_step": n_cams,
                        "triangles": 2 * (n - 1) ** 2, "rays_per_step": int(rays_step),
                        "traversal": args.traversal,
-                       "parallelism": f"tiles{world}" + (f"+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}_gather" if world > 1 else ""),
+                       "parallelism": f"tiles{world}" + (f"+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}_gather" if use_pg else ""),
                        "gather_verified": verified},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_pg:
         dist.barrier()
         dist.destroy_process_group()
     scene.close()

@@ -43,6 +43,7 @@ struct HostScene {
   int accel_items = 0;   // treelets
   float accel_box[6] = {0, 0, 0, 0, 0, 0};
   std::vector<DevAncestry> ancestry;  // max(nodes, leaves) entries, see DevAncestry
+  int quot_ok = 0;  // every triangle v0 coordinate passes quot_coord_ok (rt_internal.h)
 };
 
 // Cuts the reference tree into treelets of <= K leaves and appends a SAH tree over them

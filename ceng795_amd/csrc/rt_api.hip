@@ -23,6 +23,8 @@ hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevP
 int max_supported_depth();
 hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream);
 unsigned long long read_reset_exact_fallbacks();
+hipError_t launch_quot_check(unsigned long long seed, long long count, unsigned long long* counts,
+                             hipStream_t stream);
 bool diag_build();
 void write_png(const std::string& path, const float* rgb, int w, int h);
 }  // namespace rt
@@ -95,7 +97,8 @@ int guarded(F&& f) {
 template <typename T>
 T* upload(const std::vector<T>& v, const char* what) {
   T* p = nullptr;
-  const size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+  // +64 B: the kernels may fetch a record with one 64-byte scalar load past its 48 bytes
+  const size_t bytes = v.size() * sizeof(T) + 64;
   hip_check(hipMalloc(&p, bytes), what);
   if (!v.empty()) hip_check(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice), what);
   return p;
@@ -138,6 +141,13 @@ size_t frame_floats(const HostScene& h, int sel_tiles) {
 
 int occ_words(const HostScene& h) { return std::max(1, ((int)h.lights.size() + 31) / 32); }
 
+// A counter buffer: kCounterRows x kCounterWidth ray counters, then 8 u64 = 16 int packet
+// counters of the persistent traversal kernels (zeroed by every launch).
+constexpr size_t kCounterAlloc = (size_t)kCounterWidth * kCounterRows + 8;
+int* work_counters(unsigned long long* counters) {
+  return reinterpret_cast<int*>(counters + (size_t)kCounterWidth * kCounterRows);
+}
+
 int create_from_host(rt_scene* s, int device) {
   if (device < 0) hip_check(hipGetDevice(&device), "hipGetDevice");
   s->device = device;
@@ -165,7 +175,8 @@ int create_from_host(rt_scene* s, int device) {
   s->d_anc = upload(h.ancestry, "upload ancestry");
   s->d_mats = upload(h.materials, "upload materials");
   s->d_lights = upload(h.lights, "upload lights");
-  hip_check(hipMalloc(&s->d_counters, sizeof(unsigned long long) * kCounterWidth * kCounterRows),
+  // ray counters + the persistent traversal kernels' 16 packet counters (RenderParams::work)
+  hip_check(hipMalloc(&s->d_counters, sizeof(unsigned long long) * kCounterAlloc),
             "alloc counters");
   hip_check(hipMemset(s->d_counters, 0, sizeof(unsigned long long) * kCounterWidth * kCounterRows),
             "zero counters");
@@ -212,6 +223,7 @@ RenderParams make_params(const rt_scene* s, int cam, int row0, int row_stride, i
   P.root_ref = h.root_ref;
   std::memcpy(P.root_box, h.root_box, sizeof P.root_box);
   P.accel_root = h.accel_root;
+  P.quot_ok = h.quot_ok;
   std::memcpy(P.accel_box, h.accel_box, sizeof P.accel_box);
   P.anc = s->d_anc;
   std::memcpy(P.cam_e, c.e, 12);
@@ -236,6 +248,7 @@ RenderParams make_params(const rt_scene* s, int cam, int row0, int row_stride, i
   P.occ = s->d_occ;
   P.occ_words = occ_words(h);
   P.counters = counters ? s->d_counters : nullptr;
+  P.work = work_counters(s->d_counters);  // shared by the scene's rt_render_device calls
   return P;
 }
 
@@ -511,6 +524,25 @@ int rt_debug_counters(rt_scene* s, long long* out16) {
   });
 }
 
+int rt_debug_quotient_check(int device, unsigned long long seed, long long count,
+                            long long* out2) {
+  if (!out2 || count < 0) return set_error(RT_E_INVALID, "rt_debug_quotient_check: bad argument");
+  return guarded([&] {
+    DeviceGuard g(device);
+    unsigned long long* d = nullptr;
+    hip_check(hipMalloc(&d, 2 * sizeof *d), "alloc");
+    std::unique_ptr<unsigned long long, void (*)(unsigned long long*)> hold(
+        d, [](unsigned long long* p) { (void)hipFree(p); });
+    hip_check(hipMemset(d, 0, 2 * sizeof *d), "clear");
+    hip_check(launch_quot_check(seed, count, d, nullptr), "quotient check launch");
+    unsigned long long h[2];
+    hip_check(hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost), "read");
+    out2[0] = (long long)h[0];
+    out2[1] = (long long)h[1];
+    return RT_OK;
+  });
+}
+
 int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt_stats* stats) {
   return guarded([&] {
       check_render_args(s, cam, row0, row_stride);
@@ -544,11 +576,12 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
         hip_check(hipEventCreate(&e1), "event");
         // Counters are per scene; this call reports its own deltas via a private buffer.
         unsigned long long* d_cnt = nullptr;
-        hip_check(hipMalloc(&d_cnt, sizeof(unsigned long long) * kCounterWidth * kCounterRows), "alloc counters");
+        hip_check(hipMalloc(&d_cnt, sizeof(unsigned long long) * kCounterAlloc), "alloc counters");
         hip_check(hipMemsetAsync(d_cnt, 0, sizeof(unsigned long long) * kCounterWidth * kCounterRows, stream),
                   "zero counters");
         RenderParams P = make_params(s, cam, row0, row_stride, 0, 1, 0, d_out, true);
         P.counters = d_cnt;
+        P.work = work_counters(d_cnt);
         hip_check(hipMalloc(&d_hits, sizeof(int2_t) * kTile * kTile * (size_t)std::max(1, P.num_sel_tiles)),
                   "alloc hit records");
         P.hits = d_hits;

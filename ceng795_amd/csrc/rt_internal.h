@@ -61,6 +61,14 @@ struct alignas(16) DevPrim {
 };
 static_assert(sizeof(DevPrim) == 48, "prim record is three 16-byte loads");
 
+// Range in which the triangle test's three divisions (v0 - o) / det may share one reciprocal
+// (tri_quotients in rt_kernels.hip): a coordinate is 0 or 2^-26 <= |x| <= 2^48, so every
+// difference v0 - o is 0 or 2^-49 <= |v0 - o| <= 2^49.
+inline bool quot_coord_ok(float x) {
+  const float a = x < 0 ? -x : x;
+  return a == 0.0f || (a >= 0x1p-26f && a <= 0x1p48f);
+}
+
 // Reference ancestry for the culling tree's exact guard (accel_build.cpp): entry i holds
 // reference node i's own box and parent (-1 at the root), and the node holding leaf i.
 struct alignas(16) DevAncestry {
@@ -118,6 +126,9 @@ struct RenderParams {
   // reference ancestry a guard walks when its fast test cannot decide
   int accel_root;
   float accel_box[6];
+  // every triangle's v0 coordinate is 0 or in [2^-26, 2^48] (quot_coord_ok): the triangle
+  // test may take the shared-reciprocal quotient path (rt_kernels.hip, tri_quotients)
+  int quot_ok;
   const struct DevAncestry* anc;
   // camera (rt_camera)
   float cam_e[3], cam_tl[3], cam_su[3], cam_sv[3];
@@ -127,6 +138,8 @@ struct RenderParams {
   // tiles over (rows x width), row-major; this launch does tile_begin + i*tile_step
   int tiles_x, tiles_total, tile_begin, tile_step, num_sel_tiles;
   int tile_major;
+  int tile_block;  // traversal kernels: workgroups take 2-D blocks of tiles (rt_kernels.hip)
+  int* work;       // 16 packet counters for persistent traversal waves (null: one packet/wave)
   // jittered MSAA (HW2/Scene.cpp:32-69): 0 = pixel centres; else this launch traces sample
   // msaa_s = x*n + y of every pixel, whose minstd_rand0 draws 2s+1, 2s+2 are
   // u0 * msaa_mul[0], u0 * msaa_mul[1] (mod 2^31-1), u0 the pixel's seeded state.

@@ -64,9 +64,15 @@ struct LaneRay {
   V3 o, d;
   V3 r;       // v_rcp_f32 reciprocals (<= 1 ulp): the approximate slab test only
   bool skip0, skip1, skip2;  // |d_i| < 1e-6: axis ignored (HW2/bounding_box.cpp:21)
+  bool quot;  // origin and scene in the shared-reciprocal range (tri_quotients)
 };
 
-__device__ __forceinline__ LaneRay make_ray(V3 o, V3 d) {
+__device__ __forceinline__ bool quot_coord(float x) {  // quot_coord_ok of rt_internal.h
+  const float a = __builtin_fabsf(x);
+  return a == 0.0f || (a >= 0x1p-26f && a <= 0x1p48f);
+}
+
+__device__ __forceinline__ LaneRay make_ray(V3 o, V3 d, int scene_quot_ok) {
   LaneRay r;
   r.o = o;
   r.d = d;
@@ -74,6 +80,7 @@ __device__ __forceinline__ LaneRay make_ray(V3 o, V3 d) {
   r.skip0 = __builtin_fabsf(d.x) < kEps;
   r.skip1 = __builtin_fabsf(d.y) < kEps;
   r.skip2 = __builtin_fabsf(d.z) < kEps;
+  r.quot = scene_quot_ok && quot_coord(o.x) && quot_coord(o.y) && quot_coord(o.z);
   return r;
 }
 
@@ -187,14 +194,59 @@ __device__ __forceinline__ float det3_cx(V3 c1, V3 c2, V3 c3, float cx) {
   return c1.x * (c2.y * c3.z - c3.y * c2.z) + c2.x * (c3.y * c1.z - c1.y * c3.z) + c3.x * cx;
 }
 
+// Correctly rounded n / det for the three numerators with ONE reciprocal.  gfx950's IEEE
+// division is v_div_scale (num, den), y = v_rcp, e = fma(-den, y, 1), y1 = fma(e, y, y),
+// q = num * y1, r = fma(-den, q, num), q1 = fma(r, y1, q), r1 = fma(-den, q1, num),
+// v_div_fmas(r1, y1, q1), v_div_fixup(q2, den, num).  When no operand is near the exponent
+// limits, v_div_scale returns its operand unchanged with VCC = 0 and v_div_fmas is a plain
+// fma, so the sequence below (which keeps v_div_fixup: it gives a zero numerator the sign
+// num ^ den) yields the bits of `/`; only the reciprocal refinement y1 depends on det alone,
+// and it is shared.  Range: 2^-40 <= |det|
+// <= 2^40 is checked here; numerators are 0 or 2^-49 <= |n| <= 2^49 by r.quot (every v0 and
+// origin coordinate is 0 or in [2^-26, 2^48]).  Then |n / det| lies in [2^-89, 2^89],
+// exponent differences stay below 96 and nothing is subnormal, so none of v_div_scale's
+// scaling cases can arise.  Any other lane takes `/`.
+__device__ __forceinline__ float quot_step(float n, float det, float y1) {
+  const float q = n * y1;
+  const float r = __builtin_fmaf(-det, q, n);
+  const float q1 = __builtin_fmaf(r, y1, q);
+  const float r1 = __builtin_fmaf(-det, q1, n);
+  return __builtin_amdgcn_div_fixupf(__builtin_fmaf(r1, y1, q1), det, n);
+}
+
+__device__ __forceinline__ V3 tri_quotients(V3 n, float det, bool quot) {
+#ifndef RT_EXP_IEEEDIV
+  const float ad = __builtin_fabsf(det);
+  if (quot && ad >= 0x1p-40f && ad <= 0x1p40f) {
+    const float y = __builtin_amdgcn_rcpf(det);
+    const float e = __builtin_fmaf(-det, y, 1.0f);
+    const float y1 = __builtin_fmaf(e, y, y);
+    return v3(quot_step(n.x, det, y1), quot_step(n.y, det, y1), quot_step(n.z, det, y1));
+  }
+#endif
+  return n / det;
+}
+
 __device__ __forceinline__ bool tri_test(V3 v0, V3 a1, V3 a2, float cx, const LaneRay& r,
                                          float& t) {
 #ifndef RT_EXP_CX
 #define det3_cx(c1, c2, c3, cx) det3(c1, c2, c3)
 #endif
   const float det = det3_cx(a1, a2, r.d, cx);
+#ifndef RT_EXP_BRANCHY  // (RT_EXP_BRANCHY: the early-exit form, for A/B)
+  // Branch-free: every value is computed and the reference's early exits (Triangle.cpp:46-62)
+  // become one predicate with the same comparisons (a NaN fails them as there).  No
+  // exec-mask save/restore per exit; with det == 0 the quotients are inf/NaN and unused.
+  const V3 b = tri_quotients(v0 - r.o, det, r.quot);
+  const float beta = det3(b, a2, r.d);
+  const float gamma = det3(a1, b, r.d);
+  const float tt = det3_cx(a1, a2, b, cx);
+  t = tt;
+  return (det != 0.0f) & !((beta < 0.0f) | (beta > 1.0f)) &
+         !((gamma < 0.0f) | (beta + gamma > 1.0f)) & (tt > 0.0f);
+#else
   if (det == 0.0f) return false;
-  const V3 b = (v0 - r.o) / det;
+  const V3 b = tri_quotients(v0 - r.o, det, r.quot);
   const float beta = det3(b, a2, r.d);
   if (beta < 0.0f || beta > 1.0f) return false;
   const float gamma = det3(a1, b, r.d);
@@ -205,6 +257,7 @@ __device__ __forceinline__ bool tri_test(V3 v0, V3 a1, V3 a2, float cx, const La
     return true;
   }
   return false;
+#endif
 }
 
 // HW2/Sphere.h:26-52 — true for any real root, including a negative one.
@@ -228,10 +281,36 @@ __device__ __forceinline__ bool sphere_test(V3 c, float radius, const LaneRay& r
 
 // Shape::intersect of one leaf.  SPHERES == false: the scene has no spheres (host flag), so
 // the sphere code is not compiled into the traversal loop.
+// RT_EXP_X16: fetch a node / prim record with ONE s_load_dwordx16 (waited at once) instead of
+// the 4 loads of 1-8 dwords the compiler splits it into.
+typedef int v16i __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ v16i sload16(const void* p) {
+  v16i r;
+  asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
+  return r;
+}
+
 template <bool SPHERES>
 __device__ __forceinline__ bool leaf_test(const DevPrim* __restrict__ prims, int leaf,
                                           const LaneRay& r, float& t) {
+#ifdef RT_EXP_X16
+  const v16i w = sload16(prims + leaf);
+  DevPrim p;
+  p.v0[0] = __int_as_float(w[0]);
+  p.v0[1] = __int_as_float(w[1]);
+  p.v0[2] = __int_as_float(w[2]);
+  p.a1[0] = __int_as_float(w[3]);
+  p.a1[1] = __int_as_float(w[4]);
+  p.a1[2] = __int_as_float(w[5]);
+  p.a2[0] = __int_as_float(w[6]);
+  p.a2[1] = __int_as_float(w[7]);
+  p.a2[2] = __int_as_float(w[8]);
+  p.kind = w[9];
+  p.material = w[10];
+  p.cx = __int_as_float(w[11]);
+#else
   const DevPrim& p = prims[leaf];
+#endif
   const V3 v0 = ld3(p.v0);
   if (!SPHERES || p.kind == kPrimTriangle) return tri_test(v0, ld3(p.a1), ld3(p.a2), p.cx, r, t);
   return sphere_test(v0, p.a1[0], r, t);
@@ -314,10 +393,50 @@ __device__ __forceinline__ DevNode load_node(const DevNode* __restrict__ nodes, 
   N.axis = 0;
   N.pad = 0;
   return N;
+#elif defined(RT_EXP_X16)
+#ifdef RT_EXP_DUP  // scalar-cache pressure probe: a second, redundant fetch of the same node
+  (void)sload16(nodes + node);
+#endif
+  const v16i w = sload16(nodes + node);
+  DevNode N;
+  for (int a = 0; a < 3; a++)
+    for (int c = 0; c < 2; c++) {
+      N.lo[a][c] = __int_as_float(w[2 * a + c]);
+      N.hi[a][c] = __int_as_float(w[6 + 2 * a + c]);
+    }
+  N.child[0] = w[12];
+  N.child[1] = w[13];
+  N.axis = w[14];
+  N.pad = w[15];
+  return N;
 #else
   return nodes[node];
 #endif
 }
+
+// RT_EXP_PREFETCH: at the start of a visit, touch the children's records (node, or the leaf's
+// 48-B prim, which may straddle two 64-B lines) so they are in the scalar cache when the next
+// visit / the leaf test loads them.  The destination registers are retired after an explicit
+// s_waitcnt at the end of the same visit, so no load is in flight when they are reused.
+struct ChildPrefetch {
+  int a = 0, b = 0, c = 0, d = 0;
+  __device__ __forceinline__ void issue(const DevNode* __restrict__ nodes,
+                                        const DevPrim* __restrict__ prims, int c0, int c1) {
+#ifdef RT_EXP_PREFETCH
+    const char* p0 = c0 >= 0 ? (const char*)(nodes + c0) : (const char*)(prims + ~c0);
+    const char* p1 = c1 >= 0 ? (const char*)(nodes + c1) : (const char*)(prims + ~c1);
+    asm volatile("s_load_dword %0, %1, 0x0" : "=s"(a) : "s"(p0));
+    asm volatile("s_load_dword %0, %1, 0x2c" : "=s"(b) : "s"(p0));
+    asm volatile("s_load_dword %0, %1, 0x0" : "=s"(c) : "s"(p1));
+    asm volatile("s_load_dword %0, %1, 0x2c" : "=s"(d) : "s"(p1));
+#endif
+  }
+  __device__ __forceinline__ void retire() {
+#ifdef RT_EXP_PREFETCH
+    asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(a), "s"(b), "s"(c), "s"(d) : "memory");
+#endif
+  }
+};
 
 __device__ __forceinline__ bool child_box_exact(const DevNode& N, int c, const LaneRay& r) {
   const float b[6] = {N.lo[0][c], N.lo[1][c], N.lo[2][c], N.hi[0][c], N.hi[1][c], N.hi[2][c]};
@@ -486,6 +605,8 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
   int node = accel ? P.accel_root : P.root_ref;
   for (;;) {
     const DevNode N = load_node(nodes, node);
+    ChildPrefetch pf;
+    pf.issue(nodes, prims, N.child[0], N.child[1]);
     bool h0[R], h1[R];
     float t0[R], t1[R];
 #pragma unroll
@@ -503,12 +624,22 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
 #pragma unroll
         for (int k = 0; k < R; k++) {
           const bool tests = side ? h1[k] : h0[k];
-          float t;
+          float t = 0.0f;
+#ifndef RT_EXP_BRANCHY  // (RT_EXP_BRANCHY: the early-exit form, for A/B)
+          if (ballot(tests)) {  // one wave-uniform branch; the update itself is a select
+            const bool hit = leaf_test<SPHERES>(prims, ~c, r[k], t);
+            const bool take = tests & hit & (t > 0.0f) & (t < RT_INF) &
+                              ((t < best_t[k]) | ((t == best_t[k]) & (~c < best_leaf[k])));
+            best_t[k] = take ? t : best_t[k];
+            best_leaf[k] = take ? ~c : best_leaf[k];
+          }
+#else
           if (tests && leaf_test<SPHERES>(prims, ~c, r[k], t) && t > 0.0f && t < RT_INF &&
               (t < best_t[k] || (t == best_t[k] && ~c < best_leaf[k]))) {
             best_t[k] = t;
             best_leaf[k] = ~c;
           }
+#endif
         }
       }
     }
@@ -529,6 +660,7 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
       m0[k] = ballot(h0[k]);
       m1[k] = ballot(h1[k]);
     }
+    pf.retire();
     if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, everyone)) break;
   }
 }
@@ -576,6 +708,8 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
   int node = accel ? P.accel_root : P.root_ref;
   for (;;) {
     const DevNode N = load_node(nodes, node);
+    ChildPrefetch pf;
+    pf.issue(nodes, prims, N.child[0], N.child[1]);
     bool h0[R], h1[R];
     float t0[R], t1[R];
 #pragma unroll
@@ -592,10 +726,18 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
 #pragma unroll
         for (int k = 0; k < R; k++) {
           const bool tests = side ? h1[k] : h0[k];
-          float t;
+          float t = 0.0f;
+#ifndef RT_EXP_BRANCHY  // (RT_EXP_BRANCHY: the early-exit form, for A/B)
+          const bool want = tests & !occ[k];
+          if (ballot(want)) {
+            const bool hit = leaf_test<SPHERES>(prims, ~c, r[k], t);
+            occ[k] = occ[k] | (want & hit & (t > 0.0f) & (t < thr[k]));
+          }
+#else
           if (tests && !occ[k] && leaf_test<SPHERES>(prims, ~c, r[k], t) && t > 0.0f &&
               t < thr[k])
             occ[k] = true;
+#endif
         }
       }
     }
@@ -613,6 +755,7 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
       m0[k] = ballot(h0[k]) & alive[k];
       m1[k] = ballot(h1[k]) & alive[k];
     }
+    pf.retire();
     if (!any_of(alive)) break;
     if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, alive)) break;
   }
@@ -714,7 +857,7 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
   for (int k = 0; k < R; k++) {
     q[k] = packet_pixel(P, sel0 + k);
     valid[k] = q[k].valid && sel0 + k < P.num_sel_tiles;
-    ray[k] = make_ray(ld3(P.cam_e), primary_dir(P, q[k].px, q[k].py));
+    ray[k] = make_ray(ld3(P.cam_e), primary_dir(P, q[k].px, q[k].py), P.quot_ok);
     any_skip |= valid[k] && (ray[k].skip0 || ray[k].skip1 || ray[k].skip2);
   }
   Diag dg;
@@ -797,7 +940,7 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P,
         const V3 ld = ld3(L.position) - p[k];
         const V3 wi = normalize(ld);
         const float dist = length(ld);
-        sr[k] = make_ray(p[k] + wi * P.eps, wi);  // p + eps * w_i
+        sr[k] = make_ray(p[k] + wi * P.eps, wi, P.quot_ok);  // p + eps * w_i
         thr[k] = dist - P.eps;
         any_skip |= hit[k] && (sr[k].skip0 || sr[k].skip1 || sr[k].skip2);
       }
@@ -938,7 +1081,7 @@ __device__ __forceinline__ V3 local_color(const RenderParams& P, const DevNode* 
     const V3 ld = ld3(L.position) - p;
     const V3 wi = normalize(ld);
     const float dist = length(ld);
-    const LaneRay sr[1] = {make_ray(p + wi * P.eps, wi)};
+    const LaneRay sr[1] = {make_ray(p + wi * P.eps, wi, P.quot_ok)};
     const float thr[1] = {dist - P.eps};
     const bool act[1] = {shade};
     const bool sskip = ballot(shade && (sr[0].skip0 || sr[0].skip1 || sr[0].skip2)) != 0;
@@ -986,7 +1129,7 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
   unsigned long long n_shadow = 0, n_secondary = 0;
   bool first = true;
   while (ballot(active)) {
-    const LaneRay rays[1] = {make_ray(ro, rd)};
+    const LaneRay rays[1] = {make_ray(ro, rd, P.quot_ok)};
     const LaneRay& ray = rays[0];
     const bool act[1] = {active};
     const bool skip = ballot(active && (ray.skip0 || ray.skip1 || ray.skip2)) != 0;
@@ -1163,33 +1306,121 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
 #endif
 
 // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so hand each
-// XCD a contiguous run of tiles — neighbouring packets share BVH nodes through its L2.
+// XCD a contiguous run of blocks — neighbouring packets share BVH nodes through its L2.
+template <int W>
 __device__ __forceinline__ int packet_index() {
   const int nb = (int)gridDim.x, b = (int)blockIdx.x;
   const int q = nb / 8, rem = nb % 8, x = b % 8;
   const int logical = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + b / 8;
-  return uniform(logical * kWavesPerBlock + ((int)threadIdx.x >> 6));
+  return uniform(logical * W + ((int)threadIdx.x >> 6));
+}
+
+// Traversal workgroups: kTraceWaves packets, which the hardware keeps on ONE CU, so they share
+// its scalar cache.  With P.tile_block the workgroup's packets form a kBlockW x kBlockH block
+// of tiles (blocks row-major over the frame) instead of a run along a tile row: neighbouring
+// rays walk the same nodes, and the cache serves them once.  Deep trees keep 4-wave groups
+// (their LDS stack is 12 KB per wave).
+#ifndef RT_TRACE_WAVES
+#define RT_TRACE_WAVES 4
+#endif
+#ifndef RT_TRACE_BLOCK_W
+#define RT_TRACE_BLOCK_W 2
+#endif
+constexpr int kTraceWaves = RT_TRACE_WAVES;
+template <bool DEEP>
+constexpr int trace_waves() { return DEEP ? 4 : kTraceWaves; }
+
+template <int W>
+__host__ __device__ constexpr int block_w() { return W >= RT_TRACE_BLOCK_W ? RT_TRACE_BLOCK_W : W; }
+
+// Tile (= sel, tile_step 1) of logical packet p; -1 for a padding packet of an edge block.
+template <int W>
+__device__ __forceinline__ int packet_sel(const RenderParams& P, int p) {
+  if (!P.tile_block) return p;
+  constexpr int BW = block_w<W>(), BH = W / BW;
+  const int w = p % W, b = p / W;
+  const int nbx = (P.tiles_x + BW - 1) / BW;
+  const int tx = (b % nbx) * BW + w % BW, ty = (b / nbx) * BH + w / BW;
+  const int tiles_y = P.tiles_total / P.tiles_x;
+  return (tx < P.tiles_x && ty < tiles_y) ? ty * P.tiles_x + tx : -1;
+}
+
+// Workgroups of W waves the current device keeps resident at 8 waves per SIMD.
+[[maybe_unused]] static int resident_blocks(int W) {
+  static int cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev] * 32 / W;
+}
+
+// Logical packets of a traversal launch (R tiles each; with tile_block, padded to whole blocks).
+template <int W, int R>
+__host__ __device__ __forceinline__ int trace_packets(const RenderParams& P) {
+  if (!P.tile_block) return (P.num_sel_tiles + R - 1) / R;
+  constexpr int BW = block_w<W>(), BH = W / BW;
+  const int tiles_y = P.tiles_total / P.tiles_x;
+  return ((P.tiles_x + BW - 1) / BW) * ((tiles_y + BH - 1) / BH) * W;
+}
+
+// Persistent traversal waves (RenderParams::work != null): the grid holds only as many
+// workgroups as the GPU keeps resident, and every wave takes packets one at a time from a
+// counter — first from its XCD group's contiguous range (blockIdx % 8: the blocks that share
+// an XCD and its L2), then from the other groups' ranges.  Slots no longer drain workgroup by
+// workgroup as packets of unequal cost finish, and the tail of the frame is one packet long.
+// Without a work buffer: one packet per wave, XCD-remapped (packet_index).
+template <int W, int R, class F>
+__device__ __forceinline__ void for_each_packet(const RenderParams& P, F&& f) {
+  const int total = trace_packets<W, R>(P);
+  if (!P.work) {
+    const int p = packet_index<W>();
+    if (p < total) f(p);
+    return;
+  }
+  const int g0 = (int)(blockIdx.x & 7);
+  for (int k = 0; k < 8; k++) {
+    const int g = (g0 + k) & 7;
+    const int begin = (int)((long long)total * g / 8), end = (int)((long long)total * (g + 1) / 8);
+    for (;;) {
+      int p = 0;
+      if (lane_id() == 0) p = atomicAdd(&P.work[g], 1);
+      p = begin + uniform(p);
+      if (p >= end) break;
+      f(p);
+    }
+  }
 }
 
 template <bool FAST, bool DEEP, bool SPHERES, int R>
-__global__ __launch_bounds__(kWavesPerBlock * 64) RT_TRAVERSAL_OCCUPANCY void trace_primary_kernel(
+__global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY void trace_primary_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
-  const int sel0 = packet_index() * R;
-  if (sel0 >= P.num_sel_tiles) return;
+  constexpr int W = trace_waves<DEEP>();
   int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * (1 + 2 * R) * kDeepStack : nullptr;
-  primary_packet<FAST, DEEP, SPHERES, R>(P, nodes, prims, sel0, spill);
+  for_each_packet<W, R>(P, [&](int p) {
+    const int sel0 = R == 1 ? packet_sel<W>(P, p) : p * R;
+    if (sel0 >= 0 && sel0 < P.num_sel_tiles)
+      primary_packet<FAST, DEEP, SPHERES, R>(P, nodes, prims, sel0, spill);
+  });
 }
 
 template <bool FAST, bool DEEP, bool SPHERES, int R>
-__global__ __launch_bounds__(kWavesPerBlock * 64) RT_TRAVERSAL_OCCUPANCY void trace_shadow_kernel(
+__global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY void trace_shadow_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims,
     const DevLight* __restrict__ lights) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
-  const int sel0 = packet_index() * R;
-  if (sel0 >= P.num_sel_tiles) return;
+  constexpr int W = trace_waves<DEEP>();
   int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * (1 + 2 * R) * kDeepStack : nullptr;
-  shadow_packet<FAST, DEEP, SPHERES, R>(P, nodes, prims, lights, sel0, spill);
+  for_each_packet<W, R>(P, [&](int p) {
+    const int sel0 = R == 1 ? packet_sel<W>(P, p) : p * R;
+    if (sel0 >= 0 && sel0 < P.num_sel_tiles)
+      shadow_packet<FAST, DEEP, SPHERES, R>(P, nodes, prims, lights, sel0, spill);
+  });
 }
 
 template <bool FAST, bool DEEP, bool SPHERES>
@@ -1198,7 +1429,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void recursive_kernel(
     const float* __restrict__ normals, const DevMaterial* __restrict__ mats,
     const DevLight* __restrict__ lights) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
-  const int sel = packet_index();
+  const int sel = packet_index<kWavesPerBlock>();
   if (sel >= P.num_sel_tiles) return;
   int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * 3 * kDeepStack : nullptr;
   recursive_packet<FAST, DEEP, SPHERES>(P, nodes, prims, normals, mats, lights, sel, spill);
@@ -1224,13 +1455,27 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
     return;
   }
   constexpr int R = kRaysPerLane;
-  const int tblocks = (P.num_sel_tiles + kWavesPerBlock * R - 1) / (kWavesPerBlock * R);
-  const size_t tlds = DEEP ? sizeof(int) * (1 + 2 * R) * kDeepStack * kWavesPerBlock : 0;
+  constexpr int W = trace_waves<DEEP>();
+  RenderParams T = P;
+  T.tile_block = R == 1 && P.tile_begin == 0 && P.tile_step == 1;
+  int tblocks = (trace_packets<W, R>(T) + W - 1) / W;
+  const size_t tlds = DEEP ? sizeof(int) * (1 + 2 * R) * kDeepStack * W : 0;
+  RenderParams S = T;
+#ifdef RT_EXP_PERSIST
+  if (T.work) {  // persistent waves: one resident wave per slot (8 per SIMD), counters zeroed
+    tblocks = std::min(tblocks, resident_blocks(W));
+    const hipError_t e = hipMemsetAsync(T.work, 0, 16 * sizeof(int), stream);
+    if (e != hipSuccess) return;
+    S.work = T.work + 8;
+  }
+#else
+  T.work = S.work = nullptr;
+#endif
   hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, R>), dim3(tblocks),
-                     dim3(kWavesPerBlock * 64), tlds, stream, P, nodes, prims);
+                     dim3(W * 64), tlds, stream, T, nodes, prims);
   if (P.num_lights > 0)
     hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, R>), dim3(tblocks),
-                       dim3(kWavesPerBlock * 64), tlds, stream, P, nodes, prims, lights);
+                       dim3(W * 64), tlds, stream, S, nodes, prims, lights);
   hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
                      prims, normals, mats, lights);
 }
@@ -1290,6 +1535,51 @@ hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream) {
 }
 
 int max_supported_depth() { return kDeepStack; }
+
+// Self-check of tri_quotients against `/` on random operands spanning the whole fast range:
+// |det| in [2^-40, 2^40] (a quarter with all-ones mantissas, where a reciprocal is hardest),
+// numerators 0 or in [2^-49, 2^49], a quarter of them chosen so the quotient sits next to a
+// rounding midpoint.  counts[0] += mismatches, counts[1] += cases.
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void quot_check_kernel(unsigned long long seed, long long count,
+                                                         unsigned long long* counts) {
+  unsigned long long bad = 0, n = 0;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < count; i += (long long)gridDim.x * 256) {
+    const unsigned long long a = mix64(seed + 0x9E3779B97F4A7C15ull * (unsigned long long)(i + 1));
+    const unsigned long long b = mix64(a ^ 0xD1B54A32D192ED03ull);
+    const int ed = (int)(a % 81) - 40, en = (int)((a >> 8) % 99) - 49;
+    unsigned md = (unsigned)(a >> 16) & 0x7fffffu;
+    if (((a >> 40) & 3) == 0) md = 0x7fffffu - (unsigned)((a >> 42) & 3);
+    float det = __uint_as_float(((unsigned)(ed + 127) << 23) | md);
+    if ((a >> 44) & 1) det = -det;
+    float num = __uint_as_float(((unsigned)(en + 127) << 23) | ((unsigned)b & 0x7fffffu));
+    if ((b >> 23) & 1) num = -num;
+    if (((b >> 24) & 3) == 0) {  // num = det * (a quotient just off a midpoint)
+      const double q = ldexp(1.0 + (((b >> 26) & 0x7fffff) + 0.5) / 8388608.0, en - ed);
+      const float m = (float)(q * (double)det);
+      if (quot_coord(m) && __builtin_fabsf(m) >= 0x1p-49f && __builtin_fabsf(m) <= 0x1p49f) num = m;
+    }
+    if (((b >> 50) & 15) == 0) num = 0.0f;
+    const V3 got = tri_quotients(v3(num, -num, num), det, true);
+    const float want = num / det, wneg = (-num) / det;
+    bad += (unsigned)(__float_as_uint(got.x) != __float_as_uint(want)) |
+           (unsigned)(__float_as_uint(got.y) != __float_as_uint(wneg));
+    n++;
+  }
+  atomicAdd(&counts[0], bad);
+  atomicAdd(&counts[1], n);
+}
+
+hipError_t launch_quot_check(unsigned long long seed, long long count, unsigned long long* counts,
+                             hipStream_t stream) {
+  hipLaunchKernelGGL(quot_check_kernel, dim3(2048), dim3(256), 0, stream, seed, count, counts);
+  return hipGetLastError();
+}
 
 hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                          const float* normals, const DevMaterial* mats, const DevLight* lights,

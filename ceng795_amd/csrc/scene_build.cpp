@@ -353,6 +353,7 @@ void build_host_scene(const rt_scene_desc& d, HostScene& s) {
   s.prims.clear();
   s.normals.clear();
   s.leaf_src.clear();
+  s.quot_ok = 1;
   auto resolve = [&](int id) {
     while (B.objs[id].kind == kObjMesh) id = B.objs[id].a;
     return id;
@@ -369,6 +370,7 @@ void build_host_scene(const rt_scene_desc& d, HostScene& s) {
       const float rec[9] = {v0.x, v0.y, v0.z, a1.x, a1.y, a1.z, a2.x, a2.y, a2.z};
       std::memcpy(p.v0, rec, sizeof rec);
       p.cx = a1.y * a2.z - a2.y * a1.z;  // c1.y*c2.z - c2.y*c1.z with c1 = a1, c2 = a2
+      s.quot_ok &= quot_coord_ok(v0.x) & quot_coord_ok(v0.y) & quot_coord_ok(v0.z);
     } else {
       std::memcpy(p.v0, ls.center, 12);
       p.a1[0] = ls.radius;

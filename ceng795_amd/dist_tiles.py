@@ -3,23 +3,36 @@
 The reference splits a frame over host threads by interleaved rows (HW2/main.cpp:33-36,
 HW2/Scene.cpp:25).  Here the 8x8-pixel tiles (one wavefront each) of every camera's frame are
 numbered globally, camera after camera, and dealt round-robin over ranks — rank r renders
-global tiles g = r (mod world) — which balances cost the way the row interleave does.  Each
-rank writes its tiles back to back (tile-major) into HBM; rank 0 gathers the per-rank buffers
-over RCCL (one process per GPU, torch.distributed "nccl") and untiles them into row-major
-fp32 framebuffers.  There is no other exchange: the scene is replicated, rays are independent.
+global tiles g = r (mod world) — which balances cost the way the row interleave does.  There
+is no other exchange: the scene is replicated, rays are independent.
 
-TileLayout and untile() are pure bookkeeping (numpy / torch CPU) so the N>1 logic is testable
-with the gloo backend on CPU; FrameRenderer drives the GPU.
+Buffer layout.  Each rank's HBM buffer holds one fixed-size SLOT per camera
+(ceil(tiles / world) tiles, the largest share any rank gets), and the rank's tiles of that
+camera are written back to back (tile-major) at the slot's start.  Every rank's slot c has the
+same size, so camera c's shares are gathered to rank 0 by one equal-size collective
+(torch.distributed "nccl" = RCCL send/recv over xGMI), and the gather of camera c runs on a
+communication stream while the rank renders camera c + 1: only the last camera's gather of a
+step is exposed.  Rank 0 then untiles camera c with ONE index_select of 8-pixel tile rows
+(96 B, contiguous in both layouts) straight into the row-major framebuffer.
+
+TileLayout and the untile index are pure bookkeeping (numpy / torch CPU) so the N>1 logic is
+testable with the gloo backend on CPU; FrameRenderer drives the GPU.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
 TILE = 8
 TILE_FLOATS = TILE * TILE * 3
+ROW_FLOATS = TILE * 3  # one pixel row of a tile
+
+
+def tiles_of(size: Tuple[int, int]) -> Tuple[int, int]:
+    w, h = size
+    return (w + TILE - 1) // TILE, (h + TILE - 1) // TILE
 
 
 @dataclass
@@ -28,66 +41,83 @@ class CameraShare:
     tile_begin: int   # first camera-local tile of this rank
     tile_step: int    # = world
     count: int        # tiles of this camera rendered by this rank
-    offset: int       # position (in tiles) of this camera's share in the rank buffer
+    offset: int       # start (in tiles) of this camera's slot in the rank buffer
+    slot: int         # slot size in tiles (same on every rank)
 
 
 class TileLayout:
-    """Global round-robin assignment of tiles to ranks for a list of cameras."""
+    """Global round-robin assignment of tiles to ranks for a list of camera frame sizes."""
 
-    def __init__(self, tiles_per_camera: Sequence[int], world: int, rank: int):
-        self.tiles_per_camera = list(tiles_per_camera)
+    def __init__(self, sizes: Sequence[Tuple[int, int]], world: int, rank: int):
+        self.sizes = [tuple(s) for s in sizes]
+        self.tiles_per_camera = [tx * ty for tx, ty in map(tiles_of, self.sizes)]
         self.world = world
         self.rank = rank
         self.offsets = np.concatenate([[0], np.cumsum(self.tiles_per_camera)]).astype(np.int64)
         self.total = int(self.offsets[-1])
+        self.slots = [(T + world - 1) // world for T in self.tiles_per_camera]
+        self.slot_offsets = np.concatenate([[0], np.cumsum(self.slots)]).astype(np.int64)
+        self.buffer_tiles = int(self.slot_offsets[-1])
         self.per_rank = [self._shares(r) for r in range(world)]
-        self.padded_tiles = max(sum(s.count for s in shares) for shares in self.per_rank)
         self.shares = self.per_rank[rank]
         self.local_tiles = sum(s.count for s in self.shares)
 
+    def begin(self, r: int, c: int) -> int:
+        """First tile of camera c dealt to rank r (global tile g goes to rank g mod world)."""
+        return int((r - self.offsets[c]) % self.world)
+
     def _shares(self, r: int) -> List[CameraShare]:
-        out, pos = [], 0
+        out = []
         for c, T in enumerate(self.tiles_per_camera):
-            off = int(self.offsets[c])
-            begin = (r - off) % self.world
-            count = 0 if begin >= T else (T - begin + self.world - 1) // self.world
-            out.append(CameraShare(c, begin, self.world, count, pos))
-            pos += count
+            b = self.begin(r, c)
+            count = 0 if b >= T else (T - b + self.world - 1) // self.world
+            out.append(CameraShare(c, b, self.world, count, int(self.slot_offsets[c]),
+                                   self.slots[c]))
         return out
 
-    def untile_index(self) -> np.ndarray:
-        """For every global tile g (camera-major), its row in the gathered
-        [world * padded_tiles] tile array."""
-        idx = np.empty(self.total, np.int64)
-        for r, shares in enumerate(self.per_rank):
-            for s in shares:
-                if s.count == 0:
-                    continue
-                t = s.tile_begin + s.tile_step * np.arange(s.count)
-                idx[self.offsets[s.camera] + t] = r * self.padded_tiles + s.offset + np.arange(s.count)
-        return idx
+    def row_index(self, c: int) -> np.ndarray:
+        """Untile index of camera c.  The gathered slots [world, slot, 8 rows, 24 floats] are
+        viewed as 96-byte tile rows; entry (y, x) of the returned [ty*8, tx] array is the tile
+        row that becomes pixel row y, pixels 8x..8x+7, of the (tile-padded) frame."""
+        tx, ty = tiles_of(self.sizes[c])
+        t = np.arange(tx * ty, dtype=np.int64)
+        r = (t + self.offsets[c]) % self.world
+        b = (r - self.offsets[c]) % self.world
+        pos = (t - b) // self.world
+        tile_src = (r * self.slots[c] + pos).reshape(ty, tx)  # gathered tile of each frame tile
+        y = np.arange(ty * TILE, dtype=np.int64)
+        return (tile_src[y // TILE] * TILE + (y % TILE)[:, None]).astype(np.int64)
 
 
-def untile(gathered, layout: TileLayout, sizes: Sequence[tuple], index=None):
-    """gathered: torch tensor [world * padded_tiles, 192] (any device).  sizes: (w, h) per
-    camera.  Returns a list of [h, w, 3] row-major framebuffers."""
+def untile_camera(gathered_c, layout: TileLayout, c: int, index=None, out=None):
+    """gathered_c: tensor [world * slot_c, 192] (any device) — camera c's slots of every rank.
+    Returns the [h, w, 3] row-major frame (a view of `out`, a [ty*8, tx*8, 3] buffer, when
+    given)."""
     import torch
+    tx, ty = tiles_of(layout.sizes[c])
     if index is None:
-        index = torch.as_tensor(layout.untile_index(), device=gathered.device)
-    tiles = gathered.index_select(0, index)
-    frames = []
-    for c, (w, h) in enumerate(sizes):
-        tx, ty = (w + TILE - 1) // TILE, (h + TILE - 1) // TILE
-        t = tiles[layout.offsets[c]:layout.offsets[c + 1]].view(ty, tx, TILE, TILE, 3)
-        full = t.permute(0, 2, 1, 3, 4).reshape(ty * TILE, tx * TILE, 3)
-        frames.append(full[:h, :w])
-    return frames
+        index = torch.as_tensor(layout.row_index(c).reshape(-1), device=gathered_c.device)
+    if out is None:
+        out = torch.empty((ty * TILE, tx * TILE, 3), dtype=gathered_c.dtype,
+                          device=gathered_c.device)
+    torch.index_select(gathered_c.view(-1, ROW_FLOATS), 0, index, out=out.view(-1, ROW_FLOATS))
+    w, h = layout.sizes[c]
+    return out[:h, :w]
 
 
 class FrameRenderer:
     """One step = render every camera of `scene`; with gather=True, gather to rank 0 and untile.
 
-    world == 1 and gather == False renders each camera in place into a row-major frame."""
+    world == 1 and gather == False renders each camera in place into a row-major frame.
+
+    gather=True (one process per GPU): camera c's share is rendered on `stream`; an event hands
+    it to a communication stream that gathers slot c to rank 0 (RCCL) and, on rank 0, untiles
+    it, while `stream` goes on with camera c + 1.  The rank buffer alternates between two copies
+    per step, and a slot is rendered again only after its gather two steps earlier has finished
+    (per-slot events), so consecutive steps pipeline too.  Rank 0's receive buffer and frames are
+    only touched on the comm stream, in order.
+    host_staging=True (the gloo rehearsal) does the same exchange synchronously via host copies.
+    """
 
     def __init__(self, scene, layout_or_none: Optional[TileLayout], stream, gather: bool,
                  host_staging: bool = False):
@@ -97,7 +127,7 @@ class FrameRenderer:
         self.scene = scene
         self.stream = stream
         self.gather = gather
-        self.host_staging = host_staging  # gloo rehearsal: collectives on host copies
+        self.host_staging = host_staging
         self.sizes = [(scene.camera(c).width, scene.camera(c).height)
                       for c in range(scene.num_cameras)]
         self.layout = layout_or_none
@@ -107,14 +137,56 @@ class FrameRenderer:
                            for (w, h) in self.sizes]
             return
         L = self.layout
-        self.local = torch.zeros((L.padded_tiles, TILE_FLOATS), dtype=torch.float32, device=dev)
+        assert L.sizes == self.sizes, "tile layout built for other frame sizes"
         self.rank = L.rank
+        # two rank buffers, alternating per step: step k + 1 renders while step k's last
+        # slot is still being gathered
+        self.local = [torch.zeros((L.buffer_tiles, TILE_FLOATS), dtype=torch.float32, device=dev)
+                      for _ in range(2)]
+        self.buf = 0
+        self.comm = torch.cuda.Stream(device=dev)
+        self.rendered = [torch.cuda.Event() for _ in L.shares]
+        self.slot_free = [[torch.cuda.Event() for _ in L.shares] for _ in range(2)]
+        self.slot_used = [[False] * len(L.shares) for _ in range(2)]
         if L.rank == 0:
-            self.gathered = torch.empty((L.world * L.padded_tiles, TILE_FLOATS),
-                                        dtype=torch.float32, device=dev)
-            self.gather_list = list(self.gathered.view(L.world, L.padded_tiles, TILE_FLOATS))
-            self.index = torch.as_tensor(L.untile_index(), device=dev)
-        self.frames = None
+            self.gathered = [torch.empty((L.world, s.slot, TILE_FLOATS), dtype=torch.float32,
+                                         device=dev) for s in L.shares]
+            self.index = [torch.as_tensor(L.row_index(c).reshape(-1), device=dev)
+                          for c in range(len(L.shares))]
+            self.padded = []
+            for (w, h) in self.sizes:
+                tx, ty = tiles_of((w, h))
+                self.padded.append(torch.empty((ty * TILE, tx * TILE, 3), dtype=torch.float32,
+                                               device=dev))
+            self.frames = [p[:h, :w] for p, (w, h) in zip(self.padded, self.sizes)]
+        else:
+            self.frames = None
+
+    def _slot(self, sh: CameraShare):
+        return self.local[self.buf][sh.offset:sh.offset + sh.slot]
+
+    def _exchange(self, c: int, sh: CameraShare):
+        torch, dist, L = self.torch, self.dist, self.layout
+        root = self.rank == 0
+        if self.host_staging:  # gloo: host copies, synchronous
+            self.stream.synchronize()
+            host = self._slot(sh).cpu()
+            glist = list(torch.empty((L.world, sh.slot, TILE_FLOATS))) if root else None
+            dist.gather(host, glist, dst=0)
+            if root:
+                self.gathered[c].copy_(torch.stack(glist))
+                untile_camera(self.gathered[c].view(-1, TILE_FLOATS), L, c, self.index[c],
+                              self.padded[c])
+            return
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(self.rendered[c])
+            work = dist.gather(self._slot(sh), list(self.gathered[c]) if root else None, dst=0,
+                               async_op=True)
+            work.wait()  # the comm stream waits for the collective (host does not block)
+            if root:
+                untile_camera(self.gathered[c].view(-1, TILE_FLOATS), L, c, self.index[c],
+                              self.padded[c])
+            self.slot_free[self.buf][c].record(self.comm)
 
     def step(self, events=None):
         s = self.stream.cuda_stream
@@ -126,33 +198,34 @@ class FrameRenderer:
             if events is not None:
                 events[1].record(self.stream)
             return self.frames
-        for sh in self.layout.shares:
+        self.buf ^= 1
+        for c, sh in enumerate(self.layout.shares):
+            if self.slot_used[self.buf][c]:  # this slot's gather two steps ago
+                self.stream.wait_event(self.slot_free[self.buf][c])
             if sh.count:
-                self.scene.render_device(sh.camera, self.local[sh.offset].data_ptr(),
+                self.scene.render_device(sh.camera, self._slot(sh).data_ptr(),
                                          tile_begin=sh.tile_begin, tile_step=sh.tile_step,
                                          tile_major=True, stream=s)
+            self.rendered[c].record(self.stream)
+            self.slot_used[self.buf][c] = True
+            self._exchange(c, sh)
         if events is not None:
             events[1].record(self.stream)
-        if self.host_staging:
-            torch = self.torch
-            self.stream.synchronize()
-            host = self.local.cpu()
-            glist = list(torch.empty((self.layout.world, self.layout.padded_tiles, TILE_FLOATS))) \
-                if self.rank == 0 else None
-            self.dist.gather(host, glist, dst=0)
-            if self.rank == 0:
-                self.gathered.copy_(torch.cat(glist))
-        else:
-            self.dist.gather(self.local, self.gather_list if self.rank == 0 else None, dst=0)
-        if self.rank == 0:
-            self.frames = [f.contiguous() for f in
-                           untile(self.gathered, self.layout, self.sizes, self.index)]
         return self.frames
 
+    def finish(self):
+        """Make `stream` wait for every outstanding gather / untile of this renderer."""
+        if self.gather and not self.host_staging:
+            self.stream.wait_stream(self.comm)
 
-def TilePlan(scene, world: int, rank: int) -> Optional[TileLayout]:
-    """Tile layout for every camera of `scene` (None when a single rank renders in place)."""
-    if world == 1:
+
+def TilePlan(scene, world: int, rank: int, force: bool = False) -> Optional[TileLayout]:
+    """Tile layout for every camera of `scene` (None when a single rank renders in place,
+    unless `force`: the one-rank rehearsal of the gather pipeline)."""
+    if world == 1 and not force:
         return None
-    tiles = [scene.num_tiles(c) for c in range(scene.num_cameras)]
-    return TileLayout(tiles, world, rank)
+    sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
+    L = TileLayout(sizes, world, rank)
+    for c in range(scene.num_cameras):
+        assert L.tiles_per_camera[c] == scene.num_tiles(c), "tile count disagrees with the library"
+    return L

@@ -187,6 +187,12 @@ int rt_collect_stats(rt_scene* scene, rt_stats* stats);
  * test.  Returns 1 for a diagnostic build, 0 otherwise (columns 4..12 then read 0). */
 int rt_debug_counters(rt_scene* scene, long long* out16);
 
+/* Device self-check of the triangle test's shared-reciprocal quotients (rt_kernels.hip,
+ * tri_quotients) against IEEE division on `count` seeded random operand pairs of the fast
+ * range; out2[0] = mismatching quotients (must be 0), out2[1] = cases run. */
+int rt_debug_quotient_check(int device, unsigned long long seed, long long count,
+                            long long* out2);
+
 /* PNG output as HW2/main.cpp:43-57: per channel clamp(int(c), 0, 255), alpha 255. */
 int rt_write_png(const char* path, const float* rgb, int width, int height);
 

@@ -1,6 +1,7 @@
 """Multi-rank tile sharding + framebuffer gather (ceng795_amd/dist_tiles.py), exercised with
-the gloo backend on CPU.  The GPU path (bench.py, FrameRenderer) uses the same TileLayout and
-untile(); only the tile renderer differs (here: tiles cut out of known frames)."""
+the gloo backend on CPU.  The GPU path (bench.py, FrameRenderer) uses the same TileLayout,
+per-camera slots and untile_camera(); only the tile renderer differs (here: tiles cut out of
+known frames) and the collective runs on host tensors."""
 import os
 import socket
 
@@ -10,7 +11,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from ceng795_amd.dist_tiles import TILE, TILE_FLOATS, TileLayout, untile
+from ceng795_amd.dist_tiles import TILE, TILE_FLOATS, TileLayout, untile_camera
 
 SIZES = [(37, 21), (64, 40), (5, 9), (96, 64)]  # (w, h): ragged edges, tiny frames
 
@@ -38,24 +39,35 @@ def _tile(frame, t):
     return out.reshape(-1)
 
 
+def _render_local(L, frames):
+    """What rt_render_device(tile_major=True) writes: each share at its slot's start."""
+    local = torch.full((L.buffer_tiles, TILE_FLOATS), float("nan"))
+    for sh in L.shares:
+        for k in range(sh.count):
+            local[sh.offset + k] = torch.from_numpy(
+                _tile(frames[sh.camera], sh.tile_begin + k * sh.tile_step))
+    return local
+
+
+def _same(a, b):
+    return np.array_equal(np.asarray(a).view(np.uint32), np.asarray(b).view(np.uint32))
+
+
 def _worker(rank, world, port, outdir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     frames = _frames()
-    tiles = [((w + TILE - 1) // TILE) * ((h + TILE - 1) // TILE) for (w, h) in SIZES]
-    L = TileLayout(tiles, world, rank)
-    local = torch.zeros((L.padded_tiles, TILE_FLOATS))
-    for sh in L.shares:  # "render": tiles tile_begin + k*world of each camera
-        for k in range(sh.count):
-            local[sh.offset + k] = torch.from_numpy(_tile(frames[sh.camera], sh.tile_begin + k * sh.tile_step))
-    gathered = torch.empty((world * L.padded_tiles, TILE_FLOATS)) if rank == 0 else None
-    dist.gather(local, list(gathered.view(world, L.padded_tiles, TILE_FLOATS)) if rank == 0 else None,
-                dst=0)
+    L = TileLayout(SIZES, world, rank)
+    local = _render_local(L, frames)
+    ok = True
+    for c, sh in enumerate(L.shares):  # one equal-size gather per camera slot
+        glist = list(torch.empty((world, sh.slot, TILE_FLOATS))) if rank == 0 else None
+        dist.gather(local[sh.offset:sh.offset + sh.slot].contiguous(), glist, dst=0)
+        if rank == 0:
+            got = untile_camera(torch.stack(glist).view(-1, TILE_FLOATS), L, c)
+            ok &= _same(got.contiguous().numpy(), frames[c])
     if rank == 0:
-        out = untile(gathered, L, SIZES)
-        ok = all(np.array_equal(o.numpy().view(np.uint32), f.view(np.uint32))
-                 for o, f in zip(out, frames))
         with open(os.path.join(outdir, "result"), "w") as fh:
             fh.write("ok" if ok else "mismatch")
     dist.barrier()
@@ -68,18 +80,35 @@ def test_gather_reassembles_frames(tmp_path, world):
     assert (tmp_path / "result").read_text() == "ok"
 
 
+@pytest.mark.parametrize("world", [1, 2, 5, 8, 13])
+def test_untile_single_process(world):
+    """All ranks simulated in one process: gathered slots -> frames, bit for bit."""
+    frames = _frames(3)
+    layouts = [TileLayout(SIZES, world, r) for r in range(world)]
+    locals_ = [_render_local(L, frames) for L in layouts]
+    for c in range(len(SIZES)):
+        sh = layouts[0].shares[c]
+        g = torch.stack([loc[sh.offset:sh.offset + sh.slot] for loc in locals_])
+        got = untile_camera(g.view(-1, TILE_FLOATS), layouts[0], c)
+        assert _same(got.contiguous().numpy(), frames[c])
+
+
 @pytest.mark.parametrize("world", [1, 2, 5, 8])
 def test_every_tile_rendered_exactly_once(world):
-    tiles = [((w + TILE - 1) // TILE) * ((h + TILE - 1) // TILE) for (w, h) in SIZES]
-    seen = np.zeros(sum(tiles), np.int64)
+    L0 = TileLayout(SIZES, world, 0)
+    seen = np.zeros(L0.total, np.int64)
     loads = []
     for r in range(world):
-        L = TileLayout(tiles, world, r)
+        L = TileLayout(SIZES, world, r)
         loads.append(L.local_tiles)
+        assert L.buffer_tiles == L0.buffer_tiles
         for sh in L.shares:
+            assert sh.count <= sh.slot and sh.slot == L0.shares[sh.camera].slot
             for k in range(sh.count):
                 seen[L.offsets[sh.camera] + sh.tile_begin + k * sh.tile_step] += 1
     assert np.all(seen == 1)
     assert max(loads) - min(loads) <= 1  # round-robin: balanced to one tile
-    idx = TileLayout(tiles, world, 0).untile_index()
-    assert len(np.unique(idx)) == len(idx)
+    for c in range(len(SIZES)):  # the untile reads every tile row of camera c exactly once
+        idx = L0.row_index(c).reshape(-1)
+        assert len(np.unique(idx)) == len(idx)
+        assert idx.max() < world * L0.slots[c] * TILE

@@ -174,3 +174,16 @@ def test_msaa_whole_frames_only(rt, scene_dir):
         got, _ = s.render_image(0)
         assert np.array_equal(full.cpu().numpy().reshape(got.shape).view(np.uint32),
                               got.view(np.uint32))
+
+
+def test_shared_reciprocal_quotients_are_ieee(rt):
+    """tri_quotients (one v_rcp + Markstein steps for the three Cramer divisions) gives the bits
+    of IEEE `/` over its whole operand range, incl. all-ones divisor mantissas and quotients
+    next to rounding midpoints."""
+    import ctypes as C
+    from ceng795_amd import _lib
+    out = (C.c_longlong * 2)()
+    for seed in (1, 2, 3):
+        _lib.check(_lib.lib().rt_debug_quotient_check(0, seed, 1 << 26, out))
+        assert out[1] == 1 << 26
+        assert out[0] == 0, f"seed {seed}: {out[0]} quotients differ from IEEE division"

@@ -29,6 +29,13 @@ for g in "$@"; do
     sqc)
       run sqc SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_DCACHE_REQ SQC_ICACHE_HITS \
         SQC_ICACHE_MISSES SQC_TC_STALL SQC_DCACHE_BUSY_CYCLES SQC_TC_DATA_READ_REQ ;;
+    sqcbusy)  # is the scalar data cache (node / prim fetches) the limiter?
+      run sqcbusy SQC_DCACHE_BUSY_CYCLES SQC_DCACHE_INPUT_VALID_READYB SQC_DCACHE_REQ \
+        SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_DCACHE_MISSES_DUPLICATE SQC_TC_STALL \
+        SQ_WAVE_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT ;;
+    cycles)   # issue cycles by pipe
+      run cycles SQ_INST_CYCLES_SALU SQ_INST_CYCLES_SMEM SQ_INST_CYCLES_VALU SQ_INSTS_SALU \
+        SQ_INSTS_VALU SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE ;;
     *) echo "unknown group $g"; exit 2 ;;
   esac
 done
