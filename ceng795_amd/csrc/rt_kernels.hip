@@ -557,6 +557,86 @@ __device__ __forceinline__ bool advance(WaveStack<DEEP, R>& st, int c0, int c1,
   }
 }
 
+// ------------------------------------------------------------------ batched leaf tests
+// A packet reaches a leaf with only the few lanes whose rays pass over that triangle (C3:
+// ~14 of 64), so testing leaves one at a time runs the triangle test at ~20% SIMD efficiency.
+// With R == 1 the traversal instead queues (lane, leaf) pairs in a per-wave LDS list and runs
+// them 64 at a time, one pair per lane (the owner's ray fetched with ds_bpermute, the
+// triangle with a per-lane load), once 64 are pending and when the walk ends.  Results land
+// per ray by LDS atomics: closest hit = atomic min of the key (t bits << 32 | leaf), which for
+// 0 < t orders exactly like the reference's (t, DFS leaf) rule; shadow = atomic or.  The
+// queued tests are the ones the reference makes, so the answer is unchanged; only FAST
+// culling sees best_t a little later (after each flush), which can only cull less.
+// RT_EXP_NOBATCH: leaves tested where they are met (the R > 1 path always does).
+#ifndef RT_BATCH_FLUSH
+#define RT_BATCH_FLUSH 64
+#endif
+constexpr int kBatchFlush = RT_BATCH_FLUSH;  // run the queue once this many tests are pending
+constexpr int kBatchCap = kBatchFlush + 128;  // < kBatchFlush pending + 2 x 64 per visit
+#ifndef RT_TRACE_WAVES
+#define RT_TRACE_WAVES 4
+#endif
+constexpr int kLdsWaves = RT_TRACE_WAVES > kWavesPerBlock ? RT_TRACE_WAVES : kWavesPerBlock;
+
+struct WaveLeafLds {
+  unsigned long long q[kBatchCap];  // lo 32: leaf index, hi 32: lane
+  unsigned long long key[64];       // per lane: closest-hit key, or shadow flag
+};
+
+__device__ __forceinline__ WaveLeafLds& wave_leaf_lds() {
+  __shared__ WaveLeafLds s[kLdsWaves];  // 2 KiB per wave
+  return s[threadIdx.x >> 6];
+}
+
+#if defined(RT_EXP_NOBATCH)
+constexpr bool kBatchLeaves = false;
+#else
+constexpr bool kBatchLeaves = true;
+#endif
+
+constexpr unsigned long long kNoHitKey = (0x7f800000ull << 32) | 0xffffffffull;  // (+inf, -1)
+
+// Queue leaf `leaf` for the lanes of `m` (wave-uniform); n = pending entries (wave-uniform).
+__device__ __forceinline__ void batch_push(WaveLeafLds& L, int& n, int leaf, uint64_t m) {
+  const int lane = lane_id();
+  if ((m >> lane) & 1) {
+    const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    L.q[n + below] = ((unsigned long long)lane << 32) | (unsigned)leaf;
+  }
+  n += __builtin_popcountll(m);
+}
+
+__device__ __forceinline__ float lane_f(int src, float v) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
+}
+
+// Runs the n queued tests; SHADOW: 0 < t < thr of the owner sets its flag, else the owner's
+// key takes min(key, (t, leaf)) for 0 < t < inf.  All lanes of the wave take part.
+template <bool SHADOW, bool SPHERES>
+__device__ __forceinline__ void batch_flush(WaveLeafLds& L, int n, const DevPrim* __restrict__ prims,
+                                            const LaneRay& r, float thr) {
+  const int lane = lane_id();
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + lane;
+    const bool valid = i < n;
+    const unsigned long long e = valid ? L.q[i] : 0ull;
+    const int src = (int)(e >> 32), leaf = (int)(unsigned)e;
+    LaneRay rr;
+    rr.o = v3(lane_f(src, r.o.x), lane_f(src, r.o.y), lane_f(src, r.o.z));
+    rr.d = v3(lane_f(src, r.d.x), lane_f(src, r.d.y), lane_f(src, r.d.z));
+    rr.quot = __builtin_amdgcn_ds_bpermute(src << 2, (int)r.quot) != 0;
+    const float othr = SHADOW ? lane_f(src, thr) : 0.0f;
+    float t = 0.0f;
+    const bool hit = leaf_test<SPHERES>(prims, leaf, rr, t);  // leaf 0 for idle lanes: unused
+    if (SHADOW) {
+      if (valid & hit & (t > 0.0f) & (t < othr)) L.key[src] = 1ull;  // any writer: same value
+    } else if (valid & hit & (t > 0.0f) & (t < RT_INF)) {
+      atomicMin(&L.key[src], ((unsigned long long)__float_as_uint(t) << 32) | (unsigned)leaf);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ closest hit
 // R rays per lane.  Returns the reference's (t, leaf) for every active ray: leaf < 0 = miss.
 template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R>
@@ -602,8 +682,21 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
   uint64_t everyone[R];
 #pragma unroll
   for (int k = 0; k < R; k++) everyone[k] = ~0ull;
+  constexpr bool batch = kBatchLeaves && R == 1;
+  WaveLeafLds& L = wave_leaf_lds();
+  int pending = 0;
+  if (batch) L.key[lane] = kNoHitKey;
   int node = accel ? P.accel_root : P.root_ref;
   for (;;) {
+    if constexpr (batch) {  // between visits: only the ray, the stack and best_t are live
+      if (pending >= kBatchFlush) {
+        batch_flush<false, SPHERES>(L, pending, prims, r[0], 0.0f);
+        pending = 0;
+        const unsigned long long key = L.key[lane];
+        best_t[0] = __uint_as_float((unsigned)(key >> 32));
+        best_leaf[0] = (int)(unsigned)key;
+      }
+    }
     const DevNode N = load_node(nodes, node);
     ChildPrefetch pf;
     pf.issue(nodes, prims, N.child[0], N.child[1]);
@@ -616,6 +709,10 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
          dg.leaves += (N.child[0] < 0) + (N.child[1] < 0);
          dg.leaf_lanes += (N.child[0] < 0 ? __builtin_popcountll(ballot(h0[0])) : 0) +
                           (N.child[1] < 0 ? __builtin_popcountll(ballot(h1[0])) : 0));
+    if constexpr (batch) {  // queue the leaf children's tests; run them 64 at a time
+      if (N.child[0] < 0) batch_push(L, pending, ~N.child[0], ballot(h0[0]));
+      if (N.child[1] < 0) batch_push(L, pending, ~N.child[1], ballot(h1[0]));
+    } else {
 #ifndef RT_EXP_NOLEAF
 #pragma unroll 1
     for (int side = 0; side < 2; side++) {  // leaf children: Shape::intersect, 0 < t < best
@@ -647,6 +744,7 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
 #pragma unroll
     for (int k = 0; k < R; k++) best_leaf[k] -= (int)((m[k] >> lane) & 1);  // keep it observable
 #endif
+    }
     uint64_t m0[R], m1[R];
 #pragma unroll
     for (int k = 0; k < R; k++) {  // leaves are done; only inner children are entered
@@ -662,6 +760,12 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
     }
     pf.retire();
     if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, everyone)) break;
+  }
+  if constexpr (batch) {
+    if (pending) batch_flush<false, SPHERES>(L, pending, prims, r[0], 0.0f);
+    const unsigned long long key = L.key[lane];
+    best_t[0] = __uint_as_float((unsigned)(key >> 32));
+    best_leaf[0] = (int)(unsigned)key;
   }
 }
 
@@ -705,8 +809,22 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
   const int lane = lane_id();
   WaveStack<DEEP, R> st;
   st.lds = spill;
+  constexpr bool batch = kBatchLeaves && R == 1;
+  WaveLeafLds& L = wave_leaf_lds();
+  int pending = 0;
+  if (batch) L.key[lane] = 0ull;
   int node = accel ? P.accel_root : P.root_ref;
   for (;;) {
+    if constexpr (batch) {  // between visits; a lane found occluded stops entering nodes
+      if (pending >= kBatchFlush) {
+        batch_flush<true, SPHERES>(L, pending, prims, r[0], thr[0]);
+        pending = 0;
+        occ[0] = L.key[lane] != 0ull;
+        alive[0] &= ~ballot(occ[0]);
+        m[0] &= alive[0];
+        if (!m[0] && !advance(st, 0, 0, m, m, thr, thr, node, m, alive)) break;
+      }
+    }
     const DevNode N = load_node(nodes, node);
     ChildPrefetch pf;
     pf.issue(nodes, prims, N.child[0], N.child[1]);
@@ -719,6 +837,10 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
          dg.leaves += (N.child[0] < 0) + (N.child[1] < 0);
          dg.leaf_lanes += (N.child[0] < 0 ? __builtin_popcountll(ballot(h0[0])) : 0) +
                           (N.child[1] < 0 ? __builtin_popcountll(ballot(h1[0])) : 0));
+    if constexpr (batch) {  // queue the still-unoccluded lanes' leaf tests
+      if (N.child[0] < 0) batch_push(L, pending, ~N.child[0], ballot(h0[0]) & alive[0]);
+      if (N.child[1] < 0) batch_push(L, pending, ~N.child[1], ballot(h1[0]) & alive[0]);
+    } else {
 #pragma unroll 1
     for (int side = 0; side < 2; side++) {
       const int c = side ? N.child[1] : N.child[0];
@@ -741,6 +863,7 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
         }
       }
     }
+    }
     uint64_t m0[R], m1[R];
 #pragma unroll
     for (int k = 0; k < R; k++) {
@@ -758,6 +881,10 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
     pf.retire();
     if (!any_of(alive)) break;
     if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, alive)) break;
+  }
+  if constexpr (batch) {
+    if (pending) batch_flush<true, SPHERES>(L, pending, prims, r[0], thr[0]);
+    occ[0] = L.key[lane] != 0ull;
   }
 }
 
@@ -1320,9 +1447,6 @@ __device__ __forceinline__ int packet_index() {
 // of tiles (blocks row-major over the frame) instead of a run along a tile row: neighbouring
 // rays walk the same nodes, and the cache serves them once.  Deep trees keep 4-wave groups
 // (their LDS stack is 12 KB per wave).
-#ifndef RT_TRACE_WAVES
-#define RT_TRACE_WAVES 4
-#endif
 #ifndef RT_TRACE_BLOCK_W
 #define RT_TRACE_BLOCK_W 2
 #endif
