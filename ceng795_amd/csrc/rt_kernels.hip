@@ -888,6 +888,21 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
   }
 }
 
+// The kernel's RenderParams (its FIRST argument, so at offset 0 of the kernarg segment) read
+// through a pointer the compiler cannot see through: loads from it are not hoisted above this
+// point, so the persistent packet loop does not pull every field it uses into SGPRs for the
+// whole kernel (they were spilled to VGPR lanes across the traversal and reloaded per visit).
+typedef __attribute__((address_space(4))) const RenderParams KernargParams;
+__device__ __forceinline__ const RenderParams& fresh_params(const RenderParams& P) {
+#ifdef RT_EXP_NOLAUNDER
+  return P;
+#else
+  KernargParams* p = (KernargParams*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const RenderParams*)p;
+#endif
+}
+
 // ------------------------------------------------------------------ render kernels
 // Two launches per frame (wavefront style): `trace_primary` finds each pixel's closest hit and
 // writes an 8-byte {t, leaf} record; `shade` rebuilds the shading inputs from it and runs the
@@ -994,20 +1009,21 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
     closest_hit<true, FAST, DEEP, SPHERES, R>(P, nodes, prims, spill, ray, valid, t, leaf, dg);
   else
     closest_hit<false, FAST, DEEP, SPHERES, R>(P, nodes, prims, spill, ray, valid, t, leaf, dg);
+  const RenderParams& Pw = fresh_params(P);  // post-traversal fields: not live across it
   unsigned long long nvalid = 0, nhit = 0;
 #pragma unroll
   for (int k = 0; k < R; k++) {
-    if (sel0 + k < P.num_sel_tiles) {
+    if (sel0 + k < Pw.num_sel_tiles) {
       int2_t rec;
       rec.x = __float_as_int(t[k]);
       rec.y = valid[k] ? leaf[k] : -2;  // -1 miss, -2 outside the image
-      P.hits[(size_t)(sel0 + k) * (kTile * kTile) + q[k].lane] = rec;
+      Pw.hits[(size_t)(sel0 + k) * (kTile * kTile) + q[k].lane] = rec;
     }
     nvalid += __builtin_popcountll(ballot(valid[k]));
     nhit += __builtin_popcountll(ballot(valid[k] && leaf[k] >= 0));
   }
-  if (P.counters && q[0].lane == 0) {  // spread over kCounterSlots rows: no hot address
-    unsigned long long* c = counter_row(P, sel0);
+  if (Pw.counters && q[0].lane == 0) {  // spread over kCounterSlots rows: no hot address
+    unsigned long long* c = counter_row(Pw, sel0);
     atomicAdd(&c[kCntPrimary], nvalid);
     atomicAdd(&c[kCntHits], nhit);
 #ifdef RT_DIAG
@@ -1028,7 +1044,7 @@ __device__ __forceinline__ V3 hit_point(const RenderParams& P, const PacketPixel
 // Shadow rays of HW2/Scene.cpp:113-127: one bit per point light, set when the light is
 // occluded for this pixel's primary hit.  R tiles per wave as in primary_packet.
 template <bool FAST, bool DEEP, bool SPHERES, int R>
-__device__ __forceinline__ void shadow_packet(const RenderParams& P,
+__device__ __forceinline__ void shadow_packet(const RenderParams& P0,
                                               const DevNode* __restrict__ nodes,
                                               const DevPrim* __restrict__ prims,
                                               const DevLight* __restrict__ lights, int sel0,
@@ -1040,24 +1056,25 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P,
   unsigned long long nhit = 0;
 #pragma unroll
   for (int k = 0; k < R; k++) {
-    q[k] = packet_pixel(P, sel0 + k);
-    const bool inside = sel0 + k < P.num_sel_tiles;
+    q[k] = packet_pixel(P0, sel0 + k);
+    const bool inside = sel0 + k < P0.num_sel_tiles;
     pix[k] = (size_t)(sel0 + k) * (kTile * kTile) + q[k].lane;
     int2_t rec;
     rec.x = 0;
     rec.y = -2;
-    if (inside) rec = P.hits[pix[k]];
+    if (inside) rec = P0.hits[pix[k]];
     hit[k] = rec.y >= 0;
-    p[k] = hit[k] ? hit_point(P, q[k], __int_as_float(rec.x)) : v3(0, 0, 0);
+    p[k] = hit[k] ? hit_point(P0, q[k], __int_as_float(rec.x)) : v3(0, 0, 0);
     nhit += __builtin_popcountll(ballot(hit[k]));
   }
   Diag dg;
-  for (int w = 0; w < P.occ_words; w++) {
+  for (int w = 0; w < P0.occ_words; w++) {
     unsigned bits[R];
 #pragma unroll
     for (int k = 0; k < R; k++) bits[k] = 0;
-    const int lend = min(P.num_lights, 32 * (w + 1));
+    const int lend = min(P0.num_lights, 32 * (w + 1));
     for (int li = 32 * w; li < lend; li++) {
+      const RenderParams& P = fresh_params(P0);  // per light: nothing live across traversals
       const DevLight& L = lights[li];
       LaneRay sr[R];
       float thr[R];
@@ -1079,13 +1096,15 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P,
 #pragma unroll
       for (int k = 0; k < R; k++) bits[k] |= (occ[k] ? 1u : 0u) << (li - 32 * w);
     }
+    const RenderParams& Pw = fresh_params(P0);
 #pragma unroll
     for (int k = 0; k < R; k++)
-      if (sel0 + k < P.num_sel_tiles) P.occ[pix[k] * P.occ_words + w] = bits[k];
+      if (sel0 + k < Pw.num_sel_tiles) Pw.occ[pix[k] * Pw.occ_words + w] = bits[k];
   }
-  if (P.counters && q[0].lane == 0) {
-    unsigned long long* c = counter_row(P, sel0);
-    atomicAdd(&c[kCntShadow], nhit * (unsigned long long)P.num_lights);
+  const RenderParams& Pc = fresh_params(P0);
+  if (Pc.counters && q[0].lane == 0) {
+    unsigned long long* c = counter_row(Pc, sel0);
+    atomicAdd(&c[kCntShadow], nhit * (unsigned long long)Pc.num_lights);
 #ifdef RT_DIAG
     atomicAdd(&c[kCntShadNodes], dg.nodes);
     atomicAdd(&c[kCntShadNodeLanes], dg.node_lanes);
@@ -1527,9 +1546,10 @@ __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY vo
   constexpr int W = trace_waves<DEEP>();
   int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * (1 + 2 * R) * kDeepStack : nullptr;
   for_each_packet<W, R>(P, [&](int p) {
-    const int sel0 = R == 1 ? packet_sel<W>(P, p) : p * R;
-    if (sel0 >= 0 && sel0 < P.num_sel_tiles)
-      primary_packet<FAST, DEEP, SPHERES, R>(P, nodes, prims, sel0, spill);
+    const RenderParams& Q = fresh_params(P);
+    const int sel0 = R == 1 ? packet_sel<W>(Q, p) : p * R;
+    if (sel0 >= 0 && sel0 < Q.num_sel_tiles)
+      primary_packet<FAST, DEEP, SPHERES, R>(Q, nodes, prims, sel0, spill);
   });
 }
 
@@ -1541,9 +1561,10 @@ __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY vo
   constexpr int W = trace_waves<DEEP>();
   int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * (1 + 2 * R) * kDeepStack : nullptr;
   for_each_packet<W, R>(P, [&](int p) {
-    const int sel0 = R == 1 ? packet_sel<W>(P, p) : p * R;
-    if (sel0 >= 0 && sel0 < P.num_sel_tiles)
-      shadow_packet<FAST, DEEP, SPHERES, R>(P, nodes, prims, lights, sel0, spill);
+    const RenderParams& Q = fresh_params(P);
+    const int sel0 = R == 1 ? packet_sel<W>(Q, p) : p * R;
+    if (sel0 >= 0 && sel0 < Q.num_sel_tiles)
+      shadow_packet<FAST, DEEP, SPHERES, R>(Q, nodes, prims, lights, sel0, spill);
   });
 }
 
