@@ -1000,6 +1000,12 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
     q[k] = packet_pixel(P, sel0 + k);
     valid[k] = q[k].valid && sel0 + k < P.num_sel_tiles;
     ray[k] = make_ray(ld3(P.cam_e), primary_dir(P, q[k].px, q[k].py), P.quot_ok);
+#ifndef RT_EXP_UNIFORM_ORIGIN
+    // The camera origin is wave-uniform; left to itself the compiler keeps it in 3 SGPRs and
+    // copies it to VGPRs at every node visit (a VALU op takes one SGPR operand, the box
+    // coordinate already is one).  Pin it to VGPRs once.
+    asm volatile("" : "+v"(ray[k].o.x), "+v"(ray[k].o.y), "+v"(ray[k].o.z));
+#endif
     any_skip |= valid[k] && (ray[k].skip0 || ray[k].skip1 || ray[k].skip2);
   }
   Diag dg;
