@@ -1055,24 +1055,6 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
                                               const DevPrim* __restrict__ prims,
                                               const DevLight* __restrict__ lights, int sel0,
                                               int* spill) {
-  PacketPixel q[R];
-  bool hit[R];
-  V3 p[R];
-  size_t pix[R];
-  unsigned long long nhit = 0;
-#pragma unroll
-  for (int k = 0; k < R; k++) {
-    q[k] = packet_pixel(P0, sel0 + k);
-    const bool inside = sel0 + k < P0.num_sel_tiles;
-    pix[k] = (size_t)(sel0 + k) * (kTile * kTile) + q[k].lane;
-    int2_t rec;
-    rec.x = 0;
-    rec.y = -2;
-    if (inside) rec = P0.hits[pix[k]];
-    hit[k] = rec.y >= 0;
-    p[k] = hit[k] ? hit_point(P0, q[k], __int_as_float(rec.x)) : v3(0, 0, 0);
-    nhit += __builtin_popcountll(ballot(hit[k]));
-  }
   Diag dg;
   for (int w = 0; w < P0.occ_words; w++) {
     unsigned bits[R];
@@ -1080,17 +1062,28 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
     for (int k = 0; k < R; k++) bits[k] = 0;
     const int lend = min(P0.num_lights, 32 * (w + 1));
     for (int li = 32 * w; li < lend; li++) {
-      const RenderParams& P = fresh_params(P0);  // per light: nothing live across traversals
+      // per light: the pixel's hit record is re-read and its hit point rebuilt, so nothing but
+      // the occlusion bits is live across the traversal (register pressure, not traffic: the
+      // 8-B record is an L2 hit)
+      const RenderParams& P = fresh_params(P0);
       const DevLight& L = lights[li];
       LaneRay sr[R];
       float thr[R];
+      bool hit[R];
       bool any_skip = false;
 #pragma unroll
       for (int k = 0; k < R; k++) {
-        const V3 ld = ld3(L.position) - p[k];
+        const PacketPixel q = packet_pixel(P, sel0 + k);
+        int2_t rec;
+        rec.x = 0;
+        rec.y = -2;
+        if (sel0 + k < P.num_sel_tiles) rec = P.hits[(size_t)(sel0 + k) * (kTile * kTile) + q.lane];
+        hit[k] = rec.y >= 0;
+        const V3 pk = hit[k] ? hit_point(P, q, __int_as_float(rec.x)) : v3(0, 0, 0);
+        const V3 ld = ld3(L.position) - pk;
         const V3 wi = normalize(ld);
         const float dist = length(ld);
-        sr[k] = make_ray(p[k] + wi * P.eps, wi, P.quot_ok);  // p + eps * w_i
+        sr[k] = make_ray(pk + wi * P.eps, wi, P.quot_ok);  // p + eps * w_i
         thr[k] = dist - P.eps;
         any_skip |= hit[k] && (sr[k].skip0 || sr[k].skip1 || sr[k].skip2);
       }
@@ -1105,10 +1098,18 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
     const RenderParams& Pw = fresh_params(P0);
 #pragma unroll
     for (int k = 0; k < R; k++)
-      if (sel0 + k < Pw.num_sel_tiles) Pw.occ[pix[k] * Pw.occ_words + w] = bits[k];
+      if (sel0 + k < Pw.num_sel_tiles)
+        Pw.occ[((size_t)(sel0 + k) * (kTile * kTile) + lane_id()) * Pw.occ_words + w] = bits[k];
   }
   const RenderParams& Pc = fresh_params(P0);
-  if (Pc.counters && q[0].lane == 0) {
+  unsigned long long nhit = 0;
+#pragma unroll
+  for (int k = 0; k < R; k++) {
+    const bool inside = sel0 + k < Pc.num_sel_tiles;
+    nhit += __builtin_popcountll(
+        ballot(inside && Pc.hits[(size_t)(sel0 + k) * (kTile * kTile) + lane_id()].y >= 0));
+  }
+  if (Pc.counters && lane_id() == 0) {
     unsigned long long* c = counter_row(Pc, sel0);
     atomicAdd(&c[kCntShadow], nhit * (unsigned long long)Pc.num_lights);
 #ifdef RT_DIAG
