@@ -787,18 +787,20 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
   constexpr int kPer = kWinMax / kUpdThreads;
   constexpr int kWords = kWinMax / 32;
   constexpr int kChunk = 1024;  // candidates per color / apply round
+  static_assert(kWinMax <= 1024, "s_ck packs the window index in 10 bits");
+  static_assert(kTileHP * kWords <= kUpdThreads, "one thread per mask word in the scan");
   __shared__ float s_hp[kTileHP][12];  // pos, normal, w_o, attenuation
   __shared__ int s_mat[kTileHP];
   __shared__ float s_r2[kTileHP];
   __shared__ unsigned s_cnt[kTileHP];
   __shared__ unsigned s_mask[kTileHP][kWords];
   __shared__ int s_wc[kTileHP * kWords + 1];
-  __shared__ unsigned short s_ck[kTileHP * kWinMax];
+  __shared__ int s_wtot[kUpdThreads / 64];
+  __shared__ unsigned short s_ck[kTileHP * kWinMax];  // window index | multiplicity << 10
   __shared__ float s_cd2[kTileHP * kWinMax];
   __shared__ float s_ccf[kChunk][3];
   constexpr int kRRStage = 64;  // rr(n) staged per hit point per window (more: computed inline)
   __shared__ float s_rr[kTileHP][kRRStage];
-  __shared__ unsigned char s_rep[kWinMax];
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const unsigned long long t_start = S.diag == 2 ? wall_clock64() : 0;
   const int2 tile = tiles[blockIdx.x];
@@ -864,12 +866,13 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
     for (int j = 0; j < kTileHP; j++) r2w[j] = s_r2[j];
     float d2r[kPer][kTileHP];
     bool cr[kPer][kTileHP];
+    unsigned rp[kPer];  // multiplicities, kept past the next window's fetch
 #pragma unroll
     for (int q = 0; q < kPer; q++) {
       const int k = tid + q * kUpdThreads;  // a wave covers 64 consecutive deposits
       const bool live = k < total;
       const V x = ld(dep[q].x), dn = ld(dep[q].normal);
-      if (live) s_rep[k] = drep[q];
+      rp[q] = drep[q];
 #pragma unroll
       for (int j = 0; j < kTileHP; j++) {
         const V v = tp[j] - x;
@@ -885,25 +888,23 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
     fetch(base + kWinMax);  // next window in flight
     __syncthreads();
     PPM_PHASE(0)
-    // (2) candidates per hit point, in photon order
-    for (int e = tid; e < nh * nwords; e += kUpdThreads)
-      s_wc[e] = __builtin_popcount(s_mask[e / nwords][e % nwords]);
-    __syncthreads();
-    PPM_PHASE(1)
-    if (tid < 64) {  // exclusive scan of the word counts (one wave)
+    // (2) candidates per hit point, in photon order: exclusive scan of the per-word counts,
+    // one word per thread (wave scans, then the wave totals)
+    {
       const int n = nh * nwords;
-      int carry = 0;
-      for (int c0 = 0; c0 < n; c0 += 64) {
-        const int v = c0 + lane < n ? s_wc[c0 + lane] : 0;
-        int x = v;
-        for (int o = 1; o < 64; o <<= 1) {
-          const int y = __shfl_up(x, o, 64);
-          if (lane >= o) x += y;
-        }
-        if (c0 + lane < n) s_wc[c0 + lane] = carry + x - v;
-        carry += __shfl(x, 63, 64);
+      const int v = tid < n ? __builtin_popcount(s_mask[tid / nwords][tid % nwords]) : 0;
+      int x = v;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
       }
-      if (lane == 0) s_wc[n] = carry;
+      if (lane == 63) s_wtot[tid >> 6] = x;
+      __syncthreads();
+      PPM_PHASE(1)
+      int off = 0;
+      for (int w = 0; w < (tid >> 6); w++) off += s_wtot[w];
+      if (tid < n) s_wc[tid] = off + x - v;
+      if (tid == n - 1) s_wc[n] = off + x;
     }
     __syncthreads();
     PPM_PHASE(2)
@@ -915,7 +916,7 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
         if (!cr[q][j]) continue;
         const int w = k >> 5;
         const int idx = s_wc[j * nwords + w] + __builtin_popcount(s_mask[j][w] & ((1u << (k & 31)) - 1u));
-        s_ck[idx] = (unsigned short)k;
+        s_ck[idx] = (unsigned short)(k | (rp[q] << 10));
         s_cd2[idx] = d2r[q][j];
       }
     }
@@ -930,7 +931,7 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
       for (int e = c0 + tid; e < min(ncand, c0 + kChunk); e += kUpdThreads) {
         int j = 0;
         while (j + 1 < nh && s_wc[(j + 1) * nwords] <= e) j++;
-        const PDeposit d = rec[base + s_ck[e]];
+        const PDeposit d = rec[base + (s_ck[e] & 1023u)];
         const V hn = tn[j], w_i = ld(d.w_i), pf = ld(d.flux);
         const PMaterial& m = S.materials[s_mat[j]];
         V color = mk(0.0f, 0.0f, 0.0f);
@@ -953,7 +954,7 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
         const int e1 = min(my_end, c0 + kChunk);
         for (int e = max(my_beg, c0); e < e1; e++) {
           const float d2 = s_cd2[e];
-          const int reps = s_rep[s_ck[e]];
+          const int reps = (int)(s_ck[e] >> 10);
           for (int r = 0; r < reps; r++) {
             if (!(d2 <= r2)) break;
             const float rr = t_rr < kRRStage ? s_rr[tid][t_rr] : radius_reduction(cnt);
