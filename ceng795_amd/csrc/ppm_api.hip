@@ -658,9 +658,10 @@ int ppm_collect_stats(ppm_scene* s, ppm_stats* st) {
     st->hit_points = s->n_hp;
     if (s->S.diag == 2) std::fprintf(stderr, "ppm diag: windows %llu deposit-visits %llu tiles %d groups %d "
                                      "longest tile %llu ticks phases(max) stage+filter %llu "
-                                     "counts %llu scan %llu scatter %llu color %llu gate %llu\n",
+                                     "counts %llu scan %llu scatter %llu color %llu gate %llu max-window-updates %llu "
+                                     "unstaged-rr %llu\n",
                                      c[5], c[6], s->n_tiles, s->n_groups, c[7], c[8], c[9],
-                                     c[10], c[11], c[12], c[13]);
+                                     c[10], c[11], c[12], c[13], c[14], c[15]);
     s->photons = 0;
     return RT_OK;
   });

@@ -949,27 +949,37 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
       }
       __syncthreads();
       PPM_PHASE(4)
-      // (4) the exact recurrence, in photon order
+      // (4) the exact recurrence, in photon order: a candidate is applied up to its
+      // multiplicity times while it stays inside the shrinking radius (the update count is
+      // derived from cnt afterwards, so the loop carries no counter of its own)
       if (h >= 0 && S.diag != 1) {
         const int e1 = min(my_end, c0 + kChunk);
         for (int e = max(my_beg, c0); e < e1; e++) {
           const float d2 = s_cd2[e];
-          const int reps = (int)(s_ck[e] >> 10);
-          for (int r = 0; r < reps; r++) {
-            if (!(d2 <= r2)) break;
+          if (!(d2 <= r2)) continue;
+          const unsigned reps = s_ck[e] >> 10;
+          const V cf = mk(s_ccf[e - c0][0], s_ccf[e - c0][1], s_ccf[e - c0][2]);
+          unsigned r = 0;
+          do {
             const float rr = t_rr < kRRStage ? s_rr[tid][t_rr] : radius_reduction(cnt);
             t_rr++;
-            r2 = r2 * rr;
             cnt++;
-            applied++;
-            flux = (flux + mk(s_ccf[e - c0][0], s_ccf[e - c0][1], s_ccf[e - c0][2])) * rr;
-          }
+            r2 = r2 * rr;
+            flux = (flux + cf) * rr;
+          } while (++r < reps && d2 <= r2);
         }
       }
       __syncthreads();
       PPM_PHASE(5)
     }
-    if (h >= 0) s_r2[tid] = r2, s_cnt[tid] = cnt;
+    if (h >= 0) {
+      if (stats && S.diag == 2) {  // experiment counters: most updates in one window, unstaged rr(n)
+        atomicMax(&stats[14], (unsigned long long)t_rr);
+        if (t_rr > kRRStage) atomicAdd(&stats[15], (unsigned long long)(t_rr - kRRStage));
+      }
+      applied += cnt - s_cnt[tid];
+      s_r2[tid] = r2, s_cnt[tid] = cnt;
+    }
     __syncthreads();
     PPM_PHASE(5)
   }
