@@ -103,6 +103,28 @@ def cpu_baseline(xml: str, threads: int):
                       f"{sec:.3f} s each), render region only as HW2/main.cpp:26-41"}
 
 
+def stream_copy_gbps(device) -> float:
+    """Measured device-to-device copy bandwidth (read + write bytes / time) on this GPU: the
+    attainable-HBM reference SURVEY.md §8(d) asks for beside the 8 TB/s spec peak."""
+    import torch
+    n = 1 << 29  # 2 GiB of fp32 per buffer, far beyond the 256 MB Infinity Cache
+    x = torch.empty(n, dtype=torch.float32, device=device).fill_(1.0)
+    y = torch.empty_like(x)
+    for _ in range(2):
+        y.copy_(x)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    reps = 10
+    for _ in range(reps):
+        y.copy_(x)
+    b.record()
+    torch.cuda.synchronize()
+    gbps = 2 * 4 * n * reps / (a.elapsed_time(b) * 1e-3) / 1e9
+    del x, y
+    torch.cuda.empty_cache()
+    return gbps
+
+
 def pmc_traffic(workload: str):
     """HBM bytes per render launch from a committed rocprofv3 --pmc pass (profiles/), corrected
     as MI355X_MICROARCH.md §HBM prescribes; None when no such profile exists."""
@@ -230,11 +252,13 @@ def main() -> int:
             per_launch = bytes_frame * (rays_local / (ostats["primary_rays"] + ostats["shadow_rays"]))
             achieved = per_launch / (kernel_ms_avg * 1e-3) / 1e9
             traffic = pmc_traffic(args.workload) if world == 1 else None
+            copy_gbps = stream_copy_gbps(device)
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                     "traffic": traffic,
                     "algorithmic_bytes_per_launch": int(per_launch),
                     "kernel_ms_avg": round(kernel_ms_avg, 4),
+                    "stream_copy_GBps_measured": round(copy_gbps, 1),
                     "ref_order_visits_per_ray": {
                         "primary_box": round(ostats["box_tests"][0] / ostats["primary_rays"], 2),
                         "primary_tri": round(ostats["prim_tests"][0] / ostats["primary_rays"], 2),
