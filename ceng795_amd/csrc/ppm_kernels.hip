@@ -41,6 +41,8 @@ constexpr float kTestEps = 0.0001f;  // intersection_test_epsilon (PPM/include/V
 constexpr float kInf = __builtin_huge_valf();
 constexpr float kAlpha = 0.7f;       // ALPHA (Scene.cpp:13)
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 struct V {
   float x, y, z;
 };
@@ -798,7 +800,7 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
   __shared__ int s_wtot[kUpdThreads / 64];
   __shared__ unsigned short s_ck[kTileHP * kWinMax];  // window index | multiplicity << 10
   __shared__ float s_cd2[kTileHP * kWinMax];
-  __shared__ float s_ccf[kChunk][3];
+  __shared__ float4 s_ccf[kChunk];  // color * photon_flux, w = 0 (see the gate)
   constexpr int kRRStage = 64;  // rr(n) staged per hit point per window (more: computed inline)
   __shared__ float s_rr[kTileHP][kRRStage];
   const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -925,7 +927,7 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
     const int ncand = s_wc[nh * nwords];
     const int my_beg = h >= 0 ? s_wc[tid * nwords] : 0;
     const int my_end = h >= 0 ? (tid + 1 < nh ? s_wc[(tid + 1) * nwords] : ncand) : 0;
-    int t_rr = 0;  // updates made by this hit point in this window
+    const unsigned cnt_w = cnt;  // count at the window start: rr(n) is staged from there
     for (int c0 = 0; c0 < ncand; c0 += kChunk) {
       // (3) color * photon_flux for candidates [c0, c0 + kChunk)
       for (int e = c0 + tid; e < min(ncand, c0 + kChunk); e += kUpdThreads) {
@@ -945,35 +947,85 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
           }
         }
         const V cf = color * pf;
-        s_ccf[e - c0][0] = cf.x, s_ccf[e - c0][1] = cf.y, s_ccf[e - c0][2] = cf.z;
+        s_ccf[e - c0] = make_float4(cf.x, cf.y, cf.z, 0.0f);
       }
       __syncthreads();
       PPM_PHASE(4)
       // (4) the exact recurrence, in photon order: a candidate is applied up to its
       // multiplicity times while it stays inside the shrinking radius (the update count is
       // derived from cnt afterwards, so the loop carries no counter of its own)
+      // Packed fp32: (flux.x, flux.y) and (flux.z, r^2) are updated by v_pk_add/v_pk_mul
+      // pairs, each element rounded as its scalar op; r^2 + 0 = r^2 exactly (r^2 > 0).
+      // Candidates go in batches of kB: all their LDS operands are loaded up front, and the
+      // batch is applied branch-free on the assumption that each candidate is accepted, so
+      // candidate k uses the staged rr(n) k places on.  The first rejected candidate ends the
+      // batch (it changes nothing; the ones after it are redone with the right rr).  A batch
+      // holding a multiplicity > 1, or reaching past the staged rr(n), takes the scalar path
+      // for its first candidate.
       if (h >= 0 && S.diag != 1) {
+        constexpr int kB = 8;
         const int e1 = min(my_end, c0 + kChunk);
-        for (int e = max(my_beg, c0); e < e1; e++) {
-          const float d2 = s_cd2[e];
-          if (!(d2 <= r2)) continue;
-          const unsigned reps = s_ck[e] >> 10;
-          const V cf = mk(s_ccf[e - c0][0], s_ccf[e - c0][1], s_ccf[e - c0][2]);
-          unsigned r = 0;
-          do {
-            const float rr = t_rr < kRRStage ? s_rr[tid][t_rr] : radius_reduction(cnt);
-            t_rr++;
-            cnt++;
-            r2 = r2 * rr;
-            flux = (flux + cf) * rr;
-          } while (++r < reps && d2 <= r2);
+        f32x2 fxy = {flux.x, flux.y}, fzr = {flux.z, r2};
+        int e = max(my_beg, c0);
+        while (e < e1) {
+          const int nb = min(kB, e1 - e);
+          const unsigned t = cnt - cnt_w;
+          bool fast = t + kB <= (unsigned)kRRStage;
+          float d2b[kB], rrb[kB];
+          float4 cb[kB];
+#pragma unroll
+          for (int k = 0; k < kB; k++) {
+            const int ek = min(e + k, e1 - 1);
+            d2b[k] = k < nb ? s_cd2[ek] : kInf;
+            fast = fast & ((s_ck[ek] >> 10) <= 1u);
+            cb[k] = s_ccf[ek - c0];
+            rrb[k] = s_rr[tid][min(t + (unsigned)k, (unsigned)kRRStage - 1)];
+          }
+          if (fast) {
+            bool alive = true;
+            int used = 0;
+#pragma unroll
+            for (int k = 0; k < kB; k++) {
+              const bool acc = alive && d2b[k] <= fzr.y;
+              const f32x2 rr2 = {rrb[k], rrb[k]};
+              const f32x2 cxy = {cb[k].x, cb[k].y}, cz0 = {cb[k].z, cb[k].w};
+              const f32x2 nxy = (fxy + cxy) * rr2, nzr = (fzr + cz0) * rr2;
+              fxy.x = acc ? nxy.x : fxy.x;
+              fxy.y = acc ? nxy.y : fxy.y;
+              fzr.x = acc ? nzr.x : fzr.x;
+              fzr.y = acc ? nzr.y : fzr.y;
+              used += alive ? 1 : 0;  // consumed: accepted, or the first reject
+              cnt += acc ? 1u : 0u;
+              alive = acc;
+            }
+            e += min(used, nb);
+          } else {
+            const float d2 = d2b[0];
+            if (d2 <= fzr.y) {
+              const unsigned reps = s_ck[e] >> 10;
+              const f32x2 cxy = {cb[0].x, cb[0].y}, cz0 = {cb[0].z, cb[0].w};
+              unsigned r = 0;
+              do {
+                const unsigned tt = cnt - cnt_w;
+                const float rr = tt < (unsigned)kRRStage ? s_rr[tid][tt] : radius_reduction(cnt);
+                cnt++;
+                const f32x2 rr2 = {rr, rr};
+                fxy = (fxy + cxy) * rr2;
+                fzr = (fzr + cz0) * rr2;
+              } while (++r < reps && d2 <= fzr.y);
+            }
+            e++;
+          }
         }
+        flux = mk(fxy.x, fxy.y, fzr.x);
+        r2 = fzr.y;
       }
       __syncthreads();
       PPM_PHASE(5)
     }
     if (h >= 0) {
       if (stats && S.diag == 2) {  // experiment counters: most updates in one window, unstaged rr(n)
+        const unsigned t_rr = cnt - cnt_w;  // updates made by this hit point in this window
         atomicMax(&stats[14], (unsigned long long)t_rr);
         if (t_rr > kRRStage) atomicAdd(&stats[15], (unsigned long long)(t_rr - kRRStage));
       }
