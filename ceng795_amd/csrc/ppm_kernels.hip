@@ -645,6 +645,12 @@ __global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, con
 #ifndef PPM_WIN
 #define PPM_WIN 1024
 #endif
+#ifndef PPM_GATE_B
+#define PPM_GATE_B 2
+#endif
+#ifndef PPM_RR_STAGE
+#define PPM_RR_STAGE 64
+#endif
 #ifndef PPM_THREADS
 #define PPM_THREADS 512
 #endif
@@ -781,7 +787,7 @@ __global__ __launch_bounds__(256) void materialize_kernel(const unsigned* pkey, 
 //      the running value, r^2 *= rr(n), n++, flux = (flux + color * photon_flux) * rr(n) —
 //      repeated when two of its cells share the deposit's bucket.
 // The next window is fetched (coalesced) while the current one is processed.
-__global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
+__global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void group_update_kernel(
     PScene S, const PHitPoint* hps, const int* perm, const int* gstart, const int2* tiles,
     const int* list_start, const int* list_end, const PDeposit* rec,
     const unsigned char* rep, const float* rrtab, int nrr, float4* state, unsigned* nupd,
@@ -801,7 +807,7 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
   __shared__ unsigned short s_ck[kTileHP * kWinMax];  // window index | multiplicity << 10
   __shared__ float s_cd2[kTileHP * kWinMax];
   __shared__ float4 s_ccf[kChunk];  // color * photon_flux, w = 0 (see the gate)
-  constexpr int kRRStage = 64;  // rr(n) staged per hit point per window (more: computed inline)
+  constexpr int kRRStage = PPM_RR_STAGE;  // rr(n) staged per hit point per window (more: computed inline)
   __shared__ float s_rr[kTileHP][kRRStage];
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const unsigned long long t_start = S.diag == 2 ? wall_clock64() : 0;
@@ -963,7 +969,7 @@ __global__ __launch_bounds__(kUpdThreads) void group_update_kernel(
       // holding a multiplicity > 1, or reaching past the staged rr(n), takes the scalar path
       // for its first candidate.
       if (h >= 0 && S.diag != 1) {
-        constexpr int kB = 8;
+        constexpr int kB = PPM_GATE_B;
         const int e1 = min(my_end, c0 + kChunk);
         f32x2 fxy = {flux.x, flux.y}, fzr = {flux.z, r2};
         int e = max(my_beg, c0);
