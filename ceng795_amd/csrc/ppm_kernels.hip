@@ -651,6 +651,12 @@ __global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, con
 #ifndef PPM_RR_STAGE
 #define PPM_RR_STAGE 64
 #endif
+#ifndef PPM_CHUNK
+#define PPM_CHUNK 1024
+#endif
+#ifndef PPM_WPE
+#define PPM_WPE 4
+#endif
 #ifndef PPM_THREADS
 #define PPM_THREADS 512
 #endif
@@ -787,14 +793,14 @@ __global__ __launch_bounds__(256) void materialize_kernel(const unsigned* pkey, 
 //      the running value, r^2 *= rr(n), n++, flux = (flux + color * photon_flux) * rr(n) —
 //      repeated when two of its cells share the deposit's bucket.
 // The next window is fetched (coalesced) while the current one is processed.
-__global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void group_update_kernel(
+__global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM_WPE, PPM_WPE))) void group_update_kernel(
     PScene S, const PHitPoint* hps, const int* perm, const int* gstart, const int2* tiles,
     const int* list_start, const int* list_end, const PDeposit* rec,
     const unsigned char* rep, const float* rrtab, int nrr, float4* state, unsigned* nupd,
     unsigned long long* stats) {
   constexpr int kPer = kWinMax / kUpdThreads;
   constexpr int kWords = kWinMax / 32;
-  constexpr int kChunk = 1024;  // candidates per color / apply round
+  constexpr int kChunk = PPM_CHUNK;  // candidates per color / apply round
   static_assert(kWinMax <= 1024, "s_ck packs the window index in 10 bits");
   static_assert(kTileHP * kWords <= kUpdThreads, "one thread per mask word in the scan");
   __shared__ float s_hp[kTileHP][12];  // pos, normal, w_o, attenuation

@@ -1,5 +1,5 @@
 set -o pipefail
-O=gpurun_out/s4_final; mkdir -p $O
+O=${1:-gpurun_out/s5_final}; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -20 $O/gpu_tests.log; exit 1; }
 tail -1 $O/gpu_tests.log
