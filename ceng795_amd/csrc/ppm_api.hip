@@ -40,6 +40,7 @@ hipError_t launch_group_flags(const unsigned long long*, int, int*, hipStream_t)
 hipError_t launch_group_starts(const int*, const int*, int, int*, hipStream_t);
 hipError_t launch_group_tiles(const int*, int, int*, hipStream_t);
 hipError_t launch_tile_table(const int*, const int*, int, int2*, hipStream_t);
+hipError_t launch_tile_work(const int2*, int, const int*, const int*, unsigned*, hipStream_t);
 hipError_t launch_rr_table(float*, int, hipStream_t);
 hipError_t launch_materialize(const unsigned*, const unsigned*, int, const PDeposit*,
                               const unsigned*, const unsigned*, const int*, const int*, PDeposit*,
@@ -156,7 +157,8 @@ struct ppm_scene {
   DevBuf<int> bstart, bend;
   DevBuf<unsigned long long> gkeys, gkeys2;  // hit-point groups (same hash-cell range)
   DevBuf<int> gidx, perm, gflags, gid, gstart, ntile, tile_off;
-  DevBuf<int2> tiles;
+  DevBuf<int2> tiles, tiles_lpt;  // tile table; per batch, heaviest first
+  DevBuf<unsigned> tkey, tkey2;
   int n_groups = 0, n_tiles = 0;
   // photon batches
   DevBuf<PDeposit> slots;
@@ -184,6 +186,7 @@ struct ppm_scene {
     grid.release(), bstart.release(), bend.release(), slots.release(), ndep.release();
     gkeys.release(), gkeys2.release(), gidx.release(), perm.release(), gflags.release();
     gid.release(), gstart.release(), ntile.release(), tile_off.release(), tiles.release();
+    tiles_lpt.release(), tkey.release(), tkey2.release();
     dep_off.release(), dbucket.release(), dense.release(), pcount.release(), poff.release();
     list_start.release(), list_end.release(), pkey.release(), pval.release(), pkey2.release();
     pval2.release(), gb.release(), gm.release(), gnb.release(), goff.release();
@@ -196,6 +199,16 @@ struct ppm_scene {
 };
 
 namespace {
+
+// Longest-first update order (tile_work_kernel); CENG795_PPM_LPT=0 keeps the group order for
+// A/B timing.  The order cannot change results: tiles own disjoint hit points.
+bool lpt_order() {
+  static const bool on = [] {
+    const char* e = std::getenv("CENG795_PPM_LPT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 template <typename T>
 const T* own(ppm_scene* s, const std::vector<T>& v, const char* what) {
@@ -308,7 +321,7 @@ void build_grid(ppm_scene* s, int width, int height) {
     hip_check(hipStreamSynchronize(s->stream), "group hit points");
     if (err) throw std::domain_error("a hit point's radius box spans more hash cells than supported");
     s->n_groups = groups;
-    // tiles of <= 8 hit points per group (group_update_kernel)
+    // tiles of <= kTileHP (4) hit points per group (group_update_kernel)
     s->ntile.reserve(groups + 1, "alloc tile counts");
     s->tile_off.reserve(groups + 1, "alloc tile offsets");
     hip_check(launch_group_tiles(s->gstart.p, groups, s->ntile.p, s->stream), "group tiles");
@@ -444,7 +457,24 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
           hip_check(launch_materialize(s->pkey2.p, s->pval2.p, P, s->dense.p, s->dbucket.p, s->gb.p,
                                        s->gm.p, s->gnb.p, s->grec.p, s->grep.p, s->stream),
                     "materialise group lists");
-          hip_check(launch_group_update(s->S, s->hp.p, s->perm.p, s->gstart.p, s->tiles.p,
+          const int2* tiles = s->tiles.p;
+          if (lpt_order()) {
+            s->tkey.reserve(s->n_tiles, "alloc tile keys");
+            s->tkey2.reserve(s->n_tiles, "alloc tile keys");
+            s->tiles_lpt.reserve(s->n_tiles, "alloc tile order");
+            hip_check(launch_tile_work(s->tiles.p, s->n_tiles, s->list_start.p, s->list_end.p,
+                                       s->tkey.p, s->stream), "tile work");
+            bytes = 0;
+            hip_check(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, s->tkey.p, s->tkey2.p,
+                                                         s->tiles.p, s->tiles_lpt.p, s->n_tiles,
+                                                         0, 32, s->stream), "sort size");
+            s->temp.reserve(bytes, "alloc sort temp");
+            hip_check(hipcub::DeviceRadixSort::SortPairs(s->temp.p, bytes, s->tkey.p, s->tkey2.p,
+                                                         s->tiles.p, s->tiles_lpt.p, s->n_tiles,
+                                                         0, 32, s->stream), "sort tiles");
+            tiles = s->tiles_lpt.p;
+          }
+          hip_check(launch_group_update(s->S, s->hp.p, s->perm.p, s->gstart.p, tiles,
                                         s->n_tiles, s->list_start.p, s->list_end.p, s->grec.p,
                                         s->grep.p, s->rrtab.p, kRRTable, s->state.p, s->nupd.p,
                                         s->stats.p, s->stream),

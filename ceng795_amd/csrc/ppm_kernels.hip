@@ -748,6 +748,18 @@ __global__ __launch_bounds__(256) void tile_table_kernel(const int* gstart, cons
 }
 
 
+// Longest-first launch order for the update pass: a tile's work is its group's deposit-list
+// length in this batch; the complemented length sorts the heaviest tiles to the front, so the
+// hot groups' serial chains start in the first dispatch round instead of the last.
+__global__ __launch_bounds__(256) void tile_work_kernel(const int2* tiles, int ntiles,
+                                                        const int* list_start,
+                                                        const int* list_end, unsigned* key) {
+  const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (t >= ntiles) return;
+  const int g = tiles[t].x;
+  key[t] = ~(unsigned)(list_end[g] - list_start[g]);
+}
+
 // rr(n) of Scene.cpp:139-140, the radius reduction of a hit point's (n+1)-th update:
 // (n*ALPHA + ALPHA) / (n*ALPHA + 1.0), a double division rounded to float.  It depends on n
 // only, so it is tabulated once (rr_table_kernel) and staged in LDS per window.
@@ -1171,6 +1183,12 @@ hipError_t launch_tile_table(const int* gstart, const int* tile_off, int groups,
                              hipStream_t st) {
   hipLaunchKernelGGL(tile_table_kernel, dim3(blocks_for(groups)), dim3(kThreads), 0, st, gstart,
                      tile_off, groups, tiles);
+  return hipGetLastError();
+}
+hipError_t launch_tile_work(const int2* tiles, int ntiles, const int* list_start,
+                           const int* list_end, unsigned* key, hipStream_t st) {
+  hipLaunchKernelGGL(tile_work_kernel, dim3(blocks_for(ntiles)), dim3(kThreads), 0, st, tiles,
+                     ntiles, list_start, list_end, key);
   return hipGetLastError();
 }
 hipError_t launch_rr_table(float* rr, int n, hipStream_t st) {
