@@ -321,7 +321,7 @@ void build_grid(ppm_scene* s, int width, int height) {
     hip_check(hipStreamSynchronize(s->stream), "group hit points");
     if (err) throw std::domain_error("a hit point's radius box spans more hash cells than supported");
     s->n_groups = groups;
-    // tiles of <= kTileHP (4) hit points per group (group_update_kernel)
+    // tiles of <= kTileHP (3) hit points per group (group_update_kernel)
     s->ntile.reserve(groups + 1, "alloc tile counts");
     s->tile_off.reserve(groups + 1, "alloc tile offsets");
     hip_check(launch_group_tiles(s->gstart.p, groups, s->ntile.p, s->stream), "group tiles");

@@ -640,7 +640,7 @@ __global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, con
 }
 
 #ifndef PPM_TILE
-#define PPM_TILE 4
+#define PPM_TILE 3
 #endif
 #ifndef PPM_WIN
 #define PPM_WIN 1024
