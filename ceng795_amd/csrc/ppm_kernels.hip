@@ -646,7 +646,7 @@ __global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, con
 #define PPM_WIN 1024
 #endif
 #ifndef PPM_GATE_B
-#define PPM_GATE_B 2
+#define PPM_GATE_B 3
 #endif
 #ifndef PPM_RR_STAGE
 #define PPM_RR_STAGE 64
