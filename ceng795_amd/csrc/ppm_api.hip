@@ -131,10 +131,18 @@ struct DeviceGuard {
   }
 };
 
-// Deposit slot rows per photon batch: 8 GiB holds C5's 1e7 photons x 19 slots in one batch
-// (one sort, one update launch); HBM is 288 GB.
+// Deposit slot rows per photon batch: 16 GiB holds C5's 1e7 photons x 19 slots x 48 B
+// (9.1 GB) in one batch (one sort, one update launch); HBM is 288 GB.  CENG795_PPM_SLOT_MB
+// overrides it for A/B timing and to exercise the multi-batch path.
 constexpr int kRRTable = 1 << 20;  // rr(n) tabulated for n < 2^20 (larger n computed inline)
-constexpr size_t kSlotBytesPerBatch = size_t(8) << 30;
+size_t slot_bytes_per_batch() {
+  static const size_t v = [] {
+    const char* e = std::getenv("CENG795_PPM_SLOT_MB");
+    const long long mb = e ? std::atoll(e) : 0;
+    return mb > 0 ? size_t(mb) << 20 : size_t(16) << 30;
+  }();
+  return v;
+}
 
 }  // namespace
 
@@ -387,7 +395,7 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
   if (count < 0 || first < 0) throw std::invalid_argument("bad photon range");
   if (!s->grid_ready) throw std::invalid_argument("trace_photons before build_hash_grid");
   const int K = std::max(1, s->host.max_depth - 1);
-  const long long batch_max = std::max<long long>(1, (long long)(kSlotBytesPerBatch / (sizeof(PDeposit) * K)));
+  const long long batch_max = std::max<long long>(1, (long long)(slot_bytes_per_batch() / (sizeof(PDeposit) * K)));
   const int H = s->n_hp;
   for (long long done = 0; done < count;) {
     const int b = (int)std::min(count - done, batch_max);
