@@ -1,17 +1,21 @@
 #!/usr/bin/env python3
 """Headline benchmark: Mrays/s of HW2's render path (primary + shadow rays) at 1920x1080 on
-the ~1M-triangle height field (BASELINE.json configs[2], "C3"), plus the HBM-roofline fraction
-of the render kernel and the reference CPU path timed on this box's host cores.
+the ~1M-triangle height field (BASELINE.json configs[2], "C3"), plus the roofline of the
+dominant kernel and the reference CPU path timed on this box's host cores.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python bench.py --workload c5        (photon mapping, tools/bench_ppm.py)
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+    ... bench.py --workload c4 --frames 1  (one 3840x2160 frame split over the N ranks)
 
-One step = one full render of every camera in the job: N frames of 1920x1080 for N ranks.
-The 8x8-pixel tiles of all frames are dealt round-robin over the ranks (the reference deals
-rows round-robin over threads, HW2/main.cpp:33-36), each rank renders its tiles into HBM, and
-rank 0 gathers them over RCCL (torch.distributed "nccl" = RCCL over xGMI) and untiles the
-framebuffers.  Per-GPU work is fixed as N grows: "scaling": "weak".  At N = 1 the step is
+One step = one full render of every camera in the job.  By default the job has one 1920x1080
+frame per rank (N frames for N ranks, "scaling": "weak"); `--frames F` fixes the job at F
+frames instead (`--frames 1`: one frame split over all ranks, "scaling": "strong", and rank 0
+also times the same frame rendered alone to report t1 / (N * tN)).  The 8x8-pixel tiles of all
+frames are dealt round-robin over the ranks (the reference deals rows round-robin over
+threads, HW2/main.cpp:33-36), each rank renders its tiles into HBM in `--chunks` pieces per
+frame, and each piece is gathered to rank 0 over RCCL (torch.distributed "nccl" = RCCL over
+xGMI) while the next one renders; rank 0 untiles the framebuffers.  At N = 1 the step is
 exactly one C3 frame rendered in place.
 
 Printed by rank 0: ONE JSON line (see the contract in the task statement).
@@ -76,14 +80,33 @@ def algorithmic_bytes(xml: str, threads: int):
     return b, s
 
 
-def cpu_baseline(xml: str, threads: int):
+def host_cores():
+    """Host threads for the CPU baseline: the CPUs this process may run on (affinity), capped
+    by the cgroup CPU quota when one is set.  On the GPU box nproc / os.cpu_count() report the
+    whole machine while a job gets a share of it (16 CPUs per GPU); more threads than the
+    share would only time-slice.  Returns (threads, how it was determined)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    how = f"sched_getaffinity {n}"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+            how += f", cgroup cpu.max quota {quota}"
+            n = min(n, quota)
+    except (OSError, ValueError):
+        pass
+    return max(1, n), how + f", nproc {os.cpu_count()}"
+
+
+def cpu_baseline(xml: str, threads: int, how: str, reps: int = 5, warm: int = 1):
     """The reference itself (oracle/_ref/ref_harness: HW2 sources compiled unmodified) on this
-    box's host cores, rows interleaved over `threads` std::threads as HW2/main.cpp:33-36;
-    falls back to the oracle restatement (kind "port") when the reference build is absent."""
+    box's host cores, rows interleaved over `threads` std::threads as HW2/main.cpp:33-36,
+    median of `reps` renders after `warm` untimed ones; falls back to the oracle restatement
+    (kind "port") when the reference build is absent."""
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
-    reps = 3
     if os.path.exists(harness):
-        out = subprocess.run([harness, "time", xml, "0", str(threads), str(reps), "1"],
+        out = subprocess.run([harness, "time", xml, "0", str(threads), str(reps), "1", str(warm)],
                              check=True, capture_output=True, text=True).stdout
         r = json.loads(out.strip().splitlines()[-1])
         sec, rays, kind = r["seconds_median"], r["rays"], "reference"
@@ -91,16 +114,18 @@ def cpu_baseline(xml: str, threads: int):
         from oracle.cpu_ref import OracleScene
         o = OracleScene(xml)
         times = []
-        for _ in range(reps):
+        for k in range(warm + reps):
             t0 = time.perf_counter()
             _, st = o.render(0, threads=threads)
-            times.append(time.perf_counter() - t0)
+            if k >= warm:
+                times.append(time.perf_counter() - t0)
         sec = sorted(times)[len(times) // 2]
         rays, kind = st.primary_rays + st.shadow_rays, "port"
     return {"value": round(rays / sec / 1e6, 3), "unit": "Mrays/s", "cores": threads,
             "kind": kind,
-            "sample": f"full camera-0 frame, median of {reps} renders ({rays} rays, "
-                      f"{sec:.3f} s each), render region only as HW2/main.cpp:26-41"}
+            "sample": f"full camera-0 frame, median of {reps} renders after {warm} warm-up "
+                      f"({rays} rays, {sec:.3f} s each), render region only as "
+                      f"HW2/main.cpp:26-41; threads: {how}"}
 
 
 def stream_copy_gbps(device) -> float:
@@ -125,14 +150,89 @@ def stream_copy_gbps(device) -> float:
     return gbps
 
 
-def pmc_traffic(workload: str):
-    """HBM bytes per render launch from a committed rocprofv3 --pmc pass (profiles/), corrected
-    as MI355X_MICROARCH.md §HBM prescribes; None when no such profile exists."""
+def file_sha256(path: str) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(1 << 20), b""):
+            h.update(b)
+    return h.hexdigest()
+
+
+def pmc_profile(workload: str):
+    """The committed rocprofv3 --pmc summary for this workload (tools/pmc_traffic.py, separate
+    FETCH_SIZE / WRITE_SIZE / instruction-count passes, corrected as MI355X_MICROARCH.md §HBM
+    prescribes) — used only when it was measured on this very library build (sha256 of
+    libceng795_rt.so recorded in it); otherwise None, and traffic is reported as null."""
+    from ceng795_amd import _lib
     path = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+        prof = json.load(f)
+    if prof.get("lib_sha256") != file_sha256(_lib.LIB_PATH):
+        log(f"{path} was measured on another library build; traffic reported as null")
+        return None
+    return prof
+
+
+def kernel_work(xml: str):
+    """Per-frame work of the traversal kernels (tools/kernel_work.py on the RT_DIAG build, in
+    a child process): node / leaf visits and the algorithmic bytes they imply."""
+    env = dict(os.environ, CENG795_LIB="diag")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "kernel_work.py"), xml],
+                         check=True, capture_output=True, text=True, env=env, timeout=300).stdout
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def roofline_line(xml, world, local_share, kt, launches, prof):
+    # local_share: fraction of one frame's pixels a timed launch renders
+    """Roofline of the dominant kernel (trace_primary_kernel): algorithmic bytes per launch
+    (the kernel's own node / leaf fetches and its per-pixel record, tools/kernel_work.py) over
+    its HIP-event duration measured in the timed region; traffic = HBM bytes per launch of
+    that kernel from the PMC profile of this build (or null)."""
+    work = kernel_work(xml)
+    per_launch = work["primary_bytes"] * local_share
+    prim_ms = kt["primary"] / max(1, launches)
+    achieved = per_launch / (prim_ms * 1e-3) / 1e9
+    c = work["counters"]
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+            "kernel": "trace_primary_kernel",
+            "kernel_ms_avg": round(prim_ms, 4),
+            "algorithmic_bytes_per_launch": int(per_launch),
+            "bytes_model": "64 B x node visits + 48 B x leaf visits + 8 B hit record per pixel "
+                           "(tools/kernel_work.py, RT_DIAG build, same frame)",
+            "work_per_frame": {"node_visits": c["prim_node_visits"],
+                               "leaf_visits": c["prim_leaf_visits"],
+                               "lanes_per_node_visit": round(c["prim_node_lanes"] /
+                                                             max(1, c["prim_node_visits"]), 2),
+                               "leaf_lane_tests": c["prim_leaf_lanes"]},
+            "other_kernels_ms_avg": {"trace_shadow_kernel": round(kt["shadow"] / max(1, launches), 4),
+                                     "shade_kernel": round(kt["shade"] / max(1, launches), 4)},
+            "shadow_kernel_frac": None}
+    sh_ms = kt["shadow"] / max(1, launches)
+    if sh_ms > 0 and work["shadow_bytes"]:
+        roof["shadow_kernel_frac"] = round(work["shadow_bytes"] * local_share /
+                                           (sh_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+    if prof is not None and world == 1:
+        k = prof["per_kernel"].get("trace_primary_kernel", {})
+        roof["traffic"] = k.get("hbm_bytes")
+        roof["traffic_source"] = os.path.join("profiles", os.path.basename(prof["path"]))
+        if "issue" in k:
+            i = k["issue"]
+            roof["issue"] = {
+                "valu_wave_insts": i.get("SQ_INSTS_VALU"), "salu_wave_insts": i.get("SQ_INSTS_SALU"),
+                "smem_wave_insts": i.get("SQ_INSTS_SMEM"),
+                # 2 cycles per wave64 VALU instruction on a SIMD-32, 1024 SIMDs; 1 SALU per
+                # cycle per CU, 256 CUs; at 2.4 GHz, over the live kernel time
+                "valu_issue_frac": round(i["valu_issue_us_at_2.4GHz"] / (prim_ms * 1e3), 3)
+                if "valu_issue_us_at_2.4GHz" in i else None,
+                "salu_issue_frac": round(i["salu_issue_us_at_2.4GHz"] / (prim_ms * 1e3), 3)
+                if "salu_issue_us_at_2.4GHz" in i else None}
+        if "wave_states" in k:
+            roof["wave_states"] = k["wave_states"]
+    return roof
 
 
 def main() -> int:
@@ -151,6 +251,13 @@ def main() -> int:
     ap.add_argument("--gather-rehearsal", action="store_true",
                     help="run the N>1 tile/gather pipeline even at WORLD_SIZE=1 (a one-rank "
                          "process group; exercises the comm-stream gather on one GPU)")
+    ap.add_argument("--frames", type=int, default=0,
+                    help="frames per step (default: one per rank = weak scaling; 1 = one "
+                         "frame split over all ranks = strong scaling)")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="pieces per frame and rank for the gather pipeline (default 4 when "
+                         "a rank renders one frame's share, else 1)")
+    ap.add_argument("--no-roofline", action="store_true")
     args = ap.parse_args()
     if args.workload == "c5":
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
@@ -184,7 +291,9 @@ def main() -> int:
     import ceng795_amd
     from ceng795_amd import dist_tiles
 
-    n_cams = world
+    n_cams = args.frames if args.frames > 0 else world
+    strong = n_cams < world
+    chunks = args.chunks if args.chunks > 0 else (4 if n_cams == 1 and use_pg else 1)
     if rank == 0:
         xml = scene_path(args.workload, n_cams)
     if world > 1:
@@ -197,11 +306,12 @@ def main() -> int:
     plan = dist_tiles.TilePlan(scene, world, rank, force=use_pg)
     stream = torch.cuda.current_stream()
     renderer = dist_tiles.FrameRenderer(scene, plan, stream, gather=use_pg,
-                                        host_staging=args.dist_backend == "gloo")
+                                        host_staging=args.dist_backend == "gloo", chunks=chunks)
 
     # warmup (also yields the per-step ray count from the device counters)
     for _ in range(args.warmup):
         renderer.step()
+    renderer.finish()
     torch.cuda.synchronize()
     st = scene.collect_stats()
     rays_local = (st.primary_rays + st.shadow_rays + st.secondary_rays) / max(1, args.warmup)
@@ -213,78 +323,105 @@ def main() -> int:
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
+    scene.read_kernel_times()  # discard
+    scene.set_kernel_timing(True)  # HIP events around each traversal kernel, on its stream
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(args.steps):
         renderer.step(events=ev[k])
+    renderer.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    scene.set_kernel_timing(False)
+    kt, launches = scene.read_kernel_times()
     el = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    kernel_ms = [a.elapsed_time(b) for a, b in ev]
-    kernel_ms_avg = sum(kernel_ms) / len(kernel_ms)
+    render_ms = [a.elapsed_time(b) for a, b in ev]
     scene.collect_stats()  # reset counters
 
     verified = None
-    if use_pg and rank == 0 and not args.no_verify:
-        # the gathered framebuffers must equal single-GPU renders of the same cameras, bit for bit
-        verified = True
-        for c, f in enumerate(renderer.frames):
-            ref = torch.empty_like(f)
-            scene.render_device(c, ref.data_ptr(), stream=stream.cuda_stream)
+    t1_ms = None
+    if use_pg and rank == 0:
+        if not args.no_verify:
+            # the gathered framebuffers must equal single-GPU renders of the same cameras
+            verified = True
+            for c, f in enumerate(renderer.frames):
+                ref = torch.empty_like(f)
+                scene.render_device(c, ref.data_ptr(), stream=stream.cuda_stream)
+                torch.cuda.synchronize()
+                verified &= bool(torch.equal(ref.view(torch.int32), f.view(torch.int32)))
+            log(f"[rank 0] gathered frames bit-identical to single-GPU renders: {verified}")
+        if strong:
+            # t1: the same job rendered by this GPU alone, in place (no tiles, no gather)
+            frames1 = [torch.empty_like(f) for f in renderer.frames]
+            for _ in range(max(1, args.warmup)):
+                for c, f in enumerate(frames1):
+                    scene.render_device(c, f.data_ptr(), stream=stream.cuda_stream)
             torch.cuda.synchronize()
-            verified &= bool(torch.equal(ref.view(torch.int32), f.view(torch.int32)))
-        log(f"[rank 0] gathered frames bit-identical to single-GPU renders: {verified}")
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                for c, f in enumerate(frames1):
+                    scene.render_device(c, f.data_ptr(), stream=stream.cuda_stream)
+            torch.cuda.synchronize()
+            t1_ms = (time.perf_counter() - t0) / args.steps * 1e3
+            scene.collect_stats()
+    if world > 1:
+        dist.barrier()
 
     if rank == 0:
         value = rays_step * args.steps / elapsed / 1e6
-        threads = min(16, os.cpu_count() or 1)
+        threads, how = host_cores()
         roof = None
-        try:
-            bytes_frame, ostats = algorithmic_bytes(xml, threads)
-            # one launch renders this rank's share of the job's frames
-            per_launch = bytes_frame * (rays_local / (ostats["primary_rays"] + ostats["shadow_rays"]))
-            achieved = per_launch / (kernel_ms_avg * 1e-3) / 1e9
-            traffic = pmc_traffic(args.workload) if world == 1 else None
-            copy_gbps = stream_copy_gbps(device)
-            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                    "traffic": traffic,
-                    "algorithmic_bytes_per_launch": int(per_launch),
-                    "kernel_ms_avg": round(kernel_ms_avg, 4),
-                    "stream_copy_GBps_measured": round(copy_gbps, 1),
-                    "ref_order_visits_per_ray": {
-                        "primary_box": round(ostats["box_tests"][0] / ostats["primary_rays"], 2),
-                        "primary_tri": round(ostats["prim_tests"][0] / ostats["primary_rays"], 2),
-                        "shadow_box": round(ostats["box_tests"][1] / max(1, ostats["shadow_rays"]), 2),
-                        "shadow_tri": round(ostats["prim_tests"][1] / max(1, ostats["shadow_rays"]), 2)}}
-        except Exception as e:  # the oracle is a checker; never let it hide the measurement
-            log(f"roofline accounting failed: {e!r}")
+        if not args.no_roofline:
+            try:
+                # fraction of one frame's work in one launch (one rt_render_device call)
+                share = rays_local / max(1.0, rays_step / n_cams) / max(1.0, launches / args.steps)
+                prof = pmc_profile(args.workload) if world == 1 else None
+                roof = roofline_line(xml, world, share, kt, launches, prof)
+                roof["timed_launches"] = launches
+                roof["stream_copy_GBps_measured"] = round(stream_copy_gbps(device), 1)
+                bytes_ref, ostats = algorithmic_bytes(xml, threads)
+                roof["ref_order_effective_GBps"] = round(
+                    bytes_ref * n_cams / (elapsed / args.steps) / 1e9, 1)
+                roof["ref_order_model"] = ("SURVEY §8(d): 32 B x box tests + 36 B x triangle "
+                                           "tests + 16 B per hit + 12 B per pixel with the "
+                                           "reference's own visit counts (no culling), over "
+                                           "the step time; not a roofline (the kernel does not "
+                                           "make those fetches)")
+            except Exception as e:  # the checker must never hide the measurement
+                log(f"roofline accounting failed: {e!r}")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(xml, threads)
+                cpu = cpu_baseline(xml, threads, how)
             except Exception as e:
                 log(f"cpu baseline failed: {e!r}")
         n, w, h, desc = WORKLOADS[args.workload]
+        ms_step = elapsed / args.steps * 1e3
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic",
             "config": {"workload": desc, "frame": f"{w}x{h}", "frames_per_step": n_cams,
                        "triangles": 2 * (n - 1) ** 2, "rays_per_step": int(rays_step),
                        "traversal": args.traversal,
                        "parallelism": f"tiles{world}" + (f"+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}_gather" if use_pg else ""),
-                       "gather_verified": verified},
+                       "gather_chunks": chunks if use_pg else None,
+                       "gather_verified": verified,
+                       "render_ms_avg": round(sum(render_ms) / len(render_ms), 4)},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if strong and t1_ms is not None:
+            line["strong_scaling"] = {"t1_ms": round(t1_ms, 4), "tN_ms": round(ms_step, 4),
+                                      "efficiency_t1_over_N_tN": round(t1_ms / (world * ms_step), 4)}
         print(json.dumps(line), flush=True)
     if use_pg:
         dist.barrier()

@@ -86,6 +86,11 @@ SIGNATURES = {
                             C.POINTER(rt_stats)]),
     "rt_render_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                    C.c_int, C.c_void_p, C.c_void_p]),
+    "rt_render_device_range": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
+    "rt_set_kernel_timing": (C.c_int, [C.c_void_p, C.c_int]),
+    "rt_read_kernel_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_double),
+                                       C.POINTER(C.c_longlong)]),
     "rt_num_tiles": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
     "rt_collect_stats": (C.c_int, [C.c_void_p, C.POINTER(rt_stats)]),
     "rt_write_png": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
@@ -122,7 +127,7 @@ def _share_torch_hip_runtime() -> None:
         pass
 
 
-ABI_VERSION = 2  # CENG795_RT_ABI_VERSION of include/ceng795_rt.h
+ABI_VERSION = 3  # CENG795_RT_ABI_VERSION of include/ceng795_rt.h
 
 
 def lib() -> C.CDLL:

@@ -131,11 +131,17 @@ struct DeviceGuard {
   }
 };
 
-// Deposit slot rows per photon batch: 16 GiB holds C5's 1e7 photons x 19 slots x 48 B
-// (9.1 GB) in one batch (one sort, one update launch); HBM is 288 GB.  CENG795_PPM_SLOT_MB
-// overrides it for A/B timing and to exercise the multi-batch path.
+// Deposit slot rows per photon batch.  Default 16 GiB: C5's 1e7 photons x 19 slots x 48 B
+// (9.1 GB) run as one batch (one sort, one update launch).  The budget actually used is also
+// capped at a quarter of the device memory free when the pass starts (plus what the scene's
+// slots already hold), so a smaller or shared GPU falls back to more batches instead of failing
+// in hipMalloc.  ppm_set_slot_bytes sets it per scene; CENG795_PPM_SLOT_MB sets the default.
 constexpr int kRRTable = 1 << 20;  // rr(n) tabulated for n < 2^20 (larger n computed inline)
-size_t slot_bytes_per_batch() {
+struct WidenInt {
+  __host__ __device__ long long operator()(int x) const { return (long long)x; }
+};
+
+size_t default_slot_bytes() {
   static const size_t v = [] {
     const char* e = std::getenv("CENG795_PPM_SLOT_MB");
     const long long mb = e ? std::atoll(e) : 0;
@@ -184,8 +190,12 @@ struct ppm_scene {
   DevBuf<unsigned char> temp;
   DevBuf<unsigned long long> stats;  // [photons, photon_rays, deposits, updates, eye_rays]
   DevBuf<int> error;
+  DevBuf<unsigned long long> wide;  // 64-bit scratch scalar (expansion total)
+  DevBuf<unsigned long long> stats_keep;  // stats before a batch (restored when it is split)
   DevBuf<float> image;
   long long photons = 0;
+  size_t slot_bytes = 0;          // ppm_set_batching (0: default_slot_bytes())
+  long long max_updates = INT_MAX;  // ppm_set_batching: (group, deposit) pairs per batch
 
   void free_all() {
     for (void* p : owned) (void)hipFree(p);
@@ -201,6 +211,7 @@ struct ppm_scene {
     bg_start.release(), bg_end.release(), bgkey.release(), bgval.release(), bgkey2.release();
     bgval2.release(), grec.release(), grep.release(), rrtab.release();
     temp.release(), stats.release(), error.release(), image.release();
+    wide.release(), stats_keep.release();
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
   }
@@ -248,6 +259,8 @@ void create_device(ppm_scene* s, int device) {
   s->stats.reserve(16, "alloc counters");
   hip_check(hipMemset(s->stats.p, 0, 16 * sizeof(unsigned long long)), "zero counters");
   s->error.reserve(1, "alloc error flag");
+  s->wide.reserve(1, "alloc scratch scalar");
+  s->stats_keep.reserve(16, "alloc stats snapshot");
   hip_check(hipMemset(s->error.p, 0, sizeof(int)), "zero error flag");
   s->grid.reserve(1, "alloc grid");
   s->rrtab.reserve(kRRTable, "alloc radius-reduction table");
@@ -291,6 +304,9 @@ void eye_pass(ppm_scene* s, int cam) {
 void build_grid(ppm_scene* s, int width, int height) {
   if (s->eye_cam < 0) throw std::invalid_argument("build_hash_grid before the eye pass");
   const int n = s->n_hp;
+  s->grid_ready = false;
+  // a failed earlier build may have left the device error flag set: every pass reads it
+  hip_check(hipMemsetAsync(s->error.p, 0, sizeof(int), s->stream), "zero error flag");
   hip_check(launch_grid(s->hp.p, n, width, height, s->grid.p, s->state.p, s->nupd.p, s->stream),
             "build hash grid");
   s->bstart.reserve(std::max(1, n), "alloc bucket starts");
@@ -395,14 +411,22 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
   if (count < 0 || first < 0) throw std::invalid_argument("bad photon range");
   if (!s->grid_ready) throw std::invalid_argument("trace_photons before build_hash_grid");
   const int K = std::max(1, s->host.max_depth - 1);
-  const long long batch_max = std::max<long long>(1, (long long)(slot_bytes_per_batch() / (sizeof(PDeposit) * K)));
+  size_t budget = s->slot_bytes ? s->slot_bytes : default_slot_bytes();
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+    budget = std::min(budget, (free_b + s->slots.cap * sizeof(PDeposit)) / 4);
+  // slot rows and deposit counts are indexed with int: b * K < 2^31
+  long long batch_max = std::max<long long>(1, (long long)(budget / (sizeof(PDeposit) * K)));
+  batch_max = std::min<long long>(batch_max, (INT_MAX - 1) / K);
   const int H = s->n_hp;
   for (long long done = 0; done < count;) {
-    const int b = (int)std::min(count - done, batch_max);
+    int b = (int)std::min(count - done, batch_max);
     s->slots.reserve((size_t)b * K, "alloc deposit slots");
     s->ndep.reserve(b + 1, "alloc deposit counts");
     s->dep_off.reserve(b + 1, "alloc deposit offsets");
     hip_check(hipMemsetAsync(s->ndep.p + b, 0, sizeof(int), s->stream), "zero sentinel");
+    hip_check(hipMemcpyAsync(s->stats_keep.p, s->stats.p, 16 * sizeof(unsigned long long),
+                             hipMemcpyDeviceToDevice, s->stream), "stats snapshot");
     hip_check(launch_photons(s->S, s->seed, first + done, b, K, s->slots.p, s->ndep.p, s->stats.p,
                              s->stream), "photon pass");
     if (H > 0) {
@@ -428,16 +452,36 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
         s->poff.reserve(D + 1, "alloc expansion offsets");
         hip_check(launch_expand_count(s->dbucket.p, D, s->bg_start.p, s->bg_end.p, s->pcount.p,
                                       s->stream), "expansion count");
+        // the expansion size in 64 bits first: the int scan below must not wrap
+        long long* d_total = reinterpret_cast<long long*>(s->wide.p);
+        hipcub::TransformInputIterator<long long, WidenInt, const int*> wide_in(s->pcount.p,
+                                                                               WidenInt());
+        bytes = 0;
+        hip_check(hipcub::DeviceReduce::Sum(nullptr, bytes, wide_in, d_total, D, s->stream),
+                  "reduce size");
+        s->temp.reserve(bytes, "alloc reduce temp");
+        hip_check(hipcub::DeviceReduce::Sum(s->temp.p, bytes, wide_in, d_total, D, s->stream),
+                  "expansion total");
+        long long P64 = 0;
+        hip_check(hipMemcpyAsync(&P64, d_total, sizeof P64, hipMemcpyDeviceToHost, s->stream),
+                  "read expansion total");
+        hip_check(hipStreamSynchronize(s->stream), "expansion total");
+        if (P64 >= std::min<long long>(INT_MAX, s->max_updates)) {
+          // too many (group, deposit) pairs for one batch: trace a smaller batch (photon
+          // streams are per photon, so the same photons come out again) and keep it smaller
+          if (b == 1) throw std::domain_error("one photon expands to more than 2^31 updates");
+          batch_max = std::max(1, b / 2);
+          hip_check(hipMemcpyAsync(s->stats.p, s->stats_keep.p, 16 * sizeof(unsigned long long),
+                                   hipMemcpyDeviceToDevice, s->stream), "stats restore");
+          continue;
+        }
         bytes = 0;
         hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, s->pcount.p, s->poff.p, D + 1,
                                                    s->stream), "scan size");
         s->temp.reserve(bytes, "alloc scan temp");
         hip_check(hipcub::DeviceScan::ExclusiveSum(s->temp.p, bytes, s->pcount.p, s->poff.p, D + 1,
                                                    s->stream), "scan expansion");
-        int P = 0;
-        hip_check(hipMemcpyAsync(&P, s->poff.p + D, sizeof(int), hipMemcpyDeviceToHost, s->stream),
-                  "read expansion size");
-        hip_check(hipStreamSynchronize(s->stream), "expansion size");
+        const int P = (int)P64;
         hip_check(hipMemsetAsync(s->list_start.p, 0, s->n_groups * sizeof(int), s->stream), "zero");
         hip_check(hipMemsetAsync(s->list_end.p, 0, s->n_groups * sizeof(int), s->stream), "zero");
         if (P > 0) {
@@ -566,6 +610,14 @@ int ppm_settings(const ppm_scene* s, int* per_iteration, int* iterations, int* m
   *per_iteration = s->host.per_iteration;
   *iterations = s->host.iterations;
   *max_depth = s->host.max_depth;
+  return RT_OK;
+}
+
+int ppm_set_batching(ppm_scene* s, long long slot_bytes, long long max_updates) {
+  if (!s || slot_bytes < 0 || max_updates < 0)
+    return set_error(RT_E_INVALID, "ppm_set_batching: bad argument");
+  s->slot_bytes = (size_t)slot_bytes;
+  s->max_updates = max_updates ? std::min<long long>(max_updates, INT_MAX) : INT_MAX;
   return RT_OK;
 }
 

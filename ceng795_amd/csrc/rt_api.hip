@@ -2,11 +2,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <stdexcept>
 #include <string>
@@ -19,7 +21,8 @@
 namespace rt {
 hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                          const float* normals, const DevMaterial* mats, const DevLight* lights,
-                         bool fast, bool deep, bool spheres, hipStream_t stream);
+                         bool fast, bool deep, bool spheres, const hipEvent_t* marks,
+                         hipStream_t stream);
 int max_supported_depth();
 hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream);
 unsigned long long read_reset_exact_fallbacks();
@@ -30,6 +33,33 @@ void write_png(const std::string& path, const float* rgb, int w, int h);
 }  // namespace rt
 
 using namespace rt;
+
+// Device buffers of one synchronous rt_render call, kept by the scene and reused: the
+// reference calls render_image once per thread per camera (HW2/main.cpp:33-36), so a drop-in
+// pays hipMalloc / hipFree only the first time a call of that size runs.  Calls on several
+// host threads each take their own context (rt_render stays reentrant).
+struct RenderCtx {
+  hipStream_t stream = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  float* d_out = nullptr;
+  size_t out_floats = 0;
+  unsigned long long* d_cnt = nullptr;
+  rt::int2_t* d_hits = nullptr;
+  size_t hits_records = 0;
+  unsigned* d_occ = nullptr;
+  size_t occ_words = 0;
+  float* d_frames = nullptr;
+  size_t frames_floats = 0;
+  float* d_samples = nullptr;
+  size_t samples_floats = 0;
+};
+
+// Per-kernel HIP-event timing of render launches (rt_set_kernel_timing): one quad of events
+// per launch, read back by rt_read_kernel_times.
+struct KernelTiming {
+  bool on = false;
+  std::vector<std::array<hipEvent_t, 4>> pending, spare;
+};
 
 struct rt_scene {
   HostScene host;
@@ -53,6 +83,9 @@ struct rt_scene {
   float* d_samples = nullptr;  // MSAA per-sample colours [s][h][w][3]
   size_t samples_capacity = 0;
   unsigned long long msaa_seed = 0;
+  std::mutex ctx_mu;
+  std::vector<RenderCtx*> ctx_free, ctx_all;
+  KernelTiming timing;
 };
 
 namespace {
@@ -104,9 +137,28 @@ T* upload(const std::vector<T>& v, const char* what) {
   return p;
 }
 
+void free_ctx(RenderCtx* c) {
+  (void)hipFree(c->d_out);
+  (void)hipFree(c->d_cnt);
+  (void)hipFree(c->d_hits);
+  (void)hipFree(c->d_occ);
+  (void)hipFree(c->d_frames);
+  (void)hipFree(c->d_samples);
+  if (c->e0) (void)hipEventDestroy(c->e0);
+  if (c->e1) (void)hipEventDestroy(c->e1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
 void free_device(rt_scene* s) {
   int cur = 0;
   if (hipGetDevice(&cur) == hipSuccess && cur != s->device) (void)hipSetDevice(s->device);
+  for (RenderCtx* c : s->ctx_all) free_ctx(c);
+  s->ctx_all.clear();
+  s->ctx_free.clear();
+  for (auto* v : {&s->timing.pending, &s->timing.spare})
+    for (auto& q : *v)
+      for (hipEvent_t e : q) (void)hipEventDestroy(e);
   (void)hipFree(s->d_nodes);
   (void)hipFree(s->d_prims);
   (void)hipFree(s->d_normals);
@@ -276,12 +328,27 @@ unsigned powmod_minstd(unsigned a, unsigned e) {
 // One frame of camera `cam` into d_out.  Pixel-centre cameras: the render kernels write
 // d_out directly.  MSAA cameras (HW2/Scene.cpp:32-69): one render pass per sample index into
 // d_samples[s], then the resolve kernel's splat + colour / weight into d_out (row-major).
+// Events for one timed launch (nullptr when timing is off or the launch renders nothing).
+const hipEvent_t* timing_marks(rt_scene* s, const RenderParams& P) {
+  if (!s->timing.on || P.num_sel_tiles <= 0) return nullptr;
+  std::lock_guard<std::mutex> lk(s->ctx_mu);
+  KernelTiming& t = s->timing;
+  if (t.spare.empty()) {
+    std::array<hipEvent_t, 4> q{};
+    for (hipEvent_t& e : q) hip_check(hipEventCreate(&e), "timing event");
+    t.spare.push_back(q);
+  }
+  t.pending.push_back(t.spare.back());
+  t.spare.pop_back();
+  return t.pending.back().data();
+}
+
 void enqueue_frame(rt_scene* s, const RenderParams& P, int samples, float* d_samples,
                    hipStream_t stream) {
   const bool fast = s->mode == RT_TRAVERSAL_FAST;
   if (samples <= 1) {
     hip_check(launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
-                            fast, s->deep, s->has_spheres, stream),
+                            fast, s->deep, s->has_spheres, timing_marks(s, P), stream),
               "render launch");
     return;
   }
@@ -296,7 +363,7 @@ void enqueue_frame(rt_scene* s, const RenderParams& P, int samples, float* d_sam
     Q.tile_major = 0;
     Q.out = d_samples + (size_t)k * frame;
     hip_check(launch_render(Q, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
-                            fast, s->deep, s->has_spheres, stream),
+                            fast, s->deep, s->has_spheres, timing_marks(s, Q), stream),
               "render launch");
   }
   MsaaResolveParams M;
@@ -311,6 +378,51 @@ void enqueue_frame(rt_scene* s, const RenderParams& P, int samples, float* d_sam
 
 size_t sample_floats(const rt_camera& c) {
   return c.num_samples > 1 ? (size_t)c.num_samples * c.num_samples * c.width * c.height * 3 : 0;
+}
+
+}  // namespace
+
+namespace {
+
+// Grow-only device buffer.
+template <typename T>
+void ensure(T*& p, size_t& cap, size_t need, const char* what) {
+  need = std::max<size_t>(need, 1);
+  if (need <= cap) return;
+  (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  hip_check(hipMalloc(&p, need * sizeof(T)), what);
+  cap = need;
+}
+
+RenderCtx* acquire_ctx(rt_scene* s) {
+  {
+    std::lock_guard<std::mutex> lk(s->ctx_mu);
+    if (!s->ctx_free.empty()) {
+      RenderCtx* c = s->ctx_free.back();
+      s->ctx_free.pop_back();
+      return c;
+    }
+  }
+  std::unique_ptr<RenderCtx> c(new RenderCtx);
+  try {
+    hip_check(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "stream");
+    hip_check(hipEventCreate(&c->e0), "event");
+    hip_check(hipEventCreate(&c->e1), "event");
+    hip_check(hipMalloc(&c->d_cnt, sizeof(unsigned long long) * kCounterAlloc), "alloc counters");
+  } catch (...) {
+    free_ctx(c.release());
+    throw;
+  }
+  std::lock_guard<std::mutex> lk(s->ctx_mu);
+  s->ctx_all.push_back(c.get());
+  return c.release();
+}
+
+void release_ctx(rt_scene* s, RenderCtx* c) {
+  std::lock_guard<std::mutex> lk(s->ctx_mu);
+  s->ctx_free.push_back(c);
 }
 
 }  // namespace
@@ -451,6 +563,13 @@ int rt_num_tiles(const rt_scene* s, int cam, int row0, int row_stride) {
 
 int rt_render_device(rt_scene* s, int cam, int row0, int row_stride, int tile_begin,
                      int tile_step, int tile_major, float* d_out, void* stream) {
+  return rt_render_device_range(s, cam, row0, row_stride, tile_begin, tile_step, -1, tile_major,
+                                d_out, stream);
+}
+
+int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int tile_begin,
+                           int tile_step, int tile_count, int tile_major, float* d_out,
+                           void* stream) {
   return guarded([&] {
       check_render_args(s, cam, row0, row_stride);
       if (tile_begin < 0 || tile_step < 1 || !d_out)
@@ -458,6 +577,11 @@ int rt_render_device(rt_scene* s, int cam, int row0, int row_stride, int tile_be
       DeviceGuard g(s->device);
       RenderParams P =
           make_params(s, cam, row0, row_stride, tile_begin, tile_step, tile_major, d_out, true);
+      if (tile_count >= 0 && tile_count < P.num_sel_tiles) {
+        if (s->host.cameras[cam].num_samples > 1)
+          throw std::domain_error("NumSamples > 1 renders whole row-major frames only");
+        P.num_sel_tiles = tile_count;
+      }
       if (s->needs_recursion) {
         const size_t need = frame_floats(s->host, P.num_sel_tiles);
         if (need > s->frames_capacity) {
@@ -551,89 +675,95 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
       const rt_camera& c = s->host.cameras[cam];
       const TilePlan tp = plan(c, row0, row_stride);
       if (tp.rows == 0) return RT_OK;
+      RenderCtx* x = acquire_ctx(s);
+      struct Release {
+        rt_scene* s;
+        RenderCtx* x;
+        ~Release() { release_ctx(s, x); }
+      } release{s, x};
       const size_t frame = (size_t)c.width * c.height * 3;
-      float* d_out = nullptr;
-      int2_t* d_hits = nullptr;
-      unsigned* d_occ = nullptr;
-      float* d_frames = nullptr;
-      float* d_samples = nullptr;
-      hipStream_t stream = nullptr;
-      hipEvent_t e0 = nullptr, e1 = nullptr;
-      auto cleanup = [&] {
-        if (d_out) (void)hipFree(d_out);
-        if (d_hits) (void)hipFree(d_hits);
-        if (d_occ) (void)hipFree(d_occ);
-        if (d_frames) (void)hipFree(d_frames);
-        if (d_samples) (void)hipFree(d_samples);
-        if (e0) (void)hipEventDestroy(e0);
-        if (e1) (void)hipEventDestroy(e1);
-        if (stream) (void)hipStreamDestroy(stream);
-      };
-      try {
-        hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "stream");
-        hip_check(hipMalloc(&d_out, frame * sizeof(float)), "alloc frame");
-        hip_check(hipEventCreate(&e0), "event");
-        hip_check(hipEventCreate(&e1), "event");
-        // Counters are per scene; this call reports its own deltas via a private buffer.
-        unsigned long long* d_cnt = nullptr;
-        hip_check(hipMalloc(&d_cnt, sizeof(unsigned long long) * kCounterAlloc), "alloc counters");
-        hip_check(hipMemsetAsync(d_cnt, 0, sizeof(unsigned long long) * kCounterWidth * kCounterRows, stream),
-                  "zero counters");
-        RenderParams P = make_params(s, cam, row0, row_stride, 0, 1, 0, d_out, true);
-        P.counters = d_cnt;
-        P.work = work_counters(d_cnt);
-        hip_check(hipMalloc(&d_hits, sizeof(int2_t) * kTile * kTile * (size_t)std::max(1, P.num_sel_tiles)),
-                  "alloc hit records");
-        P.hits = d_hits;
-        hip_check(hipMalloc(&d_occ, sizeof(unsigned) * P.occ_words * kTile * kTile *
-                                        (size_t)std::max(1, P.num_sel_tiles)),
-                  "alloc occlusion bits");
-        P.occ = d_occ;
-        if (s->needs_recursion) {
-          hip_check(hipMalloc(&d_frames, frame_floats(s->host, P.num_sel_tiles) * sizeof(float)),
-                    "alloc ray-tree frames");
-          P.frames = d_frames;
-        }
-        if (c.num_samples > 1)
-          hip_check(hipMalloc(&d_samples, sample_floats(c) * sizeof(float)), "alloc MSAA samples");
-        hip_check(hipEventRecord(e0, stream), "event record");
-        try {
-          enqueue_frame(s, P, c.num_samples, d_samples, stream);
-        } catch (...) {
-          (void)hipFree(d_cnt);
-          throw;
-        }
-        hip_check(hipEventRecord(e1, stream), "event record");
-        // rows j = row0 + k*row_stride only: a strided 2D copy leaves the others untouched
-        const size_t row_bytes = (size_t)c.width * 3 * sizeof(float);
-        hip_check(hipMemcpy2DAsync(out_rgb + (size_t)row0 * c.width * 3, row_bytes * row_stride,
-                                   d_out + (size_t)row0 * c.width * 3, row_bytes * row_stride,
-                                   row_bytes, tp.rows, hipMemcpyDeviceToHost, stream),
-                  "copy rows");
-        std::vector<unsigned long long> cnt(kCounterWidth * kCounterRows);
-        hip_check(hipMemcpyAsync(cnt.data(), d_cnt, cnt.size() * sizeof cnt[0],
-                                 hipMemcpyDeviceToHost, stream),
-                  "copy counters");
-        hip_check(hipStreamSynchronize(stream), "synchronize");
-        (void)hipFree(d_cnt);
-        if (stats) {
-          std::memset(stats, 0, sizeof *stats);
-          for (int r = 0; r < kCounterRows; r++) {
-            stats->primary_rays += (long long)cnt[kCounterWidth * r + kCntPrimary];
-            stats->shadow_rays += (long long)cnt[kCounterWidth * r + kCntShadow];
-            stats->secondary_rays += (long long)cnt[kCounterWidth * r + kCntSecondary];
-            stats->primary_hits += (long long)cnt[kCounterWidth * r + kCntHits];
-          }
-          float ms = 0;
-          hip_check(hipEventElapsedTime(&ms, e0, e1), "elapsed");
-          stats->kernel_ms = ms;
-        }
-      } catch (...) {
-        cleanup();
-        throw;
+      ensure(x->d_out, x->out_floats, frame, "alloc frame");
+      // Counters are per scene; this call reports its own deltas via the context's buffer.
+      hip_check(hipMemsetAsync(x->d_cnt, 0, sizeof(unsigned long long) * kCounterWidth * kCounterRows,
+                               x->stream),
+                "zero counters");
+      RenderParams P = make_params(s, cam, row0, row_stride, 0, 1, 0, x->d_out, true);
+      P.counters = x->d_cnt;
+      P.work = work_counters(x->d_cnt);
+      const size_t lanes = (size_t)kTile * kTile * (size_t)std::max(1, P.num_sel_tiles);
+      ensure(x->d_hits, x->hits_records, lanes, "alloc hit records");
+      P.hits = x->d_hits;
+      ensure(x->d_occ, x->occ_words, (size_t)P.occ_words * lanes, "alloc occlusion bits");
+      P.occ = x->d_occ;
+      if (s->needs_recursion) {
+        ensure(x->d_frames, x->frames_floats, frame_floats(s->host, P.num_sel_tiles),
+               "alloc ray-tree frames");
+        P.frames = x->d_frames;
       }
-      cleanup();
+      if (c.num_samples > 1)
+        ensure(x->d_samples, x->samples_floats, sample_floats(c), "alloc MSAA samples");
+      hip_check(hipEventRecord(x->e0, x->stream), "event record");
+      enqueue_frame(s, P, c.num_samples, x->d_samples, x->stream);
+      hip_check(hipEventRecord(x->e1, x->stream), "event record");
+      // rows j = row0 + k*row_stride only: a strided 2D copy leaves the others untouched
+      const size_t row_bytes = (size_t)c.width * 3 * sizeof(float);
+      hip_check(hipMemcpy2DAsync(out_rgb + (size_t)row0 * c.width * 3, row_bytes * row_stride,
+                                 x->d_out + (size_t)row0 * c.width * 3, row_bytes * row_stride,
+                                 row_bytes, tp.rows, hipMemcpyDeviceToHost, x->stream),
+                "copy rows");
+      std::vector<unsigned long long> cnt(kCounterWidth * kCounterRows);
+      hip_check(hipMemcpyAsync(cnt.data(), x->d_cnt, cnt.size() * sizeof cnt[0],
+                               hipMemcpyDeviceToHost, x->stream),
+                "copy counters");
+      hip_check(hipStreamSynchronize(x->stream), "synchronize");
+      if (stats) {
+        std::memset(stats, 0, sizeof *stats);
+        for (int r = 0; r < kCounterRows; r++) {
+          stats->primary_rays += (long long)cnt[kCounterWidth * r + kCntPrimary];
+          stats->shadow_rays += (long long)cnt[kCounterWidth * r + kCntShadow];
+          stats->secondary_rays += (long long)cnt[kCounterWidth * r + kCntSecondary];
+          stats->primary_hits += (long long)cnt[kCounterWidth * r + kCntHits];
+        }
+        float ms = 0;
+        hip_check(hipEventElapsedTime(&ms, x->e0, x->e1), "elapsed");
+        stats->kernel_ms = ms;
+      }
       return RT_OK;
+  });
+}
+
+int rt_set_kernel_timing(rt_scene* s, int enable) {
+  if (!s) return set_error(RT_E_INVALID, "rt_set_kernel_timing: NULL scene");
+  s->timing.on = enable != 0;
+  return RT_OK;
+}
+
+int rt_read_kernel_times(rt_scene* s, double* ms4, long long* launches) {
+  if (!s || !ms4) return set_error(RT_E_INVALID, "rt_read_kernel_times: NULL argument");
+  return guarded([&] {
+    DeviceGuard g(s->device);
+    std::vector<std::array<hipEvent_t, 4>> done;
+    {
+      std::lock_guard<std::mutex> lk(s->ctx_mu);
+      done.swap(s->timing.pending);
+    }
+    double sum[4] = {0, 0, 0, 0};
+    for (auto& q : done) {
+      hip_check(hipEventSynchronize(q[3]), "timing sync");
+      float a = 0, b = 0, c = 0;
+      hip_check(hipEventElapsedTime(&a, q[0], q[1]), "elapsed");
+      hip_check(hipEventElapsedTime(&b, q[1], q[2]), "elapsed");
+      hip_check(hipEventElapsedTime(&c, q[2], q[3]), "elapsed");
+      sum[0] += a;
+      sum[1] += b;
+      sum[2] += c;
+      sum[3] += (double)a + b + c;
+    }
+    std::memcpy(ms4, sum, sizeof sum);
+    if (launches) *launches = (long long)done.size();
+    std::lock_guard<std::mutex> lk(s->ctx_mu);
+    for (auto& q : done) s->timing.spare.push_back(q);
+    return RT_OK;
   });
 }
 

@@ -1595,15 +1595,27 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void shade_kernel(
   shade_pixel(P, prims, normals, mats, lights, sel);
 }
 
+// marks (nullable): 4 events recorded before the primary kernel, after it, after the shadow
+// kernel and after the shade kernel (rt_set_kernel_timing).  A recursive scene's single kernel
+// is timed between marks 2 and 3.
+static inline void mark(const hipEvent_t* marks, int k, hipStream_t stream) {
+  if (marks) (void)hipEventRecord(marks[k], stream);
+}
+
 template <bool FAST, bool DEEP, bool SPHERES>
 static void launch_variant(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                            const float* normals, const DevMaterial* mats,
-                           const DevLight* lights, int blocks, hipStream_t stream) {
+                           const DevLight* lights, int blocks, const hipEvent_t* marks,
+                           hipStream_t stream) {
   const size_t lds = DEEP ? sizeof(int) * 3 * kDeepStack * kWavesPerBlock : 0;
   if (P.frames) {  // recursive scenes: one kernel walks each pixel's ray tree
+    mark(marks, 0, stream);
+    mark(marks, 1, stream);
+    mark(marks, 2, stream);
     hipLaunchKernelGGL((recursive_kernel<FAST, DEEP, SPHERES>), dim3(blocks),
                        dim3(kWavesPerBlock * 64), lds, stream, P, nodes, prims, normals, mats,
                        lights);
+    mark(marks, 3, stream);
     return;
   }
   constexpr int R = kRaysPerLane;
@@ -1623,13 +1635,17 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
 #else
   T.work = S.work = nullptr;
 #endif
+  mark(marks, 0, stream);
   hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, R>), dim3(tblocks),
                      dim3(W * 64), tlds, stream, T, nodes, prims);
+  mark(marks, 1, stream);
   if (P.num_lights > 0)
     hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, R>), dim3(tblocks),
                        dim3(W * 64), tlds, stream, S, nodes, prims, lights);
+  mark(marks, 2, stream);
   hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
                      prims, normals, mats, lights);
+  mark(marks, 3, stream);
 }
 
 // Gaussian splat of HW2/Scene.cpp:46-62 turned inside out: one thread per destination pixel
@@ -1735,14 +1751,15 @@ hipError_t launch_quot_check(unsigned long long seed, long long count, unsigned 
 
 hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                          const float* normals, const DevMaterial* mats, const DevLight* lights,
-                         bool fast, bool deep, bool spheres, hipStream_t stream) {
+                         bool fast, bool deep, bool spheres, const hipEvent_t* marks,
+                         hipStream_t stream) {
   if (P.num_sel_tiles <= 0) return hipSuccess;
   const int blocks = (P.num_sel_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
   const int v = (fast ? 4 : 0) | (deep ? 2 : 0) | (spheres ? 1 : 0);
   switch (v) {
 #define RT_CASE(F, D, S)                                                                  \
   case (F ? 4 : 0) | (D ? 2 : 0) | (S ? 1 : 0):                                           \
-    launch_variant<F, D, S>(P, nodes, prims, normals, mats, lights, blocks, stream); \
+    launch_variant<F, D, S>(P, nodes, prims, normals, mats, lights, blocks, marks, stream); \
     break;
     RT_CASE(true, false, false)
     RT_CASE(true, false, true)

@@ -110,17 +110,22 @@ class FrameRenderer:
 
     world == 1 and gather == False renders each camera in place into a row-major frame.
 
-    gather=True (one process per GPU): camera c's share is rendered on `stream`; an event hands
-    it to a communication stream that gathers slot c to rank 0 (RCCL) and, on rank 0, untiles
-    it, while `stream` goes on with camera c + 1.  The rank buffer alternates between two copies
-    per step, and a slot is rendered again only after its gather two steps earlier has finished
-    (per-slot events), so consecutive steps pipeline too.  Rank 0's receive buffer and frames are
-    only touched on the comm stream, in order.
-    host_staging=True (the gloo rehearsal) does the same exchange synchronously via host copies.
+    gather=True (one process per GPU): camera c's share is rendered on `stream` in `chunks`
+    pieces (rt_render_device_range); an event hands each piece to a communication stream that
+    gathers it to rank 0 (RCCL) while `stream` renders the next piece, and rank 0 untiles
+    camera c on the comm stream after its last piece.  Only the last piece of the last camera
+    of a step is exposed.  Every rank's slot has the same size, so piece j of camera c is
+    slot tiles [j*cs, (j+1)*cs) on every rank (cs = ceil(slot / chunks)); a rank whose share
+    ends earlier sends its untouched (zero) padding, which the untile index never reads.
+    The rank buffer alternates between two copies per step, and a slot is rendered again only
+    after its gather two steps earlier has finished (per-slot events), so consecutive steps
+    pipeline too.  Rank 0's receive buffer and frames are only touched on the comm stream, in
+    order.  host_staging=True (the gloo rehearsal) does the same exchange synchronously via
+    host copies.
     """
 
     def __init__(self, scene, layout_or_none: Optional[TileLayout], stream, gather: bool,
-                 host_staging: bool = False):
+                 host_staging: bool = False, chunks: int = 1):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -139,13 +144,14 @@ class FrameRenderer:
         L = self.layout
         assert L.sizes == self.sizes, "tile layout built for other frame sizes"
         self.rank = L.rank
+        self.pieces = [chunk_ranges(sh.slot, chunks) for sh in L.shares]
         # two rank buffers, alternating per step: step k + 1 renders while step k's last
         # slot is still being gathered
         self.local = [torch.zeros((L.buffer_tiles, TILE_FLOATS), dtype=torch.float32, device=dev)
                       for _ in range(2)]
         self.buf = 0
         self.comm = torch.cuda.Stream(device=dev)
-        self.rendered = [torch.cuda.Event() for _ in L.shares]
+        self.rendered = [[torch.cuda.Event() for _ in p] for p in self.pieces]
         self.slot_free = [[torch.cuda.Event() for _ in L.shares] for _ in range(2)]
         self.slot_used = [[False] * len(L.shares) for _ in range(2)]
         if L.rank == 0:
@@ -165,28 +171,32 @@ class FrameRenderer:
     def _slot(self, sh: CameraShare):
         return self.local[self.buf][sh.offset:sh.offset + sh.slot]
 
-    def _exchange(self, c: int, sh: CameraShare):
+    def _exchange(self, c: int, sh: CameraShare, j: int):
         torch, dist, L = self.torch, self.dist, self.layout
         root = self.rank == 0
+        lo, hi = self.pieces[c][j]
+        last = j == len(self.pieces[c]) - 1
         if self.host_staging:  # gloo: host copies, synchronous
             self.stream.synchronize()
-            host = self._slot(sh).cpu()
-            glist = list(torch.empty((L.world, sh.slot, TILE_FLOATS))) if root else None
+            host = self._slot(sh)[lo:hi].cpu()
+            glist = list(torch.empty((L.world, hi - lo, TILE_FLOATS))) if root else None
             dist.gather(host, glist, dst=0)
             if root:
-                self.gathered[c].copy_(torch.stack(glist))
-                untile_camera(self.gathered[c].view(-1, TILE_FLOATS), L, c, self.index[c],
-                              self.padded[c])
+                self.gathered[c][:, lo:hi].copy_(torch.stack(glist))
+                if last:
+                    untile_camera(self.gathered[c].view(-1, TILE_FLOATS), L, c, self.index[c],
+                                  self.padded[c])
             return
         with torch.cuda.stream(self.comm):
-            self.comm.wait_event(self.rendered[c])
-            work = dist.gather(self._slot(sh), list(self.gathered[c]) if root else None, dst=0,
-                               async_op=True)
+            self.comm.wait_event(self.rendered[c][j])
+            outs = [self.gathered[c][r, lo:hi] for r in range(L.world)] if root else None
+            work = dist.gather(self._slot(sh)[lo:hi], outs, dst=0, async_op=True)
             work.wait()  # the comm stream waits for the collective (host does not block)
-            if root:
-                untile_camera(self.gathered[c].view(-1, TILE_FLOATS), L, c, self.index[c],
-                              self.padded[c])
-            self.slot_free[self.buf][c].record(self.comm)
+            if last:
+                if root:
+                    untile_camera(self.gathered[c].view(-1, TILE_FLOATS), L, c, self.index[c],
+                                  self.padded[c])
+                self.slot_free[self.buf][c].record(self.comm)
 
     def step(self, events=None):
         s = self.stream.cuda_stream
@@ -202,13 +212,15 @@ class FrameRenderer:
         for c, sh in enumerate(self.layout.shares):
             if self.slot_used[self.buf][c]:  # this slot's gather two steps ago
                 self.stream.wait_event(self.slot_free[self.buf][c])
-            if sh.count:
-                self.scene.render_device(sh.camera, self._slot(sh).data_ptr(),
-                                         tile_begin=sh.tile_begin, tile_step=sh.tile_step,
-                                         tile_major=True, stream=s)
-            self.rendered[c].record(self.stream)
+            slot = self._slot(sh)
+            for j, (lo, begin, n) in enumerate(piece_calls(sh, self.pieces[c])):
+                if n > 0:
+                    self.scene.render_device(sh.camera, slot[lo].data_ptr(), tile_begin=begin,
+                                             tile_step=sh.tile_step, tile_count=n,
+                                             tile_major=True, stream=s)
+                self.rendered[c][j].record(self.stream)
+                self._exchange(c, sh, j)
             self.slot_used[self.buf][c] = True
-            self._exchange(c, sh)
         if events is not None:
             events[1].record(self.stream)
         return self.frames
@@ -217,6 +229,21 @@ class FrameRenderer:
         """Make `stream` wait for every outstanding gather / untile of this renderer."""
         if self.gather and not self.host_staging:
             self.stream.wait_stream(self.comm)
+
+
+def chunk_ranges(slot: int, chunks: int) -> List[Tuple[int, int]]:
+    """Pieces [lo, hi) of a slot of `slot` tiles, ceil(slot / chunks) tiles each (the last may
+    be shorter); the same on every rank, since every rank's slot has the same size."""
+    chunks = max(1, min(int(chunks), max(1, slot)))
+    cs = (slot + chunks - 1) // chunks
+    return [(lo, min(slot, lo + cs)) for lo in range(0, max(slot, 1), cs)] if slot else [(0, 0)]
+
+
+def piece_calls(sh: CameraShare, pieces: List[Tuple[int, int]]) -> List[Tuple[int, int, int]]:
+    """The rt_render_device_range call of each piece of a rank's share: (first slot tile,
+    first camera tile, tile count).  Slot tile k holds camera tile tile_begin + k*tile_step."""
+    return [(lo, sh.tile_begin + lo * sh.tile_step, max(0, min(hi, sh.count) - lo))
+            for lo, hi in pieces]
 
 
 def TilePlan(scene, world: int, rank: int, force: bool = False) -> Optional[TileLayout]:

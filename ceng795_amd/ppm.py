@@ -25,7 +25,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _VARIANT = os.environ.get("CENG795_PPM_LIB", "")
 LIB_PATH = os.path.join(_HERE, "lib", f"libceng795_ppm_{_VARIANT}.so" if _VARIANT else
                         "libceng795_ppm.so")
-ABI_VERSION = 1  # CENG795_PPM_ABI_VERSION
+ABI_VERSION = 2  # CENG795_PPM_ABI_VERSION
 
 _lib = None
 
@@ -52,6 +52,7 @@ SIGNATURES = {
     "ppm_image_name": (C.c_char_p, [_VP, _I]),
     "ppm_settings": (_I, [_VP, _IP, _IP, _IP]),
     "ppm_set_seed": (_I, [_VP, C.c_ulonglong]),
+    "ppm_set_batching": (_I, [_VP, C.c_longlong, C.c_longlong]),
     "ppm_eye_pass": (_I, [_VP, _I]),
     "ppm_build_hash_grid": (_I, [_VP, _I, _I, C.POINTER(C.c_double)]),
     "ppm_num_hit_points": (_I, [_VP]),
@@ -141,6 +142,10 @@ class PhotonScene:
 
     def set_seed(self, seed: int) -> None:
         check(lib().ppm_set_seed(self._h, int(seed)))
+
+    def set_batching(self, slot_bytes: int = 0, max_updates: int = 0) -> None:
+        """Photon-pass batch sizing (results do not depend on it); 0 = defaults."""
+        check(lib().ppm_set_batching(self._h, int(slot_bytes), int(max_updates)))
 
     # ------------------------------------------------------------------ reference passes
     def reset_hash_grid(self) -> None:

@@ -124,11 +124,24 @@ class Scene:
 
     def render_device(self, camera_index: int, out_ptr: int, *, starting_row: int = 0,
                       row_stride: int = 1, tile_begin: int = 0, tile_step: int = 1,
-                      tile_major: bool = False, stream: int = 0) -> None:
-        """Asynchronous render into device memory at ``out_ptr`` on HIP stream ``stream``."""
-        check(lib().rt_render_device(self._h, camera_index, starting_row, row_stride,
-                                     tile_begin, tile_step, int(tile_major),
-                                     C.c_void_p(out_ptr), C.c_void_p(stream)))
+                      tile_major: bool = False, stream: int = 0,
+                      tile_count: int = -1) -> None:
+        """Asynchronous render into device memory at ``out_ptr`` on HIP stream ``stream``
+        (tiles tile_begin + k*tile_step, k < tile_count; tile_count < 0: all of them)."""
+        check(lib().rt_render_device_range(self._h, camera_index, starting_row, row_stride,
+                                           tile_begin, tile_step, tile_count, int(tile_major),
+                                           C.c_void_p(out_ptr), C.c_void_p(stream)))
+
+    def set_kernel_timing(self, enable: bool) -> None:
+        check(lib().rt_set_kernel_timing(self._h, int(enable)))
+
+    def read_kernel_times(self):
+        """(ms summed per kernel {primary, shadow, shade, total}, launches) since the last read."""
+        ms = (C.c_double * 4)()
+        n = C.c_longlong()
+        check(lib().rt_read_kernel_times(self._h, ms, C.byref(n)))
+        keys = ("primary", "shadow", "shade", "total")
+        return dict(zip(keys, list(ms))), n.value
 
     DIAG_NAMES = ["primary_rays", "shadow_rays", "secondary_rays", "primary_hits",
                   "prim_node_visits", "prim_node_lanes", "prim_leaf_visits", "prim_leaf_lanes",

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define CENG795_PPM_ABI_VERSION 1
+#define CENG795_PPM_ABI_VERSION 2  /* 2: ppm_set_batching */
 
 typedef struct ppm_scene ppm_scene;
 
@@ -55,6 +55,13 @@ const char* ppm_image_name(const ppm_scene* scene, int camera);
 int ppm_settings(const ppm_scene* scene, int* per_iteration, int* iterations, int* max_depth);
 int ppm_set_seed(ppm_scene* scene, unsigned long long seed);
 
+/* Photon-pass batching (no effect on results: a batch of photons is traced, its deposits
+ * sorted and applied in photon order, then the next batch).  slot_bytes: device memory for
+ * one batch's deposit slots (19 x 48 B per photon at MaxRecursionDepth 20); 0 = the default
+ * (16 GiB, or CENG795_PPM_SLOT_MB), always capped at a quarter of the free device memory.
+ * max_updates: (hit-point group, deposit) pairs one batch may expand to (0 = 2^31 - 1, the
+ * limit of the 32-bit sort); a batch that would exceed it is traced again as two halves. */
+int ppm_set_batching(ppm_scene* scene, long long slot_bytes, long long max_updates);
 /* reset_hash_grid + eye_trace_lines over all rows: builds the hit points. */
 int ppm_eye_pass(ppm_scene* scene, int camera);
 /* build_hash_grid; info8 (nullable) receives {initial radius, hash scale, grid bbox min xyz,

@@ -23,7 +23,8 @@
 extern "C" {
 #endif
 
-#define CENG795_RT_ABI_VERSION 2  /* 2: MSAA cameras + rt_set_msaa_seed */
+#define CENG795_RT_ABI_VERSION 3  /* 2: MSAA cameras + rt_set_msaa_seed; 3: tile ranges,
+                                      kernel timing */
 
 enum {
   RT_OK = 0,
@@ -173,6 +174,20 @@ int rt_render(rt_scene* scene, int camera_index, int starting_row, int row_strid
 int rt_render_device(rt_scene* scene, int camera_index, int starting_row, int row_stride,
                      int tile_begin, int tile_step, int tile_major, float* d_out,
                      void* hip_stream);
+/* rt_render_device restricted to the first `tile_count` selected tiles (tile_count < 0: all):
+ * tiles tile_begin + k*tile_step for k < tile_count.  With tile_major the k-th of them lands
+ * at d_out + k*192 floats.  Lets a rank render its share of a frame in chunks and hand each
+ * chunk to the framebuffer gather while the next one renders (multi-GPU).
+ * MSAA cameras: whole frames only. */
+int rt_render_device_range(rt_scene* scene, int camera_index, int starting_row, int row_stride,
+                           int tile_begin, int tile_step, int tile_count, int tile_major,
+                           float* d_out, void* hip_stream);
+/* Per-kernel timing of render launches: while enabled, every launch records HIP events around
+ * its traversal kernels on the launch's stream.  rt_read_kernel_times returns (and resets)
+ * the summed milliseconds ms4 = {primary-ray kernel, shadow-ray kernel, shade kernel (or the
+ * recursive kernel), all three} and the number of launches timed. */
+int rt_set_kernel_timing(rt_scene* scene, int enable);
+int rt_read_kernel_times(rt_scene* scene, double* ms4, long long* launches);
 /* Seed of the per-pixel MSAA generators (see rt_render).  Replaces the reference's
  * system_clock seed (HW2/Scene.cpp:36-37) to make MSAA frames deterministic. */
 int rt_set_msaa_seed(rt_scene* scene, unsigned long long seed);

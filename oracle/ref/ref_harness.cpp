@@ -16,7 +16,8 @@
 //                                                   get_color truncates; MSAA cameras)
 //   bvh    <xml> <out.txt>                          preorder BVH topology, floats as hex bits
 //   rays   <xml> <cam> <out.bin>                    per-pixel primary hit: t, normal (hex) + hit flag
-//   time   <xml> <cam> <threads> <reps> <row_step>  median wall time of render_image over rows
+//   time   <xml> <cam> <threads> <reps> <row_step> [warm]  median wall time of render_image
+//          over rows, after `warm` untimed renders
 //                                                   j = 0 (mod row_step); prints one JSON line
 #include <algorithm>
 #include <chrono>
@@ -149,13 +150,14 @@ int main(int argc, char** argv) {
     const int row_step = std::atoi(argv[6]);
     const Image_plane& ip = scene.cameras[cam].get_image_plane();
     const int w = ip.width, h = ip.height;
+    const int warm = argc > 7 ? std::atoi(argv[7]) : 0;  // untimed warm renders first
     std::vector<double> times;
-    for (int r = 0; r < reps; r++) {
+    for (int r = 0; r < warm + reps; r++) {
       Pixel* px = new Pixel[(size_t)w * h];
       auto t0 = std::chrono::steady_clock::now();
       render_rows(scene, cam, px, 0, row_step, threads);
       auto t1 = std::chrono::steady_clock::now();
-      times.push_back(std::chrono::duration<double>(t1 - t0).count());
+      if (r >= warm) times.push_back(std::chrono::duration<double>(t1 - t0).count());
       delete[] px;
     }
     std::sort(times.begin(), times.end());

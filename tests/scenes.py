@@ -111,3 +111,15 @@ def write_c5(directory: str) -> str:
             f.write(GP.cornell(256, 256, photons=10000, iterations=1000))
         os.replace(tmp, path)
     return path
+
+
+def write_c4(directory: str) -> str:
+    """C4: the C3 mesh at 3840x2160 (BASELINE.json configs[3])."""
+    path = os.path.join(directory, "c4.xml")
+    if not os.path.exists(path):
+        spec = G.heightfield_scene(708, 3840, 2160, name="c4.png")
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(spec.to_xml())
+        os.replace(tmp, path)
+    return path

@@ -11,7 +11,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from ceng795_amd.dist_tiles import TILE, TILE_FLOATS, TileLayout, untile_camera
+from ceng795_amd.dist_tiles import (TILE, TILE_FLOATS, TileLayout, chunk_ranges, piece_calls,
+                                    untile_camera)
 
 SIZES = [(37, 21), (64, 40), (5, 9), (96, 64)]  # (w, h): ragged edges, tiny frames
 
@@ -112,3 +113,72 @@ def test_every_tile_rendered_exactly_once(world):
         idx = L0.row_index(c).reshape(-1)
         assert len(np.unique(idx)) == len(idx)
         assert idx.max() < world * L0.slots[c] * TILE
+
+
+def _render_pieces(L, frames, c, pieces):
+    """What FrameRenderer's rt_render_device_range calls write into camera c's slot."""
+    sh = L.shares[c]
+    slot = torch.zeros((sh.slot, TILE_FLOATS))
+    for lo, begin, n in piece_calls(sh, pieces):
+        for k in range(n):
+            slot[lo + k] = torch.from_numpy(_tile(frames[c], begin + k * sh.tile_step))
+    return slot
+
+
+def _split_worker(rank, world, port, outdir, size, chunks):
+    """One frame split over the ranks (C4's strong-scaling mode), gathered piece by piece."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(11)
+    w, h = size
+    frames = [rng.standard_normal((h, w, 3)).astype(np.float32)]
+    L = TileLayout([size], world, rank)
+    sh = L.shares[0]
+    pieces = chunk_ranges(sh.slot, chunks)
+    slot = _render_pieces(L, frames, 0, pieces)
+    gathered = torch.full((world, sh.slot, TILE_FLOATS), float("nan"))
+    for lo, hi in pieces:
+        outs = [gathered[r, lo:hi] for r in range(world)] if rank == 0 else None
+        if rank == 0:
+            tmp = [torch.empty(hi - lo, TILE_FLOATS) for _ in range(world)]
+            dist.gather(slot[lo:hi].contiguous(), tmp, dst=0)
+            for o, t in zip(outs, tmp):
+                o.copy_(t)
+        else:
+            dist.gather(slot[lo:hi].contiguous(), None, dst=0)
+    if rank == 0:
+        got = untile_camera(gathered.view(-1, TILE_FLOATS), L, 0)
+        ok = _same(got.contiguous().numpy(), frames[0])
+        with open(os.path.join(outdir, "result"), "w") as fh:
+            fh.write("ok" if ok else "mismatch")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,size,chunks", [(2, (3840 // 8, 2160 // 8), 4), (2, (37, 21), 3),
+                                               (3, (64, 40), 1), (3, (21, 13), 5)])
+def test_single_frame_split_in_pieces(tmp_path, world, size, chunks):
+    mp.spawn(_split_worker, args=(world, _free_port(), str(tmp_path), size, chunks),
+             nprocs=world, join=True)
+    assert (tmp_path / "result").read_text() == "ok"
+
+
+@pytest.mark.parametrize("slot,chunks", [(0, 4), (1, 4), (7, 3), (8, 4), (130, 4), (5, 1)])
+def test_chunk_ranges_cover_slot(slot, chunks):
+    pieces = chunk_ranges(slot, chunks)
+    covered = [t for lo, hi in pieces for t in range(lo, hi)]
+    assert covered == list(range(slot))
+    assert len(pieces) <= max(1, chunks)
+
+
+def test_piece_calls_cover_share():
+    for world in (1, 2, 3, 8):
+        for size in [(37, 21), (3840 // 8, 2160 // 8)]:
+            for r in range(world):
+                L = TileLayout([size], world, r)
+                sh = L.shares[0]
+                tiles = []
+                for lo, begin, n in piece_calls(sh, chunk_ranges(sh.slot, 4)):
+                    tiles += [begin + k * sh.tile_step for k in range(n)]
+                assert tiles == [sh.tile_begin + k * world for k in range(sh.count)]

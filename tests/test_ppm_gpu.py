@@ -86,3 +86,36 @@ def test_errors_are_loud(ppm, scene_dir, tmp_path):
     bad.write_text("<Scene><Objects><Sphere><Material>1</Material></Sphere></Objects></Scene>")
     with pytest.raises(ppm.RTError):
         ppm.PhotonScene(str(bad))
+
+
+@pytest.mark.parametrize("slot_bytes,max_updates", [(1 << 20, 0), (0, 5000), (256 << 10, 3000)])
+def test_batched_photon_pass_matches_oracle(ppm, scene_dir, slot_bytes, max_updates):
+    """Many batches per ppm_trace_photons call (1 MB / 256 KB of deposit slots: 20k photons
+    in ~20-80 batches), and batches split in halves when their (group, deposit) expansion
+    exceeds max_updates: the same bits as one batch, since each batch applies its deposits
+    in photon order after the previous batch's."""
+    xml = scenes.write_ppm("ppm_box", scene_dir)
+    o = OraclePPM(xml)
+    with ppm.PhotonScene(xml, seed=4) as g:
+        g.set_batching(slot_bytes, max_updates)
+        c = g.camera(0)
+        g.eye_trace_lines(0)
+        g.build_hash_grid(c.width, c.height)
+        o.eye_pass(0, seed=4)
+        o.build_hash_grid(c.width, c.height)
+        g.trace_photons(0, 20000)
+        ost = o.trace_photons(4, 0, 20000)
+        assert np.array_equal(bits(g.hit_state()), bits(o.hit_state()))
+        st = g.collect_stats()
+        assert (st.photons, st.photon_rays, st.deposits, st.updates) == \
+            (20000, ost.photon_rays, ost.deposits, ost.updates)
+
+
+def test_batching_arguments_are_checked(ppm, scene_dir):
+    xml = scenes.write_ppm("ppm_shallow", scene_dir)
+    with ppm.PhotonScene(xml) as g:
+        with pytest.raises(ppm.RTError):
+            g.set_batching(-1, 0)
+        with pytest.raises(ppm.RTError):
+            g.set_batching(0, -5)
+        g.set_batching(0, 0)

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""The traversal kernels' own work on one frame, from the RT_DIAG build
+(lib/libceng795_rt_diag.so, the same kernels plus per-wave counters): node visits, leaf visits
+and lane tests per kernel.  bench.py runs this as a child process (CENG795_LIB=diag selects the
+diagnostic library; the timed library is never instrumented) to price its roofline:
+
+    algorithmic bytes of a traversal launch = 64 B x node visits   (one DevNode scalar load
+                                                                    per packet visit)
+                                            + 48 B x leaf visits   (one DevPrim per
+                                                                    (packet, leaf) pair)
+                                            + per-pixel records    (primary: 8 B hit record
+                                                                    written; shadow: 8 B hit
+                                                                    record read + 4 B
+                                                                    occlusion word written)
+
+usage: CENG795_LIB=diag python tools/kernel_work.py <scene.xml> [--camera 0] [--traversal fast]
+prints one JSON object.
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("xml")
+    ap.add_argument("--camera", type=int, default=0)
+    ap.add_argument("--traversal", default="fast")
+    a = ap.parse_args()
+    if os.environ.get("CENG795_LIB") != "diag":
+        raise SystemExit("run with CENG795_LIB=diag (the RT_DIAG build)")
+    import torch
+    import ceng795_amd
+    with ceng795_amd.Scene(a.xml, device=0, traversal=a.traversal) as s:
+        c = s.camera(a.camera)
+        buf = torch.empty((c.height, c.width, 3), device="cuda")
+        s.debug_counters()
+        s.render_device(a.camera, buf.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        d = s.debug_counters()
+        if not d["diag_build"]:
+            raise SystemExit("not a diagnostic build")
+        pixels = c.width * c.height
+        words = max(1, (s.num_lights + 31) // 32)
+        prim = 64 * d["prim_node_visits"] + 48 * d["prim_leaf_visits"] + 8 * pixels
+        shad = (64 * d["shad_node_visits"] + 48 * d["shad_leaf_visits"]
+                + (8 + 4 * words) * pixels) if s.num_lights else 0
+        out = {"pixels": pixels, "packets": ((c.width + 7) // 8) * ((c.height + 7) // 8),
+               "counters": {k: v for k, v in d.items() if k not in ("c13", "c14", "c15")},
+               "primary_bytes": prim, "shadow_bytes": shad}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
