@@ -242,7 +242,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS) + ["c5"],
                     help="c5: the photon-mapping Cornell box (tools/bench_ppm.py), 1 GPU")
-    ap.add_argument("--traversal", default="fast", choices=["fast", "reference"])
+    ap.add_argument("--traversal", default="fast", choices=["fast", "reference", "cull"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearsal of the N>1 path on one GPU (ranks share device 0)")

@@ -24,6 +24,7 @@ RT_E_UNSUPPORTED = -5
 
 RT_TRAVERSAL_FAST = 0
 RT_TRAVERSAL_REFERENCE = 1
+RT_TRAVERSAL_CULL = 2
 
 F3 = C.c_float * 3
 

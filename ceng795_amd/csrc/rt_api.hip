@@ -21,8 +21,8 @@
 namespace rt {
 hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                          const float* normals, const DevMaterial* mats, const DevLight* lights,
-                         bool fast, bool deep, bool spheres, const hipEvent_t* marks,
-                         hipStream_t stream);
+                         bool fast, bool deep, bool spheres, bool cull,
+                         const hipEvent_t* marks, hipStream_t stream);
 int max_supported_depth();
 hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream);
 unsigned long long read_reset_exact_fallbacks();
@@ -345,10 +345,11 @@ const hipEvent_t* timing_marks(rt_scene* s, const RenderParams& P) {
 
 void enqueue_frame(rt_scene* s, const RenderParams& P, int samples, float* d_samples,
                    hipStream_t stream) {
-  const bool fast = s->mode == RT_TRAVERSAL_FAST;
+  const bool fast = s->mode != RT_TRAVERSAL_REFERENCE;
+  const bool cull = s->mode == RT_TRAVERSAL_CULL;
   if (samples <= 1) {
     hip_check(launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
-                            fast, s->deep, s->has_spheres, timing_marks(s, P), stream),
+                            fast, s->deep, s->has_spheres, cull, timing_marks(s, P), stream),
               "render launch");
     return;
   }
@@ -363,7 +364,7 @@ void enqueue_frame(rt_scene* s, const RenderParams& P, int samples, float* d_sam
     Q.tile_major = 0;
     Q.out = d_samples + (size_t)k * frame;
     hip_check(launch_render(Q, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
-                            fast, s->deep, s->has_spheres, timing_marks(s, Q), stream),
+                            fast, s->deep, s->has_spheres, cull, timing_marks(s, Q), stream),
               "render launch");
   }
   MsaaResolveParams M;
@@ -543,7 +544,8 @@ int rt_host_check_accel_xml(const char* xml_path, int treelet_leaves, long long*
 }
 
 int rt_set_traversal(rt_scene* s, int mode) {
-  if (!s || (mode != RT_TRAVERSAL_FAST && mode != RT_TRAVERSAL_REFERENCE))
+  if (!s || (mode != RT_TRAVERSAL_FAST && mode != RT_TRAVERSAL_REFERENCE &&
+             mode != RT_TRAVERSAL_CULL))
     return set_error(RT_E_INVALID, "rt_set_traversal: bad argument");
   s->mode = mode;
   return RT_OK;

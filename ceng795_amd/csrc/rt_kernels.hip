@@ -368,6 +368,9 @@ struct WaveStack {
   }
 };
 
+// Distance culling (RT_TRAVERSAL_CULL only): skip a child whose approximate entry distance
+// exceeds best_t (1 + 2^-8).  Not proven exact: a triangle whose computed t undershoots its
+// true distance by more than the margin (rays within ~1e-5 rad of its plane) could be missed.
 __device__ __forceinline__ float cull_limit(float t) { return t + t * 0x1p-8f; }
 
 // Node fetch.  Default: the wave-uniform address makes this a scalar (s_load) fetch.
@@ -639,7 +642,7 @@ __device__ __forceinline__ void batch_flush(WaveLeafLds& L, int n, const DevPrim
 
 // ------------------------------------------------------------------ closest hit
 // R rays per lane.  Returns the reference's (t, leaf) for every active ray: leaf < 0 = miss.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R>
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R, bool CULL = false>
 __device__ __forceinline__ void closest_hit(const RenderParams& P,
                                             const DevNode* __restrict__ nodes,
                                             const DevPrim* __restrict__ prims, int* spill,
@@ -750,7 +753,7 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
     for (int k = 0; k < R; k++) {  // leaves are done; only inner children are entered
       h0[k] &= N.child[0] >= 0;
       h1[k] &= N.child[1] >= 0;
-      if (FAST) {
+      if (FAST && CULL) {
         const float lim = cull_limit(best_t[k]);
         h0[k] = h0[k] && t0[k] <= lim;
         h1[k] = h1[k] && t1[k] <= lim;
@@ -772,7 +775,7 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
 // ------------------------------------------------------------------ shadow (any hit)
 // Occluded iff some leaf the ray may reach has 0 < t < thr — identical to the reference's
 // closest-hit shadow test `0 < t_closest < dist - eps` (HW2/Scene.cpp:123-127), appendix A.7.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R>
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R, bool CULL = false>
 __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* __restrict__ nodes,
                                          const DevPrim* __restrict__ prims, int* spill,
                                          const LaneRay (&r)[R], const bool (&active)[R],
@@ -870,7 +873,7 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
       alive[k] &= ~ballot(occ[k]);
       h0[k] &= N.child[0] >= 0;
       h1[k] &= N.child[1] >= 0;
-      if (FAST) {
+      if (FAST && CULL) {
         const float lim = cull_limit(thr[k]);
         h0[k] = h0[k] && t0[k] <= lim;
         h1[k] = h1[k] && t1[k] <= lim;
@@ -986,7 +989,7 @@ __device__ __forceinline__ unsigned long long* counter_row(const RenderParams& P
 
 // R selected tiles per wave (tile sel0 + k is ray k of every lane): one packet traversal
 // serves 64*R rays, so the per-visit overhead (node fetch, masks, stack) is shared.
-template <bool FAST, bool DEEP, bool SPHERES, int R>
+template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL>
 __device__ __forceinline__ void primary_packet(const RenderParams& P,
                                                const DevNode* __restrict__ nodes,
                                                const DevPrim* __restrict__ prims, int sel0,
@@ -1012,9 +1015,9 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
   float t[R];
   int leaf[R];
   if (ballot(any_skip))
-    closest_hit<true, FAST, DEEP, SPHERES, R>(P, nodes, prims, spill, ray, valid, t, leaf, dg);
+    closest_hit<true, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, ray, valid, t, leaf, dg);
   else
-    closest_hit<false, FAST, DEEP, SPHERES, R>(P, nodes, prims, spill, ray, valid, t, leaf, dg);
+    closest_hit<false, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, ray, valid, t, leaf, dg);
   const RenderParams& Pw = fresh_params(P);  // post-traversal fields: not live across it
   unsigned long long nvalid = 0, nhit = 0;
 #pragma unroll
@@ -1049,7 +1052,7 @@ __device__ __forceinline__ V3 hit_point(const RenderParams& P, const PacketPixel
 
 // Shadow rays of HW2/Scene.cpp:113-127: one bit per point light, set when the light is
 // occluded for this pixel's primary hit.  R tiles per wave as in primary_packet.
-template <bool FAST, bool DEEP, bool SPHERES, int R>
+template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL>
 __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
                                               const DevNode* __restrict__ nodes,
                                               const DevPrim* __restrict__ prims,
@@ -1089,9 +1092,9 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       }
       bool occ[R];
       if (ballot(any_skip))
-        occluded<true, FAST, DEEP, SPHERES, R>(P, nodes, prims, spill, sr, hit, thr, occ, dg);
+        occluded<true, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, sr, hit, thr, occ, dg);
       else
-        occluded<false, FAST, DEEP, SPHERES, R>(P, nodes, prims, spill, sr, hit, thr, occ, dg);
+        occluded<false, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, sr, hit, thr, occ, dg);
 #pragma unroll
       for (int k = 0; k < R; k++) bits[k] |= (occ[k] ? 1u : 0u) << (li - 32 * w);
     }
@@ -1546,7 +1549,7 @@ __device__ __forceinline__ void for_each_packet(const RenderParams& P, F&& f) {
   }
 }
 
-template <bool FAST, bool DEEP, bool SPHERES, int R>
+template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL>
 __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY void trace_primary_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
@@ -1556,11 +1559,11 @@ __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY vo
     const RenderParams& Q = fresh_params(P);
     const int sel0 = R == 1 ? packet_sel<W>(Q, p) : p * R;
     if (sel0 >= 0 && sel0 < Q.num_sel_tiles)
-      primary_packet<FAST, DEEP, SPHERES, R>(Q, nodes, prims, sel0, spill);
+      primary_packet<FAST, DEEP, SPHERES, R, CULL>(Q, nodes, prims, sel0, spill);
   });
 }
 
-template <bool FAST, bool DEEP, bool SPHERES, int R>
+template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL>
 __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY void trace_shadow_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims,
     const DevLight* __restrict__ lights) {
@@ -1571,7 +1574,7 @@ __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY vo
     const RenderParams& Q = fresh_params(P);
     const int sel0 = R == 1 ? packet_sel<W>(Q, p) : p * R;
     if (sel0 >= 0 && sel0 < Q.num_sel_tiles)
-      shadow_packet<FAST, DEEP, SPHERES, R>(Q, nodes, prims, lights, sel0, spill);
+      shadow_packet<FAST, DEEP, SPHERES, R, CULL>(Q, nodes, prims, lights, sel0, spill);
   });
 }
 
@@ -1602,7 +1605,7 @@ static inline void mark(const hipEvent_t* marks, int k, hipStream_t stream) {
   if (marks) (void)hipEventRecord(marks[k], stream);
 }
 
-template <bool FAST, bool DEEP, bool SPHERES>
+template <bool FAST, bool DEEP, bool SPHERES, bool CULL>
 static void launch_variant(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                            const float* normals, const DevMaterial* mats,
                            const DevLight* lights, int blocks, const hipEvent_t* marks,
@@ -1636,11 +1639,11 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
   T.work = S.work = nullptr;
 #endif
   mark(marks, 0, stream);
-  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, R>), dim3(tblocks),
+  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, R, CULL>), dim3(tblocks),
                      dim3(W * 64), tlds, stream, T, nodes, prims);
   mark(marks, 1, stream);
   if (P.num_lights > 0)
-    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, R>), dim3(tblocks),
+    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, R, CULL>), dim3(tblocks),
                        dim3(W * 64), tlds, stream, S, nodes, prims, lights);
   mark(marks, 2, stream);
   hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
@@ -1751,24 +1754,28 @@ hipError_t launch_quot_check(unsigned long long seed, long long count, unsigned 
 
 hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                          const float* normals, const DevMaterial* mats, const DevLight* lights,
-                         bool fast, bool deep, bool spheres, const hipEvent_t* marks,
+                         bool fast, bool deep, bool spheres, bool cull, const hipEvent_t* marks,
                          hipStream_t stream) {
   if (P.num_sel_tiles <= 0) return hipSuccess;
   const int blocks = (P.num_sel_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-  const int v = (fast ? 4 : 0) | (deep ? 2 : 0) | (spheres ? 1 : 0);
+  const int v = (fast && cull ? 8 : 0) | (fast ? 4 : 0) | (deep ? 2 : 0) | (spheres ? 1 : 0);
   switch (v) {
-#define RT_CASE(F, D, S)                                                                  \
-  case (F ? 4 : 0) | (D ? 2 : 0) | (S ? 1 : 0):                                           \
-    launch_variant<F, D, S>(P, nodes, prims, normals, mats, lights, blocks, marks, stream); \
+#define RT_CASE(F, D, S, C)                                                                  \
+  case (C ? 8 : 0) | (F ? 4 : 0) | (D ? 2 : 0) | (S ? 1 : 0):                                \
+    launch_variant<F, D, S, C>(P, nodes, prims, normals, mats, lights, blocks, marks, stream); \
     break;
-    RT_CASE(true, false, false)
-    RT_CASE(true, false, true)
-    RT_CASE(true, true, false)
-    RT_CASE(true, true, true)
-    RT_CASE(false, false, false)
-    RT_CASE(false, false, true)
-    RT_CASE(false, true, false)
-    RT_CASE(false, true, true)
+    RT_CASE(true, false, false, false)
+    RT_CASE(true, false, true, false)
+    RT_CASE(true, true, false, false)
+    RT_CASE(true, true, true, false)
+    RT_CASE(false, false, false, false)
+    RT_CASE(false, false, true, false)
+    RT_CASE(false, true, false, false)
+    RT_CASE(false, true, true, false)
+    RT_CASE(true, false, false, true)
+    RT_CASE(true, false, true, true)
+    RT_CASE(true, true, false, true)
+    RT_CASE(true, true, true, true)
 #undef RT_CASE
   }
   return hipGetLastError();

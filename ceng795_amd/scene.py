@@ -88,7 +88,8 @@ class Scene:
                           tuple(c.top_left), tuple(c.s_u), tuple(c.s_v))
 
     def set_traversal(self, mode: str) -> None:
-        m = {"fast": _lib.RT_TRAVERSAL_FAST, "reference": _lib.RT_TRAVERSAL_REFERENCE}[mode]
+        m = {"fast": _lib.RT_TRAVERSAL_FAST, "reference": _lib.RT_TRAVERSAL_REFERENCE,
+             "cull": _lib.RT_TRAVERSAL_CULL}[mode]
         check(lib().rt_set_traversal(self._h, m))
 
     def set_msaa_seed(self, seed: int) -> None:

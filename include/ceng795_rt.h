@@ -106,12 +106,17 @@ typedef struct rt_stats {
   double kernel_ms;             /* HIP-event time of the render kernel(s)  */
 } rt_stats;
 
-/* Traversal modes.  Both give the reference's result; see DESIGN.md §Traversal. */
+/* Traversal modes.  FAST and REFERENCE give the reference's result on every input (DESIGN.md
+ * §4.1); CULL is faster on some scenes but rests on an unproven numerical assumption. */
 enum {
-  RT_TRAVERSAL_FAST = 0,        /* near-first order, distance culling (default) */
-  RT_TRAVERSAL_REFERENCE = 1    /* visits every box the reference visits       */
+  RT_TRAVERSAL_FAST = 0,        /* culling tree over reference treelets, near-first order,
+                                   batched leaf tests (default; exact)                        */
+  RT_TRAVERSAL_REFERENCE = 1,   /* visits every box the reference visits, in its order        */
+  RT_TRAVERSAL_CULL = 2         /* FAST + distance culling: skips a child whose entry distance
+                                   exceeds best_t (1 + 2^-8) — exact unless a triangle's fp32 t
+                                   undershoots its true distance by that much (rays within
+                                   ~1e-5 rad of its plane); opt-in, never the default        */
 };
-
 typedef struct rt_scene rt_scene;
 
 /* Replaces Scene::Scene's object + BVH construction (HW2/Scene.cpp:378-449 and

@@ -26,6 +26,11 @@ CATALOGUE = {
                       "root is a sphere: negative-t hits shaded (Sphere.h:43-45)"),
     "single_triangle": (lambda: G.single_triangle_scene(64, 64), "root is a triangle"),
     "c2": (lambda: G.heightfield_scene(187, 800, 800, name="c2.png"), "C2 69k tris 800x800"),
+    # grazing rays: the fp32 triangle test's t is ill-conditioned (exactness of any culling)
+    "graze_plane": (lambda: G.grazing_plane_scene(64, 96, 64),
+                    "flat grid, rays 1e-7..1e-4 rad above its plane"),
+    "graze_hf": (lambda: G.grazing_heightfield_scene(187, 256, 64),
+                 "C2 height field skimmed at < 1e-3 rad"),
 }
 
 # Scenes whose MaxRecursionDepth > 0 with mirror / dielectric materials.
@@ -52,7 +57,7 @@ MSAA = {
 }
 
 SMALL = ["c1", "hf_small", "hf_side", "soup1", "soup2", "soup3", "single_sphere",
-         "single_triangle"]
+         "single_triangle", "graze_plane", "graze_hf"]
 
 
 def write(name: str, directory: str) -> str:

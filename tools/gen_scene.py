@@ -153,6 +153,38 @@ class SceneSpec:
         return "\n".join(out) + "\n"
 
 
+# --------------------------------------------------------------------------- grazing rays
+def grazing_plane_scene(n: int, width: int, height: int, cam_height: float = 1e-3,
+                        rows_angle: Tuple[float, float] = (1e-7, 1e-4)) -> SceneSpec:
+    """A flat n x n vertex grid on y = 0 (x in [-50, 50], z in [-2000, 0]) seen by a camera
+    cam_height above it looking along -z: row angles below the horizon run over rows_angle
+    (radians), so rays meet the triangles' plane at grazing angles down to ~1e-7, where the
+    fp32 Cramer quotients of Triangle::intersect (HW2/Triangle.cpp:35-65) are ill-conditioned
+    and a hit's computed t can be far from its true distance."""
+    lines = []
+    for j in range(n):
+        z = -2000.0 + 2000.0 * j / (n - 1)
+        for i in range(n):
+            x = -50.0 + 100.0 * i / (n - 1)
+            lines.append("%.6f %.6f %.6f" % (x, 0.0, z))
+    lo, hi = rows_angle
+    cam = Camera((0, cam_height, 0), (0, 0, -1), (0, 1, 0), (-0.5, 0.5, -hi, -lo), 1,
+                 width, height, "graze_plane.png")
+    return SceneSpec(
+        cameras=[cam], ambient=(25, 25, 25), lights=[((0, 10, -50), (5e5, 5e5, 5e5))],
+        materials=[Material(ambient=(1, 1, 1), diffuse=(1, 1, 1), specular=(1, 1, 1), phong=1)],
+        vertex_text="\n".join(lines), meshes=[(1, "\n".join(heightfield_faces(n)))])
+
+
+def grazing_heightfield_scene(n: int, width: int, height: int) -> SceneSpec:
+    """The height field of SURVEY §8(d) seen from just above its highest point, looking along
+    -z with row angles 0..1e-3 rad below the horizon: rays skim the bumps."""
+    spec = heightfield_scene(n, width, height)
+    spec.cameras = [Camera((0, -1.42, -1.9), (0, 0, -1), (0, 1, 0), (-0.6, 0.6, -1e-3, 0.0), 1,
+                           width, height, "graze_hf.png")]
+    return spec
+
+
 # --------------------------------------------------------------------------- heightfield
 def heightfield_vertices(n: int, seed: int = 795) -> List[str]:
     rng = random.Random(seed)

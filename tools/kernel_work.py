@@ -29,10 +29,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("xml")
     ap.add_argument("--camera", type=int, default=0)
-    ap.add_argument("--traversal", default="fast")
+    ap.add_argument("--traversal", default="fast", choices=["fast", "reference", "cull"])
     a = ap.parse_args()
-    if os.environ.get("CENG795_LIB") != "diag":
-        raise SystemExit("run with CENG795_LIB=diag (the RT_DIAG build)")
+    if "diag" not in os.environ.get("CENG795_LIB", ""):
+        raise SystemExit("run with CENG795_LIB=diag (an RT_DIAG build)")
     import torch
     import ceng795_amd
     with ceng795_amd.Scene(a.xml, device=0, traversal=a.traversal) as s:
