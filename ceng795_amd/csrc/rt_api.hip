@@ -29,6 +29,7 @@ unsigned long long read_reset_exact_fallbacks();
 hipError_t launch_quot_check(unsigned long long seed, long long count, unsigned long long* counts,
                              hipStream_t stream);
 bool diag_build();
+long long read_reset_timeline(unsigned long long* out, long long max_values);
 void write_png(const std::string& path, const float* rgb, int w, int h);
 }  // namespace rt
 
@@ -193,13 +194,8 @@ size_t frame_floats(const HostScene& h, int sel_tiles) {
 
 int occ_words(const HostScene& h) { return std::max(1, ((int)h.lights.size() + 31) / 32); }
 
-// A counter buffer: kCounterRows x kCounterWidth ray counters, then 8 u64 = 16 int packet
-// counters of the persistent traversal kernels (zeroed by every launch).
-constexpr size_t kCounterAlloc = (size_t)kCounterWidth * kCounterRows + 8;
-int* work_counters(unsigned long long* counters) {
-  return reinterpret_cast<int*>(counters + (size_t)kCounterWidth * kCounterRows);
-}
-
+// A counter buffer: kCounterRows x kCounterWidth ray counters.
+constexpr size_t kCounterAlloc = (size_t)kCounterWidth * kCounterRows;
 int create_from_host(rt_scene* s, int device) {
   if (device < 0) hip_check(hipGetDevice(&device), "hipGetDevice");
   s->device = device;
@@ -227,10 +223,10 @@ int create_from_host(rt_scene* s, int device) {
   s->d_anc = upload(h.ancestry, "upload ancestry");
   s->d_mats = upload(h.materials, "upload materials");
   s->d_lights = upload(h.lights, "upload lights");
-  // ray counters + the persistent traversal kernels' 16 packet counters (RenderParams::work)
+  // ray counters
   hip_check(hipMalloc(&s->d_counters, sizeof(unsigned long long) * kCounterAlloc),
             "alloc counters");
-  hip_check(hipMemset(s->d_counters, 0, sizeof(unsigned long long) * kCounterWidth * kCounterRows),
+  hip_check(hipMemset(s->d_counters, 0, sizeof(unsigned long long) * kCounterAlloc),
             "zero counters");
   size_t most = 1;
   for (const rt_camera& c : h.cameras) {
@@ -300,7 +296,6 @@ RenderParams make_params(const rt_scene* s, int cam, int row0, int row_stride, i
   P.occ = s->d_occ;
   P.occ_words = occ_words(h);
   P.counters = counters ? s->d_counters : nullptr;
-  P.work = work_counters(s->d_counters);  // shared by the scene's rt_render_device calls
   return P;
 }
 
@@ -650,6 +645,13 @@ int rt_debug_counters(rt_scene* s, long long* out16) {
   });
 }
 
+long long rt_debug_timeline(unsigned long long* out, long long max_values) {
+  if (!out || max_values < 0) return set_error(RT_E_INVALID, "rt_debug_timeline: bad argument");
+  const long long n = read_reset_timeline(out, max_values);
+  if (n < 0) return set_error(RT_E_INVALID, "rt_debug_timeline: buffer too small or copy failed");
+  return n;
+}
+
 int rt_debug_quotient_check(int device, unsigned long long seed, long long count,
                             long long* out2) {
   if (!out2 || count < 0) return set_error(RT_E_INVALID, "rt_debug_quotient_check: bad argument");
@@ -691,7 +693,6 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
                 "zero counters");
       RenderParams P = make_params(s, cam, row0, row_stride, 0, 1, 0, x->d_out, true);
       P.counters = x->d_cnt;
-      P.work = work_counters(x->d_cnt);
       const size_t lanes = (size_t)kTile * kTile * (size_t)std::max(1, P.num_sel_tiles);
       ensure(x->d_hits, x->hits_records, lanes, "alloc hit records");
       P.hits = x->d_hits;

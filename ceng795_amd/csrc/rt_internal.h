@@ -27,7 +27,9 @@ enum : int {
   // RT_DIAG builds only: packet-level traversal work
   kCntPrimNodes = 4, kCntPrimNodeLanes = 5, kCntPrimLeaves = 6, kCntPrimLeafLanes = 7,
   kCntShadNodes = 8, kCntShadNodeLanes = 9, kCntShadLeaves = 10, kCntShadLeafLanes = 11,
-  kCntExactBox = 12
+  kCntExactBox = 12,
+  // subtree sharing: pieces run by a wave other than the packet's owner
+  kCntShared = 13
 };
 
 // DevNode::pad of the culling-tree nodes (accel_build.cpp); reference nodes have pad == 0.
@@ -91,9 +93,13 @@ struct DevLight {
   float pad[2];
 };
 
+// Primary-hit record, 8 B per pixel: x = DFS leaf index (-1 miss, -2 outside the image),
+// y = the bits of t.  As one little-endian u64 it is the key (t bits << 32) | leaf whose
+// minimum is the reference's (t, DFS leaf) rule (rt_kernels.hip, batch_flush).
 struct alignas(8) int2_t {
   int32_t x, y;
 };
+
 
 enum RootKind : int32_t { kRootNode = 0, kRootTriangle = 1, kRootSphere = 2 };
 
@@ -139,7 +145,6 @@ struct RenderParams {
   int tiles_x, tiles_total, tile_begin, tile_step, num_sel_tiles;
   int tile_major;
   int tile_block;  // traversal kernels: workgroups take 2-D blocks of tiles (rt_kernels.hip)
-  int* work;       // 16 packet counters for persistent traversal waves (null: one packet/wave)
   // jittered MSAA (HW2/Scene.cpp:32-69): 0 = pixel centres; else this launch traces sample
   // msaa_s = x*n + y of every pixel, whose minstd_rand0 draws 2s+1, 2s+2 are
   // u0 * msaa_mul[0], u0 * msaa_mul[1] (mod 2^31-1), u0 the pixel's seeded state.

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "rt_internal.h"
 
@@ -350,6 +351,20 @@ struct WaveStack {
     }
     sp++;
   }
+  // The oldest entry (lane 0: the shallowest pending subtree) and its removal, for donation
+  // (!DEEP, R == 1 only): entries 1..sp-1 move down one lane.
+  __device__ __forceinline__ void bottom(int& n, uint64_t& m) const {
+    n = __builtin_amdgcn_readlane(node, 0);
+    m = (uint64_t)(unsigned)__builtin_amdgcn_readlane(mlo[0], 0) |
+        ((uint64_t)(unsigned)__builtin_amdgcn_readlane(mhi[0], 0) << 32);
+  }
+  __device__ __forceinline__ void drop_bottom() {
+    const int src = (lane_id() + 1) << 2;
+    node = __builtin_amdgcn_ds_bpermute(src, node);
+    mlo[0] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)mlo[0]);
+    mhi[0] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)mhi[0]);
+    sp--;
+  }
   __device__ __forceinline__ void pop(int& n, uint64_t (&m)[R]) {
     sp--;
     if (!DEEP) {
@@ -579,17 +594,12 @@ constexpr int kBatchCap = kBatchFlush + 128;  // < kBatchFlush pending + 2 x 64 
 #ifndef RT_TRACE_WAVES
 #define RT_TRACE_WAVES 4
 #endif
-constexpr int kLdsWaves = RT_TRACE_WAVES > kWavesPerBlock ? RT_TRACE_WAVES : kWavesPerBlock;
 
 struct WaveLeafLds {
   unsigned long long q[kBatchCap];  // lo 32: leaf index, hi 32: lane
   unsigned long long key[64];       // per lane: closest-hit key, or shadow flag
 };
 
-__device__ __forceinline__ WaveLeafLds& wave_leaf_lds() {
-  __shared__ WaveLeafLds s[kLdsWaves];  // 2 KiB per wave
-  return s[threadIdx.x >> 6];
-}
 
 #if defined(RT_EXP_NOBATCH)
 constexpr bool kBatchLeaves = false;
@@ -640,14 +650,130 @@ __device__ __forceinline__ void batch_flush(WaveLeafLds& L, int n, const DevPrim
   }
 }
 
+// ------------------------------------------------------------------ subtree sharing
+// A workgroup's packets cost unequal amounts (tools/timeline.py: C3 primary packets take 60 to
+// 265 us), and a workgroup keeps its slot until its last wave ends, so waves that finish early
+// idle while a heavy packet runs: the C3 primary kernel held ~90 % of its wave slots in the bulk
+// of the frame and spent its last 40 % draining.  With sharing, the waves of a workgroup split
+// their packets' traversals between them through LDS.  A wave without work raises its bit in
+// `want` and waits at its inbox; a traversing wave that sees a raised bit (checked every 4th
+// visit) claims that wave (atomic and of the bit) and hands it its OLDEST stack entry — the
+// shallowest pending subtree — as (owner packet, light, node, lane mask).  The helper rebuilds
+// the owner packet's rays bit for bit and traverses that subtree exactly as the owner would.
+// Each piece's answer merges into the owner's per-lane result in LDS — closest hit by 64-bit
+// min of the (t bits, DFS leaf) key (the reference's rule, §4.1), shadow by or — and after a
+// workgroup barrier every wave writes its own packet.  A claimed wave's bit stays clear until
+// it is idle again, so `want` == all waves means nobody traverses and nobody can hand out work:
+// every wave then leaves.  Workgroup-local and lock-free: LDS atomics only (a lock taken and
+// released in a polling loop measured as a livelock on gfx950).
+struct ShareEntry {
+  unsigned long long mask;
+  int node, owner, light, pad;
+};
+
+template <int W>
+struct BlockShare {
+  int want;     // bit i: wave i waits for work
+  int flag[W];  // inbox i is full
+  int sel[W];   // each wave's own packet (tile), -1 for none
+  ShareEntry box[W];
+  unsigned long long res[W][64];  // per packet and lane: primary key / shadow light bits
+};
+
+__device__ __forceinline__ int lds_load(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+struct NoDonor {
+  static constexpr bool kOn = false;
+  __device__ __forceinline__ bool tick() { return false; }
+  __device__ __forceinline__ bool donate(int, uint64_t) { return false; }
+};
+
+// The donation policy of one traversal piece in a sharing workgroup.
+template <int W>
+struct Sharer {
+  static constexpr bool kOn = true;
+  BlockShare<W>* S;
+  int owner, light, visits;  // wave-uniform
+  __device__ __forceinline__ bool tick() {
+#ifdef RT_EXP_NODONATE
+    return false;
+#else
+    return (++visits & 3) == 0 && lds_load(&S->want) != 0;
+#endif
+  }
+  __device__ __forceinline__ bool donate(int node, uint64_t mask) {
+    int ok = 0;
+    if (lane_id() == 0) {
+      int m = lds_load(&S->want);
+      while (m) {
+        const int i = __builtin_ctz((unsigned)m), bit = 1 << i;
+        const int old = atomicAnd(&S->want, ~bit);
+        if (old & bit) {  // wave i is ours
+          S->box[i].mask = mask;
+          S->box[i].node = node;
+          S->box[i].owner = owner;
+          S->box[i].light = light;
+          __hip_atomic_store(&S->flag[i], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          ok = 1;
+          break;
+        }
+        m = old & ~bit;
+      }
+    }
+    return uniform(ok) != 0;
+  }
+};
+
+// Called by a wave whose current piece is done: raises its want bit and waits for an entry.
+// False once every wave of the workgroup wants work (no one is left to hand any out).
+template <int W>
+__device__ __forceinline__ bool share_next(BlockShare<W>& S, int& owner, int& node, uint64_t& mask,
+                                           int& light) {
+  const int wv = (int)threadIdx.x >> 6;
+  int got = 0, o = 0, n = 0, l = 0;
+  unsigned lo = 0, hi = 0;
+  if (lane_id() == 0) {
+    atomicOr(&S.want, 1 << wv);
+    for (;;) {
+      if (__hip_atomic_load(&S.flag[wv], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        const ShareEntry& e = S.box[wv];
+        lo = (unsigned)e.mask;
+        hi = (unsigned)(e.mask >> 32);
+        n = e.node;
+        o = e.owner;
+        l = e.light;
+        __hip_atomic_store(&S.flag[wv], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        got = 1;
+        break;
+      }
+      if (lds_load(&S.want) == (1 << W) - 1) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  if (!uniform(got)) return false;
+  owner = uniform(o);
+  node = uniform(n);
+  light = uniform(l);
+  mask = (uint64_t)(unsigned)uniform((int)lo) | ((uint64_t)(unsigned)uniform((int)hi) << 32);
+  return true;
+}
+
 // ------------------------------------------------------------------ closest hit
 // R rays per lane.  Returns the reference's (t, leaf) for every active ray: leaf < 0 = miss.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R, bool CULL = false>
+// DN: the donation policy (NoDonor, or Sharer in sharing workgroups, R == 1 and !DEEP only);
+// start_node >= 0: traverse the shared subtree (start_node, start_mask) instead of the tree.
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R, bool CULL = false,
+          class DN = NoDonor>
 __device__ __forceinline__ void closest_hit(const RenderParams& P,
                                             const DevNode* __restrict__ nodes,
-                                            const DevPrim* __restrict__ prims, int* spill,
+                                            const DevPrim* __restrict__ prims, int* spill, WaveLeafLds& L,
                                             const LaneRay (&r)[R], const bool (&active)[R],
-                                            float (&best_t)[R], int (&best_leaf)[R], Diag& dg) {
+                                            float (&best_t)[R], int (&best_leaf)[R], Diag& dg,
+                                            DN& dn, int start_node = -1,
+                                            uint64_t start_mask = 0) {
+  static_assert(!DN::kOn || (R == 1 && !DEEP), "donation needs the one-ray-per-lane lane stack");
 #pragma unroll
   for (int k = 0; k < R; k++) {
     best_t[k] = RT_INF;
@@ -665,17 +791,22 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
     return;
   }
   const bool accel = FAST && P.accel_root >= 0;  // culling tree over treelets (§4.4)
+  const bool task = DN::kOn && start_node >= 0;
   uint64_t m[R];
+  if (task) {
+    m[0] = start_mask & ballot(active[0]);
+  } else {
 #pragma unroll
-  for (int k = 0; k < R; k++) {
-    float tn, tf;
-    bool acc, und;
-    if (accel) {
-      slab_span<SKIP>(P.accel_box, r[k], tn, tf);
-      m[k] = ballot(active[k] && decide_cull(tn, tf));
-    } else {
-      slab_fast<SKIP>(P.root_box, r[k], tn, acc, und);
-      m[k] = ballot(active[k] && (acc || (und && box_exact(P.root_box, r[k]))));
+    for (int k = 0; k < R; k++) {
+      float tn, tf;
+      bool acc, und;
+      if (accel) {
+        slab_span<SKIP>(P.accel_box, r[k], tn, tf);
+        m[k] = ballot(active[k] && decide_cull(tn, tf));
+      } else {
+        slab_fast<SKIP>(P.root_box, r[k], tn, acc, und);
+        m[k] = ballot(active[k] && (acc || (und && box_exact(P.root_box, r[k]))));
+      }
     }
   }
   if (!any_of(m)) return;
@@ -686,10 +817,9 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
 #pragma unroll
   for (int k = 0; k < R; k++) everyone[k] = ~0ull;
   constexpr bool batch = kBatchLeaves && R == 1;
-  WaveLeafLds& L = wave_leaf_lds();
   int pending = 0;
   if (batch) L.key[lane] = kNoHitKey;
-  int node = accel ? P.accel_root : P.root_ref;
+  int node = task ? start_node : (accel ? P.accel_root : P.root_ref);
   for (;;) {
     if constexpr (batch) {  // between visits: only the ray, the stack and best_t are live
       if (pending >= kBatchFlush) {
@@ -698,6 +828,14 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
         const unsigned long long key = L.key[lane];
         best_t[0] = __uint_as_float((unsigned)(key >> 32));
         best_leaf[0] = (int)(unsigned)key;
+      }
+    }
+    if constexpr (DN::kOn) {  // hand the oldest pending subtree to the work queue
+      if (dn.tick() && st.sp > 0) {
+        int n0;
+        uint64_t m0;
+        st.bottom(n0, m0);
+        if (dn.donate(n0, m0)) st.drop_bottom();
       }
     }
     const DevNode N = load_node(nodes, node);
@@ -775,11 +913,14 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
 // ------------------------------------------------------------------ shadow (any hit)
 // Occluded iff some leaf the ray may reach has 0 < t < thr — identical to the reference's
 // closest-hit shadow test `0 < t_closest < dist - eps` (HW2/Scene.cpp:123-127), appendix A.7.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R, bool CULL = false>
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R, bool CULL = false,
+          class DN = NoDonor>
 __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* __restrict__ nodes,
-                                         const DevPrim* __restrict__ prims, int* spill,
+                                         const DevPrim* __restrict__ prims, int* spill, WaveLeafLds& L,
                                          const LaneRay (&r)[R], const bool (&active)[R],
-                                         const float (&thr)[R], bool (&occ)[R], Diag& dg) {
+                                         const float (&thr)[R], bool (&occ)[R], Diag& dg,
+                                         DN& dn, int start_node = -1, uint64_t start_mask = 0) {
+  static_assert(!DN::kOn || (R == 1 && !DEEP), "donation needs the one-ray-per-lane lane stack");
 #pragma unroll
   for (int k = 0; k < R; k++) occ[k] = false;
   if (P.root_kind != kRootNode) {
@@ -792,31 +933,35 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
     return;
   }
   const bool accel = FAST && P.accel_root >= 0;
+  const bool task = DN::kOn && start_node >= 0;
   uint64_t m[R], alive[R];
+  if (task) {
+    m[0] = alive[0] = start_mask & ballot(active[0] && thr[0] > 0.0f);
+  } else {
 #pragma unroll
-  for (int k = 0; k < R; k++) {
-    float tn, tf;
-    bool acc, und;
-    // thr <= 0 (or NaN): nothing can satisfy 0 < t < thr
-    if (accel) {
-      slab_span<SKIP>(P.accel_box, r[k], tn, tf);
-      m[k] = ballot(active[k] && thr[k] > 0.0f && decide_cull(tn, tf));
-    } else {
-      slab_fast<SKIP>(P.root_box, r[k], tn, acc, und);
-      m[k] = ballot(active[k] && thr[k] > 0.0f &&
-                    (acc || (und && box_exact(P.root_box, r[k]))));
+    for (int k = 0; k < R; k++) {
+      float tn, tf;
+      bool acc, und;
+      // thr <= 0 (or NaN): nothing can satisfy 0 < t < thr
+      if (accel) {
+        slab_span<SKIP>(P.accel_box, r[k], tn, tf);
+        m[k] = ballot(active[k] && thr[k] > 0.0f && decide_cull(tn, tf));
+      } else {
+        slab_fast<SKIP>(P.root_box, r[k], tn, acc, und);
+        m[k] = ballot(active[k] && thr[k] > 0.0f &&
+                      (acc || (und && box_exact(P.root_box, r[k]))));
+      }
+      alive[k] = m[k];
     }
-    alive[k] = m[k];
   }
   if (!any_of(m)) return;
   const int lane = lane_id();
   WaveStack<DEEP, R> st;
   st.lds = spill;
   constexpr bool batch = kBatchLeaves && R == 1;
-  WaveLeafLds& L = wave_leaf_lds();
   int pending = 0;
   if (batch) L.key[lane] = 0ull;
-  int node = accel ? P.accel_root : P.root_ref;
+  int node = task ? start_node : (accel ? P.accel_root : P.root_ref);
   for (;;) {
     if constexpr (batch) {  // between visits; a lane found occluded stops entering nodes
       if (pending >= kBatchFlush) {
@@ -826,6 +971,15 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
         alive[0] &= ~ballot(occ[0]);
         m[0] &= alive[0];
         if (!m[0] && !advance(st, 0, 0, m, m, thr, thr, node, m, alive)) break;
+      }
+    }
+    if constexpr (DN::kOn) {  // hand the oldest pending subtree (still-unoccluded lanes) over
+      if (dn.tick() && st.sp > 0) {
+        int n0;
+        uint64_t m0;
+        st.bottom(n0, m0);
+        m0 &= alive[0];
+        if (!m0 || dn.donate(n0, m0)) st.drop_bottom();
       }
     }
     const DevNode N = load_node(nodes, node);
@@ -987,13 +1141,19 @@ __device__ __forceinline__ unsigned long long* counter_row(const RenderParams& P
   return P.counters + kCounterWidth * (sel % kCounterSlots);
 }
 
+__device__ __forceinline__ unsigned long long hit_key(int2_t rec) {
+  return ((unsigned long long)(unsigned)rec.y << 32) | (unsigned)rec.x;
+}
+__device__ __forceinline__ float hit_t(int2_t rec) { return __int_as_float(rec.y); }
+__device__ __forceinline__ int hit_leaf(int2_t rec) { return rec.x; }
+
 // R selected tiles per wave (tile sel0 + k is ray k of every lane): one packet traversal
 // serves 64*R rays, so the per-visit overhead (node fetch, masks, stack) is shared.
 template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL>
 __device__ __forceinline__ void primary_packet(const RenderParams& P,
                                                const DevNode* __restrict__ nodes,
                                                const DevPrim* __restrict__ prims, int sel0,
-                                               int* spill) {
+                                               int* spill, WaveLeafLds& L) {
   PacketPixel q[R];
   LaneRay ray[R];
   bool valid[R];
@@ -1014,18 +1174,21 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
   Diag dg;
   float t[R];
   int leaf[R];
+  NoDonor nd;
   if (ballot(any_skip))
-    closest_hit<true, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, ray, valid, t, leaf, dg);
+    closest_hit<true, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, L, ray, valid, t, leaf,
+                                                    dg, nd);
   else
-    closest_hit<false, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, ray, valid, t, leaf, dg);
+    closest_hit<false, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, L, ray, valid, t, leaf,
+                                                     dg, nd);
   const RenderParams& Pw = fresh_params(P);  // post-traversal fields: not live across it
   unsigned long long nvalid = 0, nhit = 0;
 #pragma unroll
   for (int k = 0; k < R; k++) {
     if (sel0 + k < Pw.num_sel_tiles) {
-      int2_t rec;
-      rec.x = __float_as_int(t[k]);
-      rec.y = valid[k] ? leaf[k] : -2;  // -1 miss, -2 outside the image
+      int2_t rec;  // key layout: leaf low, t bits high (rt_internal.h)
+      rec.x = valid[k] ? leaf[k] : -2;  // -1 miss, -2 outside the image
+      rec.y = __float_as_int(t[k]);
       Pw.hits[(size_t)(sel0 + k) * (kTile * kTile) + q[k].lane] = rec;
     }
     nvalid += __builtin_popcountll(ballot(valid[k]));
@@ -1044,6 +1207,33 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
   }
 }
 
+// One piece of a packet in a sharing workgroup: the closest hit of tile sel's rays over the
+// whole tree (node < 0) or over the shared subtree (node, mask); returns this lane's key.
+template <bool FAST, bool SPHERES, bool CULL, int W>
+__device__ __forceinline__ unsigned long long primary_piece(const RenderParams& P,
+                                                            const DevNode* __restrict__ nodes,
+                                                            const DevPrim* __restrict__ prims,
+                                                            int sel, WaveLeafLds& L, Sharer<W>& sh,
+                                                            int node, uint64_t mask, Diag& dg) {
+  const PacketPixel q = packet_pixel(P, sel);
+  const bool valid[1] = {q.valid};
+  LaneRay ray[1] = {make_ray(ld3(P.cam_e), primary_dir(P, q.px, q.py), P.quot_ok)};
+  asm volatile("" : "+v"(ray[0].o.x), "+v"(ray[0].o.y), "+v"(ray[0].o.z));  // (primary_packet)
+  const bool any_skip = valid[0] && (ray[0].skip0 || ray[0].skip1 || ray[0].skip2);
+  float t[1];
+  int leaf[1];
+  if (ballot(any_skip))
+    closest_hit<true, FAST, false, SPHERES, 1, CULL>(P, nodes, prims, nullptr, L, ray, valid, t,
+                                                     leaf, dg, sh, node, mask);
+  else
+    closest_hit<false, FAST, false, SPHERES, 1, CULL>(P, nodes, prims, nullptr, L, ray, valid, t,
+                                                      leaf, dg, sh, node, mask);
+  int2_t rec;
+  rec.x = leaf[0];
+  rec.y = __float_as_int(t[0]);
+  return leaf[0] >= 0 ? hit_key(rec) : kNoHitKey;
+}
+
 // Hit point and normal of a primary hit, rebuilt from its {t, leaf} record exactly as
 // trace_ray computes them (HW2/Scene.cpp:101-105; Sphere.h:42,50 for sphere normals).
 __device__ __forceinline__ V3 hit_point(const RenderParams& P, const PacketPixel& q, float t) {
@@ -1057,7 +1247,7 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
                                               const DevNode* __restrict__ nodes,
                                               const DevPrim* __restrict__ prims,
                                               const DevLight* __restrict__ lights, int sel0,
-                                              int* spill) {
+                                              int* spill, WaveLeafLds& L) {
   Diag dg;
   for (int w = 0; w < P0.occ_words; w++) {
     unsigned bits[R];
@@ -1069,7 +1259,7 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       // the occlusion bits is live across the traversal (register pressure, not traffic: the
       // 8-B record is an L2 hit)
       const RenderParams& P = fresh_params(P0);
-      const DevLight& L = lights[li];
+      const DevLight& lt = lights[li];
       LaneRay sr[R];
       float thr[R];
       bool hit[R];
@@ -1078,12 +1268,12 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       for (int k = 0; k < R; k++) {
         const PacketPixel q = packet_pixel(P, sel0 + k);
         int2_t rec;
-        rec.x = 0;
-        rec.y = -2;
+        rec.x = -2;
+        rec.y = 0;
         if (sel0 + k < P.num_sel_tiles) rec = P.hits[(size_t)(sel0 + k) * (kTile * kTile) + q.lane];
-        hit[k] = rec.y >= 0;
-        const V3 pk = hit[k] ? hit_point(P, q, __int_as_float(rec.x)) : v3(0, 0, 0);
-        const V3 ld = ld3(L.position) - pk;
+        hit[k] = hit_leaf(rec) >= 0;
+        const V3 pk = hit[k] ? hit_point(P, q, hit_t(rec)) : v3(0, 0, 0);
+        const V3 ld = ld3(lt.position) - pk;
         const V3 wi = normalize(ld);
         const float dist = length(ld);
         sr[k] = make_ray(pk + wi * P.eps, wi, P.quot_ok);  // p + eps * w_i
@@ -1091,10 +1281,11 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
         any_skip |= hit[k] && (sr[k].skip0 || sr[k].skip1 || sr[k].skip2);
       }
       bool occ[R];
+      NoDonor nd;
       if (ballot(any_skip))
-        occluded<true, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, sr, hit, thr, occ, dg);
+        occluded<true, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, L, sr, hit, thr, occ, dg, nd);
       else
-        occluded<false, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, sr, hit, thr, occ, dg);
+        occluded<false, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, L, sr, hit, thr, occ, dg, nd);
 #pragma unroll
       for (int k = 0; k < R; k++) bits[k] |= (occ[k] ? 1u : 0u) << (li - 32 * w);
     }
@@ -1110,7 +1301,7 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
   for (int k = 0; k < R; k++) {
     const bool inside = sel0 + k < Pc.num_sel_tiles;
     nhit += __builtin_popcountll(
-        ballot(inside && Pc.hits[(size_t)(sel0 + k) * (kTile * kTile) + lane_id()].y >= 0));
+        ballot(inside && hit_leaf(Pc.hits[(size_t)(sel0 + k) * (kTile * kTile) + lane_id()]) >= 0));
   }
   if (Pc.counters && lane_id() == 0) {
     unsigned long long* c = counter_row(Pc, sel0);
@@ -1124,6 +1315,38 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
   }
 }
 
+// One piece of a packet's shadow rays in a sharing workgroup: point light li for tile sel0
+// (HW2/Scene.cpp:113-127 as in shadow_packet), over the whole tree (start_node < 0) or over a
+// shared subtree.  Returns this lane's occlusion.
+template <bool FAST, bool SPHERES, bool CULL, class DN>
+__device__ __forceinline__ bool shadow_piece(const RenderParams& P0,
+                                            const DevNode* __restrict__ nodes,
+                                            const DevPrim* __restrict__ prims,
+                                            const DevLight* __restrict__ lights, int sel0, int li,
+                                            int* spill, WaveLeafLds& L, DN& dn, int start_node,
+                                            uint64_t start_mask, Diag& dg) {
+  const RenderParams& P = P0;
+  const DevLight& lt = lights[li];
+  const PacketPixel q = packet_pixel(P, sel0);
+  const int2_t rec = P.hits[(size_t)sel0 * (kTile * kTile) + q.lane];
+  bool hit[1] = {hit_leaf(rec) >= 0};
+  const V3 pk = hit[0] ? hit_point(P, q, hit_t(rec)) : v3(0, 0, 0);
+  const V3 ld = ld3(lt.position) - pk;
+  const V3 wi = normalize(ld);
+  const float dist = length(ld);
+  LaneRay sr[1] = {make_ray(pk + wi * P.eps, wi, P.quot_ok)};  // p + eps * w_i
+  float thr[1] = {dist - P.eps};
+  const bool any_skip = hit[0] && (sr[0].skip0 || sr[0].skip1 || sr[0].skip2);
+  bool occ[1];
+  if (ballot(any_skip))
+    occluded<true, FAST, false, SPHERES, 1, CULL>(P, nodes, prims, spill, L, sr, hit, thr, occ, dg,
+                                                  dn, start_node, start_mask);
+  else
+    occluded<false, FAST, false, SPHERES, 1, CULL>(P, nodes, prims, spill, L, sr, hit, thr, occ,
+                                                   dg, dn, start_node, start_mask);
+  return occ[0];
+}
+
 // Local shading of HW2/Scene.cpp:101-138 given the occlusion bits, in the reference's
 // accumulation order: ambient, then per light diffuse then specular.  No traversal here, so
 // the fp64 pow (HW2 calls ::pow(double, double)) costs no occupancy in the traversal kernels.
@@ -1135,13 +1358,13 @@ __device__ __forceinline__ void shade_pixel(const RenderParams& P,
   const PacketPixel q = packet_pixel(P, sel);
   const size_t pix = (size_t)sel * (kTile * kTile) + q.lane;
   const int2_t rec = P.hits[pix];
-  const bool valid = rec.y != -2;
-  const bool hit = rec.y >= 0;
+  const bool valid = hit_leaf(rec) != -2;
+  const bool hit = hit_leaf(rec) >= 0;
   V3 color = v3(0.0f, 0.0f, 0.0f);
   if (hit) {
-    const int leaf = rec.y;
+    const int leaf = hit_leaf(rec);
     const V3 e = ld3(P.cam_e);
-    const V3 p = hit_point(P, q, __int_as_float(rec.x));
+    const V3 p = hit_point(P, q, hit_t(rec));
     const DevPrim& pr = prims[leaf];
     const V3 n = pr.kind == kPrimTriangle ? ld3(normals + 4 * leaf) : normalize(p - ld3(pr.v0));
     const DevMaterial& m = mats[pr.material];
@@ -1225,7 +1448,7 @@ template <bool FAST, bool DEEP, bool SPHERES>
 __device__ __forceinline__ V3 local_color(const RenderParams& P, const DevNode* __restrict__ nodes,
                                           const DevPrim* __restrict__ prims,
                                           const DevMaterial* __restrict__ mats,
-                                          const DevLight* __restrict__ lights, int* spill,
+                                          const DevLight* __restrict__ lights, int* spill, WaveLeafLds& L,
                                           bool shade, V3 o, V3 p, V3 n, int mat, Diag& dg,
                                           unsigned long long& shadow_rays) {
   V3 color = v3(0.0f, 0.0f, 0.0f);
@@ -1233,8 +1456,8 @@ __device__ __forceinline__ V3 local_color(const RenderParams& P, const DevNode* 
   if (shade) color = color + ld3(m.ambient) * ld3(P.ambient);
   const V3 w0 = shade ? normalize(o - p) : v3(0, 0, 0);
   for (int li = 0; li < P.num_lights; li++) {
-    const DevLight& L = lights[li];
-    const V3 ld = ld3(L.position) - p;
+    const DevLight& lt = lights[li];
+    const V3 ld = ld3(lt.position) - p;
     const V3 wi = normalize(ld);
     const float dist = length(ld);
     const LaneRay sr[1] = {make_ray(p + wi * P.eps, wi, P.quot_ok)};
@@ -1242,13 +1465,14 @@ __device__ __forceinline__ V3 local_color(const RenderParams& P, const DevNode* 
     const bool act[1] = {shade};
     const bool sskip = ballot(shade && (sr[0].skip0 || sr[0].skip1 || sr[0].skip2)) != 0;
     bool occ[1];
+    NoDonor nd;
     if (sskip)
-      occluded<true, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, sr, act, thr, occ, dg);
+      occluded<true, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, L, sr, act, thr, occ, dg, nd);
     else
-      occluded<false, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, sr, act, thr, occ, dg);
+      occluded<false, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, L, sr, act, thr, occ, dg, nd);
     shadow_rays += __builtin_popcountll(ballot(shade));
     if (shade && !occ[0]) {
-      const V3 I = ld3(L.intensity);
+      const V3 I = ld3(lt.intensity);
       const float d2 = dist * dist;
       color = color + ((ld3(m.diffuse) * I) * dot(n, wi)) / d2;
       const float cos_s = __builtin_fmaxf(dot(n, normalize(w0 + wi)), 0.0f);
@@ -1266,7 +1490,7 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
                                                  const float* __restrict__ normals,
                                                  const DevMaterial* __restrict__ mats,
                                                  const DevLight* __restrict__ lights, int sel,
-                                                 int* spill) {
+                                                 int* spill, WaveLeafLds& L) {
   const PacketPixel q = packet_pixel(P, sel);
   const size_t lanes_total = (size_t)P.num_sel_tiles * (kTile * kTile);
   const size_t g = (size_t)sel * (kTile * kTile) + q.lane;
@@ -1291,10 +1515,11 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
     const bool skip = ballot(active && (ray.skip0 || ray.skip1 || ray.skip2)) != 0;
     float ts[1];
     int leaves[1];
+    NoDonor nd;
     if (skip)
-      closest_hit<true, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, rays, act, ts, leaves, dg);
+      closest_hit<true, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, L, rays, act, ts, leaves, dg, nd);
     else
-      closest_hit<false, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, rays, act, ts, leaves, dg);
+      closest_hit<false, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, L, rays, act, ts, leaves, dg, nd);
     const float t = ts[0];
     const int leaf = leaves[0];
     const bool hit = active && leaf >= 0;
@@ -1308,7 +1533,7 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
       n = pr.kind == kPrimTriangle ? ld3(normals + 4 * leaf) : normalize(p - ld3(pr.v0));
       mat = pr.material;
     }
-    const V3 local = local_color<FAST, DEEP, SPHERES>(P, nodes, prims, mats, lights, spill,
+    const V3 local = local_color<FAST, DEEP, SPHERES>(P, nodes, prims, mats, lights, spill, L,
                                                       hit && !medium, ray.o, p, n, mat, dg,
                                                       n_shadow);
     if (active) {
@@ -1498,20 +1723,6 @@ __device__ __forceinline__ int packet_sel(const RenderParams& P, int p) {
   return (tx < P.tiles_x && ty < tiles_y) ? ty * P.tiles_x + tx : -1;
 }
 
-// Workgroups of W waves the current device keeps resident at 8 waves per SIMD.
-[[maybe_unused]] static int resident_blocks(int W) {
-  static int cus[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  if (!cus[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    cus[dev] = n;
-  }
-  return cus[dev] * 32 / W;
-}
-
 // Logical packets of a traversal launch (R tiles each; with tile_block, padded to whole blocks).
 template <int W, int R>
 __host__ __device__ __forceinline__ int trace_packets(const RenderParams& P) {
@@ -1521,46 +1732,189 @@ __host__ __device__ __forceinline__ int trace_packets(const RenderParams& P) {
   return ((P.tiles_x + BW - 1) / BW) * ((tiles_y + BH - 1) / BH) * W;
 }
 
-// Persistent traversal waves (RenderParams::work != null): the grid holds only as many
-// workgroups as the GPU keeps resident, and every wave takes packets one at a time from a
-// counter — first from its XCD group's contiguous range (blockIdx % 8: the blocks that share
-// an XCD and its L2), then from the other groups' ranges.  Slots no longer drain workgroup by
-// workgroup as packets of unequal cost finish, and the tail of the frame is one packet long.
-// Without a work buffer: one packet per wave, XCD-remapped (packet_index).
-template <int W, int R, class F>
-__device__ __forceinline__ void for_each_packet(const RenderParams& P, F&& f) {
-  const int total = trace_packets<W, R>(P);
-  if (!P.work) {
-    const int p = packet_index<W>();
-    if (p < total) f(p);
-    return;
+// RT_TIMELINE (experiment builds only): every traversal wave records its start and end on the
+// 100 MHz clock and its own tile, so tools/timeline.py can draw the occupancy curve of a launch.
+#ifdef RT_TIMELINE
+constexpr int kTimelineWaves = 1 << 18;
+__device__ unsigned long long g_timeline[2][kTimelineWaves][3];
+#define TL_BEGIN                                                   \
+  int tl_sel = -1;                                                  \
+  const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime()
+#define TL_SEL(x) tl_sel = (x)
+#define TL_END(k)                                                                         \
+  do {                                                                                    \
+    const unsigned long long tl1 = __builtin_amdgcn_s_memrealtime();                      \
+    const int wid = (int)blockIdx.x * (int)(blockDim.x >> 6) + ((int)threadIdx.x >> 6);   \
+    if (lane_id() == 0 && wid < kTimelineWaves) {                                         \
+      g_timeline[k][wid][0] = tl0;                                                        \
+      g_timeline[k][wid][1] = tl1;                                                        \
+      g_timeline[k][wid][2] = (unsigned long long)(long long)tl_sel;                       \
+    }                                                                                     \
+  } while (0)
+#else
+#define TL_BEGIN
+#define TL_SEL(x)
+#define TL_END(k)
+#endif
+
+// Sharing workgroups (RT_EXP_SHARE, R == 1, lane stack; see "subtree sharing"): each wave
+// starts with its own packet, and every piece of work, own or shared, goes through the one call
+// site in the loop.  Bit-identical, but slower on C3, so off by default: every
+// wave traverses its own packet alone.
+#ifdef RT_EXP_SHARE
+constexpr bool kShare = true;
+#else
+constexpr bool kShare = false;
+#endif
+
+template <bool FAST, bool SPHERES, bool CULL, int W>
+__device__ __forceinline__ void share_primary(const RenderParams& P, const DevNode* __restrict__ nodes,
+                                              const DevPrim* __restrict__ prims, int sel,
+                                              WaveLeafLds& L, BlockShare<W>& SH) {
+  const int wv = (int)threadIdx.x >> 6, lane = lane_id();
+  if (threadIdx.x == 0) SH.want = 0;
+  if (lane == 0) {
+    SH.sel[wv] = sel;
+    SH.flag[wv] = 0;
   }
-  const int g0 = (int)(blockIdx.x & 7);
-  for (int k = 0; k < 8; k++) {
-    const int g = (g0 + k) & 7;
-    const int begin = (int)((long long)total * g / 8), end = (int)((long long)total * (g + 1) / 8);
-    for (;;) {
-      int p = 0;
-      if (lane_id() == 0) p = atomicAdd(&P.work[g], 1);
-      p = begin + uniform(p);
-      if (p >= end) break;
-      f(p);
+  SH.res[wv][lane] = kNoHitKey;
+  __syncthreads();
+  Sharer<W> sh;
+  sh.S = &SH;
+  sh.light = 0;
+  Diag dg;
+  int owner = wv, node = -1, light = 0;
+  uint64_t mask = 0;
+  bool have = sel >= 0;
+  unsigned long long shared = 0;
+  for (;;) {
+    if (!have && !share_next(SH, owner, node, mask, light)) break;
+    const int tsel = uniform(SH.sel[owner]);
+    sh.owner = owner;
+    sh.visits = 0;
+    const unsigned long long key =
+        primary_piece<FAST, SPHERES, CULL, W>(fresh_params(P), nodes, prims, tsel, L, sh,
+                                               have ? -1 : node, mask, dg);
+    if (key != kNoHitKey) atomicMin(&SH.res[owner][lane], key);
+    shared += have ? 0 : 1;
+    have = false;
+  }
+  __syncthreads();  // every piece of every packet of the workgroup has merged
+  const RenderParams& Pw = fresh_params(P);
+  if (sel >= 0) {
+    const PacketPixel q = packet_pixel(Pw, sel);
+    const unsigned long long key = SH.res[wv][lane];
+    int2_t rec;  // key layout: leaf low, t bits high (rt_internal.h)
+    rec.x = q.valid ? (int)(unsigned)key : -2;  // -1 miss, -2 outside the image
+    rec.y = (int)(unsigned)(key >> 32);
+    Pw.hits[(size_t)sel * (kTile * kTile) + q.lane] = rec;
+    const unsigned long long nvalid = __builtin_popcountll(ballot(q.valid));
+    const unsigned long long nhit = __builtin_popcountll(ballot(q.valid && rec.x >= 0));
+    if (Pw.counters && lane == 0) {
+      unsigned long long* c = counter_row(Pw, sel);
+      atomicAdd(&c[kCntPrimary], nvalid);
+      atomicAdd(&c[kCntHits], nhit);
     }
+  }
+  if (Pw.counters && lane == 0) {
+    unsigned long long* c = counter_row(Pw, (int)blockIdx.x);
+    if (shared) atomicAdd(&c[kCntShared], shared);
+#ifdef RT_DIAG
+    atomicAdd(&c[kCntPrimNodes], dg.nodes);
+    atomicAdd(&c[kCntPrimNodeLanes], dg.node_lanes);
+    atomicAdd(&c[kCntPrimLeaves], dg.leaves);
+    atomicAdd(&c[kCntPrimLeafLanes], dg.leaf_lanes);
+#endif
   }
 }
 
+// Shadow rays in a sharing workgroup, 32 lights (one occlusion word) at a time: the waves split
+// the word's (packet, light) traversals, merge the occlusion bits per packet in LDS, and write
+// the word after a workgroup barrier.
+template <bool FAST, bool SPHERES, bool CULL, int W>
+__device__ __forceinline__ void share_shadow(const RenderParams& P, const DevNode* __restrict__ nodes,
+                                             const DevPrim* __restrict__ prims,
+                                             const DevLight* __restrict__ lights, int sel,
+                                             WaveLeafLds& L, BlockShare<W>& SH) {
+  const int wv = (int)threadIdx.x >> 6, lane = lane_id();
+  const int nl = P.num_lights, words = P.occ_words;
+  if (lane == 0) SH.sel[wv] = sel;
+  Sharer<W> sh;
+  sh.S = &SH;
+  Diag dg;
+  unsigned long long shared = 0;
+  for (int w = 0; w < words; w++) {
+    if (threadIdx.x == 0) SH.want = 0;
+    if (lane == 0) SH.flag[wv] = 0;
+    SH.res[wv][lane] = 0ull;
+    __syncthreads();
+    const int lend = min(nl, 32 * (w + 1));
+    int li = 32 * w, owner = wv, node = -1, light = 0;
+    uint64_t mask = 0;
+    for (;;) {
+      const bool have = sel >= 0 && li < lend;
+      if (have) {
+        owner = wv;
+        light = li++;
+      } else if (!share_next(SH, owner, node, mask, light)) {
+        break;
+      }
+      sh.owner = owner;
+      sh.light = light;
+      sh.visits = 0;
+      const bool occ = shadow_piece<FAST, SPHERES, CULL>(fresh_params(P), nodes, prims, lights,
+                                                         uniform(SH.sel[owner]), light, nullptr, L,
+                                                         sh, have ? -1 : node, mask, dg);
+      if (occ) atomicOr(&SH.res[owner][lane], 1ull << (light & 31));
+      shared += have ? 0 : 1;
+    }
+    __syncthreads();  // every piece of this word has merged
+    if (sel >= 0) {
+      const RenderParams& Pw = fresh_params(P);
+      Pw.occ[((size_t)sel * (kTile * kTile) + lane) * words + w] = (unsigned)SH.res[wv][lane];
+    }
+  }
+  const RenderParams& Pc = fresh_params(P);
+  if (sel >= 0) {
+    const bool hit = hit_leaf(Pc.hits[(size_t)sel * (kTile * kTile) + lane]) >= 0;
+    const unsigned long long nhit = __builtin_popcountll(ballot(hit));
+    if (Pc.counters && lane == 0)
+      atomicAdd(&counter_row(Pc, sel)[kCntShadow], nhit * (unsigned long long)nl);
+  }
+  if (Pc.counters && lane == 0) {
+    unsigned long long* c = counter_row(Pc, (int)blockIdx.x);
+    if (shared) atomicAdd(&c[kCntShared], shared);
+#ifdef RT_DIAG
+    atomicAdd(&c[kCntShadNodes], dg.nodes);
+    atomicAdd(&c[kCntShadNodeLanes], dg.node_lanes);
+    atomicAdd(&c[kCntShadLeaves], dg.leaves);
+    atomicAdd(&c[kCntShadLeafLanes], dg.leaf_lanes);
+#endif
+  }
+}
+
+// Traversal kernels: one packet per wave, XCD-remapped blocks of 2-D tile blocks.
 template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL>
 __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY void trace_primary_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
   constexpr int W = trace_waves<DEEP>();
+  __shared__ WaveLeafLds leaf_lds[W];  // 2 KiB per wave
   int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * (1 + 2 * R) * kDeepStack : nullptr;
-  for_each_packet<W, R>(P, [&](int p) {
-    const RenderParams& Q = fresh_params(P);
-    const int sel0 = R == 1 ? packet_sel<W>(Q, p) : p * R;
-    if (sel0 >= 0 && sel0 < Q.num_sel_tiles)
-      primary_packet<FAST, DEEP, SPHERES, R, CULL>(Q, nodes, prims, sel0, spill);
-  });
+  WaveLeafLds& L = leaf_lds[threadIdx.x >> 6];
+  TL_BEGIN;
+  const RenderParams& Q = fresh_params(P);
+  const int p = packet_index<W>();
+  int sel = p < trace_packets<W, R>(Q) ? (R == 1 ? packet_sel<W>(Q, p) : p * R) : -1;
+  if (sel >= Q.num_sel_tiles) sel = -1;
+  TL_SEL(sel);
+  if constexpr (kShare && R == 1 && !DEEP) {
+    __shared__ BlockShare<W> SH;
+    share_primary<FAST, SPHERES, CULL, W>(P, nodes, prims, sel, L, SH);
+  } else if (sel >= 0) {
+    primary_packet<FAST, DEEP, SPHERES, R, CULL>(Q, nodes, prims, sel, spill, L);
+  }
+  TL_END(0);
 }
 
 template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL>
@@ -1569,13 +1923,22 @@ __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY vo
     const DevLight* __restrict__ lights) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
   constexpr int W = trace_waves<DEEP>();
+  __shared__ WaveLeafLds leaf_lds[W];  // 2 KiB per wave
   int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * (1 + 2 * R) * kDeepStack : nullptr;
-  for_each_packet<W, R>(P, [&](int p) {
-    const RenderParams& Q = fresh_params(P);
-    const int sel0 = R == 1 ? packet_sel<W>(Q, p) : p * R;
-    if (sel0 >= 0 && sel0 < Q.num_sel_tiles)
-      shadow_packet<FAST, DEEP, SPHERES, R, CULL>(Q, nodes, prims, lights, sel0, spill);
-  });
+  WaveLeafLds& L = leaf_lds[threadIdx.x >> 6];
+  TL_BEGIN;
+  const RenderParams& Q = fresh_params(P);
+  const int p = packet_index<W>();
+  int sel = p < trace_packets<W, R>(Q) ? (R == 1 ? packet_sel<W>(Q, p) : p * R) : -1;
+  if (sel >= Q.num_sel_tiles) sel = -1;
+  TL_SEL(sel);
+  if constexpr (kShare && R == 1 && !DEEP) {
+    __shared__ BlockShare<W> SH;
+    share_shadow<FAST, SPHERES, CULL, W>(P, nodes, prims, lights, sel, L, SH);
+  } else if (sel >= 0) {
+    shadow_packet<FAST, DEEP, SPHERES, R, CULL>(Q, nodes, prims, lights, sel, spill, L);
+  }
+  TL_END(1);
 }
 
 template <bool FAST, bool DEEP, bool SPHERES>
@@ -1584,10 +1947,11 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void recursive_kernel(
     const float* __restrict__ normals, const DevMaterial* __restrict__ mats,
     const DevLight* __restrict__ lights) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
+  __shared__ WaveLeafLds leaf_lds[kWavesPerBlock];
   const int sel = packet_index<kWavesPerBlock>();
   if (sel >= P.num_sel_tiles) return;
   int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * 3 * kDeepStack : nullptr;
-  recursive_packet<FAST, DEEP, SPHERES>(P, nodes, prims, normals, mats, lights, sel, spill);
+  recursive_packet<FAST, DEEP, SPHERES>(P, nodes, prims, normals, mats, lights, sel, spill, leaf_lds[threadIdx.x >> 6]);
 }
 
 __global__ __launch_bounds__(kWavesPerBlock * 64) void shade_kernel(
@@ -1628,16 +1992,6 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
   int tblocks = (trace_packets<W, R>(T) + W - 1) / W;
   const size_t tlds = DEEP ? sizeof(int) * (1 + 2 * R) * kDeepStack * W : 0;
   RenderParams S = T;
-#ifdef RT_EXP_PERSIST
-  if (T.work) {  // persistent waves: one resident wave per slot (8 per SIMD), counters zeroed
-    tblocks = std::min(tblocks, resident_blocks(W));
-    const hipError_t e = hipMemsetAsync(T.work, 0, 16 * sizeof(int), stream);
-    if (e != hipSuccess) return;
-    S.work = T.work + 8;
-  }
-#else
-  T.work = S.work = nullptr;
-#endif
   mark(marks, 0, stream);
   hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, R, CULL>), dim3(tblocks),
                      dim3(W * 64), tlds, stream, T, nodes, prims);
@@ -1788,6 +2142,23 @@ unsigned long long read_reset_exact_fallbacks() {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_exact_fallbacks), &z, sizeof z);
   return v;
 #else
+  return 0;
+#endif
+}
+
+// Copies (and clears) the RT_TIMELINE wave records: out[2][kTimelineWaves][3] start/end
+// ticks of the 100 MHz clock and tile (sel, -1 for none).  Returns the number of values written, 0 in other builds.
+long long read_reset_timeline(unsigned long long* out, long long max_values) {
+#ifdef RT_TIMELINE
+  const long long n = 2ll * kTimelineWaves * 3;
+  if (max_values < n) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_timeline), n * sizeof *out) != hipSuccess) return -1;
+  std::vector<unsigned long long> z((size_t)n, 0ull);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_timeline), z.data(), n * sizeof *out) != hipSuccess) return -1;
+  return n;
+#else
+  (void)out;
+  (void)max_values;
   return 0;
 #endif
 }

@@ -207,6 +207,11 @@ int rt_collect_stats(rt_scene* scene, rt_stats* stats);
  * test.  Returns 1 for a diagnostic build, 0 otherwise (columns 4..12 then read 0). */
 int rt_debug_counters(rt_scene* scene, long long* out16);
 
+/* RT_TIMELINE experiment builds (tools/timeline.py): copies and clears the per-wave start/end
+ * ticks (100 MHz clock) and tile of the last traversal launches, out[2 kernels][2^18 waves][3].
+ * Returns the number of values written (0 in other builds) or a negative RT_E_* code. */
+long long rt_debug_timeline(unsigned long long* out, long long max_values);
+
 /* Device self-check of the triangle test's shared-reciprocal quotients (rt_kernels.hip,
  * tri_quotients) against IEEE division on `count` seeded random operand pairs of the fast
  * range; out2[0] = mismatching quotients (must be 0), out2[1] = cases run. */

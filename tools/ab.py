@@ -5,6 +5,7 @@ interleaved (A B C A B C ...) so device clock drift hits every variant alike.
 
     python tools/ab.py base,nocx --rounds 3
     python tools/ab.py t0,t4,occ7@4     (tK / lib@K: treelet size K of the culling tree, 0 = none)
+    python tools/ab.py base,base:CENG795_RT_STEAL=0   (lib:VAR=VAL[:VAR=VAL]: extra environment)
 """
 import argparse
 import json
@@ -26,7 +27,11 @@ def main():
     for _ in range(a.rounds):
         for v in a.variants.split(","):
             env = dict(os.environ)
-            lib, _, k = v.partition("@")  # <lib>@K: treelet size K of the culling tree
+            v_lib, *assigns = v.split(":")
+            for a_ in assigns:
+                key, _, val = a_.partition("=")
+                env[key] = val
+            lib, _, k = v_lib.partition("@")  # <lib>@K: treelet size K of the culling tree
             if lib[:1] == "t" and lib[1:].isdigit():  # tK: production lib
                 lib, k = "base", lib[1:]
             env["CENG795_LIB"] = "" if lib == "base" else lib
