@@ -49,6 +49,8 @@ struct RenderCtx {
   size_t hits_records = 0;
   unsigned* d_occ = nullptr;
   size_t occ_words = 0;
+  unsigned* d_sched = nullptr;  // per tile: traversal cost, then the shadow dispatch order
+  size_t sched_words = 0;
   float* d_frames = nullptr;
   size_t frames_floats = 0;
   float* d_samples = nullptr;
@@ -78,6 +80,7 @@ struct rt_scene {
   unsigned long long* d_counters = nullptr;
   int2_t* d_hits = nullptr;  // rt_render_device's primary-hit records (largest camera)
   unsigned* d_occ = nullptr; // rt_render_device's occlusion bits
+  unsigned* d_sched = nullptr;  // rt_render_device's tile costs + shadow order (2 x tiles)
   float* d_frames = nullptr; // rt_render_device's ray-tree frames (recursive scenes)
   size_t frames_capacity = 0;
   size_t hits_capacity = 0;  // records
@@ -143,6 +146,7 @@ void free_ctx(RenderCtx* c) {
   (void)hipFree(c->d_cnt);
   (void)hipFree(c->d_hits);
   (void)hipFree(c->d_occ);
+  (void)hipFree(c->d_sched);
   (void)hipFree(c->d_frames);
   (void)hipFree(c->d_samples);
   if (c->e0) (void)hipEventDestroy(c->e0);
@@ -169,6 +173,7 @@ void free_device(rt_scene* s) {
   (void)hipFree(s->d_counters);
   (void)hipFree(s->d_hits);
   (void)hipFree(s->d_occ);
+  (void)hipFree(s->d_sched);
   (void)hipFree(s->d_frames);
   (void)hipFree(s->d_samples);
   if (cur != s->device) (void)hipSetDevice(cur);
@@ -196,6 +201,21 @@ int occ_words(const HostScene& h) { return std::max(1, ((int)h.lights.size() + 3
 
 // A counter buffer: kCounterRows x kCounterWidth ray counters.
 constexpr size_t kCounterAlloc = (size_t)kCounterWidth * kCounterRows;
+// CENG795_RT_ORDER=0 turns the heavy-first shadow dispatch off (A/B experiments); the
+// order cannot change any result, only which tiles start first.
+bool order_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CENG795_RT_ORDER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+void set_schedule(RenderParams& P, unsigned* sched) {
+  // (the buffer holds 2 x the camera's tiles; a launch uses its first 2 x num_sel_tiles)
+  P.tile_cost = order_enabled() ? sched : nullptr;
+  P.tile_order = order_enabled() ? reinterpret_cast<int*>(sched) + P.num_sel_tiles : nullptr;
+}
+
 int create_from_host(rt_scene* s, int device) {
   if (device < 0) hip_check(hipGetDevice(&device), "hipGetDevice");
   s->device = device;
@@ -235,6 +255,8 @@ int create_from_host(rt_scene* s, int device) {
   }
   hip_check(hipMalloc(&s->d_hits, most * sizeof(int2_t)), "alloc hit records");
   hip_check(hipMalloc(&s->d_occ, most * sizeof(unsigned) * occ_words(h)), "alloc occlusion bits");
+  hip_check(hipMalloc(&s->d_sched, 2 * (most / (kTile * kTile)) * sizeof(unsigned)),
+            "alloc tile schedule");
   s->hits_capacity = most;
   return RT_OK;
 }
@@ -295,6 +317,7 @@ RenderParams make_params(const rt_scene* s, int cam, int row0, int row_stride, i
   P.hits = s->d_hits;
   P.occ = s->d_occ;
   P.occ_words = occ_words(h);
+  set_schedule(P, s->d_sched);
   P.counters = counters ? s->d_counters : nullptr;
   return P;
 }
@@ -698,6 +721,8 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
       P.hits = x->d_hits;
       ensure(x->d_occ, x->occ_words, (size_t)P.occ_words * lanes, "alloc occlusion bits");
       P.occ = x->d_occ;
+      ensure(x->d_sched, x->sched_words, 2 * lanes / (kTile * kTile), "alloc tile schedule");
+      set_schedule(P, x->d_sched);
       if (s->needs_recursion) {
         ensure(x->d_frames, x->frames_floats, frame_floats(s->host, P.num_sel_tiles),
                "alloc ray-tree frames");

@@ -155,6 +155,11 @@ struct RenderParams {
   int2_t* hits;   // num_sel_tiles * 64 records {t bits, leaf}: trace_primary -> shadow, shade
   unsigned* occ;  // num_sel_tiles * 64 * occ_words light-occlusion bits: trace_shadow -> shade
   int occ_words;  // ceil(num_lights / 32)
+  // heavy-first shadow dispatch (null: off): trace_primary stores each tile's traversal time
+  // (100 MHz ticks) in tile_cost[sel]; order_kernel sorts the tiles by it, slowest first, into
+  // tile_order, which trace_shadow walks instead of the frame's block order
+  unsigned* tile_cost;
+  int* tile_order;
   float* frames;  // recursive scenes only: (max_depth+1) * 28 * lanes ray-tree frames, else null
   // kCounterRows rows of kCounterWidth u64 (columns: kCnt*)
   unsigned long long* counters;

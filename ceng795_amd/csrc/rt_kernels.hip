@@ -1912,7 +1912,11 @@ __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY vo
     __shared__ BlockShare<W> SH;
     share_primary<FAST, SPHERES, CULL, W>(P, nodes, prims, sel, L, SH);
   } else if (sel >= 0) {
+    const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
     primary_packet<FAST, DEEP, SPHERES, R, CULL>(Q, nodes, prims, sel, spill, L);
+    const RenderParams& Pw = fresh_params(P);
+    if (R == 1 && Pw.tile_cost && lane_id() == 0)  // the shadow kernel's dispatch order
+      Pw.tile_cost[sel] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - c0, 0xffffffffull);
   }
   TL_END(0);
 }
@@ -1928,8 +1932,14 @@ __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY vo
   WaveLeafLds& L = leaf_lds[threadIdx.x >> 6];
   TL_BEGIN;
   const RenderParams& Q = fresh_params(P);
-  const int p = packet_index<W>();
-  int sel = p < trace_packets<W, R>(Q) ? (R == 1 ? packet_sel<W>(Q, p) : p * R) : -1;
+  int sel;
+  if (R == 1 && Q.tile_order) {  // slowest primary tiles first, in plain block order
+    const int p = uniform((int)blockIdx.x * W + ((int)threadIdx.x >> 6));
+    sel = p < Q.num_sel_tiles ? uniform(Q.tile_order[p]) : -1;
+  } else {
+    const int p = packet_index<W>();
+    sel = p < trace_packets<W, R>(Q) ? (R == 1 ? packet_sel<W>(Q, p) : p * R) : -1;
+  }
   if (sel >= Q.num_sel_tiles) sel = -1;
   TL_SEL(sel);
   if constexpr (kShare && R == 1 && !DEEP) {
@@ -1962,6 +1972,38 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void shade_kernel(
   shade_pixel(P, prims, normals, mats, lights, sel);
 }
 
+// Heavy-first dispatch order for the shadow kernel: the tiles sorted by their primary traversal
+// time, slowest first (a bucket sort on 8 steps per octave; order inside a bucket is free).
+// The slow primary tiles are where the slow shadow tiles are (tools/timeline.py tile maps), and
+// a kernel's tail is set by the slow tiles that start last.  One workgroup.
+constexpr int kOrderBuckets = 256;
+__device__ __forceinline__ int cost_bucket(unsigned c) {
+  c = c ? c : 1u;
+  const int msb = 31 - __builtin_clz(c);
+  const int frac = msb >= 3 ? (int)((c >> (msb - 3)) & 7u) : (int)((c << (3 - msb)) & 7u);
+  return min(kOrderBuckets - 1, msb * 8 + frac);
+}
+
+__global__ __launch_bounds__(1024) void order_kernel(const unsigned* __restrict__ cost,
+                                                     int* __restrict__ order, int n) {
+  __shared__ int hist[kOrderBuckets];
+  const int tid = (int)threadIdx.x;
+  for (int i = tid; i < kOrderBuckets; i += 1024) hist[i] = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += 1024) atomicAdd(&hist[cost_bucket(cost[i])], 1);
+  __syncthreads();
+  if (tid == 0) {  // exclusive offsets, heaviest bucket first
+    int run = 0;
+    for (int b = kOrderBuckets - 1; b >= 0; b--) {
+      const int c = hist[b];
+      hist[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += 1024) order[atomicAdd(&hist[cost_bucket(cost[i])], 1)] = i;
+}
+
 // marks (nullable): 4 events recorded before the primary kernel, after it, after the shadow
 // kernel and after the shade kernel (rt_set_kernel_timing).  A recursive scene's single kernel
 // is timed between marks 2 and 3.
@@ -1992,12 +2034,19 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
   int tblocks = (trace_packets<W, R>(T) + W - 1) / W;
   const size_t tlds = DEEP ? sizeof(int) * (1 + 2 * R) * kDeepStack * W : 0;
   RenderParams S = T;
+  S.tile_cost = nullptr;  // (read by the shadow kernel through tile_order only)
+  const bool ordered = R == 1 && P.num_lights > 0 && T.tile_order != nullptr;
+  if (!ordered) T.tile_cost = S.tile_cost = nullptr, T.tile_order = S.tile_order = nullptr;
   mark(marks, 0, stream);
   hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, R, CULL>), dim3(tblocks),
                      dim3(W * 64), tlds, stream, T, nodes, prims);
   mark(marks, 1, stream);
+  if (ordered)
+    hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, stream, T.tile_cost, T.tile_order,
+                       T.num_sel_tiles);
+  const int sblocks = ordered ? (T.num_sel_tiles + W - 1) / W : tblocks;
   if (P.num_lights > 0)
-    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, R, CULL>), dim3(tblocks),
+    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, R, CULL>), dim3(sblocks),
                        dim3(W * 64), tlds, stream, S, nodes, prims, lights);
   mark(marks, 2, stream);
   hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
