@@ -70,6 +70,7 @@ float widen_up(float x) { return x + std::fabs(x) * 0x1p-20f + 0x1p-100f; }
 struct SahBuilder {
   std::vector<Item>& items;
   std::vector<DevNode>& nodes;
+  bool pairs = true;  // two-leaf treelets as leaf pairs (kAccelPair*)
   int depth = 0;  // max over leaves of (SAH levels + treelet height)
 
   static constexpr int kBins = 32;
@@ -157,7 +158,15 @@ struct SahBuilder {
         const int b = ranges[side][0], e = ranges[side][1];
         if (e - b == 1) {
           const Item& it = items[b];
-          N.child[side] = it.ref;
+          int ref = it.ref;
+          if (pairs && ref >= 0) {  // a reference node whose children are two consecutive leaves
+            const DevNode& R = nodes[ref];
+            if (R.pad == 0 && R.child[0] < 0 && R.child[1] < 0 && ~R.child[1] == ~R.child[0] + 1) {
+              ref = R.child[0];
+              N.pad |= side ? kAccelPair1 : kAccelPair0;
+            }
+          }
+          N.child[side] = ref;
           N.pad |= side ? kAccelGuard1 : kAccelGuard0;
           for (int a = 0; a < 3; a++) {
             N.lo[a][side] = it.box[a];
@@ -262,6 +271,8 @@ void build_accel(HostScene& s, int K) {
   }
   // The node array is appended to; nothing else refers to the indices past the reference's.
   SahBuilder B{items, s.nodes};
+  const char* pe = std::getenv("CENG795_RT_PAIRS");  // =0: visit two-leaf treelets (A/B)
+  B.pairs = !(pe && pe[0] == '0');
   const int root = B.build(0, (int)items.size());
   Box u;
   for (const Item& it : items) u.grow(it.box);
@@ -351,10 +362,20 @@ std::string check_accel(const HostScene& s, int K, long long stats[4]) {
         if (N.lo[a][side] != g[a] || N.hi[a][side] != g[a + 3])
           return "guard box differs from the reference box it stands for";
       std::vector<int> lv;
+      const bool pair = (N.pad & (side ? kAccelPair1 : kAccelPair0)) != 0;
       if (c >= 0) {
+        if (pair) return "leaf pair stored as a node";
         if (c >= nref) return "guarded child is not a reference node";
         ref_leaves(c, lv);
         if ((int)lv.size() > K) return "treelet larger than K";
+      } else if (pair) {  // the two leaf children, in DFS order, of the guard's reference node
+        if ((size_t)~c + 1 >= nleaf) return "leaf pair past the last leaf";
+        const int holder = s.ancestry[~c].leaf_parent;
+        if (holder < 0 || s.ancestry[~c + 1].leaf_parent != holder ||
+            s.nodes[holder].child[0] != c || s.nodes[holder].child[1] != ~(~c + 1))
+          return "leaf pair " + std::to_string(~c) + " is not one node's two leaves";
+        lv.push_back(~c);
+        lv.push_back(~c + 1);
       } else {
         lv.push_back(~c);
         lone++;

@@ -35,7 +35,11 @@ enum : int {
 // DevNode::pad of the culling-tree nodes (accel_build.cpp); reference nodes have pad == 0.
 // Guard bit set: that child is a treelet root (node index or ~leaf) behind a reachability
 // guard; clear: an inner culling node tested conservatively.
-enum : int32_t { kAccelGuard0 = 1, kAccelGuard1 = 2, kAccelNode = 4 };
+// culling nodes (accel_build.cpp): pad = kAccelNode | guard bits | leaf-pair bits.  A guarded
+// child with its pair bit set is a treelet of two leaves, stored as ~first leaf (its second
+// leaf is the next one in DFS order): the kernels queue both leaf tests at once instead of
+// visiting the treelet's root, whose own box is the guard already tested.
+enum : int32_t { kAccelGuard0 = 1, kAccelGuard1 = 2, kAccelNode = 4, kAccelPair0 = 8, kAccelPair1 = 16 };
 constexpr int kDefaultTreeletLeaves = 2;
 
 struct alignas(16) DevNode {
@@ -45,7 +49,7 @@ struct alignas(16) DevNode {
   float hi[3][2];
   int32_t child[2];  // >= 0: internal node index; < 0: leaf index ~child
   int32_t axis;      // split dimension of THIS node (Bounding_volume_hierarchy.cpp:8)
-  int32_t pad;       // 0: reference node; else kAccelNode | guard bits
+  int32_t pad;       // 0: reference node; else kAccelNode | guard bits | pair bits
 };
 static_assert(sizeof(DevNode) == 64, "node must be one 64-byte scalar load");
 

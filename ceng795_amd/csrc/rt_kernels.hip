@@ -590,7 +590,7 @@ __device__ __forceinline__ bool advance(WaveStack<DEEP, R>& st, int c0, int c1,
 #define RT_BATCH_FLUSH 64
 #endif
 constexpr int kBatchFlush = RT_BATCH_FLUSH;  // run the queue once this many tests are pending
-constexpr int kBatchCap = kBatchFlush + 128;  // < kBatchFlush pending + 2 x 64 per visit
+constexpr int kBatchCap = kBatchFlush + 256;  // < kBatchFlush pending + 2 pairs x 64 per visit
 #ifndef RT_TRACE_WAVES
 #define RT_TRACE_WAVES 4
 #endif
@@ -847,35 +847,47 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
     for (int k = 0; k < R; k++)
       visit_node<SKIP>(P, N, r[k], (m[k] >> lane) & 1, h0[k], h1[k], t0[k], t1[k]);
     DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(any_of(m));
-         dg.leaves += (N.child[0] < 0) + (N.child[1] < 0);
-         dg.leaf_lanes += (N.child[0] < 0 ? __builtin_popcountll(ballot(h0[0])) : 0) +
-                          (N.child[1] < 0 ? __builtin_popcountll(ballot(h1[0])) : 0));
+         const int nl0 = N.child[0] < 0 ? 1 + ((N.pad & kAccelPair0) != 0) : 0;
+         const int nl1 = N.child[1] < 0 ? 1 + ((N.pad & kAccelPair1) != 0) : 0;
+         dg.leaves += nl0 + nl1;
+         dg.leaf_lanes += nl0 * __builtin_popcountll(ballot(h0[0])) +
+                          nl1 * __builtin_popcountll(ballot(h1[0])));
     if constexpr (batch) {  // queue the leaf children's tests; run them 64 at a time
-      if (N.child[0] < 0) batch_push(L, pending, ~N.child[0], ballot(h0[0]));
-      if (N.child[1] < 0) batch_push(L, pending, ~N.child[1], ballot(h1[0]));
+      if (N.child[0] < 0) {
+        const uint64_t b = ballot(h0[0]);
+        batch_push(L, pending, ~N.child[0], b);
+        if (N.pad & kAccelPair0) batch_push(L, pending, ~N.child[0] + 1, b);
+      }
+      if (N.child[1] < 0) {
+        const uint64_t b = ballot(h1[0]);
+        batch_push(L, pending, ~N.child[1], b);
+        if (N.pad & kAccelPair1) batch_push(L, pending, ~N.child[1] + 1, b);
+      }
     } else {
 #ifndef RT_EXP_NOLEAF
 #pragma unroll 1
-    for (int side = 0; side < 2; side++) {  // leaf children: Shape::intersect, 0 < t < best
+    for (int slot = 0; slot < 4; slot++) {  // leaf children: Shape::intersect, 0 < t < best
+      const int side = slot >> 1;             // (slot & 1: the second leaf of a leaf pair)
       const int c = side ? N.child[1] : N.child[0];
-      if (c < 0) {
+      if (c < 0 && (!(slot & 1) || (N.pad & (side ? kAccelPair1 : kAccelPair0)))) {
+        const int leaf = ~c + (slot & 1);
 #pragma unroll
         for (int k = 0; k < R; k++) {
           const bool tests = side ? h1[k] : h0[k];
           float t = 0.0f;
 #ifndef RT_EXP_BRANCHY  // (RT_EXP_BRANCHY: the early-exit form, for A/B)
           if (ballot(tests)) {  // one wave-uniform branch; the update itself is a select
-            const bool hit = leaf_test<SPHERES>(prims, ~c, r[k], t);
+            const bool hit = leaf_test<SPHERES>(prims, leaf, r[k], t);
             const bool take = tests & hit & (t > 0.0f) & (t < RT_INF) &
-                              ((t < best_t[k]) | ((t == best_t[k]) & (~c < best_leaf[k])));
+                              ((t < best_t[k]) | ((t == best_t[k]) & (leaf < best_leaf[k])));
             best_t[k] = take ? t : best_t[k];
-            best_leaf[k] = take ? ~c : best_leaf[k];
+            best_leaf[k] = take ? leaf : best_leaf[k];
           }
 #else
-          if (tests && leaf_test<SPHERES>(prims, ~c, r[k], t) && t > 0.0f && t < RT_INF &&
-              (t < best_t[k] || (t == best_t[k] && ~c < best_leaf[k]))) {
+          if (tests && leaf_test<SPHERES>(prims, leaf, r[k], t) && t > 0.0f && t < RT_INF &&
+              (t < best_t[k] || (t == best_t[k] && leaf < best_leaf[k]))) {
             best_t[k] = t;
-            best_leaf[k] = ~c;
+            best_leaf[k] = leaf;
           }
 #endif
         }
@@ -991,17 +1003,29 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
     for (int k = 0; k < R; k++)
       visit_node<SKIP>(P, N, r[k], (m[k] >> lane) & 1, h0[k], h1[k], t0[k], t1[k]);
     DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(any_of(m));
-         dg.leaves += (N.child[0] < 0) + (N.child[1] < 0);
-         dg.leaf_lanes += (N.child[0] < 0 ? __builtin_popcountll(ballot(h0[0])) : 0) +
-                          (N.child[1] < 0 ? __builtin_popcountll(ballot(h1[0])) : 0));
+         const int nl0 = N.child[0] < 0 ? 1 + ((N.pad & kAccelPair0) != 0) : 0;
+         const int nl1 = N.child[1] < 0 ? 1 + ((N.pad & kAccelPair1) != 0) : 0;
+         dg.leaves += nl0 + nl1;
+         dg.leaf_lanes += nl0 * __builtin_popcountll(ballot(h0[0])) +
+                          nl1 * __builtin_popcountll(ballot(h1[0])));
     if constexpr (batch) {  // queue the still-unoccluded lanes' leaf tests
-      if (N.child[0] < 0) batch_push(L, pending, ~N.child[0], ballot(h0[0]) & alive[0]);
-      if (N.child[1] < 0) batch_push(L, pending, ~N.child[1], ballot(h1[0]) & alive[0]);
+      if (N.child[0] < 0) {
+        const uint64_t b = ballot(h0[0]) & alive[0];
+        batch_push(L, pending, ~N.child[0], b);
+        if (N.pad & kAccelPair0) batch_push(L, pending, ~N.child[0] + 1, b);
+      }
+      if (N.child[1] < 0) {
+        const uint64_t b = ballot(h1[0]) & alive[0];
+        batch_push(L, pending, ~N.child[1], b);
+        if (N.pad & kAccelPair1) batch_push(L, pending, ~N.child[1] + 1, b);
+      }
     } else {
 #pragma unroll 1
-    for (int side = 0; side < 2; side++) {
+    for (int slot = 0; slot < 4; slot++) {  // (slot & 1: the second leaf of a leaf pair)
+      const int side = slot >> 1;
       const int c = side ? N.child[1] : N.child[0];
-      if (c < 0) {
+      if (c < 0 && (!(slot & 1) || (N.pad & (side ? kAccelPair1 : kAccelPair0)))) {
+        const int leaf = ~c + (slot & 1);
 #pragma unroll
         for (int k = 0; k < R; k++) {
           const bool tests = side ? h1[k] : h0[k];
@@ -1009,11 +1033,11 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
 #ifndef RT_EXP_BRANCHY  // (RT_EXP_BRANCHY: the early-exit form, for A/B)
           const bool want = tests & !occ[k];
           if (ballot(want)) {
-            const bool hit = leaf_test<SPHERES>(prims, ~c, r[k], t);
+            const bool hit = leaf_test<SPHERES>(prims, leaf, r[k], t);
             occ[k] = occ[k] | (want & hit & (t > 0.0f) & (t < thr[k]));
           }
 #else
-          if (tests && !occ[k] && leaf_test<SPHERES>(prims, ~c, r[k], t) && t > 0.0f &&
+          if (tests && !occ[k] && leaf_test<SPHERES>(prims, leaf, r[k], t) && t > 0.0f &&
               t < thr[k])
             occ[k] = true;
 #endif
