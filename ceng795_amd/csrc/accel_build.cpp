@@ -191,10 +191,128 @@ struct SahBuilder {
   }
 };
 
+// Reference subtree height (internal-node levels): the stack a guarded treelet of more than
+// two leaves can need.
+int ref_height(const std::vector<DevNode>& nodes, int n) {
+  int h = 0;
+  for (int side = 0; side < 2; side++)
+    if (nodes[n].child[side] >= 0) h = std::max(h, ref_height(nodes, nodes[n].child[side]));
+  return h + 1;
+}
+
+// Collapses the binary culling tree (nodes[nref..], rooted at `root`) into 4-wide nodes that
+// replace it: each wide node takes a binary node's two slots and repeatedly opens the inner
+// slot with the largest box (surface area) into its two children, up to four slots.  Every
+// slot keeps its box, guard and pair flags, so the acceptance tests are the binary tree's.
+// Returns the tagged wide root; `stack` receives a bound on the traversal stack.
+int collapse_wide(std::vector<DevNode>& nodes, int nref, int root, int& stack) {
+  const std::vector<DevNode> bin(nodes.begin() + nref, nodes.end());
+  nodes.resize(nref);
+  struct Slot {
+    int ref;
+    bool guard, pair;
+    float box[6];
+  };
+  auto slot_of = [&](int bnode, int side) {
+    const DevNode& N = bin[bnode - nref];
+    Slot sl;
+    sl.ref = N.child[side];
+    sl.guard = (N.pad & (side ? kAccelGuard1 : kAccelGuard0)) != 0;
+    sl.pair = (N.pad & (side ? kAccelPair1 : kAccelPair0)) != 0;
+    for (int a = 0; a < 3; a++) {
+      sl.box[a] = N.lo[a][side];
+      sl.box[a + 3] = N.hi[a][side];
+    }
+    return sl;
+  };
+  auto area = [](const float* b) {
+    const double dx = (double)b[3] - b[0], dy = (double)b[4] - b[1], dz = (double)b[5] - b[2];
+    return dx * dy + dy * dz + dz * dx;
+  };
+  struct Job {
+    int bnode, parent, slot;
+  };
+  std::vector<Job> todo{{root, -1, 0}};
+  int wroot = -1;
+  std::vector<int> order;  // wide nodes in preorder
+  while (!todo.empty()) {
+    const Job j = todo.back();
+    todo.pop_back();
+    Slot sl[4];
+    int n = 2;
+    sl[0] = slot_of(j.bnode, 0);
+    sl[1] = slot_of(j.bnode, 1);
+    while (n < 4) {
+      int best = -1;
+      double ba = -1.0;
+      for (int k = 0; k < n; k++)
+        if (!sl[k].guard && area(sl[k].box) > ba) {
+          ba = area(sl[k].box);
+          best = k;
+        }
+      if (best < 0) break;
+      const int bn = sl[best].ref;
+      sl[best] = slot_of(bn, 0);
+      sl[n++] = slot_of(bn, 1);
+    }
+    const int w = (int)nodes.size();
+    nodes.resize(w + 2);
+    DevNode4 W;
+    std::memset(&W, 0, sizeof W);
+    for (int k = 0; k < 4; k++) {
+      for (int a = 0; a < 3; a++) {  // (empty slots: an inverted box, never read)
+        W.lo[a][k] = k < n ? sl[k].box[a] : 1.0f;
+        W.hi[a][k] = k < n ? sl[k].box[a + 3] : -1.0f;
+      }
+      if (k >= n) continue;
+      W.flags |= kWideValid << k;
+      if (sl[k].guard) {
+        W.child[k] = sl[k].ref;
+        W.flags |= kWideGuard << k;
+        if (sl[k].pair) W.flags |= kWidePair << k;
+      }
+    }
+    std::memcpy(&nodes[w], &W, sizeof W);
+    if (j.parent >= 0) {
+      DevNode4 P;
+      std::memcpy(&P, &nodes[j.parent], sizeof P);
+      P.child[j.slot] = w | kWideTag;
+      std::memcpy(&nodes[j.parent], &P, sizeof P);
+    } else {
+      wroot = w;
+    }
+    order.push_back(w);
+    for (int k = n - 1; k >= 0; k--)
+      if (!sl[k].guard) todo.push_back({sl[k].ref, w, k});
+  }
+  // stack bound, bottom-up: a visit pushes at most (slots - 1) entries
+  std::vector<int> need(nodes.size(), 0);
+  for (auto it = order.rbegin(); it != order.rend(); ++it) {
+    DevNode4 W;
+    std::memcpy(&W, &nodes[*it], sizeof W);
+    int slots = 0, deepest = 0;
+    for (int k = 0; k < 4; k++) {
+      if (!(W.flags & (kWideValid << k))) continue;
+      slots++;
+      const int c = W.child[k];
+      if (!(W.flags & (kWideGuard << k)))
+        deepest = std::max(deepest, need[c & ~kWideTag]);
+      else if (c >= 0)
+        deepest = std::max(deepest, ref_height(nodes, c));
+    }
+    need[*it] = slots - 1 + deepest;
+  }
+  stack = need[wroot] + 1;
+  return wroot | kWideTag;
+}
+
 }  // namespace
 
+// Kernels built without the batched leaf queue cannot walk wide nodes (rt_kernels.hip).
+bool wide_nodes_supported();
+
 void build_accel(HostScene& s, int K) {
-  if (s.accel_root >= 0) s.nodes.resize(s.accel_root);  // drop an earlier culling tree
+  if (s.accel_root >= 0) s.nodes.resize(s.accel_root & ~kWideTag);  // drop an earlier culling tree
   s.accel_root = -1;
   s.accel_depth = 0;
   s.accel_items = 0;
@@ -283,6 +401,12 @@ void build_accel(HostScene& s, int K) {
   s.accel_root = root;
   s.accel_depth = B.depth + 1;
   s.accel_items = (int)items.size();
+  const char* we = std::getenv("CENG795_RT_WIDE");  // =0: keep the binary culling tree (A/B)
+  if (!(we && we[0] == '0') && wide_nodes_supported()) {
+    int stack = 0;
+    s.accel_root = collapse_wide(s.nodes, nn, root, stack);
+    s.accel_depth = stack;
+  }
 }
 
 int accel_treelet_leaves() {
@@ -300,7 +424,7 @@ namespace rt {
 std::string check_accel(const HostScene& s, int K, long long stats[4]) {
   for (int i = 0; i < 4; i++) stats[i] = 0;
   if (s.accel_root < 0) return "";
-  const int nref = s.accel_root;  // culling nodes follow the reference's
+  const int nref = s.accel_root & ~kWideTag;  // culling nodes follow the reference's
   const size_t nleaf = s.prims.size();
   auto box_of = [&](int ref_node) { return s.ancestry[ref_node].box; };
   // ancestry: each reference node's box is its parent's child slot; leaves point at holders
@@ -321,6 +445,54 @@ std::string check_accel(const HostScene& s, int K, long long stats[4]) {
   }
   for (int a = 0; a < 6; a++)
     if (s.ancestry[0].box[a] != s.root_box[a]) return "root box differs from ancestry";
+  // the slots of a culling node, binary (DevNode, kAccelNode) or wide (DevNode4, tagged)
+  struct Slot {
+    int ref;
+    bool guard, pair;
+    float box[6];
+  };
+  auto slots_of = [&](int node, std::vector<Slot>& out, std::string& err) {
+    out.clear();
+    const int idx = node & ~kWideTag;
+    if (idx < nref || (size_t)idx >= s.nodes.size()) {
+      err = "culling child is not a culling node";
+      return;
+    }
+    if (node & kWideTag) {
+      if ((size_t)idx + 1 >= s.nodes.size()) {
+        err = "wide node past the end";
+        return;
+      }
+      DevNode4 W;
+      std::memcpy(&W, &s.nodes[idx], sizeof W);
+      for (int k = 0; k < 4; k++) {
+        if (!(W.flags & (kWideValid << k))) continue;
+        Slot sl{W.child[k], (W.flags & (kWideGuard << k)) != 0, (W.flags & (kWidePair << k)) != 0, {}};
+        for (int a = 0; a < 3; a++) {
+          sl.box[a] = W.lo[a][k];
+          sl.box[a + 3] = W.hi[a][k];
+        }
+        if (!sl.guard && !(sl.ref & kWideTag)) err = "inner slot of a wide node is not wide";
+        out.push_back(sl);
+      }
+      if (out.size() < 2) err = "wide node with fewer than two slots";
+    } else {
+      const DevNode& N = s.nodes[idx];
+      if (!(N.pad & kAccelNode)) {
+        err = "culling child is not a culling node";
+        return;
+      }
+      for (int side = 0; side < 2; side++) {
+        Slot sl{N.child[side], (N.pad & (side ? kAccelGuard1 : kAccelGuard0)) != 0,
+                (N.pad & (side ? kAccelPair1 : kAccelPair0)) != 0, {}};
+        for (int a = 0; a < 3; a++) {
+          sl.box[a] = N.lo[a][side];
+          sl.box[a + 3] = N.hi[a][side];
+        }
+        out.push_back(sl);
+      }
+    }
+  };
   std::vector<int> seen(nleaf, 0);
   long long lone = 0, items = 0;
   struct Frame {
@@ -341,34 +513,33 @@ std::string check_accel(const HostScene& s, int K, long long stats[4]) {
   };
   std::vector<float> lo(s.nodes.size() * 3), hi(s.nodes.size() * 3);
   std::vector<int> order;  // culling nodes in preorder, for the bottom-up union pass
+  std::vector<Slot> sl;
+  std::string err;
   while (!todo.empty()) {
     const Frame f = todo.back();
     todo.pop_back();
-    const DevNode& N = s.nodes[f.node];
-    if (f.node < nref || !(N.pad & kAccelNode)) return "culling child is not a culling node";
+    slots_of(f.node, sl, err);
+    if (!err.empty()) return err;
     order.push_back(f.node);
     stats[2] = std::max<long long>(stats[2], f.depth);
-    for (int side = 0; side < 2; side++) {
-      const int c = N.child[side];
-      const bool guard = (N.pad & (side ? kAccelGuard1 : kAccelGuard0)) != 0;
-      if (!guard) {
-        if (c < nref) return "unguarded child is not a culling node";
+    for (const Slot& x : sl) {
+      const int c = x.ref;
+      if (!x.guard) {
+        if (x.pair) return "pair flag on an inner slot";
         todo.push_back({c, f.depth + 1});
         continue;
       }
       items++;
       const float* g = c >= 0 ? box_of(c) : box_of(s.ancestry[~c].leaf_parent);
-      for (int a = 0; a < 3; a++)
-        if (N.lo[a][side] != g[a] || N.hi[a][side] != g[a + 3])
-          return "guard box differs from the reference box it stands for";
+      for (int a = 0; a < 6; a++)
+        if (x.box[a] != g[a]) return "guard box differs from the reference box it stands for";
       std::vector<int> lv;
-      const bool pair = (N.pad & (side ? kAccelPair1 : kAccelPair0)) != 0;
       if (c >= 0) {
-        if (pair) return "leaf pair stored as a node";
+        if (x.pair) return "leaf pair stored as a node";
         if (c >= nref) return "guarded child is not a reference node";
         ref_leaves(c, lv);
         if ((int)lv.size() > K) return "treelet larger than K";
-      } else if (pair) {  // the two leaf children, in DFS order, of the guard's reference node
+      } else if (x.pair) {  // the two leaf children, in DFS order, of the guard's reference node
         if ((size_t)~c + 1 >= nleaf) return "leaf pair past the last leaf";
         const int holder = s.ancestry[~c].leaf_parent;
         if (holder < 0 || s.ancestry[~c + 1].leaf_parent != holder ||
@@ -386,31 +557,29 @@ std::string check_accel(const HostScene& s, int K, long long stats[4]) {
   }
   for (size_t l = 0; l < nleaf; l++)
     if (!seen[l]) return "leaf " + std::to_string(l) + " in no treelet";
-  // containment: every culling slot box contains every guard box below it
+  // containment: every inner slot box contains every guard box below it
   for (auto it = order.rbegin(); it != order.rend(); ++it) {
-    const DevNode& N = s.nodes[*it];
+    slots_of(*it, sl, err);
     float ulo[3] = {INFINITY, INFINITY, INFINITY}, uhi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int side = 0; side < 2; side++) {
-      const int c = N.child[side];
-      const bool guard = (N.pad & (side ? kAccelGuard1 : kAccelGuard0)) != 0;
-      const float* clo = guard ? nullptr : &lo[(size_t)c * 3];
-      const float* chi = guard ? nullptr : &hi[(size_t)c * 3];
+    for (const Slot& x : sl) {
+      const size_t ci = (size_t)(x.ref & ~kWideTag) * 3;
       for (int a = 0; a < 3; a++) {
-        const float l = guard ? N.lo[a][side] : clo[a], h = guard ? N.hi[a][side] : chi[a];
-        if (!guard && (N.lo[a][side] > l || N.hi[a][side] < h))
+        const float l = x.guard ? x.box[a] : lo[ci + a], h = x.guard ? x.box[a + 3] : hi[ci + a];
+        if (!x.guard && (x.box[a] > l || x.box[a + 3] < h))
           return "culling box does not contain the guard boxes below it";
         ulo[a] = std::min(ulo[a], l);
         uhi[a] = std::max(uhi[a], h);
       }
     }
+    const size_t me = (size_t)(*it & ~kWideTag) * 3;
     for (int a = 0; a < 3; a++) {
-      lo[(size_t)*it * 3 + a] = ulo[a];
-      hi[(size_t)*it * 3 + a] = uhi[a];
+      lo[me + a] = ulo[a];
+      hi[me + a] = uhi[a];
     }
   }
+  const size_t r0 = (size_t)nref * 3;
   for (int a = 0; a < 3; a++)
-    if (s.accel_box[a] > lo[(size_t)s.accel_root * 3 + a] ||
-        s.accel_box[a + 3] < hi[(size_t)s.accel_root * 3 + a])
+    if (s.accel_box[a] > lo[r0 + a] || s.accel_box[a + 3] < hi[r0 + a])
       return "culling root box does not contain the tree";
   stats[0] = items;
   stats[1] = (long long)order.size();

@@ -21,7 +21,7 @@
 namespace rt {
 hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                          const float* normals, const DevMaterial* mats, const DevLight* lights,
-                         bool fast, bool deep, bool spheres, bool cull,
+                         bool fast, bool deep, bool spheres, bool cull, bool wide_only,
                          const hipEvent_t* marks, hipStream_t stream);
 int max_supported_depth();
 hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream);
@@ -71,6 +71,7 @@ struct rt_scene {
   bool deep = false;
   bool needs_recursion = false;
   bool has_spheres = false;
+  bool wide_only = false;  // the fast walk meets 4-wide culling nodes only (launch_render)
   DevNode* d_nodes = nullptr;
   DevPrim* d_prims = nullptr;
   float* d_normals = nullptr;
@@ -216,6 +217,20 @@ void set_schedule(RenderParams& P, unsigned* sched) {
   P.tile_order = order_enabled() ? reinterpret_cast<int*>(sched) + P.num_sel_tiles : nullptr;
 }
 
+// True when the culling tree is 4-wide and no slot leads to a binary node (every guarded slot
+// is a leaf or a leaf pair), so the fast walk never visits a binary node.
+bool wide_only_tree(const HostScene& h) {
+  if (h.accel_root < 0 || !(h.accel_root & kWideTag)) return false;
+  for (size_t n = (size_t)(h.accel_root & ~kWideTag); n + 1 < h.nodes.size(); n += 2) {
+    DevNode4 W;
+    std::memcpy(&W, &h.nodes[n], sizeof W);
+    for (int k = 0; k < 4; k++)
+      if ((W.flags & (kWideValid << k)) && (W.flags & (kWideGuard << k)) && W.child[k] >= 0)
+        return false;
+  }
+  return true;
+}
+
 int create_from_host(rt_scene* s, int device) {
   if (device < 0) hip_check(hipGetDevice(&device), "hipGetDevice");
   s->device = device;
@@ -232,6 +247,7 @@ int create_from_host(rt_scene* s, int device) {
                                 " levels is not supported");
   s->deep = std::max(h.depth, h.accel_depth) > kLaneStack - 2;
   for (const DevPrim& p : h.prims) s->has_spheres |= p.kind == kPrimSphere;
+  s->wide_only = wide_only_tree(h);
   for (const DevMaterial& m : h.materials) {
     const bool mirror = m.mirror[0] != 0 || m.mirror[1] != 0 || m.mirror[2] != 0;
     const bool glass = m.transparency[0] != 0 || m.transparency[1] != 0 || m.transparency[2] != 0;
@@ -367,7 +383,7 @@ void enqueue_frame(rt_scene* s, const RenderParams& P, int samples, float* d_sam
   const bool cull = s->mode == RT_TRAVERSAL_CULL;
   if (samples <= 1) {
     hip_check(launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
-                            fast, s->deep, s->has_spheres, cull, timing_marks(s, P), stream),
+                            fast, s->deep, s->has_spheres, cull, s->wide_only, timing_marks(s, P), stream),
               "render launch");
     return;
   }
@@ -382,7 +398,7 @@ void enqueue_frame(rt_scene* s, const RenderParams& P, int samples, float* d_sam
     Q.tile_major = 0;
     Q.out = d_samples + (size_t)k * frame;
     hip_check(launch_render(Q, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
-                            fast, s->deep, s->has_spheres, cull, timing_marks(s, Q), stream),
+                            fast, s->deep, s->has_spheres, cull, s->wide_only, timing_marks(s, Q), stream),
               "render launch");
   }
   MsaaResolveParams M;

@@ -53,6 +53,24 @@ struct alignas(16) DevNode {
 };
 static_assert(sizeof(DevNode) == 64, "node must be one 64-byte scalar load");
 
+// 4-wide culling node (accel_build.cpp, collapse of the binary SAH tree): two consecutive
+// DevNode slots of `nodes`, referred to as (index of the first slot) | kWideTag, so a stack
+// entry says which kind it holds before the fetch.  Slot c of a wide node is valid when
+// flags bit kWideValid << c is set; it is then either a guarded treelet (bit kWideGuard << c:
+// child = ~leaf, with kWidePair << c the leaf pair ~child, ~child + 1, or a reference node
+// for treelets of more than two leaves) tested with the guard rule, or an inner wide node
+// (child = its tagged index) tested conservatively.
+constexpr int32_t kWideTag = 1 << 30;
+enum : int32_t { kWideGuard = 1, kWidePair = 16, kWideValid = 256 };
+struct alignas(16) DevNode4 {
+  float lo[3][4];
+  float hi[3][4];
+  int32_t child[4];
+  int32_t flags;  // kWideGuard << c | kWidePair << c | kWideValid << c
+  int32_t pad[3];
+};
+static_assert(sizeof(DevNode4) == 2 * sizeof(DevNode), "a wide node is two node slots");
+
 enum PrimKind : int32_t { kPrimTriangle = 0, kPrimSphere = 1 };
 
 struct alignas(16) DevPrim {

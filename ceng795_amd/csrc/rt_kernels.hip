@@ -650,6 +650,106 @@ __device__ __forceinline__ void batch_flush(WaveLeafLds& L, int n, const DevPrim
   }
 }
 
+// ------------------------------------------------------------------ wide culling nodes
+// Kernels with the batched leaf queue and one ray per lane walk the 4-wide culling tree
+// (accel_build.cpp collapse_wide); others get the binary one.
+bool wide_nodes_supported() { return kBatchLeaves && kRaysPerLane == 1; }
+
+__device__ __forceinline__ DevNode4 load_node4(const DevNode* __restrict__ nodes, int idx) {
+  return *reinterpret_cast<const DevNode4*>(nodes + idx);
+}
+
+// One packet visit of a wide culling node (R == 1, batched leaves), slot by slot with the
+// binary tree's rules (visit_node): a guarded slot accepts on a decided guard test (else
+// guard_exact), and its leaf or leaf pair goes straight to the leaf queue; an inner slot
+// culls only on a sure reject.  Of the entered inner slots one becomes `node` (SHADOW: the
+// nearest by the entry distance of the first entering lane, so occluders turn up early) and
+// the others are pushed.  `alive`: lanes still searching.  Up to 4 slots x 2 leaves x 64 lanes
+// of leaf tests are queued per visit, so the queue is run in between when it could overflow.
+// Returns false when the walk is over.
+template <bool SKIP, bool SHADOW, bool DEEP, bool SPHERES>
+__device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode* __restrict__ nodes,
+                                           const DevPrim* __restrict__ prims, WaveLeafLds& L,
+                                           int& pending, const LaneRay& r, float thr, int& node,
+                                           uint64_t& m, uint64_t alive, WaveStack<DEEP, 1>& st,
+                                           Diag& dg) {
+  const DevNode4 N = load_node4(nodes, node & ~kWideTag);
+  const bool in = (m >> lane_id()) & 1;
+  const int fl = N.flags;
+  DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m));
+  int nxt = -1;
+  uint64_t nm = 0;
+  float nkey = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    if (!(fl & (kWideValid << c))) continue;
+    const float b[6] = {N.lo[0][c], N.lo[1][c], N.lo[2][c], N.hi[0][c], N.hi[1][c], N.hi[2][c]};
+    float tn, tf;
+    slab_span<SKIP>(b, r, tn, tf);
+    bool sin, sout;
+    decide_sure(tn, tf, sin, sout);
+    const int ch = N.child[c];
+    const bool guard = (fl & (kWideGuard << c)) != 0;
+    bool h;
+    if (guard) {
+      h = in & sin;
+      const bool u = in & !(sin | sout);
+      if (ballot(u)) {
+        if (u) h = guard_exact(P, ch, r);
+        DIAG(if (u) atomicAdd(&g_exact_fallbacks, 1ull));
+      }
+    } else {
+      h = in & !sout;
+    }
+    const uint64_t hm = ballot(h) & alive;
+    if (!hm) continue;
+    if (guard && ch < 0) {  // a leaf, or a leaf pair
+      const bool pair = (fl & (kWidePair << c)) != 0;
+      if (pending > kBatchCap - 128) {
+        batch_flush<SHADOW, SPHERES>(L, pending, prims, r, thr);
+        pending = 0;
+      }
+      batch_push(L, pending, ~ch, hm);
+      if (pair) batch_push(L, pending, ~ch + 1, hm);
+      DIAG(dg.leaves += 1 + pair; dg.leaf_lanes += (1 + pair) * __builtin_popcountll(hm));
+      continue;
+    }
+    uint64_t mm[1] = {hm};
+    if (SHADOW) {
+      const float key = __int_as_float(
+          __builtin_amdgcn_readlane(__float_as_int(tn), (int)__builtin_ctzll(hm)));
+      if (nxt < 0 || key < nkey) {
+        if (nxt >= 0) {
+          uint64_t pm[1] = {nm};
+          st.push(nxt, pm);
+        }
+        nxt = ch;
+        nm = hm;
+        nkey = key;
+      } else {
+        st.push(ch, mm);
+      }
+    } else if (nxt < 0) {
+      nxt = ch;
+      nm = hm;
+    } else {
+      st.push(ch, mm);
+    }
+  }
+  if (nxt >= 0) {
+    node = nxt;
+    m = nm;
+    return true;
+  }
+  for (;;) {
+    if (st.sp == 0) return false;
+    uint64_t mm[1];
+    st.pop(node, mm);
+    m = mm[0] & alive;
+    if (m) return true;
+  }
+}
+
 // ------------------------------------------------------------------ subtree sharing
 // A workgroup's packets cost unequal amounts (tools/timeline.py: C3 primary packets take 60 to
 // 265 us), and a workgroup keeps its slot until its last wave ends, so waves that finish early
@@ -765,7 +865,7 @@ __device__ __forceinline__ bool share_next(BlockShare<W>& S, int& owner, int& no
 // DN: the donation policy (NoDonor, or Sharer in sharing workgroups, R == 1 and !DEEP only);
 // start_node >= 0: traverse the shared subtree (start_node, start_mask) instead of the tree.
 template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R, bool CULL = false,
-          class DN = NoDonor>
+          class DN = NoDonor, bool WO = false>
 __device__ __forceinline__ void closest_hit(const RenderParams& P,
                                             const DevNode* __restrict__ nodes,
                                             const DevPrim* __restrict__ prims, int* spill, WaveLeafLds& L,
@@ -836,6 +936,16 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
         uint64_t m0;
         st.bottom(n0, m0);
         if (dn.donate(n0, m0)) st.drop_bottom();
+      }
+    }
+    if constexpr (batch && FAST) {  // a wide culling node (WO: every node the walk meets is one)
+      if (WO || (node & kWideTag)) {
+        uint64_t mm = m[0];
+        const bool more = visit_wide<SKIP, false, DEEP, SPHERES>(P, nodes, prims, L, pending, r[0],
+                                                                0.0f, node, mm, ~0ull, st, dg);
+        m[0] = mm;
+        if (!more) break;
+        continue;
       }
     }
     const DevNode N = load_node(nodes, node);
@@ -926,7 +1036,7 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P,
 // Occluded iff some leaf the ray may reach has 0 < t < thr — identical to the reference's
 // closest-hit shadow test `0 < t_closest < dist - eps` (HW2/Scene.cpp:123-127), appendix A.7.
 template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R, bool CULL = false,
-          class DN = NoDonor>
+          class DN = NoDonor, bool WO = false>
 __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* __restrict__ nodes,
                                          const DevPrim* __restrict__ prims, int* spill, WaveLeafLds& L,
                                          const LaneRay (&r)[R], const bool (&active)[R],
@@ -992,6 +1102,16 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
         st.bottom(n0, m0);
         m0 &= alive[0];
         if (!m0 || dn.donate(n0, m0)) st.drop_bottom();
+      }
+    }
+    if constexpr (batch && FAST) {  // a wide culling node (WO: every node the walk meets is one)
+      if (WO || (node & kWideTag)) {
+        uint64_t mm = m[0];
+        const bool more = visit_wide<SKIP, true, DEEP, SPHERES>(P, nodes, prims, L, pending, r[0],
+                                                               thr[0], node, mm, alive[0], st, dg);
+        m[0] = mm;
+        if (!more) break;
+        continue;
       }
     }
     const DevNode N = load_node(nodes, node);
@@ -1173,7 +1293,7 @@ __device__ __forceinline__ int hit_leaf(int2_t rec) { return rec.x; }
 
 // R selected tiles per wave (tile sel0 + k is ray k of every lane): one packet traversal
 // serves 64*R rays, so the per-visit overhead (node fetch, masks, stack) is shared.
-template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL>
+template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL, bool WO = false>
 __device__ __forceinline__ void primary_packet(const RenderParams& P,
                                                const DevNode* __restrict__ nodes,
                                                const DevPrim* __restrict__ prims, int sel0,
@@ -1200,10 +1320,10 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
   int leaf[R];
   NoDonor nd;
   if (ballot(any_skip))
-    closest_hit<true, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, L, ray, valid, t, leaf,
+    closest_hit<true, FAST, DEEP, SPHERES, R, CULL, NoDonor, WO>(P, nodes, prims, spill, L, ray, valid, t, leaf,
                                                     dg, nd);
   else
-    closest_hit<false, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, L, ray, valid, t, leaf,
+    closest_hit<false, FAST, DEEP, SPHERES, R, CULL, NoDonor, WO>(P, nodes, prims, spill, L, ray, valid, t, leaf,
                                                      dg, nd);
   const RenderParams& Pw = fresh_params(P);  // post-traversal fields: not live across it
   unsigned long long nvalid = 0, nhit = 0;
@@ -1266,7 +1386,7 @@ __device__ __forceinline__ V3 hit_point(const RenderParams& P, const PacketPixel
 
 // Shadow rays of HW2/Scene.cpp:113-127: one bit per point light, set when the light is
 // occluded for this pixel's primary hit.  R tiles per wave as in primary_packet.
-template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL>
+template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL, bool WO = false>
 __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
                                               const DevNode* __restrict__ nodes,
                                               const DevPrim* __restrict__ prims,
@@ -1307,9 +1427,9 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       bool occ[R];
       NoDonor nd;
       if (ballot(any_skip))
-        occluded<true, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, L, sr, hit, thr, occ, dg, nd);
+        occluded<true, FAST, DEEP, SPHERES, R, CULL, NoDonor, WO>(P, nodes, prims, spill, L, sr, hit, thr, occ, dg, nd);
       else
-        occluded<false, FAST, DEEP, SPHERES, R, CULL>(P, nodes, prims, spill, L, sr, hit, thr, occ, dg, nd);
+        occluded<false, FAST, DEEP, SPHERES, R, CULL, NoDonor, WO>(P, nodes, prims, spill, L, sr, hit, thr, occ, dg, nd);
 #pragma unroll
       for (int k = 0; k < R; k++) bits[k] |= (occ[k] ? 1u : 0u) << (li - 32 * w);
     }
@@ -1918,7 +2038,7 @@ __device__ __forceinline__ void share_shadow(const RenderParams& P, const DevNod
 }
 
 // Traversal kernels: one packet per wave, XCD-remapped blocks of 2-D tile blocks.
-template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL>
+template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL, bool WO = false>
 __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY void trace_primary_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
@@ -1937,7 +2057,7 @@ __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY vo
     share_primary<FAST, SPHERES, CULL, W>(P, nodes, prims, sel, L, SH);
   } else if (sel >= 0) {
     const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
-    primary_packet<FAST, DEEP, SPHERES, R, CULL>(Q, nodes, prims, sel, spill, L);
+    primary_packet<FAST, DEEP, SPHERES, R, CULL, WO>(Q, nodes, prims, sel, spill, L);
     const RenderParams& Pw = fresh_params(P);
     if (R == 1 && Pw.tile_cost && lane_id() == 0)  // the shadow kernel's dispatch order
       Pw.tile_cost[sel] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - c0, 0xffffffffull);
@@ -1945,7 +2065,7 @@ __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY vo
   TL_END(0);
 }
 
-template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL>
+template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL, bool WO = false>
 __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY void trace_shadow_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims,
     const DevLight* __restrict__ lights) {
@@ -1970,7 +2090,7 @@ __global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY vo
     __shared__ BlockShare<W> SH;
     share_shadow<FAST, SPHERES, CULL, W>(P, nodes, prims, lights, sel, L, SH);
   } else if (sel >= 0) {
-    shadow_packet<FAST, DEEP, SPHERES, R, CULL>(Q, nodes, prims, lights, sel, spill, L);
+    shadow_packet<FAST, DEEP, SPHERES, R, CULL, WO>(Q, nodes, prims, lights, sel, spill, L);
   }
   TL_END(1);
 }
@@ -2035,7 +2155,7 @@ static inline void mark(const hipEvent_t* marks, int k, hipStream_t stream) {
   if (marks) (void)hipEventRecord(marks[k], stream);
 }
 
-template <bool FAST, bool DEEP, bool SPHERES, bool CULL>
+template <bool FAST, bool DEEP, bool SPHERES, bool CULL, bool WO = false>
 static void launch_variant(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                            const float* normals, const DevMaterial* mats,
                            const DevLight* lights, int blocks, const hipEvent_t* marks,
@@ -2062,7 +2182,7 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
   const bool ordered = R == 1 && P.num_lights > 0 && T.tile_order != nullptr;
   if (!ordered) T.tile_cost = S.tile_cost = nullptr, T.tile_order = S.tile_order = nullptr;
   mark(marks, 0, stream);
-  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, R, CULL>), dim3(tblocks),
+  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, R, CULL, WO>), dim3(tblocks),
                      dim3(W * 64), tlds, stream, T, nodes, prims);
   mark(marks, 1, stream);
   if (ordered)
@@ -2070,7 +2190,7 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
                        T.num_sel_tiles);
   const int sblocks = ordered ? (T.num_sel_tiles + W - 1) / W : tblocks;
   if (P.num_lights > 0)
-    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, R, CULL>), dim3(sblocks),
+    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, R, CULL, WO>), dim3(sblocks),
                        dim3(W * 64), tlds, stream, S, nodes, prims, lights);
   mark(marks, 2, stream);
   hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
@@ -2181,28 +2301,34 @@ hipError_t launch_quot_check(unsigned long long seed, long long count, unsigned 
 
 hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                          const float* normals, const DevMaterial* mats, const DevLight* lights,
-                         bool fast, bool deep, bool spheres, bool cull, const hipEvent_t* marks,
-                         hipStream_t stream) {
+                         bool fast, bool deep, bool spheres, bool cull, bool wide_only,
+                         const hipEvent_t* marks, hipStream_t stream) {
   if (P.num_sel_tiles <= 0) return hipSuccess;
   const int blocks = (P.num_sel_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-  const int v = (fast && cull ? 8 : 0) | (fast ? 4 : 0) | (deep ? 2 : 0) | (spheres ? 1 : 0);
+  // wide_only (the culling tree is 4-wide and reaches no binary node): kernels without the
+  // binary visit path, which costs the wide walk registers when compiled in
+  const bool wo = wide_only && fast && !deep && !cull && kRaysPerLane == 1 && kBatchLeaves;
+  const int v = (wo ? 16 : 0) | (fast && cull ? 8 : 0) | (fast ? 4 : 0) | (deep ? 2 : 0) |
+                (spheres ? 1 : 0);
   switch (v) {
-#define RT_CASE(F, D, S, C)                                                                  \
-  case (C ? 8 : 0) | (F ? 4 : 0) | (D ? 2 : 0) | (S ? 1 : 0):                                \
-    launch_variant<F, D, S, C>(P, nodes, prims, normals, mats, lights, blocks, marks, stream); \
+#define RT_CASE(F, D, S, C, W)                                                                    \
+  case (W ? 16 : 0) | (C ? 8 : 0) | (F ? 4 : 0) | (D ? 2 : 0) | (S ? 1 : 0):                      \
+    launch_variant<F, D, S, C, W>(P, nodes, prims, normals, mats, lights, blocks, marks, stream); \
     break;
-    RT_CASE(true, false, false, false)
-    RT_CASE(true, false, true, false)
-    RT_CASE(true, true, false, false)
-    RT_CASE(true, true, true, false)
-    RT_CASE(false, false, false, false)
-    RT_CASE(false, false, true, false)
-    RT_CASE(false, true, false, false)
-    RT_CASE(false, true, true, false)
-    RT_CASE(true, false, false, true)
-    RT_CASE(true, false, true, true)
-    RT_CASE(true, true, false, true)
-    RT_CASE(true, true, true, true)
+    RT_CASE(true, false, false, false, true)
+    RT_CASE(true, false, true, false, true)
+    RT_CASE(true, false, false, false, false)
+    RT_CASE(true, false, true, false, false)
+    RT_CASE(true, true, false, false, false)
+    RT_CASE(true, true, true, false, false)
+    RT_CASE(false, false, false, false, false)
+    RT_CASE(false, false, true, false, false)
+    RT_CASE(false, true, false, false, false)
+    RT_CASE(false, true, true, false, false)
+    RT_CASE(true, false, false, true, false)
+    RT_CASE(true, false, true, true, false)
+    RT_CASE(true, true, false, true, false)
+    RT_CASE(true, true, true, true, false)
 #undef RT_CASE
   }
   return hipGetLastError();
