@@ -185,14 +185,39 @@ def kernel_work(xml: str):
     return json.loads(out.strip().splitlines()[-1])
 
 
-def roofline_line(xml, world, local_share, kt, launches, prof):
+def isolated_kernel_times(scene, stream, frames: int):
+    """HIP-event kernel times of `frames` whole-frame renders of camera 0, one at a time on one
+    stream (no other frame in flight): each kernel's own duration, for the roofline."""
+    import torch
+    cam = scene.camera(0)
+    buf = torch.empty((cam.height, cam.width, 3), dtype=torch.float32, device="cuda")
+    scene.render_device(0, buf.data_ptr(), stream=stream.cuda_stream)  # warm
+    torch.cuda.synchronize()
+    scene.read_kernel_times()
+    scene.set_kernel_timing(True)
+    for _ in range(frames):
+        scene.render_device(0, buf.data_ptr(), stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    scene.set_kernel_timing(False)
+    kt, n = scene.read_kernel_times()
+    scene.collect_stats()
+    return kt, n
+
+
+def roofline_line(xml, world, local_share, kt, launches, prof, kt_iso=None, n_iso=0):
     # local_share: fraction of one frame's pixels a timed launch renders
     """Roofline of the dominant kernel (trace_primary_kernel): algorithmic bytes per launch
     (the kernel's own node / leaf fetches and its per-pixel record, tools/kernel_work.py) over
-    its HIP-event duration measured in the timed region; traffic = HBM bytes per launch of
-    that kernel from the PMC profile of this build (or null)."""
+    its HIP-event duration.  With frames in flight the timed region's launches share the GPU
+    with another frame's kernels, which stretches their start-to-end times; the roofline then
+    uses the same launches run one frame at a time right after the timed region (kt_iso), and
+    reports the timed-region average beside it.  traffic = HBM bytes per launch of that kernel
+    from the PMC profile of this build (or null)."""
     work = kernel_work(xml)
     per_launch = work["primary_bytes"] * local_share
+    prim_ms_timed = kt["primary"] / max(1, launches)
+    if kt_iso is not None and n_iso:
+        kt, launches, per_launch = kt_iso, n_iso, work["primary_bytes"]
     prim_ms = kt["primary"] / max(1, launches)
     achieved = per_launch / (prim_ms * 1e-3) / 1e9
     c = work["counters"]
@@ -200,10 +225,15 @@ def roofline_line(xml, world, local_share, kt, launches, prof):
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
             "kernel": "trace_primary_kernel",
             "kernel_ms_avg": round(prim_ms, 4),
+            "kernel_ms_avg_timed_region": round(prim_ms_timed, 4),
+            "kernel_timing": "one frame at a time after the timed region" if kt_iso is not None
+                             and n_iso else "timed region",
             "algorithmic_bytes_per_launch": int(per_launch),
-            "bytes_model": "64 B x node visits + 48 B x leaf visits + 8 B hit record per pixel "
-                           "(tools/kernel_work.py, RT_DIAG build, same frame)",
+            "bytes_model": "128 B x 4-wide node visits + 64 B x binary node visits + 48 B x leaf "
+                           "visits + 8 B hit record per pixel (tools/kernel_work.py, RT_DIAG "
+                           "build, same frame)",
             "work_per_frame": {"node_visits": c["prim_node_visits"],
+                               "wide_node_visits": c.get("prim_wide_visits"),
                                "leaf_visits": c["prim_leaf_visits"],
                                "lanes_per_node_visit": round(c["prim_node_lanes"] /
                                                              max(1, c["prim_node_visits"]), 2),
@@ -258,6 +288,14 @@ def main() -> int:
                     help="pieces per frame and rank for the gather pipeline (default 4 when "
                          "a rank renders one frame's share, else 1)")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight on one GPU: consecutive steps on that many streams, so "
+                         "one frame's sparsely occupied last waves overlap the next frame (whole-"
+                         "frame modes; 1 = one frame at a time)")
+    ap.add_argument("--tiles", action="store_true",
+                    help="deal 8x8 tiles of every frame round-robin over the ranks even when the "
+                         "job has a frame per rank (the strong-scaling layout; default then: "
+                         "whole frames per rank)")
     args = ap.parse_args()
     if args.workload == "c5":
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
@@ -293,6 +331,7 @@ def main() -> int:
 
     n_cams = args.frames if args.frames > 0 else world
     strong = n_cams < world
+    tiled = strong or args.tiles  # else whole frames per rank (FrameOwners)
     chunks = args.chunks if args.chunks > 0 else (4 if n_cams == 1 and use_pg else 1)
     if rank == 0:
         xml = scene_path(args.workload, n_cams)
@@ -303,10 +342,19 @@ def main() -> int:
     scene = ceng795_amd.Scene(xml, device=device, traversal=args.traversal)
     log(f"[rank {rank}] scene loaded + uploaded in {time.perf_counter() - t0:.2f} s, "
         f"BVH depth {scene.bvh_depth}")
-    plan = dist_tiles.TilePlan(scene, world, rank, force=use_pg)
     stream = torch.cuda.current_stream()
-    renderer = dist_tiles.FrameRenderer(scene, plan, stream, gather=use_pg,
-                                        host_staging=args.dist_backend == "gloo", chunks=chunks)
+    if use_pg and not tiled:
+        owners = dist_tiles.FrameOwners(n_cams, world, rank)
+        sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
+        renderer = dist_tiles.FrameGatherRenderer(scene, owners, sizes, stream,
+                                                  host_staging=args.dist_backend == "gloo",
+                                                  inflight=args.inflight,
+                                                  device=torch.device("cuda", device))
+    else:
+        plan = dist_tiles.TilePlan(scene, world, rank, force=use_pg)
+        renderer = dist_tiles.FrameRenderer(scene, plan, stream, gather=use_pg,
+                                            host_staging=args.dist_backend == "gloo", chunks=chunks,
+                                            inflight=args.inflight)
 
     # warmup (also yields the per-step ray count from the device counters)
     for _ in range(args.warmup):
@@ -383,7 +431,8 @@ def main() -> int:
                 # fraction of one frame's work in one launch (one rt_render_device call)
                 share = rays_local / max(1.0, rays_step / n_cams) / max(1.0, launches / args.steps)
                 prof = pmc_profile(args.workload) if world == 1 else None
-                roof = roofline_line(xml, world, share, kt, launches, prof)
+                kt_iso, n_iso = isolated_kernel_times(scene, stream, max(3, args.steps // 2))
+                roof = roofline_line(xml, world, share, kt, launches, prof, kt_iso, n_iso)
                 roof["timed_launches"] = launches
                 roof["stream_copy_GBps_measured"] = round(stream_copy_gbps(device), 1)
                 bytes_ref, ostats = algorithmic_bytes(xml, threads)
@@ -413,8 +462,10 @@ def main() -> int:
             "config": {"workload": desc, "frame": f"{w}x{h}", "frames_per_step": n_cams,
                        "triangles": 2 * (n - 1) ** 2, "rays_per_step": int(rays_step),
                        "traversal": args.traversal,
-                       "parallelism": f"tiles{world}" + (f"+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}_gather" if use_pg else ""),
-                       "gather_chunks": chunks if use_pg else None,
+                       "parallelism": (f"tiles{world}" if tiled and use_pg else f"frames{world}") +
+                                      (f"+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}_gather" if use_pg else ""),
+                       "frames_in_flight": renderer.inflight if hasattr(renderer, "inflight") else 1,
+                       "gather_chunks": chunks if use_pg and tiled else None,
                        "gather_verified": verified,
                        "render_ms_avg": round(sum(render_ms) / len(render_ms), 4)},
             "roofline": roof, "cpu_baseline": cpu,

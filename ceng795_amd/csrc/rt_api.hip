@@ -87,6 +87,21 @@ struct rt_scene {
   size_t hits_capacity = 0;  // records
   float* d_samples = nullptr;  // MSAA per-sample colours [s][h][w][3]
   size_t samples_capacity = 0;
+  // rt_render_device scratch of every further stream the scene renders on (the first one uses
+  // the buffers above): frames on different streams may be in flight together
+  struct StreamScratch {
+    void* stream;
+    int2_t* hits;
+    unsigned* occ;
+    unsigned* sched;
+    float* frames;
+    size_t frames_capacity;
+    float* samples;
+    size_t samples_capacity;
+  };
+  void* first_stream = nullptr;
+  bool first_stream_set = false;
+  std::vector<StreamScratch> streams;
   unsigned long long msaa_seed = 0;
   std::mutex ctx_mu;
   std::vector<RenderCtx*> ctx_free, ctx_all;
@@ -177,6 +192,13 @@ void free_device(rt_scene* s) {
   (void)hipFree(s->d_sched);
   (void)hipFree(s->d_frames);
   (void)hipFree(s->d_samples);
+  for (auto& x : s->streams) {
+    (void)hipFree(x.hits);
+    (void)hipFree(x.occ);
+    (void)hipFree(x.sched);
+    (void)hipFree(x.frames);
+    (void)hipFree(x.samples);
+  }
   if (cur != s->device) (void)hipSetDevice(cur);
 }
 
@@ -603,6 +625,50 @@ int rt_render_device(rt_scene* s, int cam, int row0, int row_stride, int tile_be
                                 d_out, stream);
 }
 
+// The scratch buffers of `stream`: the scene's own for the first stream it renders on, a set
+// of its own (same sizes) for each further one.
+struct Scratch {
+  int2_t** hits;
+  unsigned** occ;
+  unsigned** sched;
+  float** frames;
+  size_t* frames_capacity;
+  float** samples;
+  size_t* samples_capacity;
+};
+Scratch scratch_for(rt_scene* s, void* stream) {
+  std::lock_guard<std::mutex> lk(s->ctx_mu);
+  if (!s->first_stream_set) {
+    s->first_stream_set = true;
+    s->first_stream = stream;
+  }
+  if (stream == s->first_stream)
+    return {&s->d_hits, &s->d_occ, &s->d_sched, &s->d_frames, &s->frames_capacity,
+            &s->d_samples, &s->samples_capacity};
+  for (auto& x : s->streams)
+    if (x.stream == stream)
+      return {&x.hits, &x.occ, &x.sched, &x.frames, &x.frames_capacity, &x.samples,
+              &x.samples_capacity};
+  rt_scene::StreamScratch x{stream, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0};
+  const size_t most = s->hits_capacity;
+  try {
+    hip_check(hipMalloc(&x.hits, most * sizeof(int2_t)), "alloc hit records");
+    hip_check(hipMalloc(&x.occ, most * sizeof(unsigned) * occ_words(s->host)),
+              "alloc occlusion bits");
+    hip_check(hipMalloc(&x.sched, 2 * (most / (kTile * kTile)) * sizeof(unsigned)),
+              "alloc tile schedule");
+  } catch (...) {
+    (void)hipFree(x.hits);
+    (void)hipFree(x.occ);
+    (void)hipFree(x.sched);
+    throw;
+  }
+  s->streams.push_back(x);
+  auto& y = s->streams.back();
+  return {&y.hits, &y.occ, &y.sched, &y.frames, &y.frames_capacity, &y.samples,
+          &y.samples_capacity};
+}
+
 int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int tile_begin,
                            int tile_step, int tile_count, int tile_major, float* d_out,
                            void* stream) {
@@ -611,8 +677,12 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
       if (tile_begin < 0 || tile_step < 1 || !d_out)
         throw std::invalid_argument("rt_render_device: bad tile selection / output");
       DeviceGuard g(s->device);
+      const Scratch sc = scratch_for(s, stream);
       RenderParams P =
           make_params(s, cam, row0, row_stride, tile_begin, tile_step, tile_major, d_out, true);
+      P.hits = *sc.hits;
+      P.occ = *sc.occ;
+      set_schedule(P, *sc.sched);
       if (tile_count >= 0 && tile_count < P.num_sel_tiles) {
         if (s->host.cameras[cam].num_samples > 1)
           throw std::domain_error("NumSamples > 1 renders whole row-major frames only");
@@ -620,29 +690,29 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
       }
       if (s->needs_recursion) {
         const size_t need = frame_floats(s->host, P.num_sel_tiles);
-        if (need > s->frames_capacity) {
-          (void)hipFree(s->d_frames);
-          s->d_frames = nullptr;
-          s->frames_capacity = 0;
-          hip_check(hipMalloc(&s->d_frames, need * sizeof(float)), "alloc ray-tree frames");
-          s->frames_capacity = need;
+        if (need > *sc.frames_capacity) {
+          (void)hipFree(*sc.frames);
+          *sc.frames = nullptr;
+          *sc.frames_capacity = 0;
+          hip_check(hipMalloc(sc.frames, need * sizeof(float)), "alloc ray-tree frames");
+          *sc.frames_capacity = need;
         }
-        P.frames = s->d_frames;
+        P.frames = *sc.frames;
       }
       const rt_camera& c = s->host.cameras[cam];
       if (c.num_samples > 1) {
         if (tile_begin != 0 || tile_step != 1 || tile_major)
           throw std::domain_error("NumSamples > 1 renders whole row-major frames only");
         const size_t need = sample_floats(c);
-        if (need > s->samples_capacity) {
-          (void)hipFree(s->d_samples);
-          s->d_samples = nullptr;
-          s->samples_capacity = 0;
-          hip_check(hipMalloc(&s->d_samples, need * sizeof(float)), "alloc MSAA samples");
-          s->samples_capacity = need;
+        if (need > *sc.samples_capacity) {
+          (void)hipFree(*sc.samples);
+          *sc.samples = nullptr;
+          *sc.samples_capacity = 0;
+          hip_check(hipMalloc(sc.samples, need * sizeof(float)), "alloc MSAA samples");
+          *sc.samples_capacity = need;
         }
       }
-      enqueue_frame(s, P, c.num_samples, s->d_samples, (hipStream_t)stream);
+      enqueue_frame(s, P, c.num_samples, *sc.samples, (hipStream_t)stream);
       return RT_OK;
   });
 }

@@ -29,7 +29,9 @@ enum : int {
   kCntShadNodes = 8, kCntShadNodeLanes = 9, kCntShadLeaves = 10, kCntShadLeafLanes = 11,
   kCntExactBox = 12,
   // subtree sharing: pieces run by a wave other than the packet's owner
-  kCntShared = 13
+  kCntShared = 13,
+  // RT_DIAG builds: the node visits above that were 4-wide culling nodes (128 B each)
+  kCntPrimWide = 14, kCntShadWide = 15
 };
 
 // DevNode::pad of the culling-tree nodes (accel_build.cpp); reference nodes have pad == 0.

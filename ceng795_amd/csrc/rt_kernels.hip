@@ -43,7 +43,7 @@ constexpr int kRaysPerLane = RT_RAYS_PER_LANE;  // tiles per wave in the travers
 #define DIAG(stmt)
 #endif
 struct Diag {  // per-wave traversal work (RT_DIAG builds)
-  unsigned long long nodes = 0, node_lanes = 0, leaves = 0, leaf_lanes = 0, exact = 0;
+  unsigned long long nodes = 0, node_lanes = 0, leaves = 0, leaf_lanes = 0, exact = 0, wide = 0;
 };
 
 // ------------------------------------------------------------------ vector helpers
@@ -676,7 +676,7 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
   const DevNode4 N = load_node4(nodes, node & ~kWideTag);
   const bool in = (m >> lane_id()) & 1;
   const int fl = N.flags;
-  DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m));
+  DIAG(dg.nodes++; dg.wide++; dg.node_lanes += __builtin_popcountll(m));
   int nxt = -1;
   uint64_t nm = 0;
   float nkey = 0.0f;
@@ -1347,6 +1347,7 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
     atomicAdd(&c[kCntPrimNodeLanes], dg.node_lanes);
     atomicAdd(&c[kCntPrimLeaves], dg.leaves);
     atomicAdd(&c[kCntPrimLeafLanes], dg.leaf_lanes);
+    atomicAdd(&c[kCntPrimWide], dg.wide);
 #endif
   }
 }
@@ -1455,6 +1456,7 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
     atomicAdd(&c[kCntShadNodeLanes], dg.node_lanes);
     atomicAdd(&c[kCntShadLeaves], dg.leaves);
     atomicAdd(&c[kCntShadLeafLanes], dg.leaf_lanes);
+    atomicAdd(&c[kCntShadWide], dg.wide);
 #endif
   }
 }
@@ -1968,6 +1970,7 @@ __device__ __forceinline__ void share_primary(const RenderParams& P, const DevNo
     atomicAdd(&c[kCntPrimNodeLanes], dg.node_lanes);
     atomicAdd(&c[kCntPrimLeaves], dg.leaves);
     atomicAdd(&c[kCntPrimLeafLanes], dg.leaf_lanes);
+    atomicAdd(&c[kCntPrimWide], dg.wide);
 #endif
   }
 }
@@ -2033,6 +2036,7 @@ __device__ __forceinline__ void share_shadow(const RenderParams& P, const DevNod
     atomicAdd(&c[kCntShadNodeLanes], dg.node_lanes);
     atomicAdd(&c[kCntShadLeaves], dg.leaves);
     atomicAdd(&c[kCntShadLeafLanes], dg.leaf_lanes);
+    atomicAdd(&c[kCntShadWide], dg.wide);
 #endif
   }
 }

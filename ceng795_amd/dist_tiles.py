@@ -108,7 +108,10 @@ def untile_camera(gathered_c, layout: TileLayout, c: int, index=None, out=None):
 class FrameRenderer:
     """One step = render every camera of `scene`; with gather=True, gather to rank 0 and untile.
 
-    world == 1 and gather == False renders each camera in place into a row-major frame.
+    world == 1 and gather == False renders each camera in place into a row-major frame.  With
+    inflight = F > 1 consecutive steps go to F streams in turn (each with its own frames and,
+    in the library, its own scratch), so a frame's last, sparsely occupied waves overlap the
+    next frame's work; finish() joins them back into `stream`.
 
     gather=True (one process per GPU): camera c's share is rendered on `stream` in `chunks`
     pieces (rt_render_device_range); an event hands each piece to a communication stream that
@@ -125,7 +128,7 @@ class FrameRenderer:
     """
 
     def __init__(self, scene, layout_or_none: Optional[TileLayout], stream, gather: bool,
-                 host_staging: bool = False, chunks: int = 1):
+                 host_staging: bool = False, chunks: int = 1, inflight: int = 1):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -138,8 +141,13 @@ class FrameRenderer:
         self.layout = layout_or_none
         dev = torch.device("cuda", torch.cuda.current_device())
         if not gather:
-            self.frames = [torch.empty((h, w, 3), dtype=torch.float32, device=dev)
-                           for (w, h) in self.sizes]
+            self.inflight = max(1, int(inflight))
+            self.streams = [stream] + [torch.cuda.Stream(device=dev)
+                                       for _ in range(self.inflight - 1)]
+            self.frame_sets = [[torch.empty((h, w, 3), dtype=torch.float32, device=dev)
+                                for (w, h) in self.sizes] for _ in range(self.inflight)]
+            self.frames = self.frame_sets[0]
+            self.k = 0
             return
         L = self.layout
         assert L.sizes == self.sizes, "tile layout built for other frame sizes"
@@ -203,10 +211,16 @@ class FrameRenderer:
         if events is not None:
             events[0].record(self.stream)
         if not self.gather:
+            slot = self.k % self.inflight
+            self.k += 1
+            st = self.streams[slot]
+            if events is not None and slot:
+                events[0].record(st)
+            self.frames = self.frame_sets[slot]
             for c, f in enumerate(self.frames):
-                self.scene.render_device(c, f.data_ptr(), stream=s)
+                self.scene.render_device(c, f.data_ptr(), stream=st.cuda_stream)
             if events is not None:
-                events[1].record(self.stream)
+                events[1].record(st)
             return self.frames
         self.buf ^= 1
         for c, sh in enumerate(self.layout.shares):
@@ -229,6 +243,112 @@ class FrameRenderer:
         """Make `stream` wait for every outstanding gather / untile of this renderer."""
         if self.gather and not self.host_staging:
             self.stream.wait_stream(self.comm)
+        elif not self.gather:
+            for st in self.streams[1:]:
+                self.stream.wait_stream(st)
+
+
+class FrameOwners:
+    """Whole-frame assignment for jobs of at least one frame per rank (weak scaling): camera c
+    belongs to rank c mod world.  Gather round j collects cameras j*world .. j*world + world-1
+    (one frame from every rank; a rank with no camera in the round sends padding)."""
+
+    def __init__(self, n_cams: int, world: int, rank: int):
+        self.n_cams, self.world, self.rank = n_cams, world, rank
+        self.rounds = (n_cams + world - 1) // world
+        self.owned = [j * world + rank for j in range(self.rounds)]  # may exceed n_cams - 1
+
+    def camera(self, j: int, r: int) -> int:
+        return j * self.world + r
+
+
+class FrameGatherRenderer:
+    """One step = every rank renders its own whole frames (FrameOwners) in place and rank 0
+    gathers them: per round j, one equal-size collective of full row-major frames (RCCL over
+    xGMI with backend "nccl", host copies with gloo).  Unlike the tile deal of FrameRenderer,
+    a rank's frame is one launch of a full frame, so per-launch work does not shrink as the
+    world grows.  Consecutive steps alternate over `inflight` render streams, each with its own
+    send / receive buffers; a buffer set is rendered again only after its gathers `inflight`
+    steps earlier have finished (events), and rank 0's frames of a step are complete once
+    finish() has joined the streams.
+
+    render(c, out, stream) writes camera c's [h, w, 3] frame into tensor `out` on `stream`
+    (None: the scene's rt_render_device), so the same bookkeeping runs in the gloo tests."""
+
+    def __init__(self, scene, owners: FrameOwners, sizes, stream, host_staging=False,
+                 inflight=2, device=None, render=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.owners, self.stream, self.host_staging = owners, stream, host_staging
+        self.sizes = [tuple(x) for x in sizes]
+        assert len(set(self.sizes)) == 1, "every frame of a gather round must have one size"
+        w, h = self.sizes[0]
+        self.render = render or (lambda c, out, st: scene.render_device(
+            c, out.data_ptr(), stream=st.cuda_stream))
+        self.inflight = max(1, int(inflight)) if not host_staging else 1
+        dev = device
+        self.streams = [stream] + ([torch.cuda.Stream(device=dev)
+                                    for _ in range(self.inflight - 1)] if not host_staging else [])
+        self.comm = torch.cuda.Stream(device=dev) if not host_staging else None
+        W = owners.world
+        self.send = [[torch.zeros((h, w, 3), dtype=torch.float32, device=dev)
+                      for _ in range(owners.rounds)] for _ in range(self.inflight)]
+        self.recv = None
+        if owners.rank == 0:
+            self.recv = [[torch.empty((h, w, 3), dtype=torch.float32, device=dev)
+                          for _ in range(owners.rounds * W)] for _ in range(self.inflight)]
+        self.done = [torch.cuda.Event() if not host_staging else None for _ in range(self.inflight)]
+        self.used = [False] * self.inflight
+        self.k = 0
+        self.frames = None
+
+    def step(self, events=None):
+        torch, dist, O = self.torch, self.dist, self.owners
+        slot = self.k % self.inflight
+        self.k += 1
+        st = self.streams[slot] if not self.host_staging else self.stream
+        if events is not None and st is not None:
+            events[0].record(st)
+        if self.used[slot] and not self.host_staging:  # its gathers `inflight` steps ago
+            st.wait_event(self.done[slot])
+        for j in range(O.rounds):
+            c = O.camera(j, O.rank)
+            if c < O.n_cams:
+                self.render(c, self.send[slot][j], st)
+            outs = ([self.recv[slot][O.camera(j, r)] for r in range(O.world)]
+                    if O.rank == 0 else None)
+            if self.host_staging:
+                if st is not None:
+                    st.synchronize()
+                host = self.send[slot][j].cpu()
+                hl = list(torch.empty((O.world,) + tuple(host.shape))) if O.rank == 0 else None
+                dist.gather(host, hl, dst=0)
+                if O.rank == 0:
+                    for r in range(O.world):
+                        outs[r].copy_(hl[r])
+                continue
+            ev = torch.cuda.Event()
+            ev.record(st)
+            with torch.cuda.stream(self.comm):
+                self.comm.wait_event(ev)
+                work = dist.gather(self.send[slot][j], outs, dst=0, async_op=True)
+                work.wait()  # the comm stream waits for the collective
+        if not self.host_staging:
+            self.done[slot].record(self.comm)
+            self.used[slot] = True
+        if events is not None and st is not None:
+            events[1].record(st)
+        self.frames = self.recv[slot][:O.n_cams] if O.rank == 0 else None
+        return self.frames
+
+    def finish(self):
+        """Make `stream` wait for every render stream and every outstanding gather."""
+        if self.host_staging:
+            return
+        for st in self.streams[1:]:
+            self.stream.wait_stream(st)
+        self.stream.wait_stream(self.comm)
 
 
 def chunk_ranges(slot: int, chunks: int) -> List[Tuple[int, int]]:

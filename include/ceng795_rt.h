@@ -173,9 +173,11 @@ int rt_render(rt_scene* scene, int camera_index, int starting_row, int row_strid
  *   tile_major == 1: d_out holds the selected tiles back to back, 8*8*3 floats each
  *                    (pixels outside the image are written as 0).
  * MSAA cameras: only the whole frame, row-major (tile_begin 0, tile_step 1, tile_major 0).
- * Asynchronous on `hip_stream` (a hipStream_t, NULL = default stream).  stats may be NULL;
- * when given, ray counts are filled after the caller synchronises the stream and calls
- * rt_collect_stats. */
+ * Asynchronous on `hip_stream` (a hipStream_t, NULL = default stream).  Ray counts
+ * accumulate on the device until rt_collect_stats.  Calls on one stream run in order and share
+ * that stream's scratch buffers (hit records, occlusion bits, tile schedule); each further
+ * stream a scene renders on gets scratch of its own, so frames on different streams may be
+ * in flight at the same time (their outputs must not overlap). */
 int rt_render_device(rt_scene* scene, int camera_index, int starting_row, int row_stride,
                      int tile_begin, int tile_step, int tile_major, float* d_out,
                      void* hip_stream);

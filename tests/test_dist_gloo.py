@@ -182,3 +182,42 @@ def test_piece_calls_cover_share():
                 for lo, begin, n in piece_calls(sh, chunk_ranges(sh.slot, 4)):
                     tiles += [begin + k * sh.tile_step for k in range(n)]
                 assert tiles == [sh.tile_begin + k * world for k in range(sh.count)]
+
+
+# --------------------------------------------------------------------------- whole frames per rank
+def _frame_worker(rank, world, port, outdir, n_cams):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ceng795_amd.dist_tiles import FrameGatherRenderer, FrameOwners
+    w, h = 24, 16
+    rng = np.random.default_rng(11)
+    truth = [rng.standard_normal((h, w, 3)).astype(np.float32) for _ in range(n_cams)]
+    rendered = []
+
+    def render(c, out, stream):  # what rt_render_device writes for camera c
+        rendered.append(c)
+        out.copy_(torch.from_numpy(truth[c]))
+
+    owners = FrameOwners(n_cams, world, rank)
+    R = FrameGatherRenderer(None, owners, [(w, h)] * n_cams, None, host_staging=True,
+                            device="cpu", render=render)
+    for _ in range(2):  # two steps: buffers reused
+        frames = R.step()
+    R.finish()
+    assert sorted(set(rendered)) == [c for c in range(n_cams) if c % world == rank]
+    if rank == 0:
+        assert len(frames) == n_cams
+        ok = all(_same(frames[c].numpy(), truth[c]) for c in range(n_cams))
+        with open(os.path.join(outdir, "frames_ok"), "w") as f:
+            f.write("1" if ok else "0")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_cams", [(2, 2), (2, 4), (3, 4)])
+def test_whole_frames_per_rank_gather(tmp_path, world, n_cams):
+    """Weak-scaling layout: camera c rendered whole by rank c mod world, gathered per round
+    (a rank with no camera in the last round sends padding, which rank 0 drops)."""
+    mp.spawn(_frame_worker, args=(world, _free_port(), str(tmp_path), n_cams), nprocs=world,
+             join=True)
+    assert open(os.path.join(tmp_path, "frames_ok")).read() == "1"

@@ -4,8 +4,8 @@
 and lane tests per kernel.  bench.py runs this as a child process (CENG795_LIB=diag selects the
 diagnostic library; the timed library is never instrumented) to price its roofline:
 
-    algorithmic bytes of a traversal launch = 64 B x node visits   (one DevNode scalar load
-                                                                    per packet visit)
+    algorithmic bytes of a traversal launch = 64 B x binary node visits + 128 B x 4-wide node
+                                              visits (one node's scalar loads per packet visit)
                                             + 48 B x leaf visits   (one DevPrim per
                                                                     (packet, leaf) pair)
                                             + per-pixel records    (primary: 8 B hit record
@@ -46,11 +46,13 @@ def main():
             raise SystemExit("not a diagnostic build")
         pixels = c.width * c.height
         words = max(1, (s.num_lights + 31) // 32)
-        prim = 64 * d["prim_node_visits"] + 48 * d["prim_leaf_visits"] + 8 * pixels
-        shad = (64 * d["shad_node_visits"] + 48 * d["shad_leaf_visits"]
-                + (8 + 4 * words) * pixels) if s.num_lights else 0
+        node_bytes = lambda n, wide: 64 * (n - wide) + 128 * wide  # noqa: E731
+        prim = (node_bytes(d["prim_node_visits"], d["prim_wide_visits"])
+                + 48 * d["prim_leaf_visits"] + 8 * pixels)
+        shad = (node_bytes(d["shad_node_visits"], d["shad_wide_visits"])
+                + 48 * d["shad_leaf_visits"] + (8 + 4 * words) * pixels) if s.num_lights else 0
         out = {"pixels": pixels, "packets": ((c.width + 7) // 8) * ((c.height + 7) // 8),
-               "counters": {k: v for k, v in d.items() if k not in ("c13", "c14", "c15")},
+               "counters": {k: v for k, v in d.items() if k != "shared_pieces"},
                "primary_bytes": prim, "shadow_bytes": shad}
     print(json.dumps(out))
 
