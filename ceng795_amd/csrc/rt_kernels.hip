@@ -1828,8 +1828,11 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
 
 // Traversal kernels hide their dependent node loads with occupancy: hold them to 8 waves/SIMD
 // (<= 64 VGPRs, <= 100 SGPRs); the compiler otherwise settles at 7 on SGPR count.
+#ifndef RT_TRACE_MIN_WAVES  // (A/B: fewer waves per SIMD, more registers per wave)
+#define RT_TRACE_MIN_WAVES 8
+#endif
 #ifndef RT_TRAVERSAL_OCCUPANCY
-#define RT_TRAVERSAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(8, 8)))
+#define RT_TRAVERSAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_TRACE_MIN_WAVES, 8)))
 #endif
 
 // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so hand each

@@ -159,6 +159,9 @@ class FrameRenderer:
                       for _ in range(2)]
         self.buf = 0
         self.comm = torch.cuda.Stream(device=dev)
+        # pieces alternate between two render streams (the library gives each its own scratch),
+        # so one piece's last, sparsely occupied waves overlap the next piece
+        self.pstreams = [stream, torch.cuda.Stream(device=dev)]
         self.rendered = [[torch.cuda.Event() for _ in p] for p in self.pieces]
         self.slot_free = [[torch.cuda.Event() for _ in L.shares] for _ in range(2)]
         self.slot_used = [[False] * len(L.shares) for _ in range(2)]
@@ -223,16 +226,20 @@ class FrameRenderer:
                 events[1].record(st)
             return self.frames
         self.buf ^= 1
+        k = 0
         for c, sh in enumerate(self.layout.shares):
             if self.slot_used[self.buf][c]:  # this slot's gather two steps ago
-                self.stream.wait_event(self.slot_free[self.buf][c])
+                for ps in self.pstreams:
+                    ps.wait_event(self.slot_free[self.buf][c])
             slot = self._slot(sh)
             for j, (lo, begin, n) in enumerate(piece_calls(sh, self.pieces[c])):
+                ps = self.pstreams[k % 2] if not self.host_staging else self.stream
+                k += 1
                 if n > 0:
                     self.scene.render_device(sh.camera, slot[lo].data_ptr(), tile_begin=begin,
                                              tile_step=sh.tile_step, tile_count=n,
-                                             tile_major=True, stream=s)
-                self.rendered[c][j].record(self.stream)
+                                             tile_major=True, stream=ps.cuda_stream)
+                self.rendered[c][j].record(ps)
                 self._exchange(c, sh, j)
             self.slot_used[self.buf][c] = True
         if events is not None:
@@ -242,6 +249,7 @@ class FrameRenderer:
     def finish(self):
         """Make `stream` wait for every outstanding gather / untile of this renderer."""
         if self.gather and not self.host_staging:
+            self.stream.wait_stream(self.pstreams[1])
             self.stream.wait_stream(self.comm)
         elif not self.gather:
             for st in self.streams[1:]:
