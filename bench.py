@@ -204,6 +204,27 @@ def isolated_kernel_times(scene, stream, frames: int):
     return kt, n
 
 
+def host_buffer_rate(scene, rays_frame: float, frames: int = 5):
+    """The drop-in host-buffer call (rt_render = Scene::render_image filling a host Image, HW2/
+    Scene.h:34-35) on camera 0, one frame at a time: render + device-to-host copy of the float
+    RGB frame, into a pageable numpy array and into a pinned one.  Mrays/s; never `value`."""
+    import numpy as np
+    import torch
+    cam = scene.camera(0)
+    out = {}
+    pinned = torch.empty((cam.height, cam.width, 3), dtype=torch.float32, pin_memory=True)
+    for kind, arr in (("pageable", np.empty((cam.height, cam.width, 3), np.float32)),
+                      ("pinned", pinned.numpy())):
+        scene.render_image(0, arr)  # warm
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            scene.render_image(0, arr)
+        sec = (time.perf_counter() - t0) / frames
+        out[kind] = {"Mrays_s": round(rays_frame / sec / 1e6, 1), "ms_per_frame": round(sec * 1e3, 3)}
+    out["frame_bytes"] = cam.height * cam.width * 3 * 4
+    return out
+
+
 def roofline_line(xml, world, local_share, kt, launches, prof, kt_iso=None, n_iso=0):
     # local_share: fraction of one frame's pixels a timed launch renders
     """Roofline of the dominant kernel (trace_primary_kernel): algorithmic bytes per launch
@@ -445,6 +466,12 @@ def main() -> int:
                                            "make those fetches)")
             except Exception as e:  # the checker must never hide the measurement
                 log(f"roofline accounting failed: {e!r}")
+        host_rate = None
+        if world == 1:
+            try:
+                host_rate = host_buffer_rate(scene, rays_step / n_cams)
+            except Exception as e:
+                log(f"host-buffer rate failed: {e!r}")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -468,7 +495,7 @@ def main() -> int:
                        "gather_chunks": chunks if use_pg and tiled else None,
                        "gather_verified": verified,
                        "render_ms_avg": round(sum(render_ms) / len(render_ms), 4)},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "pcie_inclusive": host_rate,
         }
         if strong and t1_ms is not None:
             line["strong_scaling"] = {"t1_ms": round(t1_ms, 4), "tN_ms": round(ms_step, 4),

@@ -182,6 +182,34 @@ def test_msaa_whole_frames_only(rt, scene_dir):
                               got.view(np.uint32))
 
 
+@pytest.mark.parametrize("name", ["hf_side", "msaa4"])
+def test_frames_in_flight_on_several_streams(rt, scene_dir, name):
+    """bench.py keeps two frames in flight: every stream a scene renders on gets its own
+    scratch (rt_api.hip scratch_for), so frames queued on three streams without host syncs in
+    between must each equal the oracle's frame bit for bit."""
+    import torch
+    xml = scenes.write(name, scene_dir)
+    o = OracleScene(xml)
+    with rt.Scene(xml) as s:
+        s.set_msaa_seed(0)
+        ncam = s.num_cameras
+        refs = [o.render_msaa(c, seed=0, threads=THREADS)[0] if name.startswith("msaa")
+                else oracle_frame(xml, c)[0] for c in range(ncam)]
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        jobs = []
+        for k in range(9):
+            cam = k % ncam
+            c = s.camera(cam)
+            buf = torch.full((c.height, c.width, 3), -1.0, dtype=torch.float32, device="cuda")
+            streams[k % 3].wait_stream(torch.cuda.current_stream())  # the fill comes first
+            s.render_device(cam, buf.data_ptr(), stream=streams[k % 3].cuda_stream)
+            jobs.append((cam, buf))
+        torch.cuda.synchronize()
+        for k, (cam, buf) in enumerate(jobs):
+            got = buf.cpu().numpy()
+            assert np.array_equal(got.view(np.uint32), refs[cam].view(np.uint32)), (name, k, cam)
+
+
 def test_shared_reciprocal_quotients_are_ieee(rt):
     """tri_quotients (one v_rcp + Markstein steps for the three Cramer divisions) gives the bits
     of IEEE `/` over its whole operand range, incl. all-ones divisor mantissas and quotients
