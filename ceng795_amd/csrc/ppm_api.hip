@@ -43,11 +43,11 @@ hipError_t launch_tile_table(const int*, const int*, int, int2*, hipStream_t);
 hipError_t launch_tile_work(const int2*, int, const int*, const int*, unsigned*, hipStream_t);
 hipError_t launch_rr_table(float*, int, hipStream_t);
 hipError_t launch_materialize(const unsigned*, const unsigned*, int, const PDeposit*,
-                              const unsigned*, const unsigned*, const int*, const int*, PDeposit*,
-                              unsigned char*, hipStream_t);
+                              const unsigned*, const unsigned*, const int*, const int*, float4*,
+                              hipStream_t);
 hipError_t launch_group_update(const PScene&, const PHitPoint*, const int*, const int*,
-                               const int2*, int, const int*, const int*, const PDeposit*,
-                               const unsigned char*, const float*, int, float4*, unsigned*,
+                               const int2*, int, const int*, const int*, const float4*,
+                               const PDeposit*, const float*, int, float4*, unsigned*,
                                unsigned long long*, hipStream_t);
 hipError_t launch_density(const PHitPoint*, const float4*, const int*, int, double, float*,
                           hipStream_t);
@@ -184,8 +184,7 @@ struct ppm_scene {
   DevBuf<unsigned> gb;                           // per group: buckets, multiplicity
   DevBuf<int> gm, gnb, goff, bg_start, bg_end;
   DevBuf<unsigned> bgkey, bgval, bgkey2, bgval2;  // bucket -> groups
-  DevBuf<PDeposit> grec;                         // per-group deposit lists, materialised
-  DevBuf<unsigned char> grep;
+  DevBuf<float4> gpos;  // per-group deposit lists, materialised (position, index | multiplicity)
   DevBuf<float> rrtab;                           // rr(n), n < kRRTable
   DevBuf<unsigned char> temp;
   DevBuf<unsigned long long> stats;  // [photons, photon_rays, deposits, updates, eye_rays]
@@ -193,11 +192,17 @@ struct ppm_scene {
   DevBuf<unsigned long long> wide;  // 64-bit scratch scalar (expansion total)
   DevBuf<unsigned long long> stats_keep;  // stats before a batch (restored when it is split)
   DevBuf<float> image;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> upd_events;  // update-kernel launches since the last collection
   long long photons = 0;
   size_t slot_bytes = 0;          // ppm_set_batching (0: default_slot_bytes())
   long long max_updates = INT_MAX;  // ppm_set_batching: (group, deposit) pairs per batch
 
+  void drop_update_events() {
+    for (auto& ev : upd_events) (void)hipEventDestroy(ev.first), (void)hipEventDestroy(ev.second);
+    upd_events.clear();
+  }
   void free_all() {
+    drop_update_events();
     for (void* p : owned) (void)hipFree(p);
     owned.clear();
     hp.release(), state.release(), nupd.release(), pix_cnt.release(), pix_off.release();
@@ -209,7 +214,7 @@ struct ppm_scene {
     list_start.release(), list_end.release(), pkey.release(), pval.release(), pkey2.release();
     pval2.release(), gb.release(), gm.release(), gnb.release(), goff.release();
     bg_start.release(), bg_end.release(), bgkey.release(), bgval.release(), bgkey2.release();
-    bgval2.release(), grec.release(), grep.release(), rrtab.release();
+    bgval2.release(), gpos.release(), rrtab.release();
     temp.release(), stats.release(), error.release(), image.release();
     wide.release(), stats_keep.release();
     if (stream) (void)hipStreamDestroy(stream);
@@ -256,11 +261,11 @@ void create_device(ppm_scene* s, int device) {
   if (const char* d = std::getenv("CENG795_PPM_DIAG")) S.diag = std::atoi(d);  // experiments
   std::memcpy(S.light_pos, h.lights.data(), 12);  // lights[0] (Scene.cpp:97)
   std::memcpy(S.light_intensity, h.lights.data() + 3, 12);
-  s->stats.reserve(16, "alloc counters");
-  hip_check(hipMemset(s->stats.p, 0, 16 * sizeof(unsigned long long)), "zero counters");
+  s->stats.reserve(kStatSlots, "alloc counters");
+  hip_check(hipMemset(s->stats.p, 0, kStatSlots * sizeof(unsigned long long)), "zero counters");
   s->error.reserve(1, "alloc error flag");
   s->wide.reserve(1, "alloc scratch scalar");
-  s->stats_keep.reserve(16, "alloc stats snapshot");
+  s->stats_keep.reserve(kStatSlots, "alloc stats snapshot");
   hip_check(hipMemset(s->error.p, 0, sizeof(int)), "zero error flag");
   s->grid.reserve(1, "alloc grid");
   s->rrtab.reserve(kRRTable, "alloc radius-reduction table");
@@ -425,7 +430,7 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
     s->ndep.reserve(b + 1, "alloc deposit counts");
     s->dep_off.reserve(b + 1, "alloc deposit offsets");
     hip_check(hipMemsetAsync(s->ndep.p + b, 0, sizeof(int), s->stream), "zero sentinel");
-    hip_check(hipMemcpyAsync(s->stats_keep.p, s->stats.p, 16 * sizeof(unsigned long long),
+    hip_check(hipMemcpyAsync(s->stats_keep.p, s->stats.p, kStatSlots * sizeof(unsigned long long),
                              hipMemcpyDeviceToDevice, s->stream), "stats snapshot");
     hip_check(launch_photons(s->S, s->seed, first + done, b, K, s->slots.p, s->ndep.p, s->stats.p,
                              s->stream), "photon pass");
@@ -466,12 +471,13 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
         hip_check(hipMemcpyAsync(&P64, d_total, sizeof P64, hipMemcpyDeviceToHost, s->stream),
                   "read expansion total");
         hip_check(hipStreamSynchronize(s->stream), "expansion total");
-        if (P64 >= std::min<long long>(INT_MAX, s->max_updates)) {
-          // too many (group, deposit) pairs for one batch: trace a smaller batch (photon
-          // streams are per photon, so the same photons come out again) and keep it smaller
+        if (P64 >= std::min<long long>(INT_MAX, s->max_updates) || D >= kMaxBatchDeposits) {
+          // too many (group, deposit) pairs, or deposits, for one batch (the pair records
+          // index deposits in 27 bits): trace a smaller batch (photon streams are per photon,
+          // so the same photons come out again) and keep it smaller
           if (b == 1) throw std::domain_error("one photon expands to more than 2^31 updates");
           batch_max = std::max(1, b / 2);
-          hip_check(hipMemcpyAsync(s->stats.p, s->stats_keep.p, 16 * sizeof(unsigned long long),
+          hip_check(hipMemcpyAsync(s->stats.p, s->stats_keep.p, kStatSlots * sizeof(unsigned long long),
                                    hipMemcpyDeviceToDevice, s->stream), "stats restore");
           continue;
         }
@@ -504,10 +510,9 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
                                                        s->stream), "sort expansion by group");
           hip_check(launch_bucket_bounds(s->pkey2.p, P, s->list_start.p, s->list_end.p, s->stream),
                     "group list bounds");
-          s->grec.reserve(P, "alloc group deposit lists");
-          s->grep.reserve(P, "alloc group multiplicities");
+          s->gpos.reserve(P, "alloc group deposit lists");
           hip_check(launch_materialize(s->pkey2.p, s->pval2.p, P, s->dense.p, s->dbucket.p, s->gb.p,
-                                       s->gm.p, s->gnb.p, s->grec.p, s->grep.p, s->stream),
+                                       s->gm.p, s->gnb.p, s->gpos.p, s->stream),
                     "materialise group lists");
           const int2* tiles = s->tiles.p;
           if (lpt_order()) {
@@ -526,11 +531,17 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
                                                          0, 32, s->stream), "sort tiles");
             tiles = s->tiles_lpt.p;
           }
+          hipEvent_t e0, e1;
+          hip_check(hipEventCreate(&e0), "event");
+          hip_check(hipEventCreate(&e1), "event");
+          s->upd_events.emplace_back(e0, e1);
+          hip_check(hipEventRecord(e0, s->stream), "event");
           hip_check(launch_group_update(s->S, s->hp.p, s->perm.p, s->gstart.p, tiles,
-                                        s->n_tiles, s->list_start.p, s->list_end.p, s->grec.p,
-                                        s->grep.p, s->rrtab.p, kRRTable, s->state.p, s->nupd.p,
+                                        s->n_tiles, s->list_start.p, s->list_end.p, s->gpos.p,
+                                        s->dense.p, s->rrtab.p, kRRTable, s->state.p, s->nupd.p,
                                         s->stats.p, s->stream),
                     "hit-point updates");
+          hip_check(hipEventRecord(e1, s->stream), "event");
         }
       }
     }
@@ -735,7 +746,7 @@ int ppm_collect_stats(ppm_scene* s, ppm_stats* st) {
     check_scene(s);
     if (!st) throw std::invalid_argument("ppm_collect_stats: NULL output");
     DeviceGuard g(s->device);
-    unsigned long long c[16];
+    unsigned long long c[kStatSlots];
     hip_check(hipMemcpyAsync(c, s->stats.p, sizeof c, hipMemcpyDeviceToHost, s->stream), "read counters");
     hip_check(hipMemsetAsync(s->stats.p, 0, sizeof c, s->stream), "reset counters");
     hip_check(hipStreamSynchronize(s->stream), "counters");
@@ -746,12 +757,22 @@ int ppm_collect_stats(ppm_scene* s, ppm_stats* st) {
     st->updates = (long long)c[3];
     st->eye_rays = (long long)c[4];
     st->hit_points = s->n_hp;
+    st->update_deposit_visits = (long long)c[6];
+    st->update_candidates = (long long)c[16];
+    st->update_launches = (long long)s->upd_events.size();
+    st->update_ms = 0;
+    for (auto& ev : s->upd_events) {
+      float ms = 0;
+      hip_check(hipEventElapsedTime(&ms, ev.first, ev.second), "update time");
+      st->update_ms += ms;
+    }
+    s->drop_update_events();
     if (s->S.diag == 2) std::fprintf(stderr, "ppm diag: windows %llu deposit-visits %llu tiles %d groups %d "
                                      "longest tile %llu ticks phases(max) stage+filter %llu "
                                      "counts %llu scan %llu scatter %llu color %llu gate %llu max-window-updates %llu "
-                                     "unstaged-rr %llu\n",
+                                     "unstaged-rr %llu candidates %llu max-tile-candidates %llu max-wave-updates %llu max-tile-windows %llu\n",
                                      c[5], c[6], s->n_tiles, s->n_groups, c[7], c[8], c[9],
-                                     c[10], c[11], c[12], c[13], c[14], c[15]);
+                                     c[10], c[11], c[12], c[13], c[14], c[15], c[16], c[17], c[18], c[19]);
     s->photons = 0;
     return RT_OK;
   });
@@ -773,8 +794,9 @@ int ppm_render(ppm_scene* s, int cam, int threads, float* out, ppm_stats* stats)
         for (int k = 0; k < 5; k++) (void)hipEventDestroy(e[k]);
       }
     } guard{ev};
-    hip_check(hipMemsetAsync(s->stats.p, 0, 16 * sizeof(unsigned long long), s->stream), "zero counters");
+    hip_check(hipMemsetAsync(s->stats.p, 0, kStatSlots * sizeof(unsigned long long), s->stream), "zero counters");
     s->photons = 0;
+    s->drop_update_events();
     hip_check(hipEventRecord(ev[0], s->stream), "event");
     eye_pass(s, cam);
     hip_check(hipEventRecord(ev[1], s->stream), "event");

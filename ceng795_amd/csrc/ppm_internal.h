@@ -12,7 +12,11 @@ constexpr int kObjSphere = 0, kObjInstance = 1;
 constexpr int kTopStack = 48;   // per-lane traversal stacks (host checks the BVH depths)
 constexpr int kMeshStack = 64;
 constexpr int kEyeStack = 24;   // eye-ray tree: <= MaxRecursionDepth (<= 20) + 1 pending
-constexpr int kMaxCells = 27;   // hash cells a hit point's radius box can touch (3 per axis)
+constexpr int kStatSlots = 32;  // device counter words (ppm_collect_stats)
+constexpr int kMaxCells = 27;
+constexpr int kRepBits = 5;  // multiplicity bits next to a deposit index (kMaxCells < 32)
+constexpr unsigned kRepMask = (1u << kRepBits) - 1u;
+constexpr long long kMaxBatchDeposits = 1ll << (32 - kRepBits);   // hash cells a hit point's radius box can touch (3 per axis)
 
 // PPM/include/Material.h (+ type resolved as Material.cpp:57-63)
 struct PMaterial {

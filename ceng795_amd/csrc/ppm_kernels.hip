@@ -643,16 +643,22 @@ __global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, con
 #define PPM_TILE 3
 #endif
 #ifndef PPM_WIN
-#define PPM_WIN 1024
+#define PPM_WIN 2048
 #endif
 #ifndef PPM_GATE_B
 #define PPM_GATE_B 3
 #endif
 #ifndef PPM_RR_STAGE
-#define PPM_RR_STAGE 64
+#define PPM_RR_STAGE 128
 #endif
 #ifndef PPM_CHUNK
 #define PPM_CHUNK 1024
+#endif
+#ifndef PPM_KGATE
+#define PPM_KGATE 0  // two-stage gate: exact, measured slower
+#endif
+#ifndef PPM_PRIO
+#define PPM_PRIO 1
 #endif
 #ifndef PPM_WPE
 #define PPM_WPE 4
@@ -773,24 +779,27 @@ __global__ __launch_bounds__(256) void rr_table_kernel(float* rr, int n) {
   if (i < n) rr[i] = radius_reduction((unsigned)i);
 }
 
-// The expanded (group, deposit) pairs, sorted by group, materialised contiguously: the
-// deposit record and its multiplicity in that group (how many of the group's cells share the
-// deposit's bucket).
+// The expanded (group, deposit) pairs, sorted by group, materialised contiguously as what the
+// update pass's filter reads for every pair: 16 B = the deposit's position and one word packing
+// its photon-order index (into `dense`, where the candidates' normal, w_i and flux are read)
+// with its multiplicity in that group (how many of the group's cells share the deposit's
+// bucket, <= kMaxCells < 32).  The host keeps a batch below 2^27 deposits.
 __global__ __launch_bounds__(256) void materialize_kernel(const unsigned* pkey, const unsigned* pval,
                                                          int n, const PDeposit* dense,
                                                          const unsigned* bucket, const unsigned* gb,
                                                          const int* gm, const int* gnb,
-                                                         PDeposit* rec, unsigned char* rep) {
+                                                         float4* pos) {
   const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (p >= n) return;
   const unsigned g = pkey[p], i = pval[p];
-  rec[p] = dense[i];
   const unsigned b = bucket[i];
   const unsigned* gbb = gb + (size_t)g * kMaxCells;
   const int nb = gnb[g];
   int u = 0;
   while (u < nb - 1 && gbb[u] != b) u++;
-  rep[p] = (unsigned char)gm[(size_t)g * kMaxCells + u];
+  const unsigned m = (unsigned)gm[(size_t)g * kMaxCells + u];
+  const float* x = dense[i].x;
+  pos[p] = make_float4(x[0], x[1], x[2], __uint_as_float((i << kRepBits) | m));
 }
 
 // One workgroup per (group, tile of <= kTileHP hit points), streaming the group's deposits
@@ -807,13 +816,12 @@ __global__ __launch_bounds__(256) void materialize_kernel(const unsigned* pkey, 
 // The next window is fetched (coalesced) while the current one is processed.
 __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM_WPE, PPM_WPE))) void group_update_kernel(
     PScene S, const PHitPoint* hps, const int* perm, const int* gstart, const int2* tiles,
-    const int* list_start, const int* list_end, const PDeposit* rec,
-    const unsigned char* rep, const float* rrtab, int nrr, float4* state, unsigned* nupd,
-    unsigned long long* stats) {
+    const int* list_start, const int* list_end, const float4* pos, const PDeposit* dense,
+    const float* rrtab, int nrr, float4* state, unsigned* nupd, unsigned long long* stats) {
   constexpr int kPer = kWinMax / kUpdThreads;
   constexpr int kWords = kWinMax / 32;
   constexpr int kChunk = PPM_CHUNK;  // candidates per color / apply round
-  static_assert(kWinMax <= 1024, "s_ck packs the window index in 10 bits");
+  static_assert(kWinMax % kUpdThreads == 0 && kWinMax % 64 == 0, "whole waves per window");
   static_assert(kTileHP * kWords <= kUpdThreads, "one thread per mask word in the scan");
   __shared__ float s_hp[kTileHP][12];  // pos, normal, w_o, attenuation
   __shared__ int s_mat[kTileHP];
@@ -822,11 +830,19 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   __shared__ unsigned s_mask[kTileHP][kWords];
   __shared__ int s_wc[kTileHP * kWords + 1];
   __shared__ int s_wtot[kUpdThreads / 64];
-  __shared__ unsigned short s_ck[kTileHP * kWinMax];  // window index | multiplicity << 10
+  __shared__ unsigned s_ck[kTileHP * kWinMax];  // photon-order index << kRepBits | multiplicity
   __shared__ float s_cd2[kTileHP * kWinMax];
   __shared__ float4 s_ccf[kChunk];  // color * photon_flux, w = 0 (see the gate)
   constexpr int kRRStage = PPM_RR_STAGE;  // rr(n) staged per hit point per window (more: computed inline)
   __shared__ float s_rr[kTileHP][kRRStage];
+#if PPM_KGATE
+  // two-stage gate (see (3a)): per hit point the radius^2 after a accepts in this window,
+  // the accepted candidates in order, and per candidate the last accept count it passes at
+  __shared__ float s_R[kTileHP][kRRStage + 1];
+  __shared__ unsigned short s_app[kTileHP][kRRStage + 1];
+  __shared__ short s_K[kChunk];
+  __shared__ int s_extra[kTileHP], s_L[kTileHP];
+#endif
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const unsigned long long t_start = S.diag == 2 ? wall_clock64() : 0;
   const int2 tile = tiles[blockIdx.x];
@@ -850,15 +866,14 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     s_r2[tid] = r2;
     s_cnt[tid] = cnt;
   }
-  unsigned long long applied = 0;
+  unsigned long long applied = 0, cands = 0;
   const int ls = list_start[g], le = list_end[g];
-  PDeposit dep[kPer];
-  unsigned char drep[kPer];
+  float4 dep[kPer];  // position, photon-order index << kRepBits | multiplicity
   auto fetch = [&](int base) {
 #pragma unroll
     for (int q = 0; q < kPer; q++) {
       const int k = base + tid + q * kUpdThreads;
-      if (k < le) dep[q] = rec[k], drep[q] = rep[k];
+      if (k < le) dep[q] = pos[k];
     }
   };
   fetch(ls);
@@ -881,6 +896,9 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     const int total = min(kWinMax, le - base);
     const int nwords = (total + 31) >> 5;
     // stage rr(n) for the updates this window can make
+#if PPM_KGATE
+    if (tid < kTileHP) s_extra[tid] = 0;
+#endif
     for (int e = tid; e < nh * kRRStage; e += kUpdThreads) {
       const int j = e / kRRStage, t = e % kRRStage;
       const unsigned n = s_cnt[j] + (unsigned)t;
@@ -892,18 +910,19 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     for (int j = 0; j < kTileHP; j++) r2w[j] = s_r2[j];
     float d2r[kPer][kTileHP];
     bool cr[kPer][kTileHP];
-    unsigned rp[kPer];  // multiplicities, kept past the next window's fetch
+    unsigned rp[kPer];  // index | multiplicity words, kept past the next window's fetch
 #pragma unroll
     for (int q = 0; q < kPer; q++) {
       const int k = tid + q * kUpdThreads;  // a wave covers 64 consecutive deposits
       const bool live = k < total;
-      const V x = ld(dep[q].x), dn = ld(dep[q].normal);
-      rp[q] = drep[q];
+      const V x = mk(dep[q].x, dep[q].y, dep[q].z);
+      rp[q] = __float_as_uint(dep[q].w);
 #pragma unroll
       for (int j = 0; j < kTileHP; j++) {
         const V v = tp[j] - x;
         d2r[q][j] = dot(v, v);
-        cr[q][j] = live && j < nh && (dot(tn[j], dn) > 1e-3f) && (d2r[q][j] <= r2w[j]);
+        // the normal test of Scene.cpp:136 is applied to the candidates (color phase)
+        cr[q][j] = live && j < nh && (d2r[q][j] <= r2w[j]);
         const unsigned long long bal = __ballot(cr[q][j]);
         if (lane == 0) {
           s_mask[j][(k - lane) >> 5] = (unsigned)bal;
@@ -942,26 +961,77 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         if (!cr[q][j]) continue;
         const int w = k >> 5;
         const int idx = s_wc[j * nwords + w] + __builtin_popcount(s_mask[j][w] & ((1u << (k & 31)) - 1u));
-        s_ck[idx] = (unsigned short)(k | (rp[q] << 10));
+        s_ck[idx] = rp[q];
         s_cd2[idx] = d2r[q][j];
+#if PPM_KGATE
+        if ((rp[q] & kRepMask) > 1u) atomicAdd(&s_extra[j], (int)(rp[q] & kRepMask) - 1);
+#endif
       }
     }
     __syncthreads();
     PPM_PHASE(3)
     const int ncand = s_wc[nh * nwords];
+    cands += (unsigned)ncand;
     const int my_beg = h >= 0 ? s_wc[tid * nwords] : 0;
     const int my_end = h >= 0 ? (tid + 1 < nh ? s_wc[(tid + 1) * nwords] : ncand) : 0;
     const unsigned cnt_w = cnt;  // count at the window start: rr(n) is staged from there
+#if PPM_KGATE
+    // (3a) Two-stage gate.  The radius^2 after a accepts in this window does not depend on
+    // WHICH candidates were accepted: R(0) = r^2 at the window start, R(a+1) = R(a) * rr(n+a)
+    // (the gate's own fp32 product; r^2 + 0 = r^2).  R is non-increasing (rr < 1), so a
+    // candidate with distance^2 d2 passes at accept count a iff a <= K = max{a : d2 <= R(a)}.
+    // One lane per hit point tabulates R up to its most possible accepts in this window (its
+    // candidates' multiplicities summed); the color phase finds every candidate's K by binary
+    // search; the gate then runs two short chains: integer acceptance (a += a <= K), and the
+    // flux recurrence over the accepted candidates only.  A hit point whose possible accepts
+    // exceed the staged rr(n) takes the one-stage path below for this window.
+    bool tabled = false;
+    if (h >= 0) {
+      const int napp = (my_end - my_beg) + s_extra[tid];
+      tabled = napp <= kRRStage && S.diag != 1;
+      s_L[tid] = tabled ? napp : -1;
+      if (tabled) {
+        float R = r2;
+        s_R[tid][0] = R;
+        for (int a = 0; a < napp; a++) {
+          R = R * s_rr[tid][a];
+          s_R[tid][a + 1] = R;
+        }
+      }
+    }
+    __syncthreads();
+    int acc_n = 0;  // accepts so far in this window (tabled hit points)
+#endif
     for (int c0 = 0; c0 < ncand; c0 += kChunk) {
       // (3) color * photon_flux for candidates [c0, c0 + kChunk)
       for (int e = c0 + tid; e < min(ncand, c0 + kChunk); e += kUpdThreads) {
         int j = 0;
         while (j + 1 < nh && s_wc[(j + 1) * nwords] <= e) j++;
-        const PDeposit d = rec[base + (s_ck[e] & 1023u)];
+        const PDeposit d = dense[s_ck[e] >> kRepBits];
         const V hn = tn[j], w_i = ld(d.w_i), pf = ld(d.flux);
         const PMaterial& m = S.materials[s_mat[j]];
         V color = mk(0.0f, 0.0f, 0.0f);
-        if (m.brdf_id == -1) {
+        // Scene.cpp:136: a deposit whose normal fails the test never updates the hit point
+        const bool normal_ok = dot(hn, ld(d.normal)) > 1e-3f;
+        if (!normal_ok) s_cd2[e] = kInf;
+#if PPM_KGATE
+        {
+          int K = -1;
+          const int L = s_L[j];
+          if (normal_ok && L >= 0) {  // d2 <= R(0): the filter used the window-start radius
+            const float d2 = s_cd2[e];
+            int lo = 0, hi = L;
+            while (lo < hi) {
+              const int mid = (lo + hi + 1) >> 1;
+              if (d2 <= s_R[j][mid]) lo = mid;
+              else hi = mid - 1;
+            }
+            K = lo;
+          }
+          s_K[e - c0] = (short)K;
+        }
+#endif
+        if (normal_ok && m.brdf_id == -1) {
           const float cos_i = dot(hn, w_i);
           if (!(cos_i > 1.0f || cos_i <= 0.0f)) {
             const V w_o = mk(s_hp[j][6], s_hp[j][7], s_hp[j][8]);
@@ -986,6 +1056,67 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
       // batch (it changes nothing; the ones after it are redone with the right rr).  A batch
       // holding a multiplicity > 1, or reaching past the staged rr(n), takes the scalar path
       // for its first candidate.
+#if PPM_PRIO
+      if (tid < 64) __builtin_amdgcn_s_setprio(3);  // the gate wave is the tile's critical path
+#endif
+#if PPM_KGATE
+      if (tabled) {
+        const int e0 = max(my_beg, c0) - c0, e1 = min(my_end, c0 + kChunk) - c0;
+        const int a0 = acc_n;
+        int a = a0;
+        // acceptance: a candidate is applied while a <= K, at most its multiplicity times
+        constexpr int kU = 8;
+        int e = e0;
+        for (; e + kU <= e1; e += kU) {
+          unsigned w[kU];
+          int Kb[kU];
+#pragma unroll
+          for (int k = 0; k < kU; k++) w[k] = s_ck[c0 + e + k], Kb[k] = s_K[e + k];
+#pragma unroll
+          for (int k = 0; k < kU; k++) {
+            const int m = (int)(w[k] & kRepMask);
+            const int n = a <= Kb[k] ? min(m, Kb[k] + 1 - a) : 0;
+            s_app[tid][a] = (unsigned short)(e + k);
+            for (int i = 1; i < n; i++) s_app[tid][a + i] = (unsigned short)(e + k);
+            a += n;
+          }
+        }
+        for (; e < e1; e++) {
+          const int m = (int)(s_ck[c0 + e] & kRepMask), K = s_K[e];
+          const int n = a <= K ? min(m, K + 1 - a) : 0;
+          for (int i = 0; i < n; i++) s_app[tid][a + i] = (unsigned short)e;
+          a += n;
+        }
+        // the flux recurrence over this chunk's accepts: flux = (flux + color*flux_p) * rr(n)
+        f32x2 fxy = {flux.x, flux.y}, fz0 = {flux.z, 0.0f};
+        int i = a0;
+        for (; i + kU <= a; i += kU) {
+          float4 cb[kU];
+          float rb[kU];
+#pragma unroll
+          for (int k = 0; k < kU; k++) cb[k] = s_ccf[s_app[tid][i + k]], rb[k] = s_rr[tid][i + k];
+#pragma unroll
+          for (int k = 0; k < kU; k++) {
+            const f32x2 rr2 = {rb[k], rb[k]};
+            const f32x2 cxy = {cb[k].x, cb[k].y}, cz0 = {cb[k].z, 0.0f};
+            fxy = (fxy + cxy) * rr2;
+            fz0 = (fz0 + cz0) * rr2;
+          }
+        }
+        for (; i < a; i++) {
+          const float4 c = s_ccf[s_app[tid][i]];
+          const float rr = s_rr[tid][i];
+          const f32x2 rr2 = {rr, rr};
+          const f32x2 cxy = {c.x, c.y}, cz0 = {c.z, 0.0f};
+          fxy = (fxy + cxy) * rr2;
+          fz0 = (fz0 + cz0) * rr2;
+        }
+        flux = mk(fxy.x, fxy.y, fz0.x);
+        r2 = s_R[tid][a];
+        cnt = cnt_w + (unsigned)a;
+        acc_n = a;
+      } else
+#endif
       if (h >= 0 && S.diag != 1) {
         constexpr int kB = PPM_GATE_B;
         const int e1 = min(my_end, c0 + kChunk);
@@ -1001,7 +1132,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
           for (int k = 0; k < kB; k++) {
             const int ek = min(e + k, e1 - 1);
             d2b[k] = k < nb ? s_cd2[ek] : kInf;
-            fast = fast & ((s_ck[ek] >> 10) <= 1u);
+            fast = fast & ((s_ck[ek] & kRepMask) <= 1u);
             cb[k] = s_ccf[ek - c0];
             rrb[k] = s_rr[tid][min(t + (unsigned)k, (unsigned)kRRStage - 1)];
           }
@@ -1026,7 +1157,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
           } else {
             const float d2 = d2b[0];
             if (d2 <= fzr.y) {
-              const unsigned reps = s_ck[e] >> 10;
+              const unsigned reps = s_ck[e] & kRepMask;
               const f32x2 cxy = {cb[0].x, cb[0].y}, cz0 = {cb[0].z, cb[0].w};
               unsigned r = 0;
               do {
@@ -1044,6 +1175,9 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         flux = mk(fxy.x, fxy.y, fzr.x);
         r2 = fzr.y;
       }
+#if PPM_PRIO
+      if (tid < 64) __builtin_amdgcn_s_setprio(0);
+#endif
       __syncthreads();
       PPM_PHASE(5)
     }
@@ -1065,12 +1199,18 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   }
   const unsigned long long tot = wave_sum(applied);
   if (stats && (tid & 63) == 0 && tot) atomicAdd(&stats[3], tot);
-  if (stats && S.diag == 2 && tid == 0) {  // experiment counters: windows, deposit-visits
-    atomicAdd(&stats[5], (unsigned long long)((le - ls + kWinMax - 1) / kWinMax));
+  if (stats && tid == 0) {  // the pass's work: (tile, deposit) pairs filtered, candidates
     atomicAdd(&stats[6], (unsigned long long)(le - ls));
+    atomicAdd(&stats[16], cands);
+  }
+  if (stats && S.diag == 2 && tid == 0) {  // experiment counters: windows, longest tile
+    atomicAdd(&stats[5], (unsigned long long)((le - ls + kWinMax - 1) / kWinMax));
     atomicMax(&stats[7], wall_clock64() - t_start);  // longest tile, in wall-clock ticks
     for (int i = 0; i < 6; i++) atomicMax(&stats[8 + i], ph[i]);
+    atomicMax(&stats[17], cands);  // most candidates in one tile
+    atomicMax(&stats[19], (unsigned long long)((le - ls + kWinMax - 1) / kWinMax));
   }
+  if (stats && S.diag == 2 && (tid & 63) == 0 && tot) atomicMax(&stats[18], tot);  // (per wave)
 #undef PPM_PHASE
 }
 
@@ -1197,21 +1337,20 @@ hipError_t launch_rr_table(float* rr, int n, hipStream_t st) {
 }
 hipError_t launch_materialize(const unsigned* pkey, const unsigned* pval, int n,
                               const PDeposit* dense, const unsigned* bucket, const unsigned* gb,
-                              const int* gm, const int* gnb, PDeposit* rec, unsigned char* rep,
-                              hipStream_t st) {
+                              const int* gm, const int* gnb, float4* pos, hipStream_t st) {
   hipLaunchKernelGGL(materialize_kernel, dim3(blocks_for(n)), dim3(kThreads), 0, st, pkey, pval,
-                     n, dense, bucket, gb, gm, gnb, rec, rep);
+                     n, dense, bucket, gb, gm, gnb, pos);
   return hipGetLastError();
 }
 hipError_t launch_group_update(const PScene& S, const PHitPoint* hps, const int* perm,
                                const int* gstart, const int2* tiles, int ntiles,
-                               const int* list_start, const int* list_end, const PDeposit* rec,
-                               const unsigned char* rep, const float* rrtab, int nrr,
+                               const int* list_start, const int* list_end, const float4* pos,
+                               const PDeposit* dense, const float* rrtab, int nrr,
                                float4* state, unsigned* nupd, unsigned long long* stats,
                                hipStream_t st) {
   if (ntiles <= 0) return hipSuccess;
   hipLaunchKernelGGL(group_update_kernel, dim3(ntiles), dim3(kUpdThreads), 0, st, S, hps, perm,
-                     gstart, tiles, list_start, list_end, rec, rep, rrtab, nrr, state, nupd,
+                     gstart, tiles, list_start, list_end, pos, dense, rrtab, nrr, state, nupd,
                      stats);
   return hipGetLastError();
 }

@@ -25,7 +25,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _VARIANT = os.environ.get("CENG795_PPM_LIB", "")
 LIB_PATH = os.path.join(_HERE, "lib", f"libceng795_ppm_{_VARIANT}.so" if _VARIANT else
                         "libceng795_ppm.so")
-ABI_VERSION = 2  # CENG795_PPM_ABI_VERSION
+ABI_VERSION = 3  # CENG795_PPM_ABI_VERSION
 
 _lib = None
 
@@ -35,7 +35,9 @@ class ppm_stats(C.Structure):
                 ("deposits", C.c_longlong), ("updates", C.c_longlong),
                 ("eye_rays", C.c_longlong), ("hit_points", C.c_longlong),
                 ("eye_ms", C.c_double), ("grid_ms", C.c_double), ("photon_ms", C.c_double),
-                ("density_ms", C.c_double)]
+                ("density_ms", C.c_double), ("update_deposit_visits", C.c_longlong),
+                ("update_candidates", C.c_longlong), ("update_launches", C.c_longlong),
+                ("update_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define CENG795_PPM_ABI_VERSION 2  /* 2: ppm_set_batching */
+#define CENG795_PPM_ABI_VERSION 3  /* 2: ppm_set_batching; 3: update-pass work in ppm_stats */
 
 typedef struct ppm_scene ppm_scene;
 
@@ -38,6 +38,11 @@ typedef struct ppm_stats {
   long long eye_rays;     /* eye-pass closest-hit queries                        */
   long long hit_points;
   double eye_ms, grid_ms, photon_ms, density_ms;  /* device time of each pass (ppm_render) */
+  /* the update pass (Scene.cpp:131-168) as the GPU runs it: (hit-point tile, deposit) pairs its
+   * filter examined, candidates it passed to the exact recurrence, and the device time of its
+   * kernel summed over the photon batches since the last collection */
+  long long update_deposit_visits, update_candidates, update_launches;
+  double update_ms;
 } ppm_stats;
 
 int ppm_abi_version(void);

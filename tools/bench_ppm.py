@@ -39,14 +39,18 @@ def scene_path() -> str:
     return path
 
 
-def cpu_baseline(xml: str, threads: int, iterations: int = 100):
+def cpu_baseline(xml: str, threads: int, how: str, iterations: int = 1000):
     """The reference itself (oracle/_ref/ppm_harness, PPM sources compiled unmodified) on
-    `threads` host threads, on a bounded sample: NumberOfIterations cut to `iterations`."""
+    `threads` host threads (the box's CPU quota), the full photon pass (NumberOfIterations
+    1000 = 1e7 photons) after a short warm-up run."""
     harness = os.path.join(ROOT, "oracle", "_ref", "ppm_harness")
     if os.path.exists(harness):
-        out = subprocess.run([harness, "render", xml, "0", os.devnull, str(threads),
-                              str(iterations)], check=True, capture_output=True, text=True).stdout
-        r = json.loads(out.strip().splitlines()[-1])
+        def one(it):
+            out = subprocess.run([harness, "render", xml, "0", os.devnull, str(threads), str(it)],
+                                 check=True, capture_output=True, text=True).stdout
+            return json.loads(out.strip().splitlines()[-1])
+        one(10)  # warm-up: page cache, CPU frequency
+        r = one(iterations)
         kind, photons, sec = "reference", r["photons_traced"], r["photon_s"]
     else:
         from oracle.ppm_ref import OraclePPM
@@ -63,7 +67,37 @@ def cpu_baseline(xml: str, threads: int, iterations: int = 100):
     return {"value": round(photons / sec / 1e6, 4), "unit": "Mphotons/s", "cores": threads,
             "kind": kind,
             "sample": f"photon pass of {photons} photons (NumberOfIterations {iterations} of "
-                      f"1000), {sec:.3f} s"}
+                      f"1000), {sec:.3f} s, after a 10-iteration warm-up run; threads: {how}"}
+
+
+def update_roofline(st, launches_per_step: int, ms_per_launch: float):
+    """Roofline of the dominant kernel, group_update_kernel: its algorithmic bytes per launch
+    (16-B position record per (tile, deposit) pair its filter examines + the 48-B deposit
+    record per candidate it passes to the recurrence; hit-point records and state are < 1 %)
+    over its HIP-event duration.  traffic: the committed PMC summary of this library build."""
+    import bench
+    alg = (16 * st.update_deposit_visits + 48 * st.update_candidates) / max(1, launches_per_step)
+    achieved = alg / (ms_per_launch * 1e-3) / 1e9
+    prof, traffic = None, None
+    path = os.path.join(ROOT, "profiles", "traffic_c5.json")
+    if os.path.exists(path):
+        from ceng795_amd import ppm
+        with open(path) as f:
+            prof = json.load(f)
+        if prof.get("lib_sha256") == bench.file_sha256(ppm.LIB_PATH):
+            traffic = prof["per_kernel"].get("group_update_kernel", {}).get("hbm_bytes")
+        else:
+            prof = None
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
+            "frac": round(achieved / 8000.0, 4), "traffic": traffic,
+            "kernel": "group_update_kernel", "kernel_ms_avg": round(ms_per_launch, 4),
+            "launches_per_step": launches_per_step,
+            "algorithmic_bytes_per_launch": int(alg),
+            "bytes_model": "16 B x (hit-point tile, deposit) pairs filtered + 48 B x candidates "
+                           "(ppm_stats.update_deposit_visits / update_candidates)",
+            "work_per_step": {"deposit_visits": st.update_deposit_visits,
+                              "candidates": st.update_candidates, "updates": st.updates},
+            "traffic_source": "profiles/traffic_c5.json" if traffic is not None else None}
 
 
 def run(steps: int, warmup: int, with_cpu: bool) -> dict:
@@ -74,13 +108,14 @@ def run(steps: int, warmup: int, with_cpu: bool) -> dict:
     scene = ppm.PhotonScene(xml, device=0, seed=1)
     for k in range(warmup):
         img, st = scene.render(0, reference_threads=REFERENCE_THREADS)
-    times, photon_ms, phases = [], [], []
+    times, photon_ms, phases, upd_ms = [], [], [], []
     for k in range(steps):
         scene.set_seed(100 + k)
         t0 = time.perf_counter()
         img, st = scene.render(0, reference_threads=REFERENCE_THREADS)
         times.append(time.perf_counter() - t0)
         photon_ms.append(st.photon_ms)
+        upd_ms.append(st.update_ms)
         phases.append((st.eye_ms, st.grid_ms, st.photon_ms, st.density_ms))
     ms_step = 1e3 * sum(times) / len(times)
     ph_ms = sum(photon_ms) / len(photon_ms)
@@ -100,8 +135,12 @@ def run(steps: int, warmup: int, with_cpu: bool) -> dict:
                                 "photon": round(avg[2], 3), "density": round(avg[3], 3)},
                    "frame_photons_per_s": round(st.photons / (ms_step / 1e3) / 1e6, 2)},
     }
+    launches = max(1, st.update_launches)  # one per photon batch (one at this size)
+    line["roofline"] = update_roofline(st, launches, sum(upd_ms) / len(upd_ms) / launches)
     if with_cpu:
-        line["cpu_baseline"] = cpu_baseline(xml, REFERENCE_THREADS)
+        import bench
+        threads, how = bench.host_cores()
+        line["cpu_baseline"] = cpu_baseline(xml, threads, how)
     return line
 
 

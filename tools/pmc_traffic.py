@@ -31,7 +31,8 @@ import subprocess
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("trace_primary_kernel", "trace_shadow_kernel", "shade_kernel", "recursive_kernel")
+KERNELS = ("trace_primary_kernel", "trace_shadow_kernel", "shade_kernel", "recursive_kernel",
+           "group_update_kernel", "photon_kernel", "materialize_kernel", "deposit_keys_kernel")
 
 
 def short(name):
