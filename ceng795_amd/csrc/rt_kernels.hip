@@ -655,8 +655,33 @@ __device__ __forceinline__ void batch_flush(WaveLeafLds& L, int n, const DevPrim
 // (accel_build.cpp collapse_wide); others get the binary one.
 bool wide_nodes_supported() { return kBatchLeaves && kRaysPerLane == 1; }
 
+// The whole 128-B node in one round trip: two s_load_dwordx16 and one wait.  Left to itself
+// the compiler splits the record into ~14 loads of 1-8 dwords in three dependent rounds (and,
+// short of SGPRs, reloads the first slot's box after the flags test).  RT_WIDE_SLOAD=0 for A/B.
+#ifndef RT_WIDE_SLOAD
+#define RT_WIDE_SLOAD 1
+#endif
 __device__ __forceinline__ DevNode4 load_node4(const DevNode* __restrict__ nodes, int idx) {
+#if RT_WIDE_SLOAD
+  v16i a, b;
+  const void* p = nodes + idx;
+  asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+               : "=s"(a), "=s"(b) : "s"(p) : "memory");
+  DevNode4 N;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+#pragma unroll
+    for (int x = 0; x < 3; x++) {
+      N.lo[x][k] = __int_as_float(a[4 * x + k]);
+      N.hi[x][k] = __int_as_float(k + 4 * x < 4 ? a[12 + 4 * x + k] : b[4 * x + k - 4]);
+    }
+    N.child[k] = b[8 + k];
+  }
+  N.flags = b[12];
+  return N;
+#else
   return *reinterpret_cast<const DevNode4*>(nodes + idx);
+#endif
 }
 
 // One packet visit of a wide culling node (R == 1, batched leaves), slot by slot with the
