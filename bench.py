@@ -309,7 +309,7 @@ def main() -> int:
                     help="pieces per frame and rank for the gather pipeline (default 4 when "
                          "a rank renders one frame's share, else 1)")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=4,
                     help="frames in flight on one GPU: consecutive steps on that many streams, so "
                          "one frame's sparsely occupied last waves overlap the next frame (whole-"
                          "frame modes; 1 = one frame at a time)")

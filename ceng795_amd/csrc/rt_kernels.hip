@@ -145,6 +145,38 @@ __device__ __forceinline__ void slab_span(const float* b, const LaneRay& r, floa
   tf = __builtin_fminf(__builtin_fminf(fx, fy), fz);
 }
 
+// Two slab spans at once (slots c and c + 1 of a wide node): b - o and * rcp as v_pk_add_f32 /
+// v_pk_mul_f32, each element rounded exactly as the scalar op, the min / max per element.
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+template <bool SKIP>
+__device__ __forceinline__ void slab_span2(const float lo[3][4], const float hi[3][4], int c,
+                                           const LaneRay& r, float tn[2], float tf[2]) {
+  const f32x2v ox = {r.o.x, r.o.x}, oy = {r.o.y, r.o.y}, oz = {r.o.z, r.o.z};
+  const f32x2v rx = {r.r.x, r.r.x}, ry = {r.r.y, r.r.y}, rz = {r.r.z, r.r.z};
+  const f32x2v ax = (f32x2v{lo[0][c], lo[0][c + 1]} - ox) * rx;
+  const f32x2v bx = (f32x2v{hi[0][c], hi[0][c + 1]} - ox) * rx;
+  const f32x2v ay = (f32x2v{lo[1][c], lo[1][c + 1]} - oy) * ry;
+  const f32x2v by = (f32x2v{hi[1][c], hi[1][c + 1]} - oy) * ry;
+  const f32x2v az = (f32x2v{lo[2][c], lo[2][c + 1]} - oz) * rz;
+  const f32x2v bz = (f32x2v{hi[2][c], hi[2][c + 1]} - oz) * rz;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    float nx = __builtin_fminf(ax[k], bx[k]), fx = __builtin_fmaxf(ax[k], bx[k]);
+    float ny = __builtin_fminf(ay[k], by[k]), fy = __builtin_fmaxf(ay[k], by[k]);
+    float nz = __builtin_fminf(az[k], bz[k]), fz = __builtin_fmaxf(az[k], bz[k]);
+    if (SKIP) {
+      nx = r.skip0 ? -RT_INF : nx;
+      fx = r.skip0 ? RT_INF : fx;
+      ny = r.skip1 ? -RT_INF : ny;
+      fy = r.skip1 ? RT_INF : fy;
+      nz = r.skip2 ? -RT_INF : nz;
+      fz = r.skip2 ? RT_INF : fz;
+    }
+    tn[k] = __builtin_fmaxf(__builtin_fmaxf(nx, ny), nz);
+    tf[k] = __builtin_fminf(__builtin_fminf(fx, fy), fz);
+  }
+}
+
 // sure_in: the reference accepts (tf >= 0, and tn <= tf decided outside a 2^-20 relative
 // band); sure_out: it rejects.  Neither: box_exact decides (NaN lands here too).  The sign of
 // each bound is exact (RN(b - o) * rcp(d) has the sign of the reference's quotient), and
@@ -661,6 +693,9 @@ bool wide_nodes_supported() { return kBatchLeaves && kRaysPerLane == 1; }
 #ifndef RT_WIDE_SLOAD
 #define RT_WIDE_SLOAD 1
 #endif
+#ifndef RT_WIDE_PK  // slab spans of a wide node's slots two at a time (packed fp32)
+#define RT_WIDE_PK 0
+#endif
 __device__ __forceinline__ DevNode4 load_node4(const DevNode* __restrict__ nodes, int idx) {
 #if RT_WIDE_SLOAD
   v16i a, b;
@@ -705,12 +740,21 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
   int nxt = -1;
   uint64_t nm = 0;
   float nkey = 0.0f;
+#if RT_WIDE_PK
+  float tn4[4], tf4[4];  // all four spans up front, two slots per packed instruction
+  slab_span2<SKIP>(N.lo, N.hi, 0, r, tn4, tf4);
+  slab_span2<SKIP>(N.lo, N.hi, 2, r, tn4 + 2, tf4 + 2);
+#endif
 #pragma unroll
   for (int c = 0; c < 4; c++) {
     if (!(fl & (kWideValid << c))) continue;
+#if RT_WIDE_PK
+    const float tn = tn4[c], tf = tf4[c];
+#else
     const float b[6] = {N.lo[0][c], N.lo[1][c], N.lo[2][c], N.hi[0][c], N.hi[1][c], N.hi[2][c]};
     float tn, tf;
     slab_span<SKIP>(b, r, tn, tf);
+#endif
     bool sin, sout;
     decide_sure(tn, tf, sin, sout);
     const int ch = N.child[c];

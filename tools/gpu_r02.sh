@@ -35,7 +35,7 @@ fi
 if [ "$WHAT" = pmc ] || [ "$WHAT" = all ]; then
   # one frame at a time, as the roofline's kernel times are taken (bench.py isolated_kernel_times)
   step prof_c3 300 rocprofv3 --kernel-trace --stats -d "$O/prof_c3" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-roofline --inflight 1
-  step prof_c3_inflight2 300 rocprofv3 --kernel-trace --stats -d "$O/prof_c3_inflight2" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-roofline
+  step prof_c3_default 300 rocprofv3 --kernel-trace --stats -d "$O/prof_c3_default" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-roofline
   BENCH_ARGS="--inflight 1" step pmc 900 bash tools/pmc_passes.sh "$O/pmc" traffic insts sq sqc cycles
   step traffic 60 python3 tools/pmc_traffic.py --fetch "$O/pmc/fetch" --write "$O/pmc/write" --insts "$O/pmc/insts" --sq "$O/pmc/sq" --workload c3 --round r02 --out "$O/traffic_c3.json"
 fi
