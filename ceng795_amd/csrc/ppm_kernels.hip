@@ -26,6 +26,7 @@
 // oracle/ppm_ref.cpp, does literally that), without atomics or locks.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdint>
 
@@ -484,85 +485,153 @@ __global__ __launch_bounds__(1024) void grid_kernel(const PHitPoint* hps, int n,
 // ------------------------------------------------------------------ photon pass
 // Photon first + i traces its chain (photon_trace's recursion never branches) and leaves
 // one deposit per diffuse hit in slots[i * K + k], k < K = max(1, MaxRecursionDepth - 1).
+//
+// Lanes are refilled (PPM_REFILL, default): Russian roulette ends ~2/3 of the chains at every
+// diffuse hit (C5: 1.36 segments per photon), so a wave that traced one photon per lane ran
+// until its longest chain ended (~4-5 segments) with most lanes idle.  Here each workgroup owns
+// a contiguous range of photons; a lane whose chain ends takes the next photon of the range
+// (one LDS atomic per wave and round) and the wave runs one segment per round for all its live
+// lanes.  Every photon is computed exactly as before (own random stream, same arithmetic, its
+// deposits in its own slots), only the lane that computes it changes.
+#ifndef PPM_REFILL
+#define PPM_REFILL 1
+#endif
+#ifndef PPM_PHOTON_BLOCKS
+#define PPM_PHOTON_BLOCKS 4096
+#endif
+struct PhotonState {
+  ppm_math::Rng rng{0, 0};
+  Ray ray;
+  V flux;
+  int depth, k;
+};
+
+// Point_light::generate_photon (Point_light.cpp:7-30): theta = 2 pi e2 on purpose
+__device__ __forceinline__ void emit_photon(const PScene& S, unsigned long long seed,
+                                            long long photon, PhotonState& P) {
+  P.rng = ppm_math::Rng(seed, (unsigned long long)photon);
+  P.flux = ld(S.light_intensity) * (float)(M_PI * 4.0f);
+  const float e1 = P.rng.uniform01();
+  const float e2 = P.rng.uniform01();
+  const V w = mk(0.0f, 1.0f, 0.0f);
+  const V u = normalize((w.x != 0.0f || w.y != 0.0f) ? mk(-w.y, w.x, 0.0f) : mk(0.0f, 1.0f, 0.0f));
+  const V v = cross(w, u);
+  const float phi = (float)(2 * M_PI * (double)e1);
+  const float theta = (float)(2 * M_PI * (double)e2);
+  float st, ct, sp, cp;
+  ppm_math::sincosf_ieee(theta, st, ct);
+  ppm_math::sincosf_ieee(phi, sp, cp);
+  P.ray = Ray{ld(S.light_pos), normalize((w * ct + (v * st) * cp) + (u * st) * sp)};
+  P.depth = 0;
+  P.k = 0;
+}
+
+// One segment of photon_trace (Scene.cpp:106-249) for photon i; false when the chain ends.
+__device__ __forceinline__ bool photon_segment(const PScene& S, int i, int K, PDeposit* slots,
+                                               PhotonState& P, unsigned long long& rays,
+                                               unsigned long long& deps) {
+  P.depth++;
+  if (P.depth >= S.max_depth) return false;
+  Hit h;
+  rays++;
+  const Ray ray = P.ray;
+  if (!closest(S, ray, h)) return false;
+  const V x = point_at(ray, h.t);
+  const V normal = hit_normal(S, ray, h);
+  const PMaterial& m = S.materials[S.objects[h.obj].material];
+  if (m.type == kMatDiffuse) {
+    const V w_i = neg(normalize(ray.d));
+    PDeposit& d = slots[(size_t)i * K + P.k];
+    d.x[0] = x.x, d.x[1] = x.y, d.x[2] = x.z;
+    d.normal[0] = normal.x, d.normal[1] = normal.y, d.normal[2] = normal.z;
+    d.w_i[0] = w_i.x, d.w_i[1] = w_i.y, d.w_i[2] = w_i.z;
+    d.flux[0] = P.flux.x, d.flux[1] = P.flux.y, d.flux[2] = P.flux.z;
+    P.k++;
+    deps++;
+    // sample_hemisphere(normal) (Scene.cpp:15-44), cosine weighted
+    const float h1 = P.rng.uniform01();
+    const float h2 = P.rng.uniform01();
+    const V hu = normalize((normal.x != 0.0f || normal.y != 0.0f) ? mk(-normal.y, normal.x, 0.0f)
+                                                                  : mk(0.0f, 1.0f, 0.0f));
+    const V hv = cross(normal, hu);
+    const float hphi = (float)(2 * M_PI * (double)h1);
+    const float htheta = ppm_math::asinf_ieee(__builtin_sqrtf(h2));
+    float hst, hct, hsp, hcp;
+    ppm_math::sincosf_ieee(htheta, hst, hct);
+    ppm_math::sincosf_ieee(hphi, hsp, hcp);
+    const V dir = normalize((normal * hct + (hv * hst) * hcp) + (hu * hst) * hsp);
+    const float prob = (float)((double)fmax0(dot(normal, dir)) / M_PI);
+    // BRDF weight (Scene.cpp:173-194): nl from the incoming ray, as the reference
+    const V nl = dot(normal, ray.d) < 0 ? normal : normal * -1;
+    V base = mk(0.0f, 0.0f, 0.0f);
+    const float cos_i = fmax0(dot(normal, w_i));
+    if (m.brdf_id == -1 && !(cos_i > 1.0f || cos_i <= 0.0f)) {
+      const float sc = fmax0(dot(nl, normalize(dir + w_i)));
+      base = ld(m.diffuse) + (ld(m.specular) * ppm_math::powf_ieee(sc, m.phong)) / cos_i;
+    }
+    base = base * fmax0(dot(normal, dir));
+    if (!(P.rng.uniform01() < prob)) return false;  // Russian roulette (Scene.cpp:196-199)
+    P.ray = Ray{x + (dir * S.eps), dir};
+    P.flux = (base * P.flux) / prob;
+  } else if (m.type == kMatMirror) {
+    const V w_o = normalize(ray.o - x);
+    const V w_r = normalize((normal * (2.0f * dot(normal, w_o))) - w_o);
+    P.ray = Ray{x + (w_r * S.eps), w_r};
+    P.flux = ld(m.mirror) * P.flux;
+  } else {
+    const Refraction R = refract_setup(S, ray, x, normal, m);
+    if (R.tir) P.ray = R.reflection;
+    else if (R.into) P.ray = P.rng.uniform01() < R.fresnel ? R.reflection : R.refraction;
+    else P.ray = R.refraction;
+  }
+  return true;
+}
+
 __global__ __launch_bounds__(256) void photon_kernel(PScene S, unsigned long long seed,
                                                      long long first, int count, int K,
                                                      PDeposit* slots, int* ndep,
                                                      unsigned long long* stats) {
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   unsigned long long rays = 0, deps = 0;
-  if (i < count) {
-    ppm_math::Rng rng(seed, (unsigned long long)(first + i));
-    // Point_light::generate_photon (Point_light.cpp:7-30): theta = 2 pi e2 on purpose
-    V flux = ld(S.light_intensity) * (float)(M_PI * 4.0f);
-    const float e1 = rng.uniform01();
-    const float e2 = rng.uniform01();
-    const V w = mk(0.0f, 1.0f, 0.0f);
-    const V u = normalize((w.x != 0.0f || w.y != 0.0f) ? mk(-w.y, w.x, 0.0f) : mk(0.0f, 1.0f, 0.0f));
-    const V v = cross(w, u);
-    const float phi = (float)(2 * M_PI * (double)e1);
-    const float theta = (float)(2 * M_PI * (double)e2);
-    float st, ct, sp, cp;
-    ppm_math::sincosf_ieee(theta, st, ct);
-    ppm_math::sincosf_ieee(phi, sp, cp);
-    Ray ray{ld(S.light_pos), normalize((w * ct + (v * st) * cp) + (u * st) * sp)};
-    int depth = 0, k = 0;
-    for (;;) {
-      depth++;
-      if (depth >= S.max_depth) break;
-      Hit h;
-      rays++;
-      if (!closest(S, ray, h)) break;
-      const V x = point_at(ray, h.t);
-      const V normal = hit_normal(S, ray, h);
-      const PMaterial& m = S.materials[S.objects[h.obj].material];
-      if (m.type == kMatDiffuse) {
-        const V w_i = neg(normalize(ray.d));
-        PDeposit& d = slots[(size_t)i * K + k];
-        d.x[0] = x.x, d.x[1] = x.y, d.x[2] = x.z;
-        d.normal[0] = normal.x, d.normal[1] = normal.y, d.normal[2] = normal.z;
-        d.w_i[0] = w_i.x, d.w_i[1] = w_i.y, d.w_i[2] = w_i.z;
-        d.flux[0] = flux.x, d.flux[1] = flux.y, d.flux[2] = flux.z;
-        k++;
-        deps++;
-        // sample_hemisphere(normal) (Scene.cpp:15-44), cosine weighted
-        const float h1 = rng.uniform01();
-        const float h2 = rng.uniform01();
-        const V hu = normalize((normal.x != 0.0f || normal.y != 0.0f) ? mk(-normal.y, normal.x, 0.0f)
-                                                                      : mk(0.0f, 1.0f, 0.0f));
-        const V hv = cross(normal, hu);
-        const float hphi = (float)(2 * M_PI * (double)h1);
-        const float htheta = ppm_math::asinf_ieee(__builtin_sqrtf(h2));
-        float hst, hct, hsp, hcp;
-        ppm_math::sincosf_ieee(htheta, hst, hct);
-        ppm_math::sincosf_ieee(hphi, hsp, hcp);
-        const V dir = normalize((normal * hct + (hv * hst) * hcp) + (hu * hst) * hsp);
-        const float prob = (float)((double)fmax0(dot(normal, dir)) / M_PI);
-        // BRDF weight (Scene.cpp:173-194): nl from the incoming ray, as the reference
-        const V nl = dot(normal, ray.d) < 0 ? normal : normal * -1;
-        V base = mk(0.0f, 0.0f, 0.0f);
-        const float cos_i = fmax0(dot(normal, w_i));
-        if (m.brdf_id == -1 && !(cos_i > 1.0f || cos_i <= 0.0f)) {
-          const float sc = fmax0(dot(nl, normalize(dir + w_i)));
-          base = ld(m.diffuse) + (ld(m.specular) * ppm_math::powf_ieee(sc, m.phong)) / cos_i;
+  PhotonState P;
+#if PPM_REFILL
+  __shared__ int s_next;
+  const int per = (int)(((long long)count + gridDim.x - 1) / gridDim.x);
+  const int beg = (int)min((long long)blockIdx.x * per, (long long)count);
+  const int end = min(count, beg + per);
+  if (threadIdx.x == 0) s_next = beg;
+  __syncthreads();
+  const int lane = (int)(threadIdx.x & 63);
+  int i = -1;  // this lane's photon (-1: none)
+  for (;;) {
+    const unsigned long long need = __ballot(i < 0);
+    if (need) {  // refill the idle lanes from the workgroup's range, in lane order
+      const int leader = __builtin_ctzll(need);
+      int base = 0;
+      if (lane == leader) base = atomicAdd(&s_next, __builtin_popcountll(need));
+      base = __shfl(base, leader, 64);
+      if (i < 0) {
+        const int idx = base + __builtin_popcountll(need & ((1ull << lane) - 1ull));
+        if (idx < end) {
+          i = idx;
+          emit_photon(S, seed, first + i, P);
         }
-        base = base * fmax0(dot(normal, dir));
-        if (!(rng.uniform01() < prob)) break;  // Russian roulette (Scene.cpp:196-199)
-        ray = Ray{x + (dir * S.eps), dir};
-        flux = (base * flux) / prob;
-      } else if (m.type == kMatMirror) {
-        const V w_o = normalize(ray.o - x);
-        const V w_r = normalize((normal * (2.0f * dot(normal, w_o))) - w_o);
-        ray = Ray{x + (w_r * S.eps), w_r};
-        flux = ld(m.mirror) * flux;
-      } else {
-        const Refraction R = refract_setup(S, ray, x, normal, m);
-        if (R.tir) ray = R.reflection;
-        else if (R.into) ray = rng.uniform01() < R.fresnel ? R.reflection : R.refraction;
-        else ray = R.refraction;
       }
     }
-    ndep[i] = k;
+    if (!__ballot(i >= 0)) break;  // range exhausted and every chain ended
+    if (i >= 0 && !photon_segment(S, i, K, slots, P, rays, deps)) {
+      ndep[i] = P.k;
+      i = -1;
+    }
   }
+#else
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i < count) {
+    emit_photon(S, seed, first + i, P);
+    while (photon_segment(S, i, K, slots, P, rays, deps)) {
+    }
+    ndep[i] = P.k;
+  }
+#endif
   const unsigned long long tr = wave_sum(rays), td = wave_sum(deps);
   if (stats && (threadIdx.x & 63) == 0) {
     if (tr) atomicAdd(&stats[1], tr);
@@ -1254,7 +1323,14 @@ hipError_t launch_grid(const PHitPoint* hps, int n, int w, int h, PGrid* grid, f
 hipError_t launch_photons(const PScene& S, unsigned long long seed, long long first, int count,
                           int K, PDeposit* slots, int* ndep, unsigned long long* stats,
                           hipStream_t st) {
-  hipLaunchKernelGGL(photon_kernel, dim3(blocks_for(count)), dim3(kThreads), 0, st, S, seed,
+#if PPM_REFILL
+  // workgroups of a contiguous photon range each (2048: 3.99 ms, 4096: 3.72 ms on C5)
+  const int blocks = std::min(blocks_for(count), PPM_PHOTON_BLOCKS);
+#else
+  const int blocks = blocks_for(count);
+#endif
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(photon_kernel, dim3(blocks), dim3(kThreads), 0, st, S, seed,
                      first, count, K, slots, ndep, stats);
   return hipGetLastError();
 }
