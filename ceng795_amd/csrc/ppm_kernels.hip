@@ -936,6 +936,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     s_cnt[tid] = cnt;
   }
   unsigned long long applied = 0, cands = 0;
+  unsigned long long d_max = 0, d_unstaged = 0;  // diag: per hit point, flushed once per tile
   const int ls = list_start[g], le = list_end[g];
   float4 dep[kPer];  // position, photon-order index << kRepBits | multiplicity
   auto fetch = [&](int base) {
@@ -1059,10 +1060,21 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
       const int napp = (my_end - my_beg) + s_extra[tid];
       tabled = napp <= kRRStage && S.diag != 1;
       s_L[tid] = tabled ? napp : -1;
-      if (tabled) {
+      if (tabled) {  // one multiply per step; the rr(n) loads go 8 at a time, off the chain
         float R = r2;
         s_R[tid][0] = R;
-        for (int a = 0; a < napp; a++) {
+        int a = 0;
+        for (; a + 8 <= napp; a += 8) {
+          float rb[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++) rb[k] = s_rr[tid][a + k];
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            R = R * rb[k];
+            s_R[tid][a + k + 1] = R;
+          }
+        }
+        for (; a < napp; a++) {
           R = R * s_rr[tid][a];
           s_R[tid][a + 1] = R;
         }
@@ -1139,15 +1151,25 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         for (; e + kU <= e1; e += kU) {
           unsigned w[kU];
           int Kb[kU];
+          unsigned rep_or = 0;
 #pragma unroll
           for (int k = 0; k < kU; k++) w[k] = s_ck[c0 + e + k], Kb[k] = s_K[e + k];
 #pragma unroll
-          for (int k = 0; k < kU; k++) {
-            const int m = (int)(w[k] & kRepMask);
-            const int n = a <= Kb[k] ? min(m, Kb[k] + 1 - a) : 0;
-            s_app[tid][a] = (unsigned short)(e + k);
-            for (int i = 1; i < n; i++) s_app[tid][a + i] = (unsigned short)(e + k);
-            a += n;
+          for (int k = 0; k < kU; k++) rep_or |= w[k] & kRepMask;
+          if (rep_or <= 1u) {  // every multiplicity 1: the chain is a += (a <= K)
+#pragma unroll
+            for (int k = 0; k < kU; k++) {
+              s_app[tid][a] = (unsigned short)(e + k);  // kept only if accepted
+              a += a <= Kb[k] ? 1 : 0;
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < kU; k++) {
+              const int m = (int)(w[k] & kRepMask);
+              const int n = a <= Kb[k] ? min(m, Kb[k] + 1 - a) : 0;
+              for (int i = 0; i < n; i++) s_app[tid][a + i] = (unsigned short)(e + k);
+              a += n;
+            }
           }
         }
         for (; e < e1; e++) {
@@ -1251,10 +1273,10 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
       PPM_PHASE(5)
     }
     if (h >= 0) {
-      if (stats && S.diag == 2) {  // experiment counters: most updates in one window, unstaged rr(n)
+      if (S.diag == 2) {  // experiment counters: most updates in one window, unstaged rr(n)
         const unsigned t_rr = cnt - cnt_w;  // updates made by this hit point in this window
-        atomicMax(&stats[14], (unsigned long long)t_rr);
-        if (t_rr > kRRStage) atomicAdd(&stats[15], (unsigned long long)(t_rr - kRRStage));
+        d_max = max(d_max, (unsigned long long)t_rr);
+        if (t_rr > kRRStage) d_unstaged += t_rr - kRRStage;
       }
       applied += cnt - s_cnt[tid];
       s_r2[tid] = r2, s_cnt[tid] = cnt;
@@ -1265,6 +1287,10 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   if (h >= 0) {
     state[h] = make_float4(flux.x, flux.y, flux.z, r2);
     nupd[h] = cnt;
+    if (stats && S.diag == 2) {
+      atomicMax(&stats[14], d_max);
+      if (d_unstaged) atomicAdd(&stats[15], d_unstaged);
+    }
   }
   const unsigned long long tot = wave_sum(applied);
   if (stats && (tid & 63) == 0 && tot) atomicAdd(&stats[3], tot);
