@@ -28,12 +28,12 @@ hipError_t launch_deposit_keys(const PDeposit*, const int*, const int*, int, int
                                unsigned*, PDeposit*, hipStream_t);
 hipError_t launch_group_buckets(const PHitPoint*, const int*, const int*, int, const PGrid*,
                                 unsigned*, int*, int*, hipStream_t);
-hipError_t launch_bucket_group_pairs(const unsigned*, const int*, const int*, int, unsigned*,
-                                     unsigned*, hipStream_t);
+hipError_t launch_bucket_group_pairs(const unsigned*, const int*, const int*, const int*, int,
+                                     unsigned*, unsigned*, hipStream_t);
 hipError_t launch_expand_count(const unsigned*, int, const int*, const int*, int*, hipStream_t);
 hipError_t launch_expand_write(const unsigned*, int, const int*, const int*, const unsigned*,
                                const int*, unsigned*, unsigned*, hipStream_t);
-hipError_t launch_bucket_bounds(const unsigned*, int, int*, int*, hipStream_t);
+hipError_t launch_bucket_bounds(const unsigned*, int, unsigned, int*, int*, hipStream_t);
 hipError_t launch_group_keys(const PHitPoint*, int, const PGrid*, unsigned long long*, int*, int*,
                             hipStream_t);
 hipError_t launch_group_flags(const unsigned long long*, int, int*, hipStream_t);
@@ -42,8 +42,7 @@ hipError_t launch_group_tiles(const int*, int, int*, hipStream_t);
 hipError_t launch_tile_table(const int*, const int*, int, int2*, hipStream_t);
 hipError_t launch_tile_work(const int2*, int, const int*, const int*, unsigned*, hipStream_t);
 hipError_t launch_rr_table(float*, int, hipStream_t);
-hipError_t launch_materialize(const unsigned*, const unsigned*, int, const PDeposit*,
-                              const unsigned*, const unsigned*, const int*, const int*, float4*,
+hipError_t launch_materialize(const unsigned*, const unsigned*, int, const PDeposit*, float4*,
                               hipStream_t);
 hipError_t launch_group_update(const PScene&, const PHitPoint*, const int*, const int*,
                                const int2*, int, const int*, const int*, const float4*,
@@ -389,7 +388,8 @@ void build_grid(ppm_scene* s, int width, int height) {
     s->bgval.reserve(npairs, "alloc bucket-group values");
     s->bgkey2.reserve(npairs, "alloc bucket-group keys");
     s->bgval2.reserve(npairs, "alloc bucket-group values");
-    hip_check(launch_bucket_group_pairs(s->gb.p, s->gnb.p, s->goff.p, groups, s->bgkey.p,
+    if (groups >= (1 << kGroupBits)) throw std::domain_error("too many hit-point groups");
+    hip_check(launch_bucket_group_pairs(s->gb.p, s->gm.p, s->gnb.p, s->goff.p, groups, s->bgkey.p,
                                         s->bgval.p, s->stream), "bucket-group pairs");
     int hbits = 1;
     while (hbits < 32 && (1ull << hbits) < (unsigned long long)n) hbits++;
@@ -404,7 +404,7 @@ void build_grid(ppm_scene* s, int width, int height) {
     s->bg_end.reserve(n, "alloc bucket-group ends");
     hip_check(hipMemsetAsync(s->bg_start.p, 0, n * sizeof(int), s->stream), "zero");
     hip_check(hipMemsetAsync(s->bg_end.p, 0, n * sizeof(int), s->stream), "zero");
-    hip_check(launch_bucket_bounds(s->bgkey2.p, npairs, s->bg_start.p, s->bg_end.p, s->stream),
+    hip_check(launch_bucket_bounds(s->bgkey2.p, npairs, ~0u, s->bg_start.p, s->bg_end.p, s->stream),
               "bucket-group bounds");
     s->list_start.reserve(groups, "alloc list starts");
     s->list_end.reserve(groups, "alloc list ends");
@@ -508,11 +508,11 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
           hip_check(hipcub::DeviceRadixSort::SortPairs(s->temp.p, bytes, s->pkey.p, s->pkey2.p,
                                                        s->pval.p, s->pval2.p, P, 0, gbits,
                                                        s->stream), "sort expansion by group");
-          hip_check(launch_bucket_bounds(s->pkey2.p, P, s->list_start.p, s->list_end.p, s->stream),
+          hip_check(launch_bucket_bounds(s->pkey2.p, P, (1u << kGroupBits) - 1u, s->list_start.p,
+                                         s->list_end.p, s->stream),
                     "group list bounds");
           s->gpos.reserve(P, "alloc group deposit lists");
-          hip_check(launch_materialize(s->pkey2.p, s->pval2.p, P, s->dense.p, s->dbucket.p, s->gb.p,
-                                       s->gm.p, s->gnb.p, s->gpos.p, s->stream),
+          hip_check(launch_materialize(s->pkey2.p, s->pval2.p, P, s->dense.p, s->gpos.p, s->stream),
                     "materialise group lists");
           const int2* tiles = s->tiles.p;
           if (lpt_order()) {

@@ -14,6 +14,7 @@ constexpr int kMeshStack = 64;
 constexpr int kEyeStack = 24;   // eye-ray tree: <= MaxRecursionDepth (<= 20) + 1 pending
 constexpr int kStatSlots = 32;  // device counter words (ppm_collect_stats)
 constexpr int kMaxCells = 27;
+constexpr int kGroupBits = 27;  // expansion keys: group | multiplicity << kGroupBits
 constexpr int kRepBits = 5;  // multiplicity bits next to a deposit index (kMaxCells < 32)
 constexpr unsigned kRepMask = (1u << kRepBits) - 1u;
 constexpr long long kMaxBatchDeposits = 1ll << (32 - kRepBits);   // hash cells a hit point's radius box can touch (3 per axis)

@@ -658,13 +658,14 @@ __global__ __launch_bounds__(256) void deposit_keys_kernel(const PDeposit* slots
   }
 }
 
+// Runs of equal (key & mask) in a sorted key array: [start[k], end[k]).
 __global__ __launch_bounds__(256) void bucket_bounds_kernel(const unsigned* keys, int n,
-                                                            int* start, int* end) {
+                                                            unsigned mask, int* start, int* end) {
   const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (i >= n) return;
-  const unsigned k = keys[i];
-  if (i == 0 || keys[i - 1] != k) start[k] = i;
-  if (i == n - 1 || keys[i + 1] != k) end[k] = i + 1;
+  const unsigned k = keys[i] & mask;
+  if (i == 0 || (keys[i - 1] & mask) != k) start[k] = i;
+  if (i == n - 1 || (keys[i + 1] & mask) != k) end[k] = i + 1;
 }
 
 // ------------------------------------------------------------------ grouped update pass
@@ -771,15 +772,18 @@ __global__ __launch_bounds__(256) void group_buckets_kernel(const PHitPoint* hps
 }
 
 // (bucket, group) pairs in group order; a stable sort by bucket makes the bucket -> groups map.
+// The value carries the group and, above kGroupBits, its multiplicity for that bucket (how many
+// of the group's cells hash there): it rides along in the expansion keys (sorted on the group
+// bits only) to the materialised records.
 __global__ __launch_bounds__(256) void bucket_group_pairs_kernel(const unsigned* gb,
-                                                                 const int* gnb,
+                                                                 const int* gm, const int* gnb,
                                                                  const int* goff, int groups,
                                                                  unsigned* key, unsigned* val) {
   const int g = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (g >= groups) return;
   for (int u = 0; u < gnb[g]; u++) {
     key[goff[g] + u] = gb[(size_t)g * kMaxCells + u];
-    val[goff[g] + u] = (unsigned)g;
+    val[goff[g] + u] = (unsigned)g | ((unsigned)gm[(size_t)g * kMaxCells + u] << kGroupBits);
   }
 }
 
@@ -855,18 +859,11 @@ __global__ __launch_bounds__(256) void rr_table_kernel(float* rr, int n) {
 // bucket, <= kMaxCells < 32).  The host keeps a batch below 2^27 deposits.
 __global__ __launch_bounds__(256) void materialize_kernel(const unsigned* pkey, const unsigned* pval,
                                                          int n, const PDeposit* dense,
-                                                         const unsigned* bucket, const unsigned* gb,
-                                                         const int* gm, const int* gnb,
                                                          float4* pos) {
   const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (p >= n) return;
-  const unsigned g = pkey[p], i = pval[p];
-  const unsigned b = bucket[i];
-  const unsigned* gbb = gb + (size_t)g * kMaxCells;
-  const int nb = gnb[g];
-  int u = 0;
-  while (u < nb - 1 && gbb[u] != b) u++;
-  const unsigned m = (unsigned)gm[(size_t)g * kMaxCells + u];
+  const unsigned i = pval[p];
+  const unsigned m = pkey[p] >> kGroupBits;  // the multiplicity rides above the group bits
   const float* x = dense[i].x;
   pos[p] = make_float4(x[0], x[1], x[2], __uint_as_float((i << kRepBits) | m));
 }
@@ -1374,10 +1371,11 @@ hipError_t launch_group_buckets(const PHitPoint* hps, const int* perm, const int
                      hps, perm, gstart, groups, grid, gb, gm, gnb);
   return hipGetLastError();
 }
-hipError_t launch_bucket_group_pairs(const unsigned* gb, const int* gnb, const int* goff,
-                                     int groups, unsigned* key, unsigned* val, hipStream_t st) {
+hipError_t launch_bucket_group_pairs(const unsigned* gb, const int* gm, const int* gnb,
+                                     const int* goff, int groups, unsigned* key, unsigned* val,
+                                     hipStream_t st) {
   hipLaunchKernelGGL(bucket_group_pairs_kernel, dim3(blocks_for(groups)), dim3(kThreads), 0, st,
-                     gb, gnb, goff, groups, key, val);
+                     gb, gm, gnb, goff, groups, key, val);
   return hipGetLastError();
 }
 hipError_t launch_expand_count(const unsigned* bucket, int n, const int* bg_start,
@@ -1393,10 +1391,10 @@ hipError_t launch_expand_write(const unsigned* bucket, int n, const int* bg_star
                      bg_start, bg_end, bg_group, off, key, val);
   return hipGetLastError();
 }
-hipError_t launch_bucket_bounds(const unsigned* keys, int n, int* start, int* end,
+hipError_t launch_bucket_bounds(const unsigned* keys, int n, unsigned mask, int* start, int* end,
                                 hipStream_t st) {
   hipLaunchKernelGGL(bucket_bounds_kernel, dim3(blocks_for(n)), dim3(kThreads), 0, st, keys, n,
-                     start, end);
+                     mask, start, end);
   return hipGetLastError();
 }
 hipError_t launch_group_keys(const PHitPoint* hps, int n, const PGrid* grid,
@@ -1438,10 +1436,9 @@ hipError_t launch_rr_table(float* rr, int n, hipStream_t st) {
   return hipGetLastError();
 }
 hipError_t launch_materialize(const unsigned* pkey, const unsigned* pval, int n,
-                              const PDeposit* dense, const unsigned* bucket, const unsigned* gb,
-                              const int* gm, const int* gnb, float4* pos, hipStream_t st) {
+                              const PDeposit* dense, float4* pos, hipStream_t st) {
   hipLaunchKernelGGL(materialize_kernel, dim3(blocks_for(n)), dim3(kThreads), 0, st, pkey, pval,
-                     n, dense, bucket, gb, gm, gnb, pos);
+                     n, dense, pos);
   return hipGetLastError();
 }
 hipError_t launch_group_update(const PScene& S, const PHitPoint* hps, const int* perm,
