@@ -25,7 +25,7 @@ hipError_t launch_grid(const PHitPoint*, int, int, int, PGrid*, float4*, unsigne
 hipError_t launch_photons(const PScene&, unsigned long long, long long, int, int, PDeposit*, int*,
                           unsigned long long*, hipStream_t);
 hipError_t launch_deposit_keys(const PDeposit*, const int*, const int*, int, int, const PGrid*,
-                               unsigned*, PDeposit*, hipStream_t);
+                               unsigned*, PDeposit*, float4*, hipStream_t);
 hipError_t launch_group_buckets(const PHitPoint*, const int*, const int*, int, const PGrid*,
                                 unsigned*, int*, int*, hipStream_t);
 hipError_t launch_bucket_group_pairs(const unsigned*, const int*, const int*, const int*, int,
@@ -42,7 +42,7 @@ hipError_t launch_group_tiles(const int*, int, int*, hipStream_t);
 hipError_t launch_tile_table(const int*, const int*, int, int2*, hipStream_t);
 hipError_t launch_tile_work(const int2*, int, const int*, const int*, unsigned*, hipStream_t);
 hipError_t launch_rr_table(float*, int, hipStream_t);
-hipError_t launch_materialize(const unsigned*, const unsigned*, int, const PDeposit*, float4*,
+hipError_t launch_materialize(const unsigned*, const unsigned*, int, const float4*, float4*,
                               hipStream_t);
 hipError_t launch_group_update(const PScene&, const PHitPoint*, const int*, const int*,
                                const int2*, int, const int*, const int*, const float4*,
@@ -178,6 +178,7 @@ struct ppm_scene {
   DevBuf<int> ndep, dep_off;
   DevBuf<unsigned> dbucket;                      // per dense deposit: its bucket
   DevBuf<PDeposit> dense;                        // deposits in photon order
+  DevBuf<float4> dpos;                           // their positions alone
   DevBuf<int> pcount, poff, list_start, list_end;  // (group, deposit) expansion
   DevBuf<unsigned> pkey, pval, pkey2, pval2;
   DevBuf<unsigned> gb;                           // per group: buckets, multiplicity
@@ -209,7 +210,7 @@ struct ppm_scene {
     gkeys.release(), gkeys2.release(), gidx.release(), perm.release(), gflags.release();
     gid.release(), gstart.release(), ntile.release(), tile_off.release(), tiles.release();
     tiles_lpt.release(), tkey.release(), tkey2.release();
-    dep_off.release(), dbucket.release(), dense.release(), pcount.release(), poff.release();
+    dep_off.release(), dbucket.release(), dense.release(), dpos.release(), pcount.release(), poff.release();
     list_start.release(), list_end.release(), pkey.release(), pval.release(), pkey2.release();
     pval2.release(), gb.release(), gm.release(), gnb.release(), goff.release();
     bg_start.release(), bg_end.release(), bgkey.release(), bgval.release(), bgkey2.release();
@@ -449,8 +450,9 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
         // deposits in photon order, with their buckets
         s->dense.reserve(D, "alloc dense deposits");
         s->dbucket.reserve(D, "alloc deposit buckets");
+        s->dpos.reserve(D, "alloc deposit positions");
         hip_check(launch_deposit_keys(s->slots.p, s->ndep.p, s->dep_off.p, b, K, s->grid.p,
-                                      s->dbucket.p, s->dense.p, s->stream), "deposit keys");
+                                      s->dbucket.p, s->dense.p, s->dpos.p, s->stream), "deposit keys");
         // each deposit into every group filed under its bucket; a stable sort by group gives
         // each group its deposit list in photon order
         s->pcount.reserve(D + 1, "alloc expansion counts");
@@ -512,7 +514,7 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
                                          s->list_end.p, s->stream),
                     "group list bounds");
           s->gpos.reserve(P, "alloc group deposit lists");
-          hip_check(launch_materialize(s->pkey2.p, s->pval2.p, P, s->dense.p, s->gpos.p, s->stream),
+          hip_check(launch_materialize(s->pkey2.p, s->pval2.p, P, s->dpos.p, s->gpos.p, s->stream),
                     "materialise group lists");
           const int2* tiles = s->tiles.p;
           if (lpt_order()) {

@@ -484,7 +484,8 @@ __global__ __launch_bounds__(1024) void grid_kernel(const PHitPoint* hps, int n,
 
 // ------------------------------------------------------------------ photon pass
 // Photon first + i traces its chain (photon_trace's recursion never branches) and leaves
-// one deposit per diffuse hit in slots[i * K + k], k < K = max(1, MaxRecursionDepth - 1).
+// one deposit per diffuse hit in slots[k * count + i], k < K = max(1, MaxRecursionDepth - 1)
+// (k-major, so deposit_keys reads the k-th deposits of consecutive photons coalesced).
 //
 // Lanes are refilled (PPM_REFILL, default): Russian roulette ends ~2/3 of the chains at every
 // diffuse hit (C5: 1.36 segments per photon), so a wave that traced one photon per lane ran
@@ -527,7 +528,7 @@ __device__ __forceinline__ void emit_photon(const PScene& S, unsigned long long 
 }
 
 // One segment of photon_trace (Scene.cpp:106-249) for photon i; false when the chain ends.
-__device__ __forceinline__ bool photon_segment(const PScene& S, int i, int K, PDeposit* slots,
+__device__ __forceinline__ bool photon_segment(const PScene& S, int i, int count, PDeposit* slots,
                                                PhotonState& P, unsigned long long& rays,
                                                unsigned long long& deps) {
   P.depth++;
@@ -541,7 +542,7 @@ __device__ __forceinline__ bool photon_segment(const PScene& S, int i, int K, PD
   const PMaterial& m = S.materials[S.objects[h.obj].material];
   if (m.type == kMatDiffuse) {
     const V w_i = neg(normalize(ray.d));
-    PDeposit& d = slots[(size_t)i * K + P.k];
+    PDeposit& d = slots[(size_t)P.k * count + i];
     d.x[0] = x.x, d.x[1] = x.y, d.x[2] = x.z;
     d.normal[0] = normal.x, d.normal[1] = normal.y, d.normal[2] = normal.z;
     d.w_i[0] = w_i.x, d.w_i[1] = w_i.y, d.w_i[2] = w_i.z;
@@ -618,7 +619,7 @@ __global__ __launch_bounds__(256) void photon_kernel(PScene S, unsigned long lon
       }
     }
     if (!__ballot(i >= 0)) break;  // range exhausted and every chain ended
-    if (i >= 0 && !photon_segment(S, i, K, slots, P, rays, deps)) {
+    if (i >= 0 && !photon_segment(S, i, count, slots, P, rays, deps)) {
       ndep[i] = P.k;
       i = -1;
     }
@@ -627,7 +628,7 @@ __global__ __launch_bounds__(256) void photon_kernel(PScene S, unsigned long lon
   const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (i < count) {
     emit_photon(S, seed, first + i, P);
-    while (photon_segment(S, i, K, slots, P, rays, deps)) {
+    while (photon_segment(S, i, count, slots, P, rays, deps)) {
     }
     ndep[i] = P.k;
   }
@@ -640,21 +641,23 @@ __global__ __launch_bounds__(256) void photon_kernel(PScene S, unsigned long lon
 }
 
 // Deposit d of photon i -> dense position offsets[i] + d (photon order), with the bucket of
-// its cell (Scene.cpp:125-130).
+// its cell (Scene.cpp:125-130), and its position alone in dpos (what materialize reads per
+// (group, deposit) pair: 16 B instead of a 48-B record's line).
 __global__ __launch_bounds__(256) void deposit_keys_kernel(const PDeposit* slots,
                                                            const int* ndep, const int* offsets,
                                                            int count, int K,
                                                            const PGrid* grid, unsigned* bucket,
-                                                           PDeposit* dense) {
+                                                           PDeposit* dense, float4* dpos) {
   const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (i >= count) return;
   const PGrid G = *grid;
   const int n = ndep[i], o = offsets[i];
   for (int k = 0; k < n; k++) {
-    const PDeposit d = slots[(size_t)i * K + k];
+    const PDeposit d = slots[(size_t)k * count + i];
     const V hh = (ld(d.x) - ld(G.bmin)) * G.hash_scale;
     bucket[o + k] = bucket_of(G, cell(hh.x), cell(hh.y), cell(hh.z));
     dense[o + k] = d;
+    dpos[o + k] = make_float4(d.x[0], d.x[1], d.x[2], 0.0f);
   }
 }
 
@@ -858,14 +861,14 @@ __global__ __launch_bounds__(256) void rr_table_kernel(float* rr, int n) {
 // with its multiplicity in that group (how many of the group's cells share the deposit's
 // bucket, <= kMaxCells < 32).  The host keeps a batch below 2^27 deposits.
 __global__ __launch_bounds__(256) void materialize_kernel(const unsigned* pkey, const unsigned* pval,
-                                                         int n, const PDeposit* dense,
+                                                         int n, const float4* dpos,
                                                          float4* pos) {
   const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (p >= n) return;
   const unsigned i = pval[p];
   const unsigned m = pkey[p] >> kGroupBits;  // the multiplicity rides above the group bits
-  const float* x = dense[i].x;
-  pos[p] = make_float4(x[0], x[1], x[2], __uint_as_float((i << kRepBits) | m));
+  const float4 x = dpos[i];
+  pos[p] = make_float4(x.x, x.y, x.z, __uint_as_float((i << kRepBits) | m));
 }
 
 // One workgroup per (group, tile of <= kTileHP hit points), streaming the group's deposits
@@ -1359,9 +1362,9 @@ hipError_t launch_photons(const PScene& S, unsigned long long seed, long long fi
 }
 hipError_t launch_deposit_keys(const PDeposit* slots, const int* ndep, const int* offsets,
                                int count, int K, const PGrid* grid, unsigned* bucket,
-                               PDeposit* dense, hipStream_t st) {
+                               PDeposit* dense, float4* dpos, hipStream_t st) {
   hipLaunchKernelGGL(deposit_keys_kernel, dim3(blocks_for(count)), dim3(kThreads), 0, st, slots,
-                     ndep, offsets, count, K, grid, bucket, dense);
+                     ndep, offsets, count, K, grid, bucket, dense, dpos);
   return hipGetLastError();
 }
 hipError_t launch_group_buckets(const PHitPoint* hps, const int* perm, const int* gstart,
@@ -1436,9 +1439,9 @@ hipError_t launch_rr_table(float* rr, int n, hipStream_t st) {
   return hipGetLastError();
 }
 hipError_t launch_materialize(const unsigned* pkey, const unsigned* pval, int n,
-                              const PDeposit* dense, float4* pos, hipStream_t st) {
+                              const float4* dpos, float4* pos, hipStream_t st) {
   hipLaunchKernelGGL(materialize_kernel, dim3(blocks_for(n)), dim3(kThreads), 0, st, pkey, pval,
-                     n, dense, pos);
+                     n, dpos, pos);
   return hipGetLastError();
 }
 hipError_t launch_group_update(const PScene& S, const PHitPoint* hps, const int* perm,
