@@ -127,6 +127,22 @@ def test_gpu_frames_match_reference_goldens(rt, scene_dir):
                 assert hashlib.sha256(got.tobytes()).hexdigest() == gc["frame_sha256"], (name, cam)
 
 
+def test_c3_frame_matches_reference_golden_hash(rt, scene_dir):
+    """C3 pinned to the reference itself, not only through the oracle: the GPU frame (both
+    traversal modes) hashes to the frame the unmodified HW2 sources rendered here."""
+    import hashlib
+    import json
+    golden = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+    xml = scenes.write_c3(scene_dir)
+    for mode in ("fast", "reference"):
+        with rt.Scene(xml, traversal=mode) as s:
+            got, st = s.render_image(0)
+            gc = golden["c3"]["cameras"][0]
+            assert got.shape[:2] == (gc["height"], gc["width"])
+            assert hashlib.sha256(got.tobytes()).hexdigest() == gc["frame_sha256"], mode
+            assert st.rays() == gc["rays"]
+
+
 @pytest.mark.slow
 def test_c3_full_resolution_matches_oracle(rt, scene_dir):
     xml = scenes.write_c3(scene_dir)
