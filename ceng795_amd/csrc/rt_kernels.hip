@@ -1900,6 +1900,10 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
 #ifndef RT_TRACE_MIN_WAVES  // (A/B: fewer waves per SIMD, more registers per wave)
 #define RT_TRACE_MIN_WAVES 8
 #endif
+#ifndef RT_PRIMARY_MIN_WAVES  // primary kernel only (A/B: RT_PRIMARY_MIN_WAVES=8)
+#define RT_PRIMARY_MIN_WAVES 7  // 32 more SGPRs for the wide node: frame 0.703 -> 0.691 ms
+#endif
+#define RT_PRIMARY_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_PRIMARY_MIN_WAVES, 8)))
 #ifndef RT_TRAVERSAL_OCCUPANCY
 #define RT_TRAVERSAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_TRACE_MIN_WAVES, 8)))
 #endif
@@ -2115,7 +2119,7 @@ __device__ __forceinline__ void share_shadow(const RenderParams& P, const DevNod
 
 // Traversal kernels: one packet per wave, XCD-remapped blocks of 2-D tile blocks.
 template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL, bool WO = false>
-__global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY void trace_primary_kernel(
+__global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_PRIMARY_OCCUPANCY void trace_primary_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
   constexpr int W = trace_waves<DEEP>();
