@@ -623,6 +623,11 @@ __device__ __forceinline__ bool advance(WaveStack<DEEP, R>& st, int c0, int c1,
 #endif
 constexpr int kBatchFlush = RT_BATCH_FLUSH;  // run the queue once this many tests are pending
 constexpr int kBatchCap = kBatchFlush + 256;  // < kBatchFlush pending + 2 pairs x 64 per visit
+#ifndef RT_SHADOW_FLUSH  // shadow rays: a smaller queue finds occluders (and stops lanes) sooner
+#define RT_SHADOW_FLUSH RT_BATCH_FLUSH
+#endif
+constexpr int kShadowFlush = RT_SHADOW_FLUSH;
+static_assert(kShadowFlush <= kBatchFlush, "the queue is sized for kBatchFlush");
 #ifndef RT_TRACE_WAVES
 #define RT_TRACE_WAVES 4
 #endif
@@ -1155,7 +1160,7 @@ __device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* _
   int node = task ? start_node : (accel ? P.accel_root : P.root_ref);
   for (;;) {
     if constexpr (batch) {  // between visits; a lane found occluded stops entering nodes
-      if (pending >= kBatchFlush) {
+      if (pending >= kShadowFlush) {
         batch_flush<true, SPHERES>(L, pending, prims, r[0], thr[0]);
         pending = 0;
         occ[0] = L.key[lane] != 0ull;
