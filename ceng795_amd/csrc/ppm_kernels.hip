@@ -901,7 +901,9 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   __shared__ int s_wtot[kUpdThreads / 64];
   __shared__ unsigned s_ck[kTileHP * kWinMax];  // photon-order index << kRepBits | multiplicity
   __shared__ float s_cd2[kTileHP * kWinMax];
-  __shared__ float4 s_ccf[kChunk];  // color * photon_flux, w = 0 (see the gate)
+  // color * photon_flux, and in w the candidate's distance^2 for the gate: negated when its
+  // multiplicity exceeds 1 (sign bit: the gate's scalar path), +inf when its normal fails
+  __shared__ float4 s_ccf[kChunk];
   constexpr int kRRStage = PPM_RR_STAGE;  // rr(n) staged per hit point per window (more: computed inline)
   __shared__ float s_rr[kTileHP][kRRStage];
 #if PPM_KGATE
@@ -1122,7 +1124,8 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
           }
         }
         const V cf = color * pf;
-        s_ccf[e - c0] = make_float4(cf.x, cf.y, cf.z, 0.0f);
+        const float d2c = !normal_ok ? kInf : ((s_ck[e] & kRepMask) > 1u ? -s_cd2[e] : s_cd2[e]);
+        s_ccf[e - c0] = make_float4(cf.x, cf.y, cf.z, d2c);
       }
       __syncthreads();
       PPM_PHASE(4)
@@ -1220,12 +1223,15 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
           float d2b[kB], rrb[kB];
           float4 cb[kB];
 #pragma unroll
-          for (int k = 0; k < kB; k++) {
+          for (int k = 0; k < kB; k++) {  // one 16-B record per candidate (+ its staged rr)
             const int ek = min(e + k, e1 - 1);
-            d2b[k] = k < nb ? s_cd2[ek] : kInf;
-            fast = fast & ((s_ck[ek] & kRepMask) <= 1u);
             cb[k] = s_ccf[ek - c0];
             rrb[k] = s_rr[tid][min(t + (unsigned)k, (unsigned)kRRStage - 1)];
+          }
+#pragma unroll
+          for (int k = 0; k < kB; k++) {
+            fast = fast & ((__float_as_uint(cb[k].w) >> 31) == 0u);  // multiplicity 1
+            d2b[k] = k < nb ? cb[k].w : kInf;
           }
           if (fast) {
             bool alive = true;
@@ -1234,7 +1240,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
             for (int k = 0; k < kB; k++) {
               const bool acc = alive && d2b[k] <= fzr.y;
               const f32x2 rr2 = {rrb[k], rrb[k]};
-              const f32x2 cxy = {cb[k].x, cb[k].y}, cz0 = {cb[k].z, cb[k].w};
+              const f32x2 cxy = {cb[k].x, cb[k].y}, cz0 = {cb[k].z, 0.0f};
               const f32x2 nxy = (fxy + cxy) * rr2, nzr = (fzr + cz0) * rr2;
               fxy.x = acc ? nxy.x : fxy.x;
               fxy.y = acc ? nxy.y : fxy.y;
@@ -1246,10 +1252,10 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
             }
             e += min(used, nb);
           } else {
-            const float d2 = d2b[0];
+            const float d2 = __builtin_fabsf(cb[0].w);
             if (d2 <= fzr.y) {
               const unsigned reps = s_ck[e] & kRepMask;
-              const f32x2 cxy = {cb[0].x, cb[0].y}, cz0 = {cb[0].z, cb[0].w};
+              const f32x2 cxy = {cb[0].x, cb[0].y}, cz0 = {cb[0].z, 0.0f};
               unsigned r = 0;
               do {
                 const unsigned tt = cnt - cnt_w;
