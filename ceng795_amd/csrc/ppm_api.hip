@@ -47,7 +47,9 @@ hipError_t launch_materialize(const unsigned*, const unsigned*, int, const float
 hipError_t launch_group_update(const PScene&, const PHitPoint*, const int*, const int*,
                                const int2*, int, const int*, const int*, const float4*,
                                const PDeposit*, const float*, int, float4*, unsigned*,
-                               unsigned long long*, hipStream_t);
+                               const long long*, float4*, unsigned long long*, hipStream_t);
+hipError_t launch_tile_compact_need(const int2*, int, const int*, const int*, long long, int,
+                                    long long*, hipStream_t);
 hipError_t launch_density(const PHitPoint*, const float4*, const int*, int, double, float*,
                           hipStream_t);
 }  // namespace ppm
@@ -185,6 +187,9 @@ struct ppm_scene {
   DevBuf<int> gm, gnb, goff, bg_start, bg_end;
   DevBuf<unsigned> bgkey, bgval, bgkey2, bgval2;  // bucket -> groups
   DevBuf<float4> gpos;  // per-group deposit lists, materialised (position, index | multiplicity)
+  DevBuf<long long> cneed, cofs;  // per tile: compaction range size, offset (update pass)
+  DevBuf<float4> cbuf;            // the compacted tile lists
+  long long compact_min = -1;     // ppm_set_update_compaction (-1: default_compact_min())
   DevBuf<float> rrtab;                           // rr(n), n < kRRTable
   DevBuf<unsigned char> temp;
   DevBuf<unsigned long long> stats;  // [photons, photon_rays, deposits, updates, eye_rays]
@@ -215,6 +220,7 @@ struct ppm_scene {
     pval2.release(), gb.release(), gm.release(), gnb.release(), goff.release();
     bg_start.release(), bg_end.release(), bgkey.release(), bgval.release(), bgkey2.release();
     bgval2.release(), gpos.release(), rrtab.release();
+    cneed.release(), cofs.release(), cbuf.release();
     temp.release(), stats.release(), error.release(), image.release();
     wide.release(), stats_keep.release();
     if (stream) (void)hipStreamDestroy(stream);
@@ -232,6 +238,19 @@ bool lpt_order() {
     return !(e && e[0] == '0');
   }();
   return on;
+}
+
+// Tile-list compaction in the update pass (group_update_kernel phase (0)): tiles whose group
+// list holds at least this many deposits copy the reachable ones first.  Results do not depend
+// on it (the copy is a superset of every window's candidates, in order).
+// CENG795_PPM_COMPACT sets the default (0: off); ppm_set_update_compaction sets it per scene.
+constexpr int kCompactShift = 2;  // scratch per compacted tile: a quarter of its list
+long long default_compact_min() {
+  static const long long v = [] {
+    const char* e = std::getenv("CENG795_PPM_COMPACT");
+    return e ? std::max(0LL, std::atoll(e)) : 65536LL;
+  }();
+  return v;
 }
 
 template <typename T>
@@ -533,6 +552,35 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
                                                          0, 32, s->stream), "sort tiles");
             tiles = s->tiles_lpt.p;
           }
+          // scratch ranges of the tiles whose lists get compacted (none: cofs stays null)
+          const long long cmin = s->compact_min >= 0 ? s->compact_min : default_compact_min();
+          const long long* cofs = nullptr;
+          if (cmin > 0) {
+            s->cneed.reserve(s->n_tiles + 1, "alloc compaction sizes");
+            s->cofs.reserve(s->n_tiles + 1, "alloc compaction offsets");
+            hip_check(launch_tile_compact_need(tiles, s->n_tiles, s->list_start.p, s->list_end.p,
+                                               cmin, kCompactShift, s->cneed.p, s->stream),
+                      "compaction sizes");
+            bytes = 0;
+            hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, s->cneed.p, s->cofs.p,
+                                                       s->n_tiles + 1, s->stream), "scan size");
+            s->temp.reserve(bytes, "alloc scan temp");
+            hip_check(hipcub::DeviceScan::ExclusiveSum(s->temp.p, bytes, s->cneed.p, s->cofs.p,
+                                                       s->n_tiles + 1, s->stream),
+                      "compaction offsets");
+            long long ctotal = 0;
+            hip_check(hipMemcpyAsync(&ctotal, s->cofs.p + s->n_tiles, sizeof ctotal,
+                                     hipMemcpyDeviceToHost, s->stream), "read compaction total");
+            hip_check(hipStreamSynchronize(s->stream), "compaction total");
+            size_t cfree = 0, ctot = 0;
+            const bool fits = hipMemGetInfo(&cfree, &ctot) == hipSuccess &&
+                              (size_t)ctotal * sizeof(float4) <=
+                                  (cfree + s->cbuf.cap * sizeof(float4)) / 4;
+            if (ctotal > 0 && fits) {
+              s->cbuf.reserve((size_t)ctotal, "alloc compacted tile lists");
+              cofs = s->cofs.p;
+            }
+          }
           hipEvent_t e0, e1;
           hip_check(hipEventCreate(&e0), "event");
           hip_check(hipEventCreate(&e1), "event");
@@ -541,7 +589,7 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
           hip_check(launch_group_update(s->S, s->hp.p, s->perm.p, s->gstart.p, tiles,
                                         s->n_tiles, s->list_start.p, s->list_end.p, s->gpos.p,
                                         s->dense.p, s->rrtab.p, kRRTable, s->state.p, s->nupd.p,
-                                        s->stats.p, s->stream),
+                                        cofs, s->cbuf.p, s->stats.p, s->stream),
                     "hit-point updates");
           hip_check(hipEventRecord(e1, s->stream), "event");
         }
@@ -623,6 +671,12 @@ int ppm_settings(const ppm_scene* s, int* per_iteration, int* iterations, int* m
   *per_iteration = s->host.per_iteration;
   *iterations = s->host.iterations;
   *max_depth = s->host.max_depth;
+  return RT_OK;
+}
+
+int ppm_set_update_compaction(ppm_scene* s, long long min_list) {
+  if (!s || min_list < -1) return set_error(RT_E_INVALID, "ppm_set_update_compaction: bad argument");
+  s->compact_min = min_list;
   return RT_OK;
 }
 
@@ -762,6 +816,9 @@ int ppm_collect_stats(ppm_scene* s, ppm_stats* st) {
     st->update_deposit_visits = (long long)c[6];
     st->update_candidates = (long long)c[16];
     st->update_launches = (long long)s->upd_events.size();
+    st->update_compacted_tiles = (long long)c[20];
+    st->update_compaction_fallbacks = (long long)c[21];
+    st->update_compacted_deposits = (long long)c[22];
     st->update_ms = 0;
     for (auto& ev : s->upd_events) {
       float ms = 0;
@@ -772,9 +829,11 @@ int ppm_collect_stats(ppm_scene* s, ppm_stats* st) {
     if (s->S.diag == 2) std::fprintf(stderr, "ppm diag: windows %llu deposit-visits %llu tiles %d groups %d "
                                      "longest tile %llu ticks phases(max) stage+filter %llu "
                                      "counts %llu scan %llu scatter %llu color %llu gate %llu max-window-updates %llu "
-                                     "unstaged-rr %llu candidates %llu max-tile-candidates %llu max-wave-updates %llu max-tile-windows %llu\n",
+                                     "unstaged-rr %llu candidates %llu max-tile-candidates %llu max-wave-updates %llu max-tile-windows %llu "
+                                     "compacted-tiles %llu fallbacks %llu compacted-deposits %llu\n",
                                      c[5], c[6], s->n_tiles, s->n_groups, c[7], c[8], c[9],
-                                     c[10], c[11], c[12], c[13], c[14], c[15], c[16], c[17], c[18], c[19]);
+                                     c[10], c[11], c[12], c[13], c[14], c[15], c[16], c[17], c[18], c[19],
+                                     c[20], c[21], c[22]);
     s->photons = 0;
     return RT_OK;
   });

@@ -718,6 +718,9 @@ __global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, con
 #ifndef PPM_WIN
 #define PPM_WIN 2048
 #endif
+#ifndef PPM_GATE2
+#define PPM_GATE2 0  // fixed-width gate bodies of PPM_GATE2 candidates (0: batches of PPM_GATE_B)
+#endif
 #ifndef PPM_GATE_B
 #define PPM_GATE_B 3
 #endif
@@ -850,6 +853,27 @@ __device__ __forceinline__ float radius_reduction(unsigned n) {
   return (float)((double)(nf + kAlpha) / ((double)nf + 1.0));
 }
 
+// Tile-list compaction (the update kernel's first phase for long lists): a tile whose group
+// list holds at least `min_len` deposits gets a scratch range of L >> shift records; the kernel
+// copies into it, in photon order, the deposits within the radius any of its hit points has
+// at the kernel start, and streams its windows over that instead.  need[ntiles] = 0 closes the
+// exclusive scan that turns the sizes into offsets.
+__global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tiles, int ntiles,
+                                                                const int* list_start,
+                                                                const int* list_end,
+                                                                long long min_len, int shift,
+                                                                long long* need) {
+  const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (t > ntiles) return;
+  if (t == ntiles) {
+    need[t] = 0;
+    return;
+  }
+  const int g = tiles[t].x;
+  const long long L = list_end[g] - list_start[g];
+  need[t] = L >= min_len ? (L >> shift) : 0;
+}
+
 __global__ __launch_bounds__(256) void rr_table_kernel(float* rr, int n) {
   const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (i < n) rr[i] = radius_reduction((unsigned)i);
@@ -883,10 +907,15 @@ __global__ __launch_bounds__(256) void materialize_kernel(const unsigned* pkey, 
 //      the running value, r^2 *= rr(n), n++, flux = (flux + color * photon_flux) * rr(n) —
 //      repeated when two of its cells share the deposit's bucket.
 // The next window is fetched (coalesced) while the current one is processed.
+// A tile with a compaction range (cofs[t] < cofs[t+1], tile_compact_need_kernel) first copies
+// the deposits its hit points can reach with their radius at the kernel start — a superset of
+// what any window's filter passes, by the same argument, with the same d2 arithmetic — and
+// runs its windows over that copy; if the copy would not fit, over the full list as before.
 __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM_WPE, PPM_WPE))) void group_update_kernel(
     PScene S, const PHitPoint* hps, const int* perm, const int* gstart, const int2* tiles,
     const int* list_start, const int* list_end, const float4* pos, const PDeposit* dense,
-    const float* rrtab, int nrr, float4* state, unsigned* nupd, unsigned long long* stats) {
+    const float* rrtab, int nrr, float4* state, unsigned* nupd, const long long* cofs,
+    float4* cbuf, unsigned long long* stats) {
   constexpr int kPer = kWinMax / kUpdThreads;
   constexpr int kWords = kWinMax / 32;
   constexpr int kChunk = PPM_CHUNK;  // candidates per color / apply round
@@ -939,16 +968,9 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   }
   unsigned long long applied = 0, cands = 0;
   unsigned long long d_max = 0, d_unstaged = 0;  // diag: per hit point, flushed once per tile
-  const int ls = list_start[g], le = list_end[g];
-  float4 dep[kPer];  // position, photon-order index << kRepBits | multiplicity
-  auto fetch = [&](int base) {
-#pragma unroll
-    for (int q = 0; q < kPer; q++) {
-      const int k = base + tid + q * kUpdThreads;
-      if (k < le) dep[q] = pos[k];
-    }
-  };
-  fetch(ls);
+  int ls = list_start[g], le = list_end[g];
+  unsigned long long visits = (unsigned long long)(le - ls);  // 16-B records the filters read
+  const float4* src = pos;
   __syncthreads();
   V tp[kTileHP], tn[kTileHP];
 #pragma unroll
@@ -956,6 +978,93 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     tp[j] = mk(s_hp[j][0], s_hp[j][1], s_hp[j][2]);
     tn[j] = mk(s_hp[j][3], s_hp[j][4], s_hp[j][5]);
   }
+  if (cofs && cofs[blockIdx.x + 1] > cofs[blockIdx.x]) {
+    // (0) compaction: rounds of 64 records per thread-row; one count per (record row, wave),
+    // scanned by wave 0, keeps the copy in photon order
+    constexpr int kCW = kUpdThreads / 64;
+    constexpr int kCPer = 64 / kCW;
+    static_assert(kCPer * kCW == 64, "one count per lane of the scanning wave");
+    __shared__ int s_cc[64], s_cp[65];
+    const long long c0 = cofs[blockIdx.x];
+    const int cap = (int)(cofs[blockIdx.x + 1] - c0);
+    float4* dst = cbuf + c0;
+    const int wave = tid >> 6;
+    float r2c[kTileHP];
+#pragma unroll
+    for (int j = 0; j < kTileHP; j++) r2c[j] = j < nh ? s_r2[j] : -1.0f;
+    float4 cd[kCPer];
+    auto cfetch = [&](int base) {
+#pragma unroll
+      for (int q = 0; q < kCPer; q++) {
+        const int k = base + tid + q * kUpdThreads;
+        if (k < le) cd[q] = pos[k];
+      }
+    };
+    cfetch(ls);
+    int kept = 0;
+    for (int base = ls; base < le; base += kCPer * kUpdThreads) {
+      float4 cw[kCPer];
+      unsigned rank[kCPer];
+      bool keep[kCPer];
+#pragma unroll
+      for (int q = 0; q < kCPer; q++) cw[q] = cd[q];
+      cfetch(base + kCPer * kUpdThreads);  // next round in flight
+#pragma unroll
+      for (int q = 0; q < kCPer; q++) {
+        const V x = mk(cw[q].x, cw[q].y, cw[q].z);
+        bool kp = false;
+#pragma unroll
+        for (int j = 0; j < kTileHP; j++) {
+          const V v = tp[j] - x;
+          kp = kp || (dot(v, v) <= r2c[j]);
+        }
+        keep[q] = kp && base + tid + q * kUpdThreads < le;
+        const unsigned long long bal = __ballot(keep[q]);
+        rank[q] = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                            __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+        if (lane == 0) s_cc[q * kCW + wave] = __builtin_popcountll(bal);
+      }
+      __syncthreads();
+      if (tid < 64) {
+        const int v = s_cc[tid];
+        int x = v;
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(x, o, 64);
+          if (lane >= o) x += y;
+        }
+        s_cp[tid] = x - v;
+        if (tid == 63) s_cp[64] = x;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < kCPer; q++) {
+        if (!keep[q]) continue;
+        const int idx = kept + s_cp[q * kCW + wave] + (int)rank[q];
+        if (idx < cap) dst[idx] = cw[q];
+      }
+      kept += s_cp[64];
+    }
+    __syncthreads();  // the copy is read by other threads of the workgroup below
+    if (kept <= cap) {
+      src = dst, ls = 0, le = kept;
+      visits += (unsigned long long)kept;
+    } else {
+      visits += (unsigned long long)(le - ls);
+    }
+    if (stats && tid == 0) {
+      atomicAdd(&stats[kept <= cap ? 20 : 21], 1ull);
+      atomicAdd(&stats[22], (unsigned long long)kept);
+    }
+  }
+  float4 dep[kPer];  // position, photon-order index << kRepBits | multiplicity
+  auto fetch = [&](int base) {
+#pragma unroll
+    for (int q = 0; q < kPer; q++) {
+      const int k = base + tid + q * kUpdThreads;
+      if (k < le) dep[q] = src[k];
+    }
+  };
+  fetch(ls);
   unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tp0 = 0;
 #define PPM_PHASE(i)                                              \
   if (S.diag == 2 && tid == 0) {                                  \
@@ -1211,6 +1320,79 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         acc_n = a;
       } else
 #endif
+#if PPM_GATE2
+      if (h >= 0 && S.diag != 1) {
+        // Fixed-width gate: every body applies exactly kG candidates (the tail padded with
+        // +inf, which is never accepted), so the next body's records are read from LDS while
+        // this one runs.  Per candidate the new state is computed unconditionally with the rr
+        // at the head of a register queue (rr(n) for the next accept), then kept or dropped by
+        // the acceptance test; an accept shifts the queue.  r^2's chain is multiply -> select,
+        // the acceptance test runs beside the multiply.  A body holding a multiplicity > 1, or
+        // reaching past the staged rr(n), takes the scalar path for its first candidate.
+        constexpr int kG = PPM_GATE2;
+        const int e1 = min(my_end, c0 + kChunk);
+        f32x2 fxy = {flux.x, flux.y}, fzr = {flux.z, r2};
+        int e = max(my_beg, c0);
+        float4 nb[kG];
+        int pf = -1;  // the candidate index nb was read from
+        while (e < e1) {
+          if (pf != e) {
+#pragma unroll
+            for (int k = 0; k < kG; k++) nb[k] = s_ccf[min(e + k, e1 - 1) - c0];
+          }
+          float4 cb[kG];
+#pragma unroll
+          for (int k = 0; k < kG; k++) cb[k] = nb[k];
+          const int n = min(kG, e1 - e);
+          const unsigned t = cnt - cnt_w;
+          float rq[kG];
+#pragma unroll
+          for (int k = 0; k < kG; k++) rq[k] = s_rr[tid][min(t + (unsigned)k, (unsigned)kRRStage - 1)];
+#pragma unroll
+          for (int k = 0; k < kG; k++) nb[k] = s_ccf[min(e + n + k, e1 - 1) - c0];  // next body
+          pf = e + n;
+          unsigned sgn = 0;
+#pragma unroll
+          for (int k = 0; k < kG; k++) sgn |= k < n ? __float_as_uint(cb[k].w) : 0u;
+          if ((sgn >> 31) == 0u && t + kG <= (unsigned)kRRStage) {
+#pragma unroll
+            for (int k = 0; k < kG; k++) {
+              const float d2 = k < n ? cb[k].w : kInf;
+              const f32x2 rr2 = {rq[0], rq[0]};
+              const f32x2 cxy = {cb[k].x, cb[k].y}, cz0 = {cb[k].z, 0.0f};
+              const f32x2 nxy = (fxy + cxy) * rr2, nzr = (fzr + cz0) * rr2;
+              const bool acc = d2 <= fzr.y;
+              fxy.x = acc ? nxy.x : fxy.x;
+              fxy.y = acc ? nxy.y : fxy.y;
+              fzr.x = acc ? nzr.x : fzr.x;
+              fzr.y = acc ? nzr.y : fzr.y;
+              cnt += acc ? 1u : 0u;
+#pragma unroll
+              for (int i = 0; i + 1 < kG - k; i++) rq[i] = acc ? rq[i + 1] : rq[i];
+            }
+            e += n;
+          } else {
+            const float d2 = __builtin_fabsf(cb[0].w);
+            if (d2 <= fzr.y) {
+              const unsigned reps = s_ck[e] & kRepMask;
+              const f32x2 cxy = {cb[0].x, cb[0].y}, cz0 = {cb[0].z, 0.0f};
+              unsigned r = 0;
+              do {
+                const unsigned tt = cnt - cnt_w;
+                const float rr = tt < (unsigned)kRRStage ? s_rr[tid][tt] : radius_reduction(cnt);
+                cnt++;
+                const f32x2 rr2 = {rr, rr};
+                fxy = (fxy + cxy) * rr2;
+                fzr = (fzr + cz0) * rr2;
+              } while (++r < reps && d2 <= fzr.y);
+            }
+            e++;
+          }
+        }
+        flux = mk(fxy.x, fxy.y, fzr.x);
+        r2 = fzr.y;
+      }
+#else
       if (h >= 0 && S.diag != 1) {
         constexpr int kB = PPM_GATE_B;
         const int e1 = min(my_end, c0 + kChunk);
@@ -1272,6 +1454,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         flux = mk(fxy.x, fxy.y, fzr.x);
         r2 = fzr.y;
       }
+#endif  // PPM_GATE2
 #if PPM_PRIO
       if (tid < 64) __builtin_amdgcn_s_setprio(0);
 #endif
@@ -1301,7 +1484,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   const unsigned long long tot = wave_sum(applied);
   if (stats && (tid & 63) == 0 && tot) atomicAdd(&stats[3], tot);
   if (stats && tid == 0) {  // the pass's work: (tile, deposit) pairs filtered, candidates
-    atomicAdd(&stats[6], (unsigned long long)(le - ls));
+    atomicAdd(&stats[6], visits);
     atomicAdd(&stats[16], cands);
   }
   if (stats && S.diag == 2 && tid == 0) {  // experiment counters: windows, longest tile
@@ -1454,12 +1637,19 @@ hipError_t launch_group_update(const PScene& S, const PHitPoint* hps, const int*
                                const int* gstart, const int2* tiles, int ntiles,
                                const int* list_start, const int* list_end, const float4* pos,
                                const PDeposit* dense, const float* rrtab, int nrr,
-                               float4* state, unsigned* nupd, unsigned long long* stats,
-                               hipStream_t st) {
+                               float4* state, unsigned* nupd, const long long* cofs,
+                               float4* cbuf, unsigned long long* stats, hipStream_t st) {
   if (ntiles <= 0) return hipSuccess;
   hipLaunchKernelGGL(group_update_kernel, dim3(ntiles), dim3(kUpdThreads), 0, st, S, hps, perm,
                      gstart, tiles, list_start, list_end, pos, dense, rrtab, nrr, state, nupd,
-                     stats);
+                     cofs, cbuf, stats);
+  return hipGetLastError();
+}
+hipError_t launch_tile_compact_need(const int2* tiles, int ntiles, const int* list_start,
+                                    const int* list_end, long long min_len, int shift,
+                                    long long* need, hipStream_t st) {
+  hipLaunchKernelGGL(tile_compact_need_kernel, dim3(blocks_for(ntiles + 1)), dim3(kThreads), 0, st,
+                     tiles, ntiles, list_start, list_end, min_len, shift, need);
   return hipGetLastError();
 }
 hipError_t launch_density(const PHitPoint* hps, const float4* state, const int* pix_offsets,

@@ -26,7 +26,8 @@
 extern "C" {
 #endif
 
-#define CENG795_PPM_ABI_VERSION 3  /* 2: ppm_set_batching; 3: update-pass work in ppm_stats */
+#define CENG795_PPM_ABI_VERSION 4  /* 2: ppm_set_batching; 3: update-pass work in ppm_stats;
+                                     4: tile-list compaction (setter + counters) */
 
 typedef struct ppm_scene ppm_scene;
 
@@ -43,6 +44,10 @@ typedef struct ppm_stats {
    * kernel summed over the photon batches since the last collection */
   long long update_deposit_visits, update_candidates, update_launches;
   double update_ms;
+  /* tiles whose deposit list was compacted before the windows (ppm_set_update_compaction),
+   * tiles whose copy did not fit its scratch range (they ran over the full list), and the
+   * deposits the compacted tiles kept */
+  long long update_compacted_tiles, update_compaction_fallbacks, update_compacted_deposits;
 } ppm_stats;
 
 int ppm_abi_version(void);
@@ -67,6 +72,11 @@ int ppm_set_seed(ppm_scene* scene, unsigned long long seed);
  * max_updates: (hit-point group, deposit) pairs one batch may expand to (0 = 2^31 - 1, the
  * limit of the 32-bit sort); a batch that would exceed it is traced again as two halves. */
 int ppm_set_batching(ppm_scene* scene, long long slot_bytes, long long max_updates);
+/* Update-pass tile-list compaction (no effect on results): a hit-point tile whose group's
+ * deposit list holds at least min_list deposits first copies, in photon order, the deposits
+ * within the radius its hit points have when the pass starts, then streams that copy.
+ * min_list: -1 = the default (65536, or CENG795_PPM_COMPACT), 0 = off. */
+int ppm_set_update_compaction(ppm_scene* scene, long long min_list);
 /* reset_hash_grid + eye_trace_lines over all rows: builds the hit points. */
 int ppm_eye_pass(ppm_scene* scene, int camera);
 /* build_hash_grid; info8 (nullable) receives {initial radius, hash scale, grid bbox min xyz,

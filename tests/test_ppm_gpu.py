@@ -119,3 +119,35 @@ def test_batching_arguments_are_checked(ppm, scene_dir):
         with pytest.raises(ppm.RTError):
             g.set_batching(0, -5)
         g.set_batching(0, 0)
+
+
+@pytest.mark.parametrize("name", list(scenes.PPM))
+@pytest.mark.parametrize("min_list", [1, 256, 0])
+def test_update_compaction_matches_oracle(ppm, scene_dir, name, min_list):
+    """Tile-list compaction (update-pass phase (0)): tiles whose group list holds >= min_list
+    deposits stream a photon-order copy of the deposits their hit points can reach; tiles
+    whose copy overflows its scratch range (a quarter of the list) fall back to the full list.
+    Either way the bits are the oracle's.  min_list 0 is the uncompacted pass."""
+    xml = scenes.write_ppm(name, scene_dir)
+    o = OraclePPM(xml)
+    with ppm.PhotonScene(xml, seed=4) as g:
+        g.set_update_compaction(min_list)
+        g.set_batching(256 << 10, 0)  # several batches: later ones start from shrunken radii
+        c = g.camera(0)
+        g.eye_trace_lines(0)
+        g.build_hash_grid(c.width, c.height)
+        o.eye_pass(0, seed=4)
+        o.build_hash_grid(c.width, c.height)
+        g.trace_photons(0, 20000)
+        ost = o.trace_photons(4, 0, 20000)
+        got, want = g.hit_state(), o.hit_state()
+        assert np.array_equal(bits(got), bits(want)), \
+            f"{(bits(got) != bits(want)).any(1).sum()} of {len(want)} hit points differ"
+        st = g.collect_stats()
+        assert st.updates == ost.updates
+        if min_list == 0:
+            assert st.update_compacted_tiles == st.update_compaction_fallbacks == 0
+        if min_list == 1:
+            assert st.update_compacted_tiles > 0, "no tile took the compacted path"
+        with pytest.raises(ppm.RTError):
+            g.set_update_compaction(-2)
