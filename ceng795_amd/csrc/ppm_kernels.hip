@@ -853,11 +853,19 @@ __device__ __forceinline__ float radius_reduction(unsigned n) {
   return (float)((double)(nf + kAlpha) / ((double)nf + 1.0));
 }
 
-// Tile-list compaction (the update kernel's first phase for long lists): a tile whose group
-// list holds at least `min_len` deposits gets a scratch range of L >> shift records; the kernel
-// copies into it, in photon order, the deposits within the radius any of its hit points has
-// at the kernel start, and streams its windows over that instead.  need[ntiles] = 0 closes the
-// exclusive scan that turns the sizes into offsets.
+// Tile-list compaction (group_update_kernel phase (0) for long lists): a tile whose group
+// list holds at least `min_len` deposits takes it in segments of kCompactSeg and gets a scratch
+// range of kCompactSeg >> shift records; per segment the kernel copies into it, in photon
+// order, the deposits within the radius any of its hit points has at the segment start, and
+// streams its windows over that copy (over the segment itself when the copy overflows).
+// need[ntiles] = 0 closes the exclusive scan that turns the sizes into offsets.
+#ifndef PPM_SEG
+#define PPM_SEG 32768
+#endif
+#ifndef PPM_CPER
+#define PPM_CPER 4
+#endif
+constexpr int kCompactSeg = PPM_SEG;
 __global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tiles, int ntiles,
                                                                 const int* list_start,
                                                                 const int* list_end,
@@ -871,7 +879,7 @@ __global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tile
   }
   const int g = tiles[t].x;
   const long long L = list_end[g] - list_start[g];
-  need[t] = L >= min_len ? (L >> shift) : 0;
+  need[t] = L >= min_len ? ((L < kCompactSeg ? L : (long long)kCompactSeg) >> shift) : 0;
 }
 
 __global__ __launch_bounds__(256) void rr_table_kernel(float* rr, int n) {
@@ -907,10 +915,11 @@ __global__ __launch_bounds__(256) void materialize_kernel(const unsigned* pkey, 
 //      the running value, r^2 *= rr(n), n++, flux = (flux + color * photon_flux) * rr(n) —
 //      repeated when two of its cells share the deposit's bucket.
 // The next window is fetched (coalesced) while the current one is processed.
-// A tile with a compaction range (cofs[t] < cofs[t+1], tile_compact_need_kernel) first copies
-// the deposits its hit points can reach with their radius at the kernel start — a superset of
-// what any window's filter passes, by the same argument, with the same d2 arithmetic — and
-// runs its windows over that copy; if the copy would not fit, over the full list as before.
+// A tile with a compaction range (cofs[t] < cofs[t+1], tile_compact_need_kernel) takes its list
+// in segments and first copies each segment's deposits its hit points can reach with their
+// radius at the segment start — a superset of what any of its windows' filters passes, by the
+// same argument, with the same d2 arithmetic — then runs the windows over that copy (over the
+// segment itself if the copy would not fit).
 __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM_WPE, PPM_WPE))) void group_update_kernel(
     PScene S, const PHitPoint* hps, const int* perm, const int* gstart, const int2* tiles,
     const int* list_start, const int* list_end, const float4* pos, const PDeposit* dense,
@@ -968,9 +977,8 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   }
   unsigned long long applied = 0, cands = 0;
   unsigned long long d_max = 0, d_unstaged = 0;  // diag: per hit point, flushed once per tile
-  int ls = list_start[g], le = list_end[g];
-  unsigned long long visits = (unsigned long long)(le - ls);  // 16-B records the filters read
-  const float4* src = pos;
+  const int list_s = list_start[g], list_e = list_end[g];
+  unsigned long long visits = 0, windows = 0;  // 16-B records the filters read; windows run
   __syncthreads();
   V tp[kTileHP], tn[kTileHP];
 #pragma unroll
@@ -978,12 +986,30 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     tp[j] = mk(s_hp[j][0], s_hp[j][1], s_hp[j][2]);
     tn[j] = mk(s_hp[j][3], s_hp[j][4], s_hp[j][5]);
   }
-  if (cofs && cofs[blockIdx.x + 1] > cofs[blockIdx.x]) {
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tp0 = 0;
+#define PPM_PHASE(i)                                              \
+  if (S.diag == 2 && tid == 0) {                                  \
+    const unsigned long long t1 = wall_clock64();                 \
+    ph[i] += t1 - tp0;                                            \
+    tp0 = t1;                                                     \
+  }
+  if (S.diag == 2 && tid == 0) tp0 = wall_clock64();
+  // A compacted tile takes its list in segments of kCompactSeg; each segment is first copied,
+  // in photon order, down to the deposits within the radius its hit points have at the
+  // segment start (its windows' filters could pass no others: the radius only shrinks).
+  const bool compact = cofs && cofs[blockIdx.x + 1] > cofs[blockIdx.x];
+  const int seg_len = compact ? kCompactSeg : max(1, list_e - list_s);
+  for (int seg = list_s; seg < list_e; seg += seg_len) {
+  const int seg_e = min(seg + seg_len, list_e);
+  int ls = seg, le = seg_e;
+  const float4* src = pos;
+  visits += (unsigned long long)(seg_e - seg);
+  if (compact) {
     // (0) compaction: rounds of 64 records per thread-row; one count per (record row, wave),
     // scanned by wave 0, keeps the copy in photon order
     constexpr int kCW = kUpdThreads / 64;
-    constexpr int kCPer = 64 / kCW;
-    static_assert(kCPer * kCW == 64, "one count per lane of the scanning wave");
+    constexpr int kCPer = PPM_CPER;  // records per thread per round (registers: 8 spill)
+    static_assert(kCPer * kCW <= 64, "one count per lane of the scanning wave");
     __shared__ int s_cc[64], s_cp[65];
     const long long c0 = cofs[blockIdx.x];
     const int cap = (int)(cofs[blockIdx.x + 1] - c0);
@@ -1026,7 +1052,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
       }
       __syncthreads();
       if (tid < 64) {
-        const int v = s_cc[tid];
+        const int v = tid < kCPer * kCW ? s_cc[tid] : 0;
         int x = v;
         for (int o = 1; o < 64; o <<= 1) {
           const int y = __shfl_up(x, o, 64);
@@ -1048,14 +1074,14 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     if (kept <= cap) {
       src = dst, ls = 0, le = kept;
       visits += (unsigned long long)kept;
-    } else {
-      visits += (unsigned long long)(le - ls);
     }
     if (stats && tid == 0) {
       atomicAdd(&stats[kept <= cap ? 20 : 21], 1ull);
       atomicAdd(&stats[22], (unsigned long long)kept);
     }
+    PPM_PHASE(0)
   }
+  windows += (unsigned long long)((le - ls + kWinMax - 1) / kWinMax);
   float4 dep[kPer];  // position, photon-order index << kRepBits | multiplicity
   auto fetch = [&](int base) {
 #pragma unroll
@@ -1065,14 +1091,6 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     }
   };
   fetch(ls);
-  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tp0 = 0;
-#define PPM_PHASE(i)                                              \
-  if (S.diag == 2 && tid == 0) {                                  \
-    const unsigned long long t1 = wall_clock64();                 \
-    ph[i] += t1 - tp0;                                            \
-    tp0 = t1;                                                     \
-  }
-  if (S.diag == 2 && tid == 0) tp0 = wall_clock64();
   for (int base = ls; base < le; base += kWinMax) {
     const int total = min(kWinMax, le - base);
     const int nwords = (total + 31) >> 5;
@@ -1473,6 +1491,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     __syncthreads();
     PPM_PHASE(5)
   }
+  }  // segments
   if (h >= 0) {
     state[h] = make_float4(flux.x, flux.y, flux.z, r2);
     nupd[h] = cnt;
@@ -1488,11 +1507,11 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     atomicAdd(&stats[16], cands);
   }
   if (stats && S.diag == 2 && tid == 0) {  // experiment counters: windows, longest tile
-    atomicAdd(&stats[5], (unsigned long long)((le - ls + kWinMax - 1) / kWinMax));
+    atomicAdd(&stats[5], windows);
     atomicMax(&stats[7], wall_clock64() - t_start);  // longest tile, in wall-clock ticks
     for (int i = 0; i < 6; i++) atomicMax(&stats[8 + i], ph[i]);
     atomicMax(&stats[17], cands);  // most candidates in one tile
-    atomicMax(&stats[19], (unsigned long long)((le - ls + kWinMax - 1) / kWinMax));
+    atomicMax(&stats[19], windows);
   }
   if (stats && S.diag == 2 && (tid & 63) == 0 && tot) atomicMax(&stats[18], tot);  // (per wave)
 #undef PPM_PHASE
