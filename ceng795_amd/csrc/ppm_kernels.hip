@@ -718,9 +718,6 @@ __global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, con
 #ifndef PPM_WIN
 #define PPM_WIN 2048
 #endif
-#ifndef PPM_GATE2
-#define PPM_GATE2 0  // fixed-width gate bodies of PPM_GATE2 candidates (0: batches of PPM_GATE_B)
-#endif
 #ifndef PPM_GATE_B
 #define PPM_GATE_B 3
 #endif
@@ -729,9 +726,6 @@ __global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, con
 #endif
 #ifndef PPM_CHUNK
 #define PPM_CHUNK 1024
-#endif
-#ifndef PPM_KGATE
-#define PPM_KGATE 0  // two-stage gate: exact, measured slower
 #endif
 #ifndef PPM_PRIO
 #define PPM_PRIO 1
@@ -928,6 +922,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   constexpr int kPer = kWinMax / kUpdThreads;
   constexpr int kWords = kWinMax / 32;
   constexpr int kChunk = PPM_CHUNK;  // candidates per color / apply round
+  constexpr int kPerHp = kChunk / kTileHP;  // ... per hit point
   static_assert(kWinMax % kUpdThreads == 0 && kWinMax % 64 == 0, "whole waves per window");
   static_assert(kTileHP * kWords <= kUpdThreads, "one thread per mask word in the scan");
   __shared__ float s_hp[kTileHP][12];  // pos, normal, w_o, attenuation
@@ -943,15 +938,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   // multiplicity exceeds 1 (sign bit: the gate's scalar path), +inf when its normal fails
   __shared__ float4 s_ccf[kChunk];
   constexpr int kRRStage = PPM_RR_STAGE;  // rr(n) staged per hit point per window (more: computed inline)
-  __shared__ float s_rr[kTileHP][kRRStage];
-#if PPM_KGATE
-  // two-stage gate (see (3a)): per hit point the radius^2 after a accepts in this window,
-  // the accepted candidates in order, and per candidate the last accept count it passes at
-  __shared__ float s_R[kTileHP][kRRStage + 1];
-  __shared__ unsigned short s_app[kTileHP][kRRStage + 1];
-  __shared__ short s_K[kChunk];
-  __shared__ int s_extra[kTileHP], s_L[kTileHP];
-#endif
+  __shared__ __attribute__((aligned(16))) float s_rr[kTileHP][kRRStage];
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const unsigned long long t_start = S.diag == 2 ? wall_clock64() : 0;
   const int2 tile = tiles[blockIdx.x];
@@ -1095,9 +1082,6 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     const int total = min(kWinMax, le - base);
     const int nwords = (total + 31) >> 5;
     // stage rr(n) for the updates this window can make
-#if PPM_KGATE
-    if (tid < kTileHP) s_extra[tid] = 0;
-#endif
     for (int e = tid; e < nh * kRRStage; e += kUpdThreads) {
       const int j = e / kRRStage, t = e % kRRStage;
       const unsigned n = s_cnt[j] + (unsigned)t;
@@ -1162,9 +1146,6 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         const int idx = s_wc[j * nwords + w] + __builtin_popcount(s_mask[j][w] & ((1u << (k & 31)) - 1u));
         s_ck[idx] = rp[q];
         s_cd2[idx] = d2r[q][j];
-#if PPM_KGATE
-        if ((rp[q] & kRepMask) > 1u) atomicAdd(&s_extra[j], (int)(rp[q] & kRepMask) - 1);
-#endif
       }
     }
     __syncthreads();
@@ -1174,49 +1155,18 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     const int my_beg = h >= 0 ? s_wc[tid * nwords] : 0;
     const int my_end = h >= 0 ? (tid + 1 < nh ? s_wc[(tid + 1) * nwords] : ncand) : 0;
     const unsigned cnt_w = cnt;  // count at the window start: rr(n) is staged from there
-#if PPM_KGATE
-    // (3a) Two-stage gate.  The radius^2 after a accepts in this window does not depend on
-    // WHICH candidates were accepted: R(0) = r^2 at the window start, R(a+1) = R(a) * rr(n+a)
-    // (the gate's own fp32 product; r^2 + 0 = r^2).  R is non-increasing (rr < 1), so a
-    // candidate with distance^2 d2 passes at accept count a iff a <= K = max{a : d2 <= R(a)}.
-    // One lane per hit point tabulates R up to its most possible accepts in this window (its
-    // candidates' multiplicities summed); the color phase finds every candidate's K by binary
-    // search; the gate then runs two short chains: integer acceptance (a += a <= K), and the
-    // flux recurrence over the accepted candidates only.  A hit point whose possible accepts
-    // exceed the staged rr(n) takes the one-stage path below for this window.
-    bool tabled = false;
-    if (h >= 0) {
-      const int napp = (my_end - my_beg) + s_extra[tid];
-      tabled = napp <= kRRStage && S.diag != 1;
-      s_L[tid] = tabled ? napp : -1;
-      if (tabled) {  // one multiply per step; the rr(n) loads go 8 at a time, off the chain
-        float R = r2;
-        s_R[tid][0] = R;
-        int a = 0;
-        for (; a + 8 <= napp; a += 8) {
-          float rb[8];
-#pragma unroll
-          for (int k = 0; k < 8; k++) rb[k] = s_rr[tid][a + k];
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            R = R * rb[k];
-            s_R[tid][a + k + 1] = R;
-          }
-        }
-        for (; a < napp; a++) {
-          R = R * s_rr[tid][a];
-          s_R[tid][a + 1] = R;
-        }
-      }
-    }
-    __syncthreads();
-    int acc_n = 0;  // accepts so far in this window (tabled hit points)
-#endif
-    for (int c0 = 0; c0 < ncand; c0 += kChunk) {
-      // (3) color * photon_flux for candidates [c0, c0 + kChunk)
-      for (int e = c0 + tid; e < min(ncand, c0 + kChunk); e += kUpdThreads) {
-        int j = 0;
-        while (j + 1 < nh && s_wc[(j + 1) * nwords] <= e) j++;
+    unsigned rbase = cnt_w;      // the gate lane's staged rr(n) start (restaged in the gate)
+    // Rounds of up to kPerHp candidates of EVERY hit point, so that the gate lanes run side by
+    // side however the window's candidates are spread over the tile's hit points.
+    int most = 0;
+    for (int j = 0; j < nh; j++)
+      most = max(most, (j + 1 < nh ? s_wc[(j + 1) * nwords] : ncand) - s_wc[j * nwords]);
+    for (int c0 = 0; c0 < most; c0 += kPerHp) {
+      // (3) color * photon_flux for candidates [c0, c0 + kPerHp) of each hit point
+      for (int x = tid; x < nh * kPerHp; x += kUpdThreads) {
+        const int j = x / kPerHp;
+        const int e = s_wc[j * nwords] + c0 + (x - j * kPerHp);
+        if (e >= (j + 1 < nh ? s_wc[(j + 1) * nwords] : ncand)) continue;
         const PDeposit d = dense[s_ck[e] >> kRepBits];
         const V hn = tn[j], w_i = ld(d.w_i), pf = ld(d.flux);
         const PMaterial& m = S.materials[s_mat[j]];
@@ -1224,23 +1174,6 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         // Scene.cpp:136: a deposit whose normal fails the test never updates the hit point
         const bool normal_ok = dot(hn, ld(d.normal)) > 1e-3f;
         if (!normal_ok) s_cd2[e] = kInf;
-#if PPM_KGATE
-        {
-          int K = -1;
-          const int L = s_L[j];
-          if (normal_ok && L >= 0) {  // d2 <= R(0): the filter used the window-start radius
-            const float d2 = s_cd2[e];
-            int lo = 0, hi = L;
-            while (lo < hi) {
-              const int mid = (lo + hi + 1) >> 1;
-              if (d2 <= s_R[j][mid]) lo = mid;
-              else hi = mid - 1;
-            }
-            K = lo;
-          }
-          s_K[e - c0] = (short)K;
-        }
-#endif
         if (normal_ok && m.brdf_id == -1) {
           const float cos_i = dot(hn, w_i);
           if (!(cos_i > 1.0f || cos_i <= 0.0f)) {
@@ -1252,7 +1185,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         }
         const V cf = color * pf;
         const float d2c = !normal_ok ? kInf : ((s_ck[e] & kRepMask) > 1u ? -s_cd2[e] : s_cd2[e]);
-        s_ccf[e - c0] = make_float4(cf.x, cf.y, cf.z, d2c);
+        s_ccf[x] = make_float4(cf.x, cf.y, cf.z, d2c);
       }
       __syncthreads();
       PPM_PHASE(4)
@@ -1270,162 +1203,31 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
 #if PPM_PRIO
       if (tid < 64) __builtin_amdgcn_s_setprio(3);  // the gate wave is the tile's critical path
 #endif
-#if PPM_KGATE
-      if (tabled) {
-        const int e0 = max(my_beg, c0) - c0, e1 = min(my_end, c0 + kChunk) - c0;
-        const int a0 = acc_n;
-        int a = a0;
-        // acceptance: a candidate is applied while a <= K, at most its multiplicity times
-        constexpr int kU = 8;
-        int e = e0;
-        for (; e + kU <= e1; e += kU) {
-          unsigned w[kU];
-          int Kb[kU];
-          unsigned rep_or = 0;
-#pragma unroll
-          for (int k = 0; k < kU; k++) w[k] = s_ck[c0 + e + k], Kb[k] = s_K[e + k];
-#pragma unroll
-          for (int k = 0; k < kU; k++) rep_or |= w[k] & kRepMask;
-          if (rep_or <= 1u) {  // every multiplicity 1: the chain is a += (a <= K)
-#pragma unroll
-            for (int k = 0; k < kU; k++) {
-              s_app[tid][a] = (unsigned short)(e + k);  // kept only if accepted
-              a += a <= Kb[k] ? 1 : 0;
-            }
-          } else {
-#pragma unroll
-            for (int k = 0; k < kU; k++) {
-              const int m = (int)(w[k] & kRepMask);
-              const int n = a <= Kb[k] ? min(m, Kb[k] + 1 - a) : 0;
-              for (int i = 0; i < n; i++) s_app[tid][a + i] = (unsigned short)(e + k);
-              a += n;
-            }
-          }
-        }
-        for (; e < e1; e++) {
-          const int m = (int)(s_ck[c0 + e] & kRepMask), K = s_K[e];
-          const int n = a <= K ? min(m, K + 1 - a) : 0;
-          for (int i = 0; i < n; i++) s_app[tid][a + i] = (unsigned short)e;
-          a += n;
-        }
-        // the flux recurrence over this chunk's accepts: flux = (flux + color*flux_p) * rr(n)
-        f32x2 fxy = {flux.x, flux.y}, fz0 = {flux.z, 0.0f};
-        int i = a0;
-        for (; i + kU <= a; i += kU) {
-          float4 cb[kU];
-          float rb[kU];
-#pragma unroll
-          for (int k = 0; k < kU; k++) cb[k] = s_ccf[s_app[tid][i + k]], rb[k] = s_rr[tid][i + k];
-#pragma unroll
-          for (int k = 0; k < kU; k++) {
-            const f32x2 rr2 = {rb[k], rb[k]};
-            const f32x2 cxy = {cb[k].x, cb[k].y}, cz0 = {cb[k].z, 0.0f};
-            fxy = (fxy + cxy) * rr2;
-            fz0 = (fz0 + cz0) * rr2;
-          }
-        }
-        for (; i < a; i++) {
-          const float4 c = s_ccf[s_app[tid][i]];
-          const float rr = s_rr[tid][i];
-          const f32x2 rr2 = {rr, rr};
-          const f32x2 cxy = {c.x, c.y}, cz0 = {c.z, 0.0f};
-          fxy = (fxy + cxy) * rr2;
-          fz0 = (fz0 + cz0) * rr2;
-        }
-        flux = mk(fxy.x, fxy.y, fz0.x);
-        r2 = s_R[tid][a];
-        cnt = cnt_w + (unsigned)a;
-        acc_n = a;
-      } else
-#endif
-#if PPM_GATE2
-      if (h >= 0 && S.diag != 1) {
-        // Fixed-width gate: every body applies exactly kG candidates (the tail padded with
-        // +inf, which is never accepted), so the next body's records are read from LDS while
-        // this one runs.  Per candidate the new state is computed unconditionally with the rr
-        // at the head of a register queue (rr(n) for the next accept), then kept or dropped by
-        // the acceptance test; an accept shifts the queue.  r^2's chain is multiply -> select,
-        // the acceptance test runs beside the multiply.  A body holding a multiplicity > 1, or
-        // reaching past the staged rr(n), takes the scalar path for its first candidate.
-        constexpr int kG = PPM_GATE2;
-        const int e1 = min(my_end, c0 + kChunk);
-        f32x2 fxy = {flux.x, flux.y}, fzr = {flux.z, r2};
-        int e = max(my_beg, c0);
-        float4 nb[kG];
-        int pf = -1;  // the candidate index nb was read from
-        while (e < e1) {
-          if (pf != e) {
-#pragma unroll
-            for (int k = 0; k < kG; k++) nb[k] = s_ccf[min(e + k, e1 - 1) - c0];
-          }
-          float4 cb[kG];
-#pragma unroll
-          for (int k = 0; k < kG; k++) cb[k] = nb[k];
-          const int n = min(kG, e1 - e);
-          const unsigned t = cnt - cnt_w;
-          float rq[kG];
-#pragma unroll
-          for (int k = 0; k < kG; k++) rq[k] = s_rr[tid][min(t + (unsigned)k, (unsigned)kRRStage - 1)];
-#pragma unroll
-          for (int k = 0; k < kG; k++) nb[k] = s_ccf[min(e + n + k, e1 - 1) - c0];  // next body
-          pf = e + n;
-          unsigned sgn = 0;
-#pragma unroll
-          for (int k = 0; k < kG; k++) sgn |= k < n ? __float_as_uint(cb[k].w) : 0u;
-          if ((sgn >> 31) == 0u && t + kG <= (unsigned)kRRStage) {
-#pragma unroll
-            for (int k = 0; k < kG; k++) {
-              const float d2 = k < n ? cb[k].w : kInf;
-              const f32x2 rr2 = {rq[0], rq[0]};
-              const f32x2 cxy = {cb[k].x, cb[k].y}, cz0 = {cb[k].z, 0.0f};
-              const f32x2 nxy = (fxy + cxy) * rr2, nzr = (fzr + cz0) * rr2;
-              const bool acc = d2 <= fzr.y;
-              fxy.x = acc ? nxy.x : fxy.x;
-              fxy.y = acc ? nxy.y : fxy.y;
-              fzr.x = acc ? nzr.x : fzr.x;
-              fzr.y = acc ? nzr.y : fzr.y;
-              cnt += acc ? 1u : 0u;
-#pragma unroll
-              for (int i = 0; i + 1 < kG - k; i++) rq[i] = acc ? rq[i + 1] : rq[i];
-            }
-            e += n;
-          } else {
-            const float d2 = __builtin_fabsf(cb[0].w);
-            if (d2 <= fzr.y) {
-              const unsigned reps = s_ck[e] & kRepMask;
-              const f32x2 cxy = {cb[0].x, cb[0].y}, cz0 = {cb[0].z, 0.0f};
-              unsigned r = 0;
-              do {
-                const unsigned tt = cnt - cnt_w;
-                const float rr = tt < (unsigned)kRRStage ? s_rr[tid][tt] : radius_reduction(cnt);
-                cnt++;
-                const f32x2 rr2 = {rr, rr};
-                fxy = (fxy + cxy) * rr2;
-                fzr = (fzr + cz0) * rr2;
-              } while (++r < reps && d2 <= fzr.y);
-            }
-            e++;
-          }
-        }
-        flux = mk(fxy.x, fxy.y, fzr.x);
-        r2 = fzr.y;
-      }
-#else
       if (h >= 0 && S.diag != 1) {
         constexpr int kB = PPM_GATE_B;
-        const int e1 = min(my_end, c0 + kChunk);
+        const int e1 = min(my_end, my_beg + c0 + kPerHp);
+        const int cbase = my_beg + c0 - tid * kPerHp;  // candidate e's record: s_ccf[e - cbase]
         f32x2 fxy = {flux.x, flux.y}, fzr = {flux.z, r2};
-        int e = max(my_beg, c0);
+        int e = my_beg + c0;
         while (e < e1) {
+          // a window with more updates than the staged rr(n) (long compacted windows): the
+          // lane restages its own row from the table, from a 16-B aligned count
+          if (cnt - rbase + kB > (unsigned)kRRStage && (cnt & ~3u) + kRRStage <= (unsigned)nrr) {
+            rbase = cnt & ~3u;
+            const float4* rt = reinterpret_cast<const float4*>(rrtab + rbase);
+            float4* row = reinterpret_cast<float4*>(&s_rr[tid][0]);
+#pragma unroll 8
+            for (int i = 0; i < kRRStage / 4; i++) row[i] = rt[i];
+          }
           const int nb = min(kB, e1 - e);
-          const unsigned t = cnt - cnt_w;
+          const unsigned t = cnt - rbase;
           bool fast = t + kB <= (unsigned)kRRStage;
           float d2b[kB], rrb[kB];
           float4 cb[kB];
 #pragma unroll
           for (int k = 0; k < kB; k++) {  // one 16-B record per candidate (+ its staged rr)
             const int ek = min(e + k, e1 - 1);
-            cb[k] = s_ccf[ek - c0];
+            cb[k] = s_ccf[ek - cbase];
             rrb[k] = s_rr[tid][min(t + (unsigned)k, (unsigned)kRRStage - 1)];
           }
 #pragma unroll
@@ -1458,7 +1260,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
               const f32x2 cxy = {cb[0].x, cb[0].y}, cz0 = {cb[0].z, 0.0f};
               unsigned r = 0;
               do {
-                const unsigned tt = cnt - cnt_w;
+                const unsigned tt = cnt - rbase;
                 const float rr = tt < (unsigned)kRRStage ? s_rr[tid][tt] : radius_reduction(cnt);
                 cnt++;
                 const f32x2 rr2 = {rr, rr};
@@ -1472,7 +1274,6 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         flux = mk(fxy.x, fxy.y, fzr.x);
         r2 = fzr.y;
       }
-#endif  // PPM_GATE2
 #if PPM_PRIO
       if (tid < 64) __builtin_amdgcn_s_setprio(0);
 #endif
