@@ -12,11 +12,15 @@
 //                            deposit {x, n, w_i, flux} in the photon's slot row.
 //   deposit_keys_kernel      compacts the deposits in (photon, bounce) order and keys each by
 //                            the hash bucket of its cell (Scene.cpp:125-130).
-//   (hipcub stable radix sort by bucket -> per-bucket deposit runs in photon order)
+//   expand_* / materialize   every deposit into each hit-point group filed under its bucket
+//                            (hit points covering the same cells form a group); a stable
+//                            radix sort by group gives each group its deposit list in photon
+//                            order, materialised as 16-B position records.
 //   group_update_kernel      the radius / flux updates of Scene.cpp:131-168, turned inside out:
-//                            hit points filed under the same buckets form a group; one wave per
-//                            group merges those buckets' deposit runs in photon order through
-//                            LDS and each lane applies them to its own hit point.
+//                            one workgroup per tile of a group's hit points streams the list in
+//                            windows (superset filter, candidates in photon order, colour
+//                            terms), one lane per hit point applies the exact recurrence; long
+//                            lists are first compacted segment by segment.
 //   density_kernel           density_estimation + Pixel::get_color (Scene.cpp:363-371).
 //
 // Why the update pass is exact: a photon's path never reads hit-point state, so the reference's
