@@ -4,19 +4,20 @@ the ~1M-triangle height field (BASELINE.json configs[2], "C3"), plus the rooflin
 dominant kernel and the reference CPU path timed on this box's host cores.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-    python bench.py --workload c5        (photon mapping, tools/bench_ppm.py)
+    python bench.py --workload c5        (photon mapping alone, tools/bench_ppm.py)
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
-    ... bench.py --workload c4 --frames 1  (one 3840x2160 frame split over the N ranks)
 
-One step = one full render of every camera in the job.  By default the job has one 1920x1080
-frame per rank (N frames for N ranks, "scaling": "weak"); `--frames F` fixes the job at F
-frames instead (`--frames 1`: one frame split over all ranks, "scaling": "strong", and rank 0
-also times the same frame rendered alone to report t1 / (N * tN)).  The 8x8-pixel tiles of all
-frames are dealt round-robin over the ranks (the reference deals rows round-robin over
-threads, HW2/main.cpp:33-36), each rank renders its tiles into HBM in `--chunks` pieces per
-frame, and each piece is gathered to rank 0 over RCCL (torch.distributed "nccl" = RCCL over
-xGMI) while the next one renders; rank 0 untiles the framebuffers.  At N = 1 the step is
-exactly one C3 frame rendered in place.
+One step = one full render of every camera in the job (default: one 1920x1080 C3 frame).
+`--gpus N` with N > 1 and no launcher starts N rank processes itself (torch.distributed.run,
+before any GPU call).  N = 1: the step is one C3 frame rendered in place, `--inflight`
+consecutive steps on as many streams.  N > 1 (default `--split tiles`): the frame's 8x8-pixel
+tiles are dealt round-robin over the ranks (the reference deals rows round-robin over threads,
+HW2/main.cpp:33-36), each rank renders its share tile-major into HBM, and the shares are
+gathered to rank 0 over RCCL (torch.distributed "nccl" = RCCL over xGMI) and untiled there,
+with `--inflight` steps in flight per rank ("scaling": "strong"); rank 0 also times the same
+frame rendered alone to report t1 / (N * tN), and the line carries a weak-scaling measurement
+(one whole frame per rank per step) as an extra key.  At N = 1 the line also carries the C5
+photon-mapping benchmark (tools/bench_ppm.py) as a `c5` sub-object.
 
 Printed by rank 0: ONE JSON line (see the contract in the task statement).
 """
@@ -242,7 +243,8 @@ def roofline_line(xml, world, local_share, kt, launches, prof, kt_iso=None, n_is
     prim_ms = kt["primary"] / max(1, launches)
     achieved = per_launch / (prim_ms * 1e-3) / 1e9
     c = work["counters"]
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+    roof = {"bound": "latency", "peak_of": "hbm", "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
             "kernel": "trace_primary_kernel",
             "kernel_ms_avg": round(prim_ms, 4),
@@ -286,45 +288,156 @@ def roofline_line(xml, world, local_share, kt, launches, prof, kt_iso=None, n_is
     return roof
 
 
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def relaunch(n: int) -> int:
+    """`--gpus N` (N > 1) without a launcher: start N rank processes with torch.distributed.run
+    (one per GPU, rendezvous on 127.0.0.1) as a child process and exit with its code.  Called
+    before anything touches the GPU; rank 0 prints the JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__),
+           *sys.argv[1:]]
+    log(f"--gpus {n} without WORLD_SIZE: launching {n} ranks: {' '.join(cmd[1:6])} ...")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL (see Environment)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def timed_steps(renderer, steps: int, world: int, coll_dev: str, events=None):
+    """Barrier + synchronize, EXACTLY `steps` renderer steps, finish + synchronize + barrier;
+    returns the max over ranks of the wall time (s)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        renderer.step(events=events[k] if events else None)
+    renderer.finish()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=coll_dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    return float(el.item())
+
+
+def synthetic_frame(w: int, h: int, seed: int = 795):
+    """Stand-in framebuffer for the CPU rehearsal: deterministic fp32 values per pixel."""
+    import numpy as np
+    return np.random.default_rng(seed).standard_normal((h, w, 3)).astype(np.float32)
+
+
+def cpu_rehearsal(args) -> int:
+    """The N>1 default path with no GPU (gloo, host tensors): the frame's tiles dealt over the
+    ranks, each rank's share written tile-major into its slot (cut from a synthetic frame
+    instead of rendered), the pipelined TileGatherRenderer exchange, rank 0's untile and a
+    bit-for-bit check against the synthetic frame.  For the multi-rank CPU tests of the
+    launcher and the exchange; "value" is pixels per second of that exchange, not Mrays/s."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from ceng795_amd import dist_tiles
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(free_port()))
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    dist.init_process_group("gloo")
+    _, w, h, desc = WORKLOADS[args.workload]
+    truth = synthetic_frame(w, h)
+    L = dist_tiles.TileLayout([(w, h)], world, rank)
+    tx, ty = dist_tiles.tiles_of((w, h))
+    pad = np.zeros((ty * 8, tx * 8, 3), np.float32)
+    pad[:h, :w] = truth
+    tiles = torch.from_numpy(pad.reshape(ty, 8, tx, 8, 3).transpose(0, 2, 1, 3, 4)
+                             .reshape(tx * ty, dist_tiles.TILE_FLOATS).copy())
+    rendered = []
+
+    def render(sh, slot, stream):
+        rendered.append(sh.count)
+        slot[:sh.count].copy_(tiles[sh.tile_begin::sh.tile_step][:sh.count])
+
+    R = dist_tiles.TileGatherRenderer(L, None, render, host_staging=True, device="cpu")
+    for _ in range(args.warmup):
+        R.step()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frames = R.step()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    assert sum(rendered) == (args.warmup + args.steps) * L.local_tiles
+    if rank == 0:
+        ok = bool(np.array_equal(frames[0].numpy().view(np.uint32), truth.view(np.uint32)))
+        print(json.dumps({"metric": "cpu rehearsal of the N>1 exchange (no rendering)",
+                          "value": round(w * h * args.steps / float(el.item()) / 1e6, 3),
+                          "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "scaling": "strong",
+                          "data": "synthetic tiles, cpu-rehearsal",
+                          "config": {"workload": desc, "parallelism": f"tiles{world}+gloo_gather",
+                                     "gather_verified": ok}}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS) + ["c5"],
-                    help="c5: the photon-mapping Cornell box (tools/bench_ppm.py), 1 GPU")
-    ap.add_argument("--traversal", default="fast", choices=["fast", "reference", "cull"])
+                    help="c5: the photon-mapping Cornell box alone (tools/bench_ppm.py), 1 GPU")
+    ap.add_argument("--traversal", default="fast", choices=["fast", "reference"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="N=1: skip the C5 (photon mapping) sub-object of the line")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="gloo: rehearsal of the N>1 path on one GPU (ranks share device 0)")
+                    help="gloo: rehearsal of the N>1 path through host copies")
     ap.add_argument("--no-verify", action="store_true",
                     help="skip rank 0's bit-for-bit check of the gathered frames")
     ap.add_argument("--gather-rehearsal", action="store_true",
-                    help="run the N>1 tile/gather pipeline even at WORLD_SIZE=1 (a one-rank "
+                    help="run the N>1 tile / gather pipeline even at WORLD_SIZE=1 (a one-rank "
                          "process group; exercises the comm-stream gather on one GPU)")
-    ap.add_argument("--frames", type=int, default=0,
-                    help="frames per step (default: one per rank = weak scaling; 1 = one "
-                         "frame split over all ranks = strong scaling)")
-    ap.add_argument("--chunks", type=int, default=0,
-                    help="pieces per frame and rank for the gather pipeline (default 4 when "
-                         "a rank renders one frame's share, else 1)")
+    ap.add_argument("--frames", type=int, default=1,
+                    help="frames (cameras) per step; --split tiles deals their tiles over the "
+                         "ranks (strong scaling at 1 frame), --split frames gives each rank "
+                         "whole frames (default then: one per rank)")
+    ap.add_argument("--split", default="tiles", choices=["tiles", "frames"])
+    ap.add_argument("--no-weak", action="store_true",
+                    help="N>1: skip the extra weak-scaling measurement (one frame per rank)")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--cpu-rehearsal", action="store_true",
+                    help="no GPU: the N>1 tile deal / gather / untile with synthetic tiles over "
+                         "gloo (tests of the launcher and the exchange)")
     ap.add_argument("--inflight", type=int, default=4,
-                    help="frames in flight on one GPU: consecutive steps on that many streams, so "
-                         "one frame's sparsely occupied last waves overlap the next frame (whole-"
-                         "frame modes; 1 = one frame at a time)")
-    ap.add_argument("--tiles", action="store_true",
-                    help="deal 8x8 tiles of every frame round-robin over the ranks even when the "
-                         "job has a frame per rank (the strong-scaling layout; default then: "
-                         "whole frames per rank)")
+                    help="frames in flight per GPU: consecutive steps on that many streams / "
+                         "buffer sets, so one frame's sparsely occupied last waves (and, N>1, "
+                         "its gather) overlap the next frame; 1 = one frame at a time")
     args = ap.parse_args()
     if args.workload == "c5":
-        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.gpus > 1:
             log("c5 (photon mapping) is a one-GPU configuration (BASELINE.json configs[4])")
             return 2
         import bench_ppm
         print(json.dumps(bench_ppm.run(args.steps, args.warmup, not args.no_cpu_baseline)))
         return 0
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return relaunch(args.gpus)
+    if args.cpu_rehearsal:
+        return cpu_rehearsal(args)
 
     import torch
     import torch.distributed as dist
@@ -339,21 +452,24 @@ def main() -> int:
     use_pg = world > 1 or args.gather_rehearsal
     if use_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29577")
+        os.environ.setdefault("MASTER_PORT", str(29577))
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group("gloo")
+    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+    host_staging = args.dist_backend == "gloo"
 
     import ceng795_amd
     from ceng795_amd import dist_tiles
 
-    n_cams = args.frames if args.frames > 0 else world
-    strong = n_cams < world
-    tiled = strong or args.tiles  # else whole frames per rank (FrameOwners)
-    chunks = args.chunks if args.chunks > 0 else (4 if n_cams == 1 and use_pg else 1)
+    if args.split == "frames" and args.frames < world:
+        args.frames = world
+    n_cams = max(1, args.frames)
+    tiled = use_pg and args.split == "tiles"
+    strong = tiled and n_cams < world  # one frame (or a few) split over more ranks
     if rank == 0:
         xml = scene_path(args.workload, n_cams)
     if world > 1:
@@ -364,18 +480,21 @@ def main() -> int:
     log(f"[rank {rank}] scene loaded + uploaded in {time.perf_counter() - t0:.2f} s, "
         f"BVH depth {scene.bvh_depth}")
     stream = torch.cuda.current_stream()
-    if use_pg and not tiled:
+    dev = torch.device("cuda", device)
+    if not use_pg:
+        renderer = dist_tiles.FrameRenderer(scene, stream, inflight=args.inflight)
+    elif tiled:
+        layout = dist_tiles.TilePlan(scene, world, rank)
+        renderer = dist_tiles.TileGatherRenderer(layout, stream,
+                                                 dist_tiles.scene_tile_renderer(scene),
+                                                 inflight=args.inflight,
+                                                 host_staging=host_staging, device=dev)
+    else:
         owners = dist_tiles.FrameOwners(n_cams, world, rank)
         sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
         renderer = dist_tiles.FrameGatherRenderer(scene, owners, sizes, stream,
-                                                  host_staging=args.dist_backend == "gloo",
-                                                  inflight=args.inflight,
-                                                  device=torch.device("cuda", device))
-    else:
-        plan = dist_tiles.TilePlan(scene, world, rank, force=use_pg)
-        renderer = dist_tiles.FrameRenderer(scene, plan, stream, gather=use_pg,
-                                            host_staging=args.dist_backend == "gloo", chunks=chunks,
-                                            inflight=args.inflight)
+                                                  host_staging=host_staging,
+                                                  inflight=args.inflight, device=dev)
 
     # warmup (also yields the per-step ray count from the device counters)
     for _ in range(args.warmup):
@@ -384,7 +503,6 @@ def main() -> int:
     torch.cuda.synchronize()
     st = scene.collect_stats()
     rays_local = (st.primary_rays + st.shadow_rays + st.secondary_rays) / max(1, args.warmup)
-    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
     rays_step = torch.tensor([rays_local], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(rays_step)
@@ -394,23 +512,9 @@ def main() -> int:
           for _ in range(args.steps)]
     scene.read_kernel_times()  # discard
     scene.set_kernel_timing(True)  # HIP events around each traversal kernel, on its stream
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for k in range(args.steps):
-        renderer.step(events=ev[k])
-    renderer.finish()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
+    elapsed = timed_steps(renderer, args.steps, world, coll_dev, ev)
     scene.set_kernel_timing(False)
     kt, launches = scene.read_kernel_times()
-    el = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
     render_ms = [a.elapsed_time(b) for a, b in ev]
     scene.collect_stats()  # reset counters
 
@@ -427,19 +531,33 @@ def main() -> int:
                 verified &= bool(torch.equal(ref.view(torch.int32), f.view(torch.int32)))
             log(f"[rank 0] gathered frames bit-identical to single-GPU renders: {verified}")
         if strong:
-            # t1: the same job rendered by this GPU alone, in place (no tiles, no gather)
-            frames1 = [torch.empty_like(f) for f in renderer.frames]
+            # t1: the same job rendered by this GPU alone, in place, with the same frames in
+            # flight (the N = 1 bench path)
+            one = dist_tiles.FrameRenderer(scene, stream, inflight=args.inflight)
             for _ in range(max(1, args.warmup)):
-                for c, f in enumerate(frames1):
-                    scene.render_device(c, f.data_ptr(), stream=stream.cuda_stream)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(args.steps):
-                for c, f in enumerate(frames1):
-                    scene.render_device(c, f.data_ptr(), stream=stream.cuda_stream)
-            torch.cuda.synchronize()
-            t1_ms = (time.perf_counter() - t0) / args.steps * 1e3
+                one.step()
+            one.finish()
+            t1_ms = timed_steps(one, args.steps, 1, coll_dev) / args.steps * 1e3
             scene.collect_stats()
+    weak = None
+    if world > 1 and strong and not args.no_weak:
+        # extra: weak scaling, one whole frame per rank per step (camera 0 everywhere)
+        owners = dist_tiles.FrameOwners(world, world, rank)
+        c0 = scene.camera(0)
+        wr = dist_tiles.FrameGatherRenderer(
+            scene, owners, [(c0.width, c0.height)] * world, stream, host_staging=host_staging,
+            inflight=args.inflight, device=dev,
+            render=lambda c, out, s: scene.render_device(0, out.data_ptr(), stream=s.cuda_stream))
+        for _ in range(args.warmup):
+            wr.step()
+        wr.finish()
+        el_w = timed_steps(wr, args.steps, world, coll_dev)
+        scene.collect_stats()
+        weak = {"value": round(world * rays_step / n_cams * args.steps / el_w / 1e6, 2),
+                "unit": "Mrays/s", "ms_per_step": round(el_w / args.steps * 1e3, 4),
+                "frames_per_step": world,
+                "parallelism": f"frames{world}+{'rccl' if coll_dev == 'cuda' else 'gloo'}_gather",
+                "note": "one whole frame per rank per step, gathered to rank 0 (weak scaling)"}
     if world > 1:
         dist.barrier()
 
@@ -480,6 +598,7 @@ def main() -> int:
                 log(f"cpu baseline failed: {e!r}")
         n, w, h, desc = WORKLOADS[args.workload]
         ms_step = elapsed / args.steps * 1e3
+        comm = "rccl" if coll_dev == "cuda" else "gloo"
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -489,10 +608,9 @@ def main() -> int:
             "config": {"workload": desc, "frame": f"{w}x{h}", "frames_per_step": n_cams,
                        "triangles": 2 * (n - 1) ** 2, "rays_per_step": int(rays_step),
                        "traversal": args.traversal,
-                       "parallelism": (f"tiles{world}" if tiled and use_pg else f"frames{world}") +
-                                      (f"+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}_gather" if use_pg else ""),
-                       "frames_in_flight": renderer.inflight if hasattr(renderer, "inflight") else 1,
-                       "gather_chunks": chunks if use_pg and tiled else None,
+                       "parallelism": (f"tiles{world}+{comm}_gather" if tiled else
+                                       f"frames{world}+{comm}_gather" if use_pg else "frames1"),
+                       "frames_in_flight": renderer.inflight,
                        "gather_verified": verified,
                        "render_ms_avg": round(sum(render_ms) / len(render_ms), 4)},
             "roofline": roof, "cpu_baseline": cpu, "pcie_inclusive": host_rate,
@@ -500,6 +618,17 @@ def main() -> int:
         if strong and t1_ms is not None:
             line["strong_scaling"] = {"t1_ms": round(t1_ms, 4), "tN_ms": round(ms_step, 4),
                                       "efficiency_t1_over_N_tN": round(t1_ms / (world * ms_step), 4)}
+        if weak is not None:
+            line["weak_scaling"] = weak
+        if world == 1 and not use_pg and not args.no_c5:
+            try:
+                import bench_ppm
+                c5 = bench_ppm.run(max(3, args.steps // 4), 1, not args.no_cpu_baseline)
+                line["c5"] = {k: c5[k] for k in ("metric", "value", "unit", "ms_per_step",
+                                                 "steps", "warmup", "config", "roofline")}
+                line["c5"]["cpu_baseline"] = c5.get("cpu_baseline")
+            except Exception as e:
+                log(f"c5 sub-benchmark failed: {e!r}")
         print(json.dumps(line), flush=True)
     if use_pg:
         dist.barrier()

@@ -24,7 +24,6 @@ RT_E_UNSUPPORTED = -5
 
 RT_TRAVERSAL_FAST = 0
 RT_TRAVERSAL_REFERENCE = 1
-RT_TRAVERSAL_CULL = 2
 
 F3 = C.c_float * 3
 
@@ -75,6 +74,12 @@ SIGNATURES = {
     "rt_scene_create": (C.c_int, [C.POINTER(rt_scene_desc), C.c_int, C.POINTER(C.c_void_p)]),
     "rt_scene_destroy": (None, [C.c_void_p]),
     "rt_scene_load_xml": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]),
+    "rt_scene_create_multi": (C.c_int, [C.POINTER(rt_scene_desc), C.c_int, C.POINTER(C.c_int),
+                                        C.POINTER(C.c_void_p)]),
+    "rt_scene_load_xml_multi": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_int),
+                                          C.POINTER(C.c_void_p)]),
+    "rt_scene_device_count": (C.c_int, [C.c_void_p]),
+    "rt_release_stream_scratch": (C.c_int, [C.c_void_p, C.c_void_p]),
     "rt_scene_num_cameras": (C.c_int, [C.c_void_p]),
     "rt_scene_camera": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(rt_camera)]),
     "rt_scene_image_name": (C.c_char_p, [C.c_void_p, C.c_int]),
@@ -129,7 +134,7 @@ def _share_torch_hip_runtime() -> None:
         pass
 
 
-ABI_VERSION = 3  # CENG795_RT_ABI_VERSION of include/ceng795_rt.h
+ABI_VERSION = 4  # CENG795_RT_ABI_VERSION of include/ceng795_rt.h
 
 
 def lib() -> C.CDLL:

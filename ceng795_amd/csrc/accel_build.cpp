@@ -308,8 +308,6 @@ int collapse_wide(std::vector<DevNode>& nodes, int nref, int root, int& stack) {
 
 }  // namespace
 
-// Kernels built without the batched leaf queue cannot walk wide nodes (rt_kernels.hip).
-bool wide_nodes_supported();
 
 void build_accel(HostScene& s, int K) {
   if (s.accel_root >= 0) s.nodes.resize(s.accel_root & ~kWideTag);  // drop an earlier culling tree
@@ -402,7 +400,7 @@ void build_accel(HostScene& s, int K) {
   s.accel_depth = B.depth + 1;
   s.accel_items = (int)items.size();
   const char* we = std::getenv("CENG795_RT_WIDE");  // =0: keep the binary culling tree (A/B)
-  if (!(we && we[0] == '0') && wide_nodes_supported()) {
+  if (!(we && we[0] == '0')) {
     int stack = 0;
     s.accel_root = collapse_wide(s.nodes, nn, root, stack);
     s.accel_depth = stack;

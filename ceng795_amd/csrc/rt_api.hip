@@ -1,5 +1,7 @@
-// C-ABI implementation (include/ceng795_rt.h): scene upload, render launches, counters.
+// C-ABI implementation (include/ceng795_rt.h): scene upload, render launches, counters,
+// multi-device frames.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <array>
@@ -21,10 +23,11 @@
 namespace rt {
 hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                          const float* normals, const DevMaterial* mats, const DevLight* lights,
-                         bool fast, bool deep, bool spheres, bool cull, bool wide_only,
+                         bool fast, bool deep, bool spheres, bool wide_only,
                          const hipEvent_t* marks, hipStream_t stream);
 int max_supported_depth();
 hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream);
+hipError_t launch_untile(const UntileParams& U, hipStream_t stream);
 unsigned long long read_reset_exact_fallbacks();
 hipError_t launch_quot_check(unsigned long long seed, long long count, unsigned long long* counts,
                              hipStream_t stream);
@@ -35,10 +38,11 @@ void write_png(const std::string& path, const float* rgb, int w, int h);
 
 using namespace rt;
 
-// Device buffers of one synchronous rt_render call, kept by the scene and reused: the
-// reference calls render_image once per thread per camera (HW2/main.cpp:33-36), so a drop-in
-// pays hipMalloc / hipFree only the first time a call of that size runs.  Calls on several
-// host threads each take their own context (rt_render stays reentrant).
+// Device buffers of one synchronous call (rt_render, and every device's share of a
+// multi-device frame), kept by the scene and reused: the reference calls render_image once per
+// thread per camera (HW2/main.cpp:33-36), so a drop-in pays hipMalloc / hipFree only the first
+// time a call of that size runs.  Calls on several host threads each take their own context
+// (rt_render stays reentrant).
 struct RenderCtx {
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -55,23 +59,43 @@ struct RenderCtx {
   size_t frames_floats = 0;
   float* d_samples = nullptr;
   size_t samples_floats = 0;
+  float* d_recv = nullptr;  // multi-device frames, first device: the gathered tiles
+  size_t recv_floats = 0;
+  float* d_image = nullptr;  // multi-device rt_render, first device: the row-major frame
+  size_t image_floats = 0;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;  // multi-device frames: caller-stream ordering
 };
 
-// Per-kernel HIP-event timing of render launches (rt_set_kernel_timing): one quad of events
-// per launch, read back by rt_read_kernel_times.
+// rt_render_device scratch of one stream (hit records, occlusion bits, tile schedule, ray-tree
+// frames, MSAA samples).  Owned through a unique_ptr, so its address is stable while the table
+// grows; `mu` serialises host threads that enqueue on the same stream.
+struct StreamScratch {
+  void* stream = nullptr;
+  std::mutex mu;
+  int2_t* hits = nullptr;
+  unsigned* occ = nullptr;
+  unsigned* sched = nullptr;
+  float* frames = nullptr;
+  size_t frames_capacity = 0;
+  float* samples = nullptr;
+  size_t samples_capacity = 0;
+};
+
+// Per-kernel HIP-event timing of render launches (rt_set_kernel_timing): one quad of events per
+// launch of the first device.  Completed quads beyond kTimingPending are folded into `sum` so
+// the list stays bounded while timing is on and nobody reads it.
 struct KernelTiming {
   bool on = false;
   std::vector<std::array<hipEvent_t, 4>> pending, spare;
+  double sum[4] = {0, 0, 0, 0};
+  long long folded = 0;
 };
+constexpr size_t kTimingPending = 256;
 
-struct rt_scene {
-  HostScene host;
+// The scene on one device: the flattened scene in HBM, the ray counters, and the buffers of
+// the calls that run there.
+struct Replica {
   int device = 0;
-  int mode = RT_TRAVERSAL_FAST;
-  bool deep = false;
-  bool needs_recursion = false;
-  bool has_spheres = false;
-  bool wide_only = false;  // the fast walk meets 4-wide culling nodes only (launch_render)
   DevNode* d_nodes = nullptr;
   DevPrim* d_prims = nullptr;
   float* d_normals = nullptr;
@@ -79,33 +103,31 @@ struct rt_scene {
   DevMaterial* d_mats = nullptr;
   DevLight* d_lights = nullptr;
   unsigned long long* d_counters = nullptr;
-  int2_t* d_hits = nullptr;  // rt_render_device's primary-hit records (largest camera)
-  unsigned* d_occ = nullptr; // rt_render_device's occlusion bits
-  unsigned* d_sched = nullptr;  // rt_render_device's tile costs + shadow order (2 x tiles)
-  float* d_frames = nullptr; // rt_render_device's ray-tree frames (recursive scenes)
-  size_t frames_capacity = 0;
-  size_t hits_capacity = 0;  // records
-  float* d_samples = nullptr;  // MSAA per-sample colours [s][h][w][3]
-  size_t samples_capacity = 0;
-  // rt_render_device scratch of every further stream the scene renders on (the first one uses
-  // the buffers above): frames on different streams may be in flight together
-  struct StreamScratch {
-    void* stream;
-    int2_t* hits;
-    unsigned* occ;
-    unsigned* sched;
-    float* frames;
-    size_t frames_capacity;
-    float* samples;
-    size_t samples_capacity;
-  };
-  void* first_stream = nullptr;
-  bool first_stream_set = false;
-  std::vector<StreamScratch> streams;
-  unsigned long long msaa_seed = 0;
-  std::mutex ctx_mu;
+  std::mutex mu;  // ctx pool and stream table
   std::vector<RenderCtx*> ctx_free, ctx_all;
+  std::vector<std::unique_ptr<StreamScratch>> streams;
+};
+
+struct rt_scene {
+  HostScene host;
+  int mode = RT_TRAVERSAL_FAST;
+  bool deep = false;
+  bool needs_recursion = false;
+  bool has_spheres = false;
+  bool wide_only = false;  // the fast walk meets 4-wide culling nodes only (launch_render)
+  size_t most = 1;         // pixel records of the largest camera frame (whole tiles)
+  unsigned long long msaa_seed = 0;
+  std::vector<std::unique_ptr<Replica>> rep;  // rep[0]: the first (output) device
+  std::mutex timing_mu;
   KernelTiming timing;
+  // multi-device scenes: one RCCL communicator per device (single process, ncclCommInitAll);
+  // multi_mu serialises the frames that use them.  copy_gather: the shares are gathered by
+  // peer copies instead (a device listed twice — the one-GPU rehearsal of the deal / gather /
+  // untile path — or CENG795_RT_GATHER=copy)
+  std::mutex multi_mu;
+  std::vector<ncclComm_t> comms;
+  bool multi = false;  // made by rt_scene_*_multi: frames go through render_multi (any count)
+  bool copy_gather = false;
 };
 
 namespace {
@@ -122,8 +144,17 @@ struct HipFailure {
   const char* what;
 };
 
+struct NcclFailure {
+  ncclResult_t err;
+  const char* what;
+};
+
 void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw HipFailure{e, what};
+}
+
+void nccl_check(ncclResult_t e, const char* what) {
+  if (e != ncclSuccess) throw NcclFailure{e, what};
 }
 
 template <typename F>
@@ -132,6 +163,8 @@ int guarded(F&& f) {
     return f();
   } catch (const HipFailure& h) {
     return set_error(RT_E_HIP, std::string(h.what) + ": " + hipGetErrorString(h.err));
+  } catch (const NcclFailure& h) {
+    return set_error(RT_E_HIP, std::string(h.what) + ": " + ncclGetErrorString(h.err));
   } catch (const std::domain_error& e) {
     return set_error(RT_E_UNSUPPORTED, e.what());
   } catch (const std::invalid_argument& e) {
@@ -165,41 +198,58 @@ void free_ctx(RenderCtx* c) {
   (void)hipFree(c->d_sched);
   (void)hipFree(c->d_frames);
   (void)hipFree(c->d_samples);
+  (void)hipFree(c->d_recv);
+  (void)hipFree(c->d_image);
+  if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+  if (c->ev_out) (void)hipEventDestroy(c->ev_out);
   if (c->e0) (void)hipEventDestroy(c->e0);
   if (c->e1) (void)hipEventDestroy(c->e1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
-void free_device(rt_scene* s) {
+void free_scratch(StreamScratch& x) {
+  (void)hipFree(x.hits);
+  (void)hipFree(x.occ);
+  (void)hipFree(x.sched);
+  (void)hipFree(x.frames);
+  (void)hipFree(x.samples);
+}
+
+void free_replica(Replica& r) {
   int cur = 0;
-  if (hipGetDevice(&cur) == hipSuccess && cur != s->device) (void)hipSetDevice(s->device);
-  for (RenderCtx* c : s->ctx_all) free_ctx(c);
-  s->ctx_all.clear();
-  s->ctx_free.clear();
-  for (auto* v : {&s->timing.pending, &s->timing.spare})
-    for (auto& q : *v)
-      for (hipEvent_t e : q) (void)hipEventDestroy(e);
-  (void)hipFree(s->d_nodes);
-  (void)hipFree(s->d_prims);
-  (void)hipFree(s->d_normals);
-  (void)hipFree(s->d_anc);
-  (void)hipFree(s->d_mats);
-  (void)hipFree(s->d_lights);
-  (void)hipFree(s->d_counters);
-  (void)hipFree(s->d_hits);
-  (void)hipFree(s->d_occ);
-  (void)hipFree(s->d_sched);
-  (void)hipFree(s->d_frames);
-  (void)hipFree(s->d_samples);
-  for (auto& x : s->streams) {
-    (void)hipFree(x.hits);
-    (void)hipFree(x.occ);
-    (void)hipFree(x.sched);
-    (void)hipFree(x.frames);
-    (void)hipFree(x.samples);
+  if (hipGetDevice(&cur) == hipSuccess && cur != r.device) (void)hipSetDevice(r.device);
+  for (RenderCtx* c : r.ctx_all) free_ctx(c);
+  r.ctx_all.clear();
+  r.ctx_free.clear();
+  for (auto& x : r.streams) free_scratch(*x);
+  r.streams.clear();
+  (void)hipFree(r.d_nodes);
+  (void)hipFree(r.d_prims);
+  (void)hipFree(r.d_normals);
+  (void)hipFree(r.d_anc);
+  (void)hipFree(r.d_mats);
+  (void)hipFree(r.d_lights);
+  (void)hipFree(r.d_counters);
+  if (cur != r.device) (void)hipSetDevice(cur);
+}
+
+void free_device(rt_scene* s) {
+  for (ncclComm_t c : s->comms) (void)ncclCommDestroy(c);
+  s->comms.clear();
+  if (!s->rep.empty()) {
+    int cur = 0;
+    const int d0 = s->rep[0]->device;
+    if (hipGetDevice(&cur) == hipSuccess && cur != d0) (void)hipSetDevice(d0);
+    for (auto* v : {&s->timing.pending, &s->timing.spare})
+      for (auto& q : *v)
+        for (hipEvent_t e : q) (void)hipEventDestroy(e);
+    if (cur != d0) (void)hipSetDevice(cur);
   }
-  if (cur != s->device) (void)hipSetDevice(cur);
+  s->timing.pending.clear();
+  s->timing.spare.clear();
+  for (auto& r : s->rep) free_replica(*r);
+  s->rep.clear();
 }
 
 struct DeviceGuard {
@@ -215,6 +265,7 @@ struct DeviceGuard {
 };
 
 constexpr int kFrameFloats = 28;  // rt_kernels.hip kFrFields
+constexpr size_t kTileFloats = (size_t)kTile * kTile * 3;
 
 size_t frame_floats(const HostScene& h, int sel_tiles) {
   return (size_t)(h.max_depth + 1) * kFrameFloats * kTile * kTile * (size_t)std::max(1, sel_tiles);
@@ -253,16 +304,28 @@ bool wide_only_tree(const HostScene& h) {
   return true;
 }
 
-int create_from_host(rt_scene* s, int device) {
-  if (device < 0) hip_check(hipGetDevice(&device), "hipGetDevice");
-  s->device = device;
-  DeviceGuard g(device);
+void upload_replica(const rt_scene* s, Replica& r) {
+  DeviceGuard g(r.device);
+  const HostScene& h = s->host;
+  r.d_nodes = upload(h.nodes, "upload nodes");
+  r.d_prims = upload(h.prims, "upload prims");
+  r.d_normals = upload(h.normals, "upload normals");
+  r.d_anc = upload(h.ancestry, "upload ancestry");
+  r.d_mats = upload(h.materials, "upload materials");
+  r.d_lights = upload(h.lights, "upload lights");
+  hip_check(hipMalloc(&r.d_counters, sizeof(unsigned long long) * kCounterAlloc), "alloc counters");
+  hip_check(hipMemset(r.d_counters, 0, sizeof(unsigned long long) * kCounterAlloc), "zero counters");
+}
+
+// Builds the culling tree once on the host, then uploads the scene to every device.  Several
+// devices: one RCCL communicator each, for the framebuffer gather (render_multi).
+int create_from_host(rt_scene* s, const std::vector<int>& devices, bool multi) {
   build_accel(s->host, accel_treelet_leaves());
   if (s->host.accel_depth > max_supported_depth()) build_accel(s->host, 0);
   if (std::getenv("CENG795_RT_VERBOSE"))
     std::fprintf(stderr, "ceng795_rt: %zu nodes (reference depth %d), culling tree root %d over "
-                 "%d treelets, depth %d\n", s->host.nodes.size(), s->host.depth,
-                 s->host.accel_root, s->host.accel_items, s->host.accel_depth);
+                 "%d treelets, depth %d, %zu device(s)\n", s->host.nodes.size(), s->host.depth,
+                 s->host.accel_root, s->host.accel_items, s->host.accel_depth, devices.size());
   const HostScene& h = s->host;
   if (h.depth > max_supported_depth())
     throw std::invalid_argument("BVH deeper than " + std::to_string(max_supported_depth()) +
@@ -275,28 +338,44 @@ int create_from_host(rt_scene* s, int device) {
     const bool glass = m.transparency[0] != 0 || m.transparency[1] != 0 || m.transparency[2] != 0;
     if ((mirror || glass) && h.max_depth > 0) s->needs_recursion = true;
   }
-  s->d_nodes = upload(h.nodes, "upload nodes");
-  s->d_prims = upload(h.prims, "upload prims");
-  s->d_normals = upload(h.normals, "upload normals");
-  s->d_anc = upload(h.ancestry, "upload ancestry");
-  s->d_mats = upload(h.materials, "upload materials");
-  s->d_lights = upload(h.lights, "upload lights");
-  // ray counters
-  hip_check(hipMalloc(&s->d_counters, sizeof(unsigned long long) * kCounterAlloc),
-            "alloc counters");
-  hip_check(hipMemset(s->d_counters, 0, sizeof(unsigned long long) * kCounterAlloc),
-            "zero counters");
-  size_t most = 1;
   for (const rt_camera& c : h.cameras) {
     const size_t tiles = (size_t)((c.width + kTile - 1) / kTile) * ((c.height + kTile - 1) / kTile);
-    most = std::max(most, tiles * kTile * kTile);
+    s->most = std::max(s->most, tiles * kTile * kTile);
   }
-  hip_check(hipMalloc(&s->d_hits, most * sizeof(int2_t)), "alloc hit records");
-  hip_check(hipMalloc(&s->d_occ, most * sizeof(unsigned) * occ_words(h)), "alloc occlusion bits");
-  hip_check(hipMalloc(&s->d_sched, 2 * (most / (kTile * kTile)) * sizeof(unsigned)),
-            "alloc tile schedule");
-  s->hits_capacity = most;
+  for (int d : devices) {
+    s->rep.push_back(std::make_unique<Replica>());
+    s->rep.back()->device = d;
+    upload_replica(s, *s->rep.back());
+  }
+  s->multi = multi;
+  if (multi) {
+    std::vector<int> distinct = devices;
+    std::sort(distinct.begin(), distinct.end());
+    const char* g = std::getenv("CENG795_RT_GATHER");
+    s->copy_gather = std::unique(distinct.begin(), distinct.end()) != distinct.end() ||
+                     (g && std::strcmp(g, "copy") == 0);
+    if (!s->copy_gather) {
+      s->comms.resize(devices.size());
+      nccl_check(ncclCommInitAll(s->comms.data(), (int)devices.size(), devices.data()),
+                 "ncclCommInitAll");
+    }
+  }
   return RT_OK;
+}
+
+std::vector<int> device_list(int device_count, const int* devices) {
+  int n = 0;
+  hip_check(hipGetDeviceCount(&n), "hipGetDeviceCount");
+  if (device_count < 1) throw std::invalid_argument("device_count must be >= 1");
+  std::vector<int> out;
+  for (int i = 0; i < device_count; i++) {
+    const int d = devices ? devices[i] : i;
+    if (d < 0 || d >= n)
+      throw std::invalid_argument("device " + std::to_string(d) + " does not exist (" +
+                                  std::to_string(n) + " visible)");
+    out.push_back(d);
+  }
+  return out;
 }
 
 struct TilePlan {
@@ -311,17 +390,18 @@ TilePlan plan(const rt_camera& c, int row0, int row_stride) {
   return p;
 }
 
-RenderParams make_params(const rt_scene* s, int cam, int row0, int row_stride, int tile_begin,
-                         int tile_step, int tile_major, float* out, bool counters) {
+RenderParams make_params(const rt_scene* s, const Replica& r, int cam, int row0, int row_stride,
+                         int tile_begin, int tile_step, int tile_major, float* out,
+                         unsigned long long* counters) {
   const HostScene& h = s->host;
   const rt_camera& c = h.cameras[cam];
   RenderParams P;
   std::memset(&P, 0, sizeof P);
-  P.nodes = s->d_nodes;
-  P.prims = s->d_prims;
-  P.normals = s->d_normals;
-  P.materials = s->d_mats;
-  P.lights = s->d_lights;
+  P.nodes = r.d_nodes;
+  P.prims = r.d_prims;
+  P.normals = r.d_normals;
+  P.materials = r.d_mats;
+  P.lights = r.d_lights;
   P.num_lights = (int)h.lights.size();
   P.max_depth = h.max_depth;
   std::memcpy(P.background, h.background, sizeof P.background);
@@ -333,7 +413,7 @@ RenderParams make_params(const rt_scene* s, int cam, int row0, int row_stride, i
   P.accel_root = h.accel_root;
   P.quot_ok = h.quot_ok;
   std::memcpy(P.accel_box, h.accel_box, sizeof P.accel_box);
-  P.anc = s->d_anc;
+  P.anc = r.d_anc;
   std::memcpy(P.cam_e, c.e, 12);
   std::memcpy(P.cam_tl, c.top_left, 12);
   std::memcpy(P.cam_su, c.s_u, 12);
@@ -352,11 +432,8 @@ RenderParams make_params(const rt_scene* s, int cam, int row0, int row_stride, i
       tile_begin < tp.tiles_total ? (tp.tiles_total - tile_begin + tile_step - 1) / tile_step : 0;
   P.tile_major = tile_major;
   P.out = out;
-  P.hits = s->d_hits;
-  P.occ = s->d_occ;
   P.occ_words = occ_words(h);
-  set_schedule(P, s->d_sched);
-  P.counters = counters ? s->d_counters : nullptr;
+  P.counters = counters;
   return P;
 }
 
@@ -381,14 +458,33 @@ unsigned powmod_minstd(unsigned a, unsigned e) {
   return (unsigned)r;
 }
 
-// One frame of camera `cam` into d_out.  Pixel-centre cameras: the render kernels write
-// d_out directly.  MSAA cameras (HW2/Scene.cpp:32-69): one render pass per sample index into
-// d_samples[s], then the resolve kernel's splat + colour / weight into d_out (row-major).
+// Folds the completed quads at the front of the pending list into the running sums.
+void fold_timing(KernelTiming& t) {
+  size_t k = 0;
+  for (; k < t.pending.size(); k++) {
+    auto& q = t.pending[k];
+    if (hipEventQuery(q[3]) != hipSuccess) break;
+    float a = 0, b = 0, c = 0;
+    if (hipEventElapsedTime(&a, q[0], q[1]) != hipSuccess ||
+        hipEventElapsedTime(&b, q[1], q[2]) != hipSuccess ||
+        hipEventElapsedTime(&c, q[2], q[3]) != hipSuccess)
+      break;
+    t.sum[0] += a;
+    t.sum[1] += b;
+    t.sum[2] += c;
+    t.sum[3] += (double)a + b + c;
+    t.folded++;
+    t.spare.push_back(q);
+  }
+  t.pending.erase(t.pending.begin(), t.pending.begin() + (long)k);
+}
+
 // Events for one timed launch (nullptr when timing is off or the launch renders nothing).
 const hipEvent_t* timing_marks(rt_scene* s, const RenderParams& P) {
   if (!s->timing.on || P.num_sel_tiles <= 0) return nullptr;
-  std::lock_guard<std::mutex> lk(s->ctx_mu);
+  std::lock_guard<std::mutex> lk(s->timing_mu);
   KernelTiming& t = s->timing;
+  if (t.pending.size() >= kTimingPending) fold_timing(t);
   if (t.spare.empty()) {
     std::array<hipEvent_t, 4> q{};
     for (hipEvent_t& e : q) hip_check(hipEventCreate(&e), "timing event");
@@ -399,13 +495,17 @@ const hipEvent_t* timing_marks(rt_scene* s, const RenderParams& P) {
   return t.pending.back().data();
 }
 
-void enqueue_frame(rt_scene* s, const RenderParams& P, int samples, float* d_samples,
-                   hipStream_t stream) {
+// One frame (or a tile subset of one) of camera `cam` into P.out.  Pixel-centre cameras: the
+// render kernels write P.out directly.  MSAA cameras (HW2/Scene.cpp:32-69): one render pass per
+// sample index into d_samples[s], then the resolve kernel's splat + colour / weight into P.out
+// (row-major).  `timed`: this launch may take kernel-timing events (the first device only).
+void enqueue_frame(rt_scene* s, const Replica& r, const RenderParams& P, int samples,
+                   float* d_samples, hipStream_t stream, bool timed) {
   const bool fast = s->mode != RT_TRAVERSAL_REFERENCE;
-  const bool cull = s->mode == RT_TRAVERSAL_CULL;
   if (samples <= 1) {
-    hip_check(launch_render(P, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
-                            fast, s->deep, s->has_spheres, cull, s->wide_only, timing_marks(s, P), stream),
+    hip_check(launch_render(P, r.d_nodes, r.d_prims, r.d_normals, r.d_mats, r.d_lights, fast,
+                            s->deep, s->has_spheres, s->wide_only,
+                            timed ? timing_marks(s, P) : nullptr, stream),
               "render launch");
     return;
   }
@@ -419,8 +519,9 @@ void enqueue_frame(rt_scene* s, const RenderParams& P, int samples, float* d_sam
     Q.msaa_seed = s->msaa_seed;
     Q.tile_major = 0;
     Q.out = d_samples + (size_t)k * frame;
-    hip_check(launch_render(Q, s->d_nodes, s->d_prims, s->d_normals, s->d_mats, s->d_lights,
-                            fast, s->deep, s->has_spheres, cull, s->wide_only, timing_marks(s, Q), stream),
+    hip_check(launch_render(Q, r.d_nodes, r.d_prims, r.d_normals, r.d_mats, r.d_lights, fast,
+                            s->deep, s->has_spheres, s->wide_only,
+                            timed ? timing_marks(s, Q) : nullptr, stream),
               "render launch");
   }
   MsaaResolveParams M;
@@ -437,10 +538,6 @@ size_t sample_floats(const rt_camera& c) {
   return c.num_samples > 1 ? (size_t)c.num_samples * c.num_samples * c.width * c.height * 3 : 0;
 }
 
-}  // namespace
-
-namespace {
-
 // Grow-only device buffer.
 template <typename T>
 void ensure(T*& p, size_t& cap, size_t need, const char* what) {
@@ -453,33 +550,196 @@ void ensure(T*& p, size_t& cap, size_t need, const char* what) {
   cap = need;
 }
 
-RenderCtx* acquire_ctx(rt_scene* s) {
+RenderCtx* acquire_ctx(Replica& r) {
   {
-    std::lock_guard<std::mutex> lk(s->ctx_mu);
-    if (!s->ctx_free.empty()) {
-      RenderCtx* c = s->ctx_free.back();
-      s->ctx_free.pop_back();
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (!r.ctx_free.empty()) {
+      RenderCtx* c = r.ctx_free.back();
+      r.ctx_free.pop_back();
       return c;
     }
   }
+  DeviceGuard g(r.device);
   std::unique_ptr<RenderCtx> c(new RenderCtx);
   try {
     hip_check(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "stream");
     hip_check(hipEventCreate(&c->e0), "event");
     hip_check(hipEventCreate(&c->e1), "event");
+    hip_check(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming), "event");
+    hip_check(hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming), "event");
     hip_check(hipMalloc(&c->d_cnt, sizeof(unsigned long long) * kCounterAlloc), "alloc counters");
   } catch (...) {
     free_ctx(c.release());
     throw;
   }
-  std::lock_guard<std::mutex> lk(s->ctx_mu);
-  s->ctx_all.push_back(c.get());
+  std::lock_guard<std::mutex> lk(r.mu);
+  r.ctx_all.push_back(c.get());
   return c.release();
 }
 
-void release_ctx(rt_scene* s, RenderCtx* c) {
-  std::lock_guard<std::mutex> lk(s->ctx_mu);
-  s->ctx_free.push_back(c);
+void release_ctx(Replica& r, RenderCtx* c) {
+  std::lock_guard<std::mutex> lk(r.mu);
+  r.ctx_free.push_back(c);
+}
+
+// Contexts of one call on several replicas, handed back on scope exit.
+struct CtxSet {
+  rt_scene* s;
+  std::vector<RenderCtx*> x;
+  CtxSet(rt_scene* sc, size_t n) : s(sc) {
+    for (size_t d = 0; d < n; d++) x.push_back(acquire_ctx(*s->rep[d]));
+  }
+  ~CtxSet() {
+    for (size_t d = 0; d < x.size(); d++) release_ctx(*s->rep[d], x[d]);
+  }
+};
+
+// Sizes a context's per-call buffers for `sel_tiles` selected tiles of camera `cam` and points
+// P at them.
+void bind_ctx(rt_scene* s, RenderCtx* x, RenderParams& P, const rt_camera& c) {
+  const size_t lanes = (size_t)kTile * kTile * (size_t)std::max(1, P.num_sel_tiles);
+  ensure(x->d_hits, x->hits_records, lanes, "alloc hit records");
+  P.hits = x->d_hits;
+  ensure(x->d_occ, x->occ_words, (size_t)P.occ_words * lanes, "alloc occlusion bits");
+  P.occ = x->d_occ;
+  ensure(x->d_sched, x->sched_words, 2 * lanes / (kTile * kTile), "alloc tile schedule");
+  set_schedule(P, x->d_sched);
+  if (s->needs_recursion) {
+    ensure(x->d_frames, x->frames_floats, frame_floats(s->host, P.num_sel_tiles),
+           "alloc ray-tree frames");
+    P.frames = x->d_frames;
+  }
+  if (c.num_samples > 1) ensure(x->d_samples, x->samples_floats, sample_floats(c), "alloc MSAA samples");
+}
+
+void add_counters(const std::vector<unsigned long long>& cnt, rt_stats* stats) {
+  for (int r = 0; r < kCounterRows; r++) {
+    stats->primary_rays += (long long)cnt[kCounterWidth * r + kCntPrimary];
+    stats->shadow_rays += (long long)cnt[kCounterWidth * r + kCntShadow];
+    stats->secondary_rays += (long long)cnt[kCounterWidth * r + kCntSecondary];
+    stats->primary_hits += (long long)cnt[kCounterWidth * r + kCntHits];
+  }
+}
+
+// One frame (rows row0 + k*row_stride) of a pixel-centre camera over every device of a
+// multi-device scene, into the row-major frame d_frame on the first device, ordered on its
+// stream s0.  The frame's 8x8 tiles are dealt round-robin over the D devices (the reference's
+// row interleave over threads, HW2/main.cpp:33-36, at tile granularity; tile t -> device
+// t mod D); each device renders its tiles tile-major into a slot of ceil(T / D) tiles on its
+// context's stream; one RCCL group of send / receive pairs (single process, one communicator
+// per device) gathers the slots onto the first device, whose untile kernel writes the rows.
+// Counters: `per_call` adds each device's rays to its context's counters (rt_render's stats),
+// else to the replica's (rt_collect_stats).  Caller holds s->multi_mu.
+void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, float* d_frame,
+                  hipStream_t s0, bool per_call) {
+  const int D = (int)s->rep.size();
+  const rt_camera& c = s->host.cameras[cam];
+  const TilePlan tp = plan(c, row0, row_stride);
+  if (tp.tiles_total == 0) return;
+  const int slot = (tp.tiles_total + D - 1) / D;
+  RenderCtx* x0 = cx.x[0];
+  {
+    DeviceGuard g(s->rep[0]->device);
+    hip_check(hipEventRecord(x0->ev_in, s0), "event record");  // d_frame's earlier work
+  }
+  for (int d = 0; d < D; d++) {
+    Replica& r = *s->rep[d];
+    RenderCtx* x = cx.x[d];
+    DeviceGuard g(r.device);
+    ensure(x->d_out, x->out_floats, (size_t)slot * kTileFloats, "alloc tile slot");
+    RenderParams P = make_params(s, r, cam, row0, row_stride, d, D, 1, x->d_out,
+                                 per_call ? x->d_cnt : r.d_counters);
+    bind_ctx(s, x, P, c);
+    enqueue_frame(s, r, P, 1, nullptr, x->stream, d == 0);
+  }
+  DeviceGuard g(s->rep[0]->device);
+  ensure(x0->d_recv, x0->recv_floats, (size_t)D * slot * kTileFloats, "alloc gathered slots");
+  const size_t count = (size_t)slot * kTileFloats;
+  if (s->copy_gather) {
+    for (int d = 0; d < D; d++) {
+      {
+        DeviceGuard gd(s->rep[d]->device);
+        hip_check(hipEventRecord(cx.x[d]->ev_out, cx.x[d]->stream), "event record");
+      }
+      hip_check(hipStreamWaitEvent(x0->stream, cx.x[d]->ev_out, 0), "wait event");
+      hip_check(hipMemcpyPeerAsync(x0->d_recv + (size_t)d * count, s->rep[0]->device,
+                                   cx.x[d]->d_out, s->rep[d]->device, count * sizeof(float),
+                                   x0->stream),
+                "gather copy");
+    }
+  } else {
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (int d = 0; d < D; d++)
+      nccl_check(ncclSend(cx.x[d]->d_out, count, ncclFloat, 0, s->comms[d], cx.x[d]->stream),
+                 "ncclSend");
+    for (int d = 0; d < D; d++)
+      nccl_check(ncclRecv(x0->d_recv + (size_t)d * count, count, ncclFloat, d, s->comms[0],
+                          x0->stream),
+                 "ncclRecv");
+    nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+  }
+  hip_check(hipStreamWaitEvent(x0->stream, x0->ev_in, 0), "wait event");
+  UntileParams U;
+  U.recv = x0->d_recv;
+  U.out = d_frame;
+  U.width = c.width;
+  U.row0 = row0;
+  U.row_stride = row_stride;
+  U.rows = tp.rows;
+  U.tiles_x = tp.tiles_x;
+  U.tiles_total = tp.tiles_total;
+  U.devices = D;
+  U.slot = slot;
+  hip_check(launch_untile(U, x0->stream), "untile launch");
+  if (s0 != x0->stream) {
+    hip_check(hipEventRecord(x0->ev_out, x0->stream), "event record");
+    hip_check(hipStreamWaitEvent(s0, x0->ev_out, 0), "wait event");
+  }
+}
+
+// The scratch of `stream` on replica r: allocated on first use at the largest camera's size.
+StreamScratch* scratch_for(rt_scene* s, Replica& r, void* stream) {
+  std::lock_guard<std::mutex> lk(r.mu);
+  for (auto& x : r.streams)
+    if (x->stream == stream) return x.get();
+  auto x = std::make_unique<StreamScratch>();
+  x->stream = stream;
+  const size_t most = s->most;
+  try {
+    hip_check(hipMalloc(&x->hits, most * sizeof(int2_t)), "alloc hit records");
+    hip_check(hipMalloc(&x->occ, most * sizeof(unsigned) * occ_words(s->host)),
+              "alloc occlusion bits");
+    hip_check(hipMalloc(&x->sched, 2 * (most / (kTile * kTile)) * sizeof(unsigned)),
+              "alloc tile schedule");
+  } catch (...) {
+    free_scratch(*x);
+    throw;
+  }
+  r.streams.push_back(std::move(x));
+  return r.streams.back().get();
+}
+
+int load_xml_into(rt_scene* s, const char* xml_path, const std::vector<int>* devices,
+                  int device_count, const int* device_ids) {
+  return guarded([&] {
+    XmlSceneStorage st;
+    rt_scene_desc d;
+    load_scene_xml(xml_path, st, d);
+    s->host.image_names = st.image_names;
+    build_host_scene(d, s->host);
+    std::vector<int> devs;
+    if (devices) {
+      devs = *devices;
+    } else {
+      devs = device_list(device_count, device_ids);
+    }
+    return create_from_host(s, devs, devices == nullptr);
+  });
+}
+
+std::vector<int> single_device(int device) {
+  if (device < 0) hip_check(hipGetDevice(&device), "hipGetDevice");
+  return {device};
 }
 
 }  // namespace
@@ -499,13 +759,32 @@ int rt_camera_from_view(const float position[3], const float gaze[3], const floa
   return RT_OK;
 }
 
+int rt_scene_create_multi(const rt_scene_desc* desc, int device_count, const int* devices,
+                          rt_scene** out) {
+  if (!desc || !out) return set_error(RT_E_INVALID, "rt_scene_create: NULL argument");
+  *out = nullptr;
+  auto s = std::make_unique<rt_scene>();
+  const int rc = guarded([&] {
+    const std::vector<int> devs = device_list(device_count, devices);
+    build_host_scene(*desc, s->host);
+    return create_from_host(s.get(), devs, true);
+  });
+  if (rc != RT_OK) {
+    free_device(s.get());
+    return rc;
+  }
+  *out = s.release();
+  return RT_OK;
+}
+
 int rt_scene_create(const rt_scene_desc* desc, int device, rt_scene** out) {
   if (!desc || !out) return set_error(RT_E_INVALID, "rt_scene_create: NULL argument");
   *out = nullptr;
   auto s = std::make_unique<rt_scene>();
   const int rc = guarded([&] {
+    const std::vector<int> devs = single_device(device);
     build_host_scene(*desc, s->host);
-    return create_from_host(s.get(), device);
+    return create_from_host(s.get(), devs, false);
   });
   if (rc != RT_OK) {
     free_device(s.get());
@@ -519,14 +798,26 @@ int rt_scene_load_xml(const char* xml_path, int device, rt_scene** out) {
   if (!xml_path || !out) return set_error(RT_E_INVALID, "rt_scene_load_xml: NULL argument");
   *out = nullptr;
   auto s = std::make_unique<rt_scene>();
-  const int rc = guarded([&] {
-    XmlSceneStorage st;
-    rt_scene_desc d;
-    load_scene_xml(xml_path, st, d);
-    s->host.image_names = st.image_names;
-    build_host_scene(d, s->host);
-    return create_from_host(s.get(), device);
+  std::vector<int> devs;
+  int rc = guarded([&] {
+    devs = single_device(device);
+    return RT_OK;
   });
+  if (rc == RT_OK) rc = load_xml_into(s.get(), xml_path, &devs, 0, nullptr);
+  if (rc != RT_OK) {
+    free_device(s.get());
+    return rc;
+  }
+  *out = s.release();
+  return RT_OK;
+}
+
+int rt_scene_load_xml_multi(const char* xml_path, int device_count, const int* devices,
+                            rt_scene** out) {
+  if (!xml_path || !out) return set_error(RT_E_INVALID, "rt_scene_load_xml_multi: NULL argument");
+  *out = nullptr;
+  auto s = std::make_unique<rt_scene>();
+  const int rc = load_xml_into(s.get(), xml_path, nullptr, device_count, devices);
   if (rc != RT_OK) {
     free_device(s.get());
     return rc;
@@ -544,6 +835,7 @@ void rt_scene_destroy(rt_scene* s) {
 int rt_scene_num_cameras(const rt_scene* s) { return s ? (int)s->host.cameras.size() : 0; }
 int rt_scene_num_lights(const rt_scene* s) { return s ? (int)s->host.lights.size() : 0; }
 int rt_scene_bvh_depth(const rt_scene* s) { return s ? s->host.depth : 0; }
+int rt_scene_device_count(const rt_scene* s) { return s ? (int)s->rep.size() : 0; }
 
 int rt_scene_camera(const rt_scene* s, int cam, rt_camera* out) {
   if (!s || !out || cam < 0 || cam >= (int)s->host.cameras.size())
@@ -600,8 +892,7 @@ int rt_host_check_accel_xml(const char* xml_path, int treelet_leaves, long long*
 }
 
 int rt_set_traversal(rt_scene* s, int mode) {
-  if (!s || (mode != RT_TRAVERSAL_FAST && mode != RT_TRAVERSAL_REFERENCE &&
-             mode != RT_TRAVERSAL_CULL))
+  if (!s || (mode != RT_TRAVERSAL_FAST && mode != RT_TRAVERSAL_REFERENCE))
     return set_error(RT_E_INVALID, "rt_set_traversal: bad argument");
   s->mode = mode;
   return RT_OK;
@@ -625,112 +916,87 @@ int rt_render_device(rt_scene* s, int cam, int row0, int row_stride, int tile_be
                                 d_out, stream);
 }
 
-// The scratch buffers of `stream`: the scene's own for the first stream it renders on, a set
-// of its own (same sizes) for each further one.
-struct Scratch {
-  int2_t** hits;
-  unsigned** occ;
-  unsigned** sched;
-  float** frames;
-  size_t* frames_capacity;
-  float** samples;
-  size_t* samples_capacity;
-};
-Scratch scratch_for(rt_scene* s, void* stream) {
-  std::lock_guard<std::mutex> lk(s->ctx_mu);
-  if (!s->first_stream_set) {
-    s->first_stream_set = true;
-    s->first_stream = stream;
-  }
-  if (stream == s->first_stream)
-    return {&s->d_hits, &s->d_occ, &s->d_sched, &s->d_frames, &s->frames_capacity,
-            &s->d_samples, &s->samples_capacity};
-  for (auto& x : s->streams)
-    if (x.stream == stream)
-      return {&x.hits, &x.occ, &x.sched, &x.frames, &x.frames_capacity, &x.samples,
-              &x.samples_capacity};
-  rt_scene::StreamScratch x{stream, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0};
-  const size_t most = s->hits_capacity;
-  try {
-    hip_check(hipMalloc(&x.hits, most * sizeof(int2_t)), "alloc hit records");
-    hip_check(hipMalloc(&x.occ, most * sizeof(unsigned) * occ_words(s->host)),
-              "alloc occlusion bits");
-    hip_check(hipMalloc(&x.sched, 2 * (most / (kTile * kTile)) * sizeof(unsigned)),
-              "alloc tile schedule");
-  } catch (...) {
-    (void)hipFree(x.hits);
-    (void)hipFree(x.occ);
-    (void)hipFree(x.sched);
-    throw;
-  }
-  s->streams.push_back(x);
-  auto& y = s->streams.back();
-  return {&y.hits, &y.occ, &y.sched, &y.frames, &y.frames_capacity, &y.samples,
-          &y.samples_capacity};
-}
-
 int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int tile_begin,
                            int tile_step, int tile_count, int tile_major, float* d_out,
                            void* stream) {
   return guarded([&] {
-      check_render_args(s, cam, row0, row_stride);
-      if (tile_begin < 0 || tile_step < 1 || !d_out)
-        throw std::invalid_argument("rt_render_device: bad tile selection / output");
-      DeviceGuard g(s->device);
-      const Scratch sc = scratch_for(s, stream);
-      RenderParams P =
-          make_params(s, cam, row0, row_stride, tile_begin, tile_step, tile_major, d_out, true);
-      P.hits = *sc.hits;
-      P.occ = *sc.occ;
-      set_schedule(P, *sc.sched);
-      if (tile_count >= 0 && tile_count < P.num_sel_tiles) {
-        if (s->host.cameras[cam].num_samples > 1)
-          throw std::domain_error("NumSamples > 1 renders whole row-major frames only");
-        P.num_sel_tiles = tile_count;
-      }
-      if (s->needs_recursion) {
-        const size_t need = frame_floats(s->host, P.num_sel_tiles);
-        if (need > *sc.frames_capacity) {
-          (void)hipFree(*sc.frames);
-          *sc.frames = nullptr;
-          *sc.frames_capacity = 0;
-          hip_check(hipMalloc(sc.frames, need * sizeof(float)), "alloc ray-tree frames");
-          *sc.frames_capacity = need;
-        }
-        P.frames = *sc.frames;
-      }
-      const rt_camera& c = s->host.cameras[cam];
-      if (c.num_samples > 1) {
-        if (tile_begin != 0 || tile_step != 1 || tile_major)
-          throw std::domain_error("NumSamples > 1 renders whole row-major frames only");
-        const size_t need = sample_floats(c);
-        if (need > *sc.samples_capacity) {
-          (void)hipFree(*sc.samples);
-          *sc.samples = nullptr;
-          *sc.samples_capacity = 0;
-          hip_check(hipMalloc(sc.samples, need * sizeof(float)), "alloc MSAA samples");
-          *sc.samples_capacity = need;
-        }
-      }
-      enqueue_frame(s, P, c.num_samples, *sc.samples, (hipStream_t)stream);
+    check_render_args(s, cam, row0, row_stride);
+    if (tile_begin < 0 || tile_step < 1 || !d_out)
+      throw std::invalid_argument("rt_render_device: bad tile selection / output");
+    const rt_camera& c = s->host.cameras[cam];
+    if (s->multi && c.num_samples <= 1) {
+      // a multi-device scene renders whole frames (rows subsets allowed) split over its devices
+      if (tile_begin != 0 || tile_step != 1 || tile_major || tile_count >= 0)
+        throw std::domain_error("multi-device scenes render whole row-major frames only");
+      std::lock_guard<std::mutex> lk(s->multi_mu);
+      CtxSet cx(s, s->rep.size());
+      render_multi(s, cx, cam, row0, row_stride, d_out, (hipStream_t)stream, false);
       return RT_OK;
+    }
+    Replica& r = *s->rep[0];
+    DeviceGuard g(r.device);
+    StreamScratch* sc = scratch_for(s, r, stream);
+    std::lock_guard<std::mutex> lk(sc->mu);
+    RenderParams P = make_params(s, r, cam, row0, row_stride, tile_begin, tile_step, tile_major,
+                                 d_out, r.d_counters);
+    P.hits = sc->hits;
+    P.occ = sc->occ;
+    set_schedule(P, sc->sched);
+    if (tile_count >= 0 && tile_count < P.num_sel_tiles) {
+      if (c.num_samples > 1) throw std::domain_error("NumSamples > 1 renders whole row-major frames only");
+      P.num_sel_tiles = tile_count;
+    }
+    if (s->needs_recursion) {
+      ensure(sc->frames, sc->frames_capacity, frame_floats(s->host, P.num_sel_tiles),
+             "alloc ray-tree frames");
+      P.frames = sc->frames;
+    }
+    if (c.num_samples > 1) {
+      if (tile_begin != 0 || tile_step != 1 || tile_major)
+        throw std::domain_error("NumSamples > 1 renders whole row-major frames only");
+      ensure(sc->samples, sc->samples_capacity, sample_floats(c), "alloc MSAA samples");
+    }
+    enqueue_frame(s, r, P, c.num_samples, sc->samples, (hipStream_t)stream, true);
+    return RT_OK;
+  });
+}
+
+int rt_release_stream_scratch(rt_scene* s, void* stream) {
+  if (!s) return set_error(RT_E_INVALID, "rt_release_stream_scratch: NULL scene");
+  return guarded([&] {
+    for (auto& rp : s->rep) {
+      Replica& r = *rp;
+      std::unique_ptr<StreamScratch> x;
+      {
+        std::lock_guard<std::mutex> lk(r.mu);
+        for (size_t k = 0; k < r.streams.size(); k++)
+          if (r.streams[k]->stream == stream) {
+            x = std::move(r.streams[k]);
+            r.streams.erase(r.streams.begin() + (long)k);
+            break;
+          }
+      }
+      if (!x) continue;
+      DeviceGuard g(r.device);
+      std::lock_guard<std::mutex> lk(x->mu);  // no enqueue on it is in progress
+      hip_check(hipStreamSynchronize((hipStream_t)stream), "synchronize stream");
+      free_scratch(*x);
+    }
+    return RT_OK;
   });
 }
 
 int rt_collect_stats(rt_scene* s, rt_stats* stats) {
   if (!s || !stats) return set_error(RT_E_INVALID, "rt_collect_stats: NULL argument");
   return guarded([&] {
-    DeviceGuard g(s->device);
-    std::vector<unsigned long long> c(kCounterWidth * kCounterRows);
-    hip_check(hipMemcpy(c.data(), s->d_counters, c.size() * sizeof c[0], hipMemcpyDeviceToHost),
-              "read counters");
-    hip_check(hipMemset(s->d_counters, 0, c.size() * sizeof c[0]), "reset counters");
     std::memset(stats, 0, sizeof *stats);
-    for (int r = 0; r < kCounterRows; r++) {
-      stats->primary_rays += (long long)c[kCounterWidth * r + kCntPrimary];
-      stats->shadow_rays += (long long)c[kCounterWidth * r + kCntShadow];
-      stats->secondary_rays += (long long)c[kCounterWidth * r + kCntSecondary];
-      stats->primary_hits += (long long)c[kCounterWidth * r + kCntHits];
+    for (auto& rp : s->rep) {
+      DeviceGuard g(rp->device);
+      std::vector<unsigned long long> c(kCounterWidth * kCounterRows);
+      hip_check(hipMemcpy(c.data(), rp->d_counters, c.size() * sizeof c[0], hipMemcpyDeviceToHost),
+                "read counters");
+      hip_check(hipMemset(rp->d_counters, 0, c.size() * sizeof c[0]), "reset counters");
+      add_counters(c, stats);
     }
     return RT_OK;
   });
@@ -739,15 +1005,18 @@ int rt_collect_stats(rt_scene* s, rt_stats* stats) {
 int rt_debug_counters(rt_scene* s, long long* out16) {
   if (!s || !out16) return set_error(RT_E_INVALID, "rt_debug_counters: NULL argument");
   return guarded([&] {
-    DeviceGuard g(s->device);
-    std::vector<unsigned long long> c(kCounterWidth * kCounterRows);
-    hip_check(hipMemcpy(c.data(), s->d_counters, c.size() * sizeof c[0], hipMemcpyDeviceToHost),
-              "read counters");
-    hip_check(hipMemset(s->d_counters, 0, c.size() * sizeof c[0]), "reset counters");
-    for (int k = 0; k < kCounterWidth; k++) {
-      unsigned long long sum = 0;
-      for (int r = 0; r < kCounterRows; r++) sum += c[kCounterWidth * r + k];
-      out16[k] = (long long)sum;
+    for (int k = 0; k < kCounterWidth; k++) out16[k] = 0;
+    for (auto& rp : s->rep) {
+      DeviceGuard g(rp->device);
+      std::vector<unsigned long long> c(kCounterWidth * kCounterRows);
+      hip_check(hipMemcpy(c.data(), rp->d_counters, c.size() * sizeof c[0], hipMemcpyDeviceToHost),
+                "read counters");
+      hip_check(hipMemset(rp->d_counters, 0, c.size() * sizeof c[0]), "reset counters");
+      for (int k = 0; k < kCounterWidth; k++) {
+        unsigned long long sum = 0;
+        for (int r = 0; r < kCounterRows; r++) sum += c[kCounterWidth * r + k];
+        out16[k] += (long long)sum;
+      }
     }
     out16[kCntExactBox] = (long long)read_reset_exact_fallbacks();
     return diag_build() ? 1 : 0;
@@ -782,72 +1051,76 @@ int rt_debug_quotient_check(int device, unsigned long long seed, long long count
 
 int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt_stats* stats) {
   return guarded([&] {
-      check_render_args(s, cam, row0, row_stride);
-      if (!out_rgb) throw std::invalid_argument("rt_render: out_rgb is NULL");
-      DeviceGuard g(s->device);
-      const rt_camera& c = s->host.cameras[cam];
-      const TilePlan tp = plan(c, row0, row_stride);
-      if (tp.rows == 0) return RT_OK;
-      RenderCtx* x = acquire_ctx(s);
-      struct Release {
-        rt_scene* s;
-        RenderCtx* x;
-        ~Release() { release_ctx(s, x); }
-      } release{s, x};
-      const size_t frame = (size_t)c.width * c.height * 3;
+    check_render_args(s, cam, row0, row_stride);
+    if (!out_rgb) throw std::invalid_argument("rt_render: out_rgb is NULL");
+    const rt_camera& c = s->host.cameras[cam];
+    const TilePlan tp = plan(c, row0, row_stride);
+    if (tp.rows == 0) return RT_OK;
+    const bool multi = s->multi && c.num_samples <= 1;
+    std::unique_lock<std::mutex> multi_lock(s->multi_mu, std::defer_lock);
+    if (multi) multi_lock.lock();
+    CtxSet cx(s, multi ? s->rep.size() : 1);
+    Replica& r = *s->rep[0];
+    RenderCtx* x = cx.x[0];
+    DeviceGuard g(r.device);
+    const size_t frame = (size_t)c.width * c.height * 3;
+    float* d_frame = nullptr;
+    if (multi) {  // (d_out holds the first device's tile slot)
+      ensure(x->d_image, x->image_floats, frame, "alloc frame");
+      d_frame = x->d_image;
+    } else {
       ensure(x->d_out, x->out_floats, frame, "alloc frame");
-      // Counters are per scene; this call reports its own deltas via the context's buffer.
-      hip_check(hipMemsetAsync(x->d_cnt, 0, sizeof(unsigned long long) * kCounterWidth * kCounterRows,
-                               x->stream),
+      d_frame = x->d_out;
+    }
+    // Counters are per scene; this call reports its own deltas via the contexts' buffers.
+    for (size_t d = 0; d < cx.x.size(); d++) {
+      DeviceGuard gd(s->rep[d]->device);
+      hip_check(hipMemsetAsync(cx.x[d]->d_cnt, 0,
+                               sizeof(unsigned long long) * kCounterWidth * kCounterRows,
+                               cx.x[d]->stream),
                 "zero counters");
-      RenderParams P = make_params(s, cam, row0, row_stride, 0, 1, 0, x->d_out, true);
-      P.counters = x->d_cnt;
-      const size_t lanes = (size_t)kTile * kTile * (size_t)std::max(1, P.num_sel_tiles);
-      ensure(x->d_hits, x->hits_records, lanes, "alloc hit records");
-      P.hits = x->d_hits;
-      ensure(x->d_occ, x->occ_words, (size_t)P.occ_words * lanes, "alloc occlusion bits");
-      P.occ = x->d_occ;
-      ensure(x->d_sched, x->sched_words, 2 * lanes / (kTile * kTile), "alloc tile schedule");
-      set_schedule(P, x->d_sched);
-      if (s->needs_recursion) {
-        ensure(x->d_frames, x->frames_floats, frame_floats(s->host, P.num_sel_tiles),
-               "alloc ray-tree frames");
-        P.frames = x->d_frames;
-      }
-      if (c.num_samples > 1)
-        ensure(x->d_samples, x->samples_floats, sample_floats(c), "alloc MSAA samples");
-      hip_check(hipEventRecord(x->e0, x->stream), "event record");
-      enqueue_frame(s, P, c.num_samples, x->d_samples, x->stream);
-      hip_check(hipEventRecord(x->e1, x->stream), "event record");
-      // rows j = row0 + k*row_stride only: a strided 2D copy leaves the others untouched
-      const size_t row_bytes = (size_t)c.width * 3 * sizeof(float);
-      hip_check(hipMemcpy2DAsync(out_rgb + (size_t)row0 * c.width * 3, row_bytes * row_stride,
-                                 x->d_out + (size_t)row0 * c.width * 3, row_bytes * row_stride,
-                                 row_bytes, tp.rows, hipMemcpyDeviceToHost, x->stream),
-                "copy rows");
-      std::vector<unsigned long long> cnt(kCounterWidth * kCounterRows);
-      hip_check(hipMemcpyAsync(cnt.data(), x->d_cnt, cnt.size() * sizeof cnt[0],
-                               hipMemcpyDeviceToHost, x->stream),
+    }
+    hip_check(hipEventRecord(x->e0, x->stream), "event record");
+    if (multi) {
+      render_multi(s, cx, cam, row0, row_stride, d_frame, x->stream, true);
+    } else {
+      RenderParams P = make_params(s, r, cam, row0, row_stride, 0, 1, 0, d_frame, x->d_cnt);
+      bind_ctx(s, x, P, c);
+      enqueue_frame(s, r, P, c.num_samples, x->d_samples, x->stream, true);
+    }
+    hip_check(hipEventRecord(x->e1, x->stream), "event record");
+    // rows j = row0 + k*row_stride only: a strided 2D copy leaves the others untouched
+    const size_t row_bytes = (size_t)c.width * 3 * sizeof(float);
+    hip_check(hipMemcpy2DAsync(out_rgb + (size_t)row0 * c.width * 3, row_bytes * row_stride,
+                               d_frame + (size_t)row0 * c.width * 3, row_bytes * row_stride,
+                               row_bytes, tp.rows, hipMemcpyDeviceToHost, x->stream),
+              "copy rows");
+    std::vector<std::vector<unsigned long long>> cnt(cx.x.size(),
+                                                     std::vector<unsigned long long>(kCounterAlloc));
+    for (size_t d = 0; d < cx.x.size(); d++) {
+      DeviceGuard gd(s->rep[d]->device);
+      hip_check(hipMemcpyAsync(cnt[d].data(), cx.x[d]->d_cnt, kCounterAlloc * sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, cx.x[d]->stream),
                 "copy counters");
-      hip_check(hipStreamSynchronize(x->stream), "synchronize");
-      if (stats) {
-        std::memset(stats, 0, sizeof *stats);
-        for (int r = 0; r < kCounterRows; r++) {
-          stats->primary_rays += (long long)cnt[kCounterWidth * r + kCntPrimary];
-          stats->shadow_rays += (long long)cnt[kCounterWidth * r + kCntShadow];
-          stats->secondary_rays += (long long)cnt[kCounterWidth * r + kCntSecondary];
-          stats->primary_hits += (long long)cnt[kCounterWidth * r + kCntHits];
-        }
-        float ms = 0;
-        hip_check(hipEventElapsedTime(&ms, x->e0, x->e1), "elapsed");
-        stats->kernel_ms = ms;
-      }
-      return RT_OK;
+    }
+    for (size_t d = 0; d < cx.x.size(); d++) {
+      DeviceGuard gd(s->rep[d]->device);
+      hip_check(hipStreamSynchronize(cx.x[d]->stream), "synchronize");
+    }
+    if (stats) {
+      std::memset(stats, 0, sizeof *stats);
+      for (auto& v : cnt) add_counters(v, stats);
+      float ms = 0;
+      hip_check(hipEventElapsedTime(&ms, x->e0, x->e1), "elapsed");
+      stats->kernel_ms = ms;
+    }
+    return RT_OK;
   });
 }
 
 int rt_set_kernel_timing(rt_scene* s, int enable) {
   if (!s) return set_error(RT_E_INVALID, "rt_set_kernel_timing: NULL scene");
+  std::lock_guard<std::mutex> lk(s->timing_mu);
   s->timing.on = enable != 0;
   return RT_OK;
 }
@@ -855,13 +1128,18 @@ int rt_set_kernel_timing(rt_scene* s, int enable) {
 int rt_read_kernel_times(rt_scene* s, double* ms4, long long* launches) {
   if (!s || !ms4) return set_error(RT_E_INVALID, "rt_read_kernel_times: NULL argument");
   return guarded([&] {
-    DeviceGuard g(s->device);
+    DeviceGuard g(s->rep[0]->device);
     std::vector<std::array<hipEvent_t, 4>> done;
+    double sum[4];
+    long long n;
     {
-      std::lock_guard<std::mutex> lk(s->ctx_mu);
+      std::lock_guard<std::mutex> lk(s->timing_mu);
       done.swap(s->timing.pending);
+      std::memcpy(sum, s->timing.sum, sizeof sum);
+      n = s->timing.folded;
+      std::memset(s->timing.sum, 0, sizeof s->timing.sum);
+      s->timing.folded = 0;
     }
-    double sum[4] = {0, 0, 0, 0};
     for (auto& q : done) {
       hip_check(hipEventSynchronize(q[3]), "timing sync");
       float a = 0, b = 0, c = 0;
@@ -874,8 +1152,8 @@ int rt_read_kernel_times(rt_scene* s, double* ms4, long long* launches) {
       sum[3] += (double)a + b + c;
     }
     std::memcpy(ms4, sum, sizeof sum);
-    if (launches) *launches = (long long)done.size();
-    std::lock_guard<std::mutex> lk(s->ctx_mu);
+    if (launches) *launches = n + (long long)done.size();
+    std::lock_guard<std::mutex> lk(s->timing_mu);
     for (auto& q : done) s->timing.spare.push_back(q);
     return RT_OK;
   });

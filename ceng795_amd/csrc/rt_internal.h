@@ -138,6 +138,16 @@ struct MsaaResolveParams {
   unsigned long long seed;
 };
 
+// Untile of a multi-device frame (rt_api.hip render_multi): the frame's tiles were dealt
+// round-robin over `devices` (tile t -> device t mod devices, slot position t / devices) and
+// gathered as recv[devices][slot][64 pixels][3]; writes the selected rows of the row-major
+// frame out[h][w][3] (logical row k = image row row0 + k*row_stride).
+struct UntileParams {
+  const float* recv;
+  float* out;
+  int width, row0, row_stride, rows, tiles_x, tiles_total, devices, slot;
+};
+
 struct RenderParams {
   const DevNode* nodes;
   const DevPrim* prims;

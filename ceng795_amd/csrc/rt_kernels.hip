@@ -1,7 +1,7 @@
 // MI355X (gfx950) render kernels: HW2's Scene::render_image -> trace_ray -> BVH::intersect ->
-// Triangle/Sphere::intersect -> Point_light shading + shadow rays, as one fused kernel.
+// Triangle/Sphere::intersect -> Point_light shading + shadow rays.
 //
-// Execution model (DESIGN.md §Kernels):
+// Execution model (DESIGN.md §4):
 //   * one wavefront = one 8x8 pixel packet; 4 packets per 256-thread workgroup;
 //   * the wave walks the BVH TOGETHER: the current node index and the 64-bit lane mask of
 //     the rays that accepted every box on the path are wave-uniform (SGPRs), so node and
@@ -13,7 +13,8 @@
 //     iff it accepted every ancestor's box (HW2/Bounding_volume_hierarchy.cpp:31-55);
 //   * closest hit = lexicographic minimum of (t, DFS leaf index) over accepted leaves, which
 //     is what the reference's left-first recursion with strict `<` returns (appendix A.5), so
-//     any visiting order gives the reference's answer.
+//     any visiting order gives the reference's answer;
+//   * leaf tests are queued per wave in LDS and run 64 at a time, one (ray, leaf) pair per lane.
 //
 // Numerics: compiled with -ffp-contract=off and this file's pragma; '/' is the correctly
 // rounded fp32 division and sqrtf is correctly rounded on gfx950 (HIP defaults), pow / exp
@@ -32,10 +33,6 @@ namespace rt {
 #define RT_INF __builtin_huge_valf()
 constexpr float kEps = 0.000001f;  // HW2/Vector3.h:7 kEpsilon
 constexpr int kCounterSlots = kCounterRows;
-#ifndef RT_RAYS_PER_LANE
-#define RT_RAYS_PER_LANE 1
-#endif
-constexpr int kRaysPerLane = RT_RAYS_PER_LANE;  // tiles per wave in the traversal kernels
 
 #ifdef RT_DIAG
 #define DIAG(stmt) stmt
@@ -43,7 +40,7 @@ constexpr int kRaysPerLane = RT_RAYS_PER_LANE;  // tiles per wave in the travers
 #define DIAG(stmt)
 #endif
 struct Diag {  // per-wave traversal work (RT_DIAG builds)
-  unsigned long long nodes = 0, node_lanes = 0, leaves = 0, leaf_lanes = 0, exact = 0, wide = 0;
+  unsigned long long nodes = 0, node_lanes = 0, leaves = 0, leaf_lanes = 0, wide = 0;
 };
 
 // ------------------------------------------------------------------ vector helpers
@@ -123,8 +120,7 @@ __device__ unsigned long long g_exact_fallbacks;  // lanes that needed box_exact
 // * rcp(d)) ours, |q' - q| <= 2^-22 |q| and sign(q') == sign(q) exactly.  The reference
 // accepts iff tmin <= tmax and tmax >= 0 (tmin, tmax finite here): the sign test is exact, and
 // the order test is decided here only outside a 2^-20 relative band; inside it the lane is
-// flagged for box_exact.  Written branch-free: both children of a node are tested together.
-// tnear (approximate entry distance) only orders and culls.
+// flagged for box_exact.  tnear (approximate entry distance) only orders.
 template <bool SKIP>
 __device__ __forceinline__ void slab_span(const float* b, const LaneRay& r, float& tn, float& tf) {
   const float ax = (b[0] - r.o.x) * r.r.x, bx = (b[3] - r.o.x) * r.r.x;
@@ -145,38 +141,6 @@ __device__ __forceinline__ void slab_span(const float* b, const LaneRay& r, floa
   tf = __builtin_fminf(__builtin_fminf(fx, fy), fz);
 }
 
-// Two slab spans at once (slots c and c + 1 of a wide node): b - o and * rcp as v_pk_add_f32 /
-// v_pk_mul_f32, each element rounded exactly as the scalar op, the min / max per element.
-typedef float f32x2v __attribute__((ext_vector_type(2)));
-template <bool SKIP>
-__device__ __forceinline__ void slab_span2(const float lo[3][4], const float hi[3][4], int c,
-                                           const LaneRay& r, float tn[2], float tf[2]) {
-  const f32x2v ox = {r.o.x, r.o.x}, oy = {r.o.y, r.o.y}, oz = {r.o.z, r.o.z};
-  const f32x2v rx = {r.r.x, r.r.x}, ry = {r.r.y, r.r.y}, rz = {r.r.z, r.r.z};
-  const f32x2v ax = (f32x2v{lo[0][c], lo[0][c + 1]} - ox) * rx;
-  const f32x2v bx = (f32x2v{hi[0][c], hi[0][c + 1]} - ox) * rx;
-  const f32x2v ay = (f32x2v{lo[1][c], lo[1][c + 1]} - oy) * ry;
-  const f32x2v by = (f32x2v{hi[1][c], hi[1][c + 1]} - oy) * ry;
-  const f32x2v az = (f32x2v{lo[2][c], lo[2][c + 1]} - oz) * rz;
-  const f32x2v bz = (f32x2v{hi[2][c], hi[2][c + 1]} - oz) * rz;
-#pragma unroll
-  for (int k = 0; k < 2; k++) {
-    float nx = __builtin_fminf(ax[k], bx[k]), fx = __builtin_fmaxf(ax[k], bx[k]);
-    float ny = __builtin_fminf(ay[k], by[k]), fy = __builtin_fmaxf(ay[k], by[k]);
-    float nz = __builtin_fminf(az[k], bz[k]), fz = __builtin_fmaxf(az[k], bz[k]);
-    if (SKIP) {
-      nx = r.skip0 ? -RT_INF : nx;
-      fx = r.skip0 ? RT_INF : fx;
-      ny = r.skip1 ? -RT_INF : ny;
-      fy = r.skip1 ? RT_INF : fy;
-      nz = r.skip2 ? -RT_INF : nz;
-      fz = r.skip2 ? RT_INF : fz;
-    }
-    tn[k] = __builtin_fmaxf(__builtin_fmaxf(nx, ny), nz);
-    tf[k] = __builtin_fminf(__builtin_fminf(fx, fy), fz);
-  }
-}
-
 // sure_in: the reference accepts (tf >= 0, and tn <= tf decided outside a 2^-20 relative
 // band); sure_out: it rejects.  Neither: box_exact decides (NaN lands here too).  The sign of
 // each bound is exact (RN(b - o) * rcp(d) has the sign of the reference's quotient), and
@@ -189,18 +153,14 @@ __device__ __forceinline__ void decide_sure(float tn, float tf, bool& sure_in, b
   sure_out = (tf < 0.0f) | (d > band);
 }
 
-__device__ __forceinline__ void decide_fast(float tn, float tf, bool& accept, bool& undecided) {
-  bool out;
-  decide_sure(tn, tf, accept, out);
-  undecided = !(accept | out);
-}
-
 template <bool SKIP>
 __device__ __forceinline__ void slab_fast(const float* b, const LaneRay& r, float& tn,
                                           bool& accept, bool& undecided) {
   float tf;
   slab_span<SKIP>(b, r, tn, tf);
-  decide_fast(tn, tf, accept, undecided);
+  bool out;
+  decide_sure(tn, tf, accept, out);
+  undecided = !(accept | out);
 }
 
 // Culling-tree boxes (accel_build.cpp) contain every reference box below them.  If the
@@ -222,11 +182,6 @@ __device__ __forceinline__ float det3(V3 c1, V3 c2, V3 c3) {
          c3.x * (c1.y * c2.z - c2.y * c1.z);
 }
 
-// det3(a1, a2, c3) with the c3-free minor `cx` = a1.y*a2.z - a2.y*a1.z precomputed (same bits)
-__device__ __forceinline__ float det3_cx(V3 c1, V3 c2, V3 c3, float cx) {
-  return c1.x * (c2.y * c3.z - c3.y * c2.z) + c2.x * (c3.y * c1.z - c1.y * c3.z) + c3.x * cx;
-}
-
 // Correctly rounded n / det for the three numerators with ONE reciprocal.  gfx950's IEEE
 // division is v_div_scale (num, den), y = v_rcp, e = fma(-den, y, 1), y1 = fma(e, y, y),
 // q = num * y1, r = fma(-den, q, num), q1 = fma(r, y1, q), r1 = fma(-den, q1, num),
@@ -234,11 +189,10 @@ __device__ __forceinline__ float det3_cx(V3 c1, V3 c2, V3 c3, float cx) {
 // limits, v_div_scale returns its operand unchanged with VCC = 0 and v_div_fmas is a plain
 // fma, so the sequence below (which keeps v_div_fixup: it gives a zero numerator the sign
 // num ^ den) yields the bits of `/`; only the reciprocal refinement y1 depends on det alone,
-// and it is shared.  Range: 2^-40 <= |det|
-// <= 2^40 is checked here; numerators are 0 or 2^-49 <= |n| <= 2^49 by r.quot (every v0 and
-// origin coordinate is 0 or in [2^-26, 2^48]).  Then |n / det| lies in [2^-89, 2^89],
-// exponent differences stay below 96 and nothing is subnormal, so none of v_div_scale's
-// scaling cases can arise.  Any other lane takes `/`.
+// and it is shared.  Range: 2^-40 <= |det| <= 2^40 is checked here; numerators are 0 or
+// 2^-49 <= |n| <= 2^49 by r.quot (every v0 and origin coordinate is 0 or in [2^-26, 2^48]).
+// Then |n / det| lies in [2^-89, 2^89], exponent differences stay below 96 and nothing is
+// subnormal, so none of v_div_scale's scaling cases can arise.  Any other lane takes `/`.
 __device__ __forceinline__ float quot_step(float n, float det, float y1) {
   const float q = n * y1;
   const float r = __builtin_fmaf(-det, q, n);
@@ -248,7 +202,6 @@ __device__ __forceinline__ float quot_step(float n, float det, float y1) {
 }
 
 __device__ __forceinline__ V3 tri_quotients(V3 n, float det, bool quot) {
-#ifndef RT_EXP_IEEEDIV
   const float ad = __builtin_fabsf(det);
   if (quot && ad >= 0x1p-40f && ad <= 0x1p40f) {
     const float y = __builtin_amdgcn_rcpf(det);
@@ -256,41 +209,21 @@ __device__ __forceinline__ V3 tri_quotients(V3 n, float det, bool quot) {
     const float y1 = __builtin_fmaf(e, y, y);
     return v3(quot_step(n.x, det, y1), quot_step(n.y, det, y1), quot_step(n.z, det, y1));
   }
-#endif
   return n / det;
 }
 
-__device__ __forceinline__ bool tri_test(V3 v0, V3 a1, V3 a2, float cx, const LaneRay& r,
-                                         float& t) {
-#ifndef RT_EXP_CX
-#define det3_cx(c1, c2, c3, cx) det3(c1, c2, c3)
-#endif
-  const float det = det3_cx(a1, a2, r.d, cx);
-#ifndef RT_EXP_BRANCHY  // (RT_EXP_BRANCHY: the early-exit form, for A/B)
-  // Branch-free: every value is computed and the reference's early exits (Triangle.cpp:46-62)
-  // become one predicate with the same comparisons (a NaN fails them as there).  No
-  // exec-mask save/restore per exit; with det == 0 the quotients are inf/NaN and unused.
+// Branch-free: every value is computed and the reference's early exits (Triangle.cpp:46-62)
+// become one predicate with the same comparisons (a NaN fails them as there).  With det == 0
+// the quotients are inf/NaN and unused.
+__device__ __forceinline__ bool tri_test(V3 v0, V3 a1, V3 a2, const LaneRay& r, float& t) {
+  const float det = det3(a1, a2, r.d);
   const V3 b = tri_quotients(v0 - r.o, det, r.quot);
   const float beta = det3(b, a2, r.d);
   const float gamma = det3(a1, b, r.d);
-  const float tt = det3_cx(a1, a2, b, cx);
+  const float tt = det3(a1, a2, b);
   t = tt;
   return (det != 0.0f) & !((beta < 0.0f) | (beta > 1.0f)) &
          !((gamma < 0.0f) | (beta + gamma > 1.0f)) & (tt > 0.0f);
-#else
-  if (det == 0.0f) return false;
-  const V3 b = tri_quotients(v0 - r.o, det, r.quot);
-  const float beta = det3(b, a2, r.d);
-  if (beta < 0.0f || beta > 1.0f) return false;
-  const float gamma = det3(a1, b, r.d);
-  if (gamma < 0.0f || beta + gamma > 1.0f) return false;
-  const float tt = det3_cx(a1, a2, b, cx);
-  if (tt > 0.0f) {
-    t = tt;
-    return true;
-  }
-  return false;
-#endif
 }
 
 // HW2/Sphere.h:26-52 — true for any real root, including a negative one.
@@ -314,177 +247,63 @@ __device__ __forceinline__ bool sphere_test(V3 c, float radius, const LaneRay& r
 
 // Shape::intersect of one leaf.  SPHERES == false: the scene has no spheres (host flag), so
 // the sphere code is not compiled into the traversal loop.
-// RT_EXP_X16: fetch a node / prim record with ONE s_load_dwordx16 (waited at once) instead of
-// the 4 loads of 1-8 dwords the compiler splits it into.
-typedef int v16i __attribute__((ext_vector_type(16)));
-__device__ __forceinline__ v16i sload16(const void* p) {
-  v16i r;
-  asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
-  return r;
-}
-
 template <bool SPHERES>
 __device__ __forceinline__ bool leaf_test(const DevPrim* __restrict__ prims, int leaf,
                                           const LaneRay& r, float& t) {
-#ifdef RT_EXP_X16
-  const v16i w = sload16(prims + leaf);
-  DevPrim p;
-  p.v0[0] = __int_as_float(w[0]);
-  p.v0[1] = __int_as_float(w[1]);
-  p.v0[2] = __int_as_float(w[2]);
-  p.a1[0] = __int_as_float(w[3]);
-  p.a1[1] = __int_as_float(w[4]);
-  p.a1[2] = __int_as_float(w[5]);
-  p.a2[0] = __int_as_float(w[6]);
-  p.a2[1] = __int_as_float(w[7]);
-  p.a2[2] = __int_as_float(w[8]);
-  p.kind = w[9];
-  p.material = w[10];
-  p.cx = __int_as_float(w[11]);
-#else
   const DevPrim& p = prims[leaf];
-#endif
   const V3 v0 = ld3(p.v0);
-  if (!SPHERES || p.kind == kPrimTriangle) return tri_test(v0, ld3(p.a1), ld3(p.a2), p.cx, r, t);
+  if (!SPHERES || p.kind == kPrimTriangle) return tri_test(v0, ld3(p.a1), ld3(p.a2), r, t);
   return sphere_test(v0, p.a1[0], r, t);
 }
 
 // ------------------------------------------------------------------ traversal stack
-// Wave-uniform (node, R lane-masks) entries — R rays per lane.  DEEP == false: entry i lives
-// in VGPR lane i (select-on-lane push / v_readlane pop, no memory traffic, 64 deep).
-// DEEP == true: a per-wave LDS array of kDeepStack entries for trees deeper than 64 levels
-// (lane 0 writes, all lanes read the broadcast word; LDS ops of one wave complete in order).
+// Wave-uniform (node, lane-mask) entries.  DEEP == false: entry i lives in VGPR lane i
+// (select-on-lane push / v_readlane pop, no memory traffic, 64 deep).  DEEP == true: a
+// per-wave LDS array of kDeepStack entries for trees deeper than 64 levels (lane 0 writes,
+// all lanes read the broadcast word; LDS ops of one wave complete in order).
 constexpr int kDeepStack = 1024;
+constexpr int kDeepWords = 3;  // node, mask lo, mask hi
 
-template <bool DEEP, int R>
+template <bool DEEP>
 struct WaveStack {
-  static constexpr int kWords = 1 + 2 * R;
   int node = 0;
-  unsigned mlo[R] = {}, mhi[R] = {};
+  unsigned mlo = 0, mhi = 0;
   int sp = 0;  // wave-uniform
   int* lds = nullptr;
 
-  __device__ __forceinline__ void push(int n, const uint64_t (&m)[R]) {
+  __device__ __forceinline__ void push(int n, uint64_t m) {
     if (!DEEP) {
       const bool mine = lane_id() == sp;  // v_cmp + v_cndmask: lane sp takes the entry
       node = mine ? n : node;
-#pragma unroll
-      for (int k = 0; k < R; k++) {
-        mlo[k] = mine ? (unsigned)m[k] : mlo[k];
-        mhi[k] = mine ? (unsigned)(m[k] >> 32) : mhi[k];
-      }
+      mlo = mine ? (unsigned)m : mlo;
+      mhi = mine ? (unsigned)(m >> 32) : mhi;
     } else if (lane_id() == 0) {
-      lds[kWords * sp] = n;
-#pragma unroll
-      for (int k = 0; k < R; k++) {
-        lds[kWords * sp + 1 + 2 * k] = (int)(unsigned)m[k];
-        lds[kWords * sp + 2 + 2 * k] = (int)(unsigned)(m[k] >> 32);
-      }
+      lds[kDeepWords * sp] = n;
+      lds[kDeepWords * sp + 1] = (int)(unsigned)m;
+      lds[kDeepWords * sp + 2] = (int)(unsigned)(m >> 32);
     }
     sp++;
   }
-  // The oldest entry (lane 0: the shallowest pending subtree) and its removal, for donation
-  // (!DEEP, R == 1 only): entries 1..sp-1 move down one lane.
-  __device__ __forceinline__ void bottom(int& n, uint64_t& m) const {
-    n = __builtin_amdgcn_readlane(node, 0);
-    m = (uint64_t)(unsigned)__builtin_amdgcn_readlane(mlo[0], 0) |
-        ((uint64_t)(unsigned)__builtin_amdgcn_readlane(mhi[0], 0) << 32);
-  }
-  __device__ __forceinline__ void drop_bottom() {
-    const int src = (lane_id() + 1) << 2;
-    node = __builtin_amdgcn_ds_bpermute(src, node);
-    mlo[0] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)mlo[0]);
-    mhi[0] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)mhi[0]);
-    sp--;
-  }
-  __device__ __forceinline__ void pop(int& n, uint64_t (&m)[R]) {
+  __device__ __forceinline__ void pop(int& n, uint64_t& m) {
     sp--;
     if (!DEEP) {
       n = __builtin_amdgcn_readlane(node, sp);
-#pragma unroll
-      for (int k = 0; k < R; k++)
-        m[k] = (uint64_t)(unsigned)__builtin_amdgcn_readlane(mlo[k], sp) |
-               ((uint64_t)(unsigned)__builtin_amdgcn_readlane(mhi[k], sp) << 32);
+      m = (uint64_t)(unsigned)__builtin_amdgcn_readlane(mlo, sp) |
+          ((uint64_t)(unsigned)__builtin_amdgcn_readlane(mhi, sp) << 32);
     } else {
-      n = uniform(lds[kWords * sp]);
-#pragma unroll
-      for (int k = 0; k < R; k++)
-        m[k] = (uint64_t)(unsigned)uniform(lds[kWords * sp + 1 + 2 * k]) |
-               ((uint64_t)(unsigned)uniform(lds[kWords * sp + 2 + 2 * k]) << 32);
+      n = uniform(lds[kDeepWords * sp]);
+      m = (uint64_t)(unsigned)uniform(lds[kDeepWords * sp + 1]) |
+          ((uint64_t)(unsigned)uniform(lds[kDeepWords * sp + 2]) << 32);
     }
   }
-};
-
-// Distance culling (RT_TRAVERSAL_CULL only): skip a child whose approximate entry distance
-// exceeds best_t (1 + 2^-8).  Not proven exact: a triangle whose computed t undershoots its
-// true distance by more than the margin (rays within ~1e-5 rad of its plane) could be missed.
-__device__ __forceinline__ float cull_limit(float t) { return t + t * 0x1p-8f; }
-
-// Node fetch.  Default: the wave-uniform address makes this a scalar (s_load) fetch.
-// RT_EXP_VNODE (experiment): four buffer_load_dwordx4 with the same address on every lane.
-__device__ __forceinline__ DevNode load_node(const DevNode* __restrict__ nodes, int node) {
-#ifdef RT_EXP_VNODE
-  DevNode N;
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  const v4f* src = reinterpret_cast<const v4f*>(nodes + node);
-  const int zero = (int)__builtin_amdgcn_mbcnt_lo(0u, 0u);  // VGPR zero: keep it a vector load
-  const v4f q0 = src[0 + zero];
-  const v4f q1 = src[1 + zero];
-  const v4f q2 = src[2 + zero];
-  const v4f q3 = src[3 + zero];
-  const float f[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
-  for (int a = 0; a < 3; a++)
-    for (int c = 0; c < 2; c++) {
-      N.lo[a][c] = f[2 * a + c];
-      N.hi[a][c] = f[6 + 2 * a + c];
+  // Pop entries until one still has a lane of `alive`; false when the stack runs empty.
+  __device__ __forceinline__ bool pop_live(int& n, uint64_t& m, uint64_t alive) {
+    for (;;) {
+      if (sp == 0) return false;
+      pop(n, m);
+      m &= alive;
+      if (m) return true;
     }
-  N.child[0] = uniform(__float_as_int(q3.x));
-  N.child[1] = uniform(__float_as_int(q3.y));
-  N.axis = 0;
-  N.pad = 0;
-  return N;
-#elif defined(RT_EXP_X16)
-#ifdef RT_EXP_DUP  // scalar-cache pressure probe: a second, redundant fetch of the same node
-  (void)sload16(nodes + node);
-#endif
-  const v16i w = sload16(nodes + node);
-  DevNode N;
-  for (int a = 0; a < 3; a++)
-    for (int c = 0; c < 2; c++) {
-      N.lo[a][c] = __int_as_float(w[2 * a + c]);
-      N.hi[a][c] = __int_as_float(w[6 + 2 * a + c]);
-    }
-  N.child[0] = w[12];
-  N.child[1] = w[13];
-  N.axis = w[14];
-  N.pad = w[15];
-  return N;
-#else
-  return nodes[node];
-#endif
-}
-
-// RT_EXP_PREFETCH: at the start of a visit, touch the children's records (node, or the leaf's
-// 48-B prim, which may straddle two 64-B lines) so they are in the scalar cache when the next
-// visit / the leaf test loads them.  The destination registers are retired after an explicit
-// s_waitcnt at the end of the same visit, so no load is in flight when they are reused.
-struct ChildPrefetch {
-  int a = 0, b = 0, c = 0, d = 0;
-  __device__ __forceinline__ void issue(const DevNode* __restrict__ nodes,
-                                        const DevPrim* __restrict__ prims, int c0, int c1) {
-#ifdef RT_EXP_PREFETCH
-    const char* p0 = c0 >= 0 ? (const char*)(nodes + c0) : (const char*)(prims + ~c0);
-    const char* p1 = c1 >= 0 ? (const char*)(nodes + c1) : (const char*)(prims + ~c1);
-    asm volatile("s_load_dword %0, %1, 0x0" : "=s"(a) : "s"(p0));
-    asm volatile("s_load_dword %0, %1, 0x2c" : "=s"(b) : "s"(p0));
-    asm volatile("s_load_dword %0, %1, 0x0" : "=s"(c) : "s"(p1));
-    asm volatile("s_load_dword %0, %1, 0x2c" : "=s"(d) : "s"(p1));
-#endif
-  }
-  __device__ __forceinline__ void retire() {
-#ifdef RT_EXP_PREFETCH
-    asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(a), "s"(b), "s"(c), "s"(d) : "memory");
-#endif
   }
 };
 
@@ -504,7 +323,7 @@ __device__ bool guard_exact(const RenderParams& P, int child, const LaneRay& r) 
   return true;
 }
 
-// One packet visit of a node of either tree, per child:
+// One packet visit of a binary node of either tree, per child:
 //   * leaf of a reference node: every lane in the node tests it (leaves have no box; the slot
 //     holds a +-1e30 box that every normalised ray accepts, so no special case is needed);
 //   * inner child of a reference node: the reference's box test (fast, else box_exact);
@@ -541,108 +360,61 @@ __device__ __forceinline__ void visit_node(const RenderParams& P, const DevNode&
   }
 }
 
-template <int R>
-__device__ __forceinline__ uint64_t any_of(const uint64_t (&m)[R]) {
-  uint64_t a = 0;
-#pragma unroll
-  for (int k = 0; k < R; k++) a |= m[k];
-  return a;
-}
-
-// Pick the next node: near child first (judged by the first lane of the first ray entering
-// both), the far one pushed; with neither, pop (masks restricted to `alive`).  Returns false
-// when the traversal is over.
-template <bool DEEP, int R>
-__device__ __forceinline__ bool advance(WaveStack<DEEP, R>& st, int c0, int c1,
-                                        const uint64_t (&m0)[R], const uint64_t (&m1)[R],
-                                        const float (&t0)[R], const float (&t1)[R], int& node,
-                                        uint64_t (&m)[R], const uint64_t (&alive)[R]) {
-  const bool e0 = any_of(m0) != 0, e1 = any_of(m1) != 0;
-  if (e0 && e1) {
-    int kk = 0;
-    uint64_t both = m0[0] & m1[0];
-#pragma unroll
-    for (int k = 1; k < R; k++)
-      if (!both && (m0[k] & m1[k])) {
-        both = m0[k] & m1[k];
-        kk = k;
-      }
+// Pick the next node after a binary visit: near child first (judged by the first lane that
+// enters both), the far one pushed; with neither, pop (masks restricted to `alive`).  Returns
+// false when the traversal is over.
+template <bool DEEP>
+__device__ __forceinline__ bool advance(WaveStack<DEEP>& st, int c0, int c1, uint64_t m0,
+                                        uint64_t m1, float t0, float t1, int& node, uint64_t& m,
+                                        uint64_t alive) {
+  if (m0 && m1) {
+    const uint64_t both = m0 & m1;
     bool near1 = false;
     if (both) {
       const int f = __builtin_ctzll(both);
-      float f0 = 0.0f, f1 = 0.0f;
-#pragma unroll
-      for (int k = 0; k < R; k++)
-        if (k == kk) {
-          f0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t0[k]), f));
-          f1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t1[k]), f));
-        }
+      const float f0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t0), f));
+      const float f1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t1), f));
       near1 = f1 < f0;
     }
     if (near1) {
       st.push(c0, m0);
       node = c1;
-#pragma unroll
-      for (int k = 0; k < R; k++) m[k] = m1[k];
+      m = m1;
     } else {
       st.push(c1, m1);
       node = c0;
-#pragma unroll
-      for (int k = 0; k < R; k++) m[k] = m0[k];
+      m = m0;
     }
     return true;
   }
-  if (e0 || e1) {
-    node = e0 ? c0 : c1;
-#pragma unroll
-    for (int k = 0; k < R; k++) m[k] = e0 ? m0[k] : m1[k];
+  if (m0 || m1) {
+    node = m0 ? c0 : c1;
+    m = m0 ? m0 : m1;
     return true;
   }
-  for (;;) {
-    if (st.sp == 0) return false;
-    st.pop(node, m);
-#pragma unroll
-    for (int k = 0; k < R; k++) m[k] &= alive[k];
-    if (any_of(m)) return true;
-  }
+  return st.pop_live(node, m, alive);
 }
 
 // ------------------------------------------------------------------ batched leaf tests
 // A packet reaches a leaf with only the few lanes whose rays pass over that triangle (C3:
 // ~14 of 64), so testing leaves one at a time runs the triangle test at ~20% SIMD efficiency.
-// With R == 1 the traversal instead queues (lane, leaf) pairs in a per-wave LDS list and runs
-// them 64 at a time, one pair per lane (the owner's ray fetched with ds_bpermute, the
-// triangle with a per-lane load), once 64 are pending and when the walk ends.  Results land
-// per ray by LDS atomics: closest hit = atomic min of the key (t bits << 32 | leaf), which for
-// 0 < t orders exactly like the reference's (t, DFS leaf) rule; shadow = atomic or.  The
-// queued tests are the ones the reference makes, so the answer is unchanged; only FAST
-// culling sees best_t a little later (after each flush), which can only cull less.
-// RT_EXP_NOBATCH: leaves tested where they are met (the R > 1 path always does).
+// The traversal instead queues (lane, leaf) pairs in a per-wave LDS list and runs them 64 at a
+// time, one pair per lane (the owner's ray fetched with ds_bpermute, the triangle with a
+// per-lane load), once kBatchFlush are pending and when the walk ends.  Results land per ray
+// by LDS atomics: closest hit = atomic min of the key (t bits << 32 | leaf), which for 0 < t
+// orders exactly like the reference's (t, DFS leaf) rule; shadow = a flag.  The queued tests
+// are the ones the reference makes, so the answer is unchanged.
 #ifndef RT_BATCH_FLUSH
 #define RT_BATCH_FLUSH 64
 #endif
-constexpr int kBatchFlush = RT_BATCH_FLUSH;  // run the queue once this many tests are pending
-constexpr int kBatchCap = kBatchFlush + 256;  // < kBatchFlush pending + 2 pairs x 64 per visit
-#ifndef RT_SHADOW_FLUSH  // shadow rays: a smaller queue finds occluders (and stops lanes) sooner
-#define RT_SHADOW_FLUSH RT_BATCH_FLUSH
-#endif
-constexpr int kShadowFlush = RT_SHADOW_FLUSH;
-static_assert(kShadowFlush <= kBatchFlush, "the queue is sized for kBatchFlush");
-#ifndef RT_TRACE_WAVES
-#define RT_TRACE_WAVES 4
-#endif
+constexpr int kBatchFlush = RT_BATCH_FLUSH;   // run the queue once this many tests are pending
+constexpr int kBatchCap = kBatchFlush + 256;  // < kBatchFlush pending + 4 leaves x 64 per visit
+constexpr int kShadowFlush = kBatchFlush;
 
 struct WaveLeafLds {
   unsigned long long q[kBatchCap];  // lo 32: leaf index, hi 32: lane
   unsigned long long key[64];       // per lane: closest-hit key, or shadow flag
 };
-
-
-#if defined(RT_EXP_NOBATCH)
-constexpr bool kBatchLeaves = false;
-#else
-constexpr bool kBatchLeaves = true;
-#endif
 
 constexpr unsigned long long kNoHitKey = (0x7f800000ull << 32) | 0xffffffffull;  // (+inf, -1)
 
@@ -687,22 +459,31 @@ __device__ __forceinline__ void batch_flush(WaveLeafLds& L, int n, const DevPrim
   }
 }
 
-// ------------------------------------------------------------------ wide culling nodes
-// Kernels with the batched leaf queue and one ray per lane walk the 4-wide culling tree
-// (accel_build.cpp collapse_wide); others get the binary one.
-bool wide_nodes_supported() { return kBatchLeaves && kRaysPerLane == 1; }
+// Queues the leaf tests of a visited binary node's leaf children for the lanes of h0 / h1.
+__device__ __forceinline__ void queue_binary_leaves(WaveLeafLds& L, int& pending, const DevNode& N,
+                                                    bool h0, bool h1, uint64_t alive, Diag& dg) {
+  if (N.child[0] < 0) {
+    const uint64_t b = ballot(h0) & alive;
+    batch_push(L, pending, ~N.child[0], b);
+    if (N.pad & kAccelPair0) batch_push(L, pending, ~N.child[0] + 1, b);
+    DIAG(const int nl = 1 + ((N.pad & kAccelPair0) != 0); dg.leaves += nl;
+         dg.leaf_lanes += nl * __builtin_popcountll(b));
+  }
+  if (N.child[1] < 0) {
+    const uint64_t b = ballot(h1) & alive;
+    batch_push(L, pending, ~N.child[1], b);
+    if (N.pad & kAccelPair1) batch_push(L, pending, ~N.child[1] + 1, b);
+    DIAG(const int nl = 1 + ((N.pad & kAccelPair1) != 0); dg.leaves += nl;
+         dg.leaf_lanes += nl * __builtin_popcountll(b));
+  }
+}
 
+// ------------------------------------------------------------------ wide culling nodes
 // The whole 128-B node in one round trip: two s_load_dwordx16 and one wait.  Left to itself
 // the compiler splits the record into ~14 loads of 1-8 dwords in three dependent rounds (and,
-// short of SGPRs, reloads the first slot's box after the flags test).  RT_WIDE_SLOAD=0 for A/B.
-#ifndef RT_WIDE_SLOAD
-#define RT_WIDE_SLOAD 1
-#endif
-#ifndef RT_WIDE_PK  // slab spans of a wide node's slots two at a time (packed fp32)
-#define RT_WIDE_PK 0
-#endif
+// short of SGPRs, reloads the first slot's box after the flags test).
+typedef int v16i __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ DevNode4 load_node4(const DevNode* __restrict__ nodes, int idx) {
-#if RT_WIDE_SLOAD
   v16i a, b;
   const void* p = nodes + idx;
   asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
@@ -719,24 +500,21 @@ __device__ __forceinline__ DevNode4 load_node4(const DevNode* __restrict__ nodes
   }
   N.flags = b[12];
   return N;
-#else
-  return *reinterpret_cast<const DevNode4*>(nodes + idx);
-#endif
 }
 
-// One packet visit of a wide culling node (R == 1, batched leaves), slot by slot with the
-// binary tree's rules (visit_node): a guarded slot accepts on a decided guard test (else
-// guard_exact), and its leaf or leaf pair goes straight to the leaf queue; an inner slot
-// culls only on a sure reject.  Of the entered inner slots one becomes `node` (SHADOW: the
-// nearest by the entry distance of the first entering lane, so occluders turn up early) and
-// the others are pushed.  `alive`: lanes still searching.  Up to 4 slots x 2 leaves x 64 lanes
-// of leaf tests are queued per visit, so the queue is run in between when it could overflow.
-// Returns false when the walk is over.
+// One packet visit of a wide culling node, slot by slot with the binary tree's rules
+// (visit_node): a guarded slot accepts on a decided guard test (else guard_exact), and its
+// leaf or leaf pair goes straight to the leaf queue; an inner slot culls only on a sure
+// reject.  Of the entered inner slots one becomes `node` (SHADOW: the nearest by the entry
+// distance of the first entering lane, so occluders turn up early) and the others are pushed.
+// `alive`: lanes still searching.  Up to 4 slots x 2 leaves x 64 lanes of leaf tests are
+// queued per visit, so the queue is run in between when it could overflow.  Returns false when
+// the walk is over.
 template <bool SKIP, bool SHADOW, bool DEEP, bool SPHERES>
 __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode* __restrict__ nodes,
                                            const DevPrim* __restrict__ prims, WaveLeafLds& L,
                                            int& pending, const LaneRay& r, float thr, int& node,
-                                           uint64_t& m, uint64_t alive, WaveStack<DEEP, 1>& st,
+                                           uint64_t& m, uint64_t alive, WaveStack<DEEP>& st,
                                            Diag& dg) {
   const DevNode4 N = load_node4(nodes, node & ~kWideTag);
   const bool in = (m >> lane_id()) & 1;
@@ -745,21 +523,12 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
   int nxt = -1;
   uint64_t nm = 0;
   float nkey = 0.0f;
-#if RT_WIDE_PK
-  float tn4[4], tf4[4];  // all four spans up front, two slots per packed instruction
-  slab_span2<SKIP>(N.lo, N.hi, 0, r, tn4, tf4);
-  slab_span2<SKIP>(N.lo, N.hi, 2, r, tn4 + 2, tf4 + 2);
-#endif
 #pragma unroll
   for (int c = 0; c < 4; c++) {
     if (!(fl & (kWideValid << c))) continue;
-#if RT_WIDE_PK
-    const float tn = tn4[c], tf = tf4[c];
-#else
     const float b[6] = {N.lo[0][c], N.lo[1][c], N.lo[2][c], N.hi[0][c], N.hi[1][c], N.hi[2][c]};
     float tn, tf;
     slab_span<SKIP>(b, r, tn, tf);
-#endif
     bool sin, sout;
     decide_sure(tn, tf, sin, sout);
     const int ch = N.child[c];
@@ -788,26 +557,22 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
       DIAG(dg.leaves += 1 + pair; dg.leaf_lanes += (1 + pair) * __builtin_popcountll(hm));
       continue;
     }
-    uint64_t mm[1] = {hm};
     if (SHADOW) {
       const float key = __int_as_float(
           __builtin_amdgcn_readlane(__float_as_int(tn), (int)__builtin_ctzll(hm)));
       if (nxt < 0 || key < nkey) {
-        if (nxt >= 0) {
-          uint64_t pm[1] = {nm};
-          st.push(nxt, pm);
-        }
+        if (nxt >= 0) st.push(nxt, nm);
         nxt = ch;
         nm = hm;
         nkey = key;
       } else {
-        st.push(ch, mm);
+        st.push(ch, hm);
       }
     } else if (nxt < 0) {
       nxt = ch;
       nm = hm;
     } else {
-      st.push(ch, mm);
+      st.push(ch, hm);
     }
   }
   if (nxt >= 0) {
@@ -815,474 +580,160 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
     m = nm;
     return true;
   }
-  for (;;) {
-    if (st.sp == 0) return false;
-    uint64_t mm[1];
-    st.pop(node, mm);
-    m = mm[0] & alive;
-    if (m) return true;
-  }
-}
-
-// ------------------------------------------------------------------ subtree sharing
-// A workgroup's packets cost unequal amounts (tools/timeline.py: C3 primary packets take 60 to
-// 265 us), and a workgroup keeps its slot until its last wave ends, so waves that finish early
-// idle while a heavy packet runs: the C3 primary kernel held ~90 % of its wave slots in the bulk
-// of the frame and spent its last 40 % draining.  With sharing, the waves of a workgroup split
-// their packets' traversals between them through LDS.  A wave without work raises its bit in
-// `want` and waits at its inbox; a traversing wave that sees a raised bit (checked every 4th
-// visit) claims that wave (atomic and of the bit) and hands it its OLDEST stack entry — the
-// shallowest pending subtree — as (owner packet, light, node, lane mask).  The helper rebuilds
-// the owner packet's rays bit for bit and traverses that subtree exactly as the owner would.
-// Each piece's answer merges into the owner's per-lane result in LDS — closest hit by 64-bit
-// min of the (t bits, DFS leaf) key (the reference's rule, §4.1), shadow by or — and after a
-// workgroup barrier every wave writes its own packet.  A claimed wave's bit stays clear until
-// it is idle again, so `want` == all waves means nobody traverses and nobody can hand out work:
-// every wave then leaves.  Workgroup-local and lock-free: LDS atomics only (a lock taken and
-// released in a polling loop measured as a livelock on gfx950).
-struct ShareEntry {
-  unsigned long long mask;
-  int node, owner, light, pad;
-};
-
-template <int W>
-struct BlockShare {
-  int want;     // bit i: wave i waits for work
-  int flag[W];  // inbox i is full
-  int sel[W];   // each wave's own packet (tile), -1 for none
-  ShareEntry box[W];
-  unsigned long long res[W][64];  // per packet and lane: primary key / shadow light bits
-};
-
-__device__ __forceinline__ int lds_load(const int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-struct NoDonor {
-  static constexpr bool kOn = false;
-  __device__ __forceinline__ bool tick() { return false; }
-  __device__ __forceinline__ bool donate(int, uint64_t) { return false; }
-};
-
-// The donation policy of one traversal piece in a sharing workgroup.
-template <int W>
-struct Sharer {
-  static constexpr bool kOn = true;
-  BlockShare<W>* S;
-  int owner, light, visits;  // wave-uniform
-  __device__ __forceinline__ bool tick() {
-#ifdef RT_EXP_NODONATE
-    return false;
-#else
-    return (++visits & 3) == 0 && lds_load(&S->want) != 0;
-#endif
-  }
-  __device__ __forceinline__ bool donate(int node, uint64_t mask) {
-    int ok = 0;
-    if (lane_id() == 0) {
-      int m = lds_load(&S->want);
-      while (m) {
-        const int i = __builtin_ctz((unsigned)m), bit = 1 << i;
-        const int old = atomicAnd(&S->want, ~bit);
-        if (old & bit) {  // wave i is ours
-          S->box[i].mask = mask;
-          S->box[i].node = node;
-          S->box[i].owner = owner;
-          S->box[i].light = light;
-          __hip_atomic_store(&S->flag[i], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-          ok = 1;
-          break;
-        }
-        m = old & ~bit;
-      }
-    }
-    return uniform(ok) != 0;
-  }
-};
-
-// Called by a wave whose current piece is done: raises its want bit and waits for an entry.
-// False once every wave of the workgroup wants work (no one is left to hand any out).
-template <int W>
-__device__ __forceinline__ bool share_next(BlockShare<W>& S, int& owner, int& node, uint64_t& mask,
-                                           int& light) {
-  const int wv = (int)threadIdx.x >> 6;
-  int got = 0, o = 0, n = 0, l = 0;
-  unsigned lo = 0, hi = 0;
-  if (lane_id() == 0) {
-    atomicOr(&S.want, 1 << wv);
-    for (;;) {
-      if (__hip_atomic_load(&S.flag[wv], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-        const ShareEntry& e = S.box[wv];
-        lo = (unsigned)e.mask;
-        hi = (unsigned)(e.mask >> 32);
-        n = e.node;
-        o = e.owner;
-        l = e.light;
-        __hip_atomic_store(&S.flag[wv], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        got = 1;
-        break;
-      }
-      if (lds_load(&S.want) == (1 << W) - 1) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  if (!uniform(got)) return false;
-  owner = uniform(o);
-  node = uniform(n);
-  light = uniform(l);
-  mask = (uint64_t)(unsigned)uniform((int)lo) | ((uint64_t)(unsigned)uniform((int)hi) << 32);
-  return true;
+  return st.pop_live(node, m, alive);
 }
 
 // ------------------------------------------------------------------ closest hit
-// R rays per lane.  Returns the reference's (t, leaf) for every active ray: leaf < 0 = miss.
-// DN: the donation policy (NoDonor, or Sharer in sharing workgroups, R == 1 and !DEEP only);
-// start_node >= 0: traverse the shared subtree (start_node, start_mask) instead of the tree.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R, bool CULL = false,
-          class DN = NoDonor, bool WO = false>
-__device__ __forceinline__ void closest_hit(const RenderParams& P,
-                                            const DevNode* __restrict__ nodes,
-                                            const DevPrim* __restrict__ prims, int* spill, WaveLeafLds& L,
-                                            const LaneRay (&r)[R], const bool (&active)[R],
-                                            float (&best_t)[R], int (&best_leaf)[R], Diag& dg,
-                                            DN& dn, int start_node = -1,
-                                            uint64_t start_mask = 0) {
-  static_assert(!DN::kOn || (R == 1 && !DEEP), "donation needs the one-ray-per-lane lane stack");
-#pragma unroll
-  for (int k = 0; k < R; k++) {
-    best_t[k] = RT_INF;
-    best_leaf[k] = -1;
-  }
+// The reference's (t, leaf) for every active ray: leaf < 0 = miss.  FAST: the culling tree
+// over reference treelets (WO: every node the fast walk meets is a 4-wide node); otherwise the
+// reference tree itself.
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, bool WO>
+__device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode* __restrict__ nodes,
+                                            const DevPrim* __restrict__ prims, int* spill,
+                                            WaveLeafLds& L, const LaneRay& r, bool active,
+                                            float& best_t, int& best_leaf, Diag& dg) {
+  best_t = RT_INF;
+  best_leaf = -1;
   if (P.root_kind != kRootNode) {  // the root IS the primitive (BVH.h:13-14): its own rule
-#pragma unroll
-    for (int k = 0; k < R; k++) {
-      float t;
-      if (active[k] && leaf_test<SPHERES>(prims, P.root_ref, r[k], t)) {
-        best_t[k] = t;
-        best_leaf[k] = P.root_ref;
-      }
+    float t;
+    if (active && leaf_test<SPHERES>(prims, P.root_ref, r, t)) {
+      best_t = t;
+      best_leaf = P.root_ref;
     }
     return;
   }
-  const bool accel = FAST && P.accel_root >= 0;  // culling tree over treelets (§4.4)
-  const bool task = DN::kOn && start_node >= 0;
-  uint64_t m[R];
-  if (task) {
-    m[0] = start_mask & ballot(active[0]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < R; k++) {
-      float tn, tf;
-      bool acc, und;
-      if (accel) {
-        slab_span<SKIP>(P.accel_box, r[k], tn, tf);
-        m[k] = ballot(active[k] && decide_cull(tn, tf));
-      } else {
-        slab_fast<SKIP>(P.root_box, r[k], tn, acc, und);
-        m[k] = ballot(active[k] && (acc || (und && box_exact(P.root_box, r[k]))));
-      }
+  const bool accel = FAST && P.accel_root >= 0;  // culling tree over treelets (§4.2)
+  uint64_t m;
+  {
+    float tn, tf;
+    bool acc, und;
+    if (accel) {
+      slab_span<SKIP>(P.accel_box, r, tn, tf);
+      m = ballot(active && decide_cull(tn, tf));
+    } else {
+      slab_fast<SKIP>(P.root_box, r, tn, acc, und);
+      m = ballot(active && (acc || (und && box_exact(P.root_box, r))));
     }
   }
-  if (!any_of(m)) return;
+  if (!m) return;
   const int lane = lane_id();
-  WaveStack<DEEP, R> st;
+  WaveStack<DEEP> st;
   st.lds = spill;
-  uint64_t everyone[R];
-#pragma unroll
-  for (int k = 0; k < R; k++) everyone[k] = ~0ull;
-  constexpr bool batch = kBatchLeaves && R == 1;
   int pending = 0;
-  if (batch) L.key[lane] = kNoHitKey;
-  int node = task ? start_node : (accel ? P.accel_root : P.root_ref);
+  L.key[lane] = kNoHitKey;
+  int node = accel ? P.accel_root : P.root_ref;
   for (;;) {
-    if constexpr (batch) {  // between visits: only the ray, the stack and best_t are live
-      if (pending >= kBatchFlush) {
-        batch_flush<false, SPHERES>(L, pending, prims, r[0], 0.0f);
-        pending = 0;
-        const unsigned long long key = L.key[lane];
-        best_t[0] = __uint_as_float((unsigned)(key >> 32));
-        best_leaf[0] = (int)(unsigned)key;
-      }
+    if (pending >= kBatchFlush) {  // between visits: only the ray and the stack are live
+      batch_flush<false, SPHERES>(L, pending, prims, r, 0.0f);
+      pending = 0;
     }
-    if constexpr (DN::kOn) {  // hand the oldest pending subtree to the work queue
-      if (dn.tick() && st.sp > 0) {
-        int n0;
-        uint64_t m0;
-        st.bottom(n0, m0);
-        if (dn.donate(n0, m0)) st.drop_bottom();
-      }
-    }
-    if constexpr (batch && FAST) {  // a wide culling node (WO: every node the walk meets is one)
+    if constexpr (FAST) {
       if (WO || (node & kWideTag)) {
-        uint64_t mm = m[0];
-        const bool more = visit_wide<SKIP, false, DEEP, SPHERES>(P, nodes, prims, L, pending, r[0],
-                                                                0.0f, node, mm, ~0ull, st, dg);
-        m[0] = mm;
-        if (!more) break;
+        if (!visit_wide<SKIP, false, DEEP, SPHERES>(P, nodes, prims, L, pending, r, 0.0f, node, m,
+                                                    ~0ull, st, dg))
+          break;
         continue;
       }
     }
-    const DevNode N = load_node(nodes, node);
-    ChildPrefetch pf;
-    pf.issue(nodes, prims, N.child[0], N.child[1]);
-    bool h0[R], h1[R];
-    float t0[R], t1[R];
-#pragma unroll
-    for (int k = 0; k < R; k++)
-      visit_node<SKIP>(P, N, r[k], (m[k] >> lane) & 1, h0[k], h1[k], t0[k], t1[k]);
-    DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(any_of(m));
-         const int nl0 = N.child[0] < 0 ? 1 + ((N.pad & kAccelPair0) != 0) : 0;
-         const int nl1 = N.child[1] < 0 ? 1 + ((N.pad & kAccelPair1) != 0) : 0;
-         dg.leaves += nl0 + nl1;
-         dg.leaf_lanes += nl0 * __builtin_popcountll(ballot(h0[0])) +
-                          nl1 * __builtin_popcountll(ballot(h1[0])));
-    if constexpr (batch) {  // queue the leaf children's tests; run them 64 at a time
-      if (N.child[0] < 0) {
-        const uint64_t b = ballot(h0[0]);
-        batch_push(L, pending, ~N.child[0], b);
-        if (N.pad & kAccelPair0) batch_push(L, pending, ~N.child[0] + 1, b);
-      }
-      if (N.child[1] < 0) {
-        const uint64_t b = ballot(h1[0]);
-        batch_push(L, pending, ~N.child[1], b);
-        if (N.pad & kAccelPair1) batch_push(L, pending, ~N.child[1] + 1, b);
-      }
-    } else {
-#ifndef RT_EXP_NOLEAF
-#pragma unroll 1
-    for (int slot = 0; slot < 4; slot++) {  // leaf children: Shape::intersect, 0 < t < best
-      const int side = slot >> 1;             // (slot & 1: the second leaf of a leaf pair)
-      const int c = side ? N.child[1] : N.child[0];
-      if (c < 0 && (!(slot & 1) || (N.pad & (side ? kAccelPair1 : kAccelPair0)))) {
-        const int leaf = ~c + (slot & 1);
-#pragma unroll
-        for (int k = 0; k < R; k++) {
-          const bool tests = side ? h1[k] : h0[k];
-          float t = 0.0f;
-#ifndef RT_EXP_BRANCHY  // (RT_EXP_BRANCHY: the early-exit form, for A/B)
-          if (ballot(tests)) {  // one wave-uniform branch; the update itself is a select
-            const bool hit = leaf_test<SPHERES>(prims, leaf, r[k], t);
-            const bool take = tests & hit & (t > 0.0f) & (t < RT_INF) &
-                              ((t < best_t[k]) | ((t == best_t[k]) & (leaf < best_leaf[k])));
-            best_t[k] = take ? t : best_t[k];
-            best_leaf[k] = take ? leaf : best_leaf[k];
-          }
-#else
-          if (tests && leaf_test<SPHERES>(prims, leaf, r[k], t) && t > 0.0f && t < RT_INF &&
-              (t < best_t[k] || (t == best_t[k] && leaf < best_leaf[k]))) {
-            best_t[k] = t;
-            best_leaf[k] = leaf;
-          }
-#endif
-        }
-      }
-    }
-#else
-#pragma unroll
-    for (int k = 0; k < R; k++) best_leaf[k] -= (int)((m[k] >> lane) & 1);  // keep it observable
-#endif
-    }
-    uint64_t m0[R], m1[R];
-#pragma unroll
-    for (int k = 0; k < R; k++) {  // leaves are done; only inner children are entered
-      h0[k] &= N.child[0] >= 0;
-      h1[k] &= N.child[1] >= 0;
-      if (FAST && CULL) {
-        const float lim = cull_limit(best_t[k]);
-        h0[k] = h0[k] && t0[k] <= lim;
-        h1[k] = h1[k] && t1[k] <= lim;
-      }
-      m0[k] = ballot(h0[k]);
-      m1[k] = ballot(h1[k]);
-    }
-    pf.retire();
-    if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, everyone)) break;
+    const DevNode N = nodes[node];
+    bool h0, h1;
+    float t0, t1;
+    visit_node<SKIP>(P, N, r, (m >> lane) & 1, h0, h1, t0, t1);
+    DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m));
+    queue_binary_leaves(L, pending, N, h0, h1, ~0ull, dg);
+    // leaves are queued; only inner children are entered
+    const uint64_t m0 = N.child[0] >= 0 ? ballot(h0) : 0ull;
+    const uint64_t m1 = N.child[1] >= 0 ? ballot(h1) : 0ull;
+    if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, ~0ull)) break;
   }
-  if constexpr (batch) {
-    if (pending) batch_flush<false, SPHERES>(L, pending, prims, r[0], 0.0f);
-    const unsigned long long key = L.key[lane];
-    best_t[0] = __uint_as_float((unsigned)(key >> 32));
-    best_leaf[0] = (int)(unsigned)key;
-  }
+  if (pending) batch_flush<false, SPHERES>(L, pending, prims, r, 0.0f);
+  const unsigned long long key = L.key[lane];
+  best_t = __uint_as_float((unsigned)(key >> 32));
+  best_leaf = (int)(unsigned)key;
 }
 
 // ------------------------------------------------------------------ shadow (any hit)
 // Occluded iff some leaf the ray may reach has 0 < t < thr — identical to the reference's
 // closest-hit shadow test `0 < t_closest < dist - eps` (HW2/Scene.cpp:123-127), appendix A.7.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, int R, bool CULL = false,
-          class DN = NoDonor, bool WO = false>
-__device__ __forceinline__ void occluded(const RenderParams& P, const DevNode* __restrict__ nodes,
-                                         const DevPrim* __restrict__ prims, int* spill, WaveLeafLds& L,
-                                         const LaneRay (&r)[R], const bool (&active)[R],
-                                         const float (&thr)[R], bool (&occ)[R], Diag& dg,
-                                         DN& dn, int start_node = -1, uint64_t start_mask = 0) {
-  static_assert(!DN::kOn || (R == 1 && !DEEP), "donation needs the one-ray-per-lane lane stack");
-#pragma unroll
-  for (int k = 0; k < R; k++) occ[k] = false;
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, bool WO>
+__device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* __restrict__ nodes,
+                                         const DevPrim* __restrict__ prims, int* spill,
+                                         WaveLeafLds& L, const LaneRay& r, bool active, float thr,
+                                         Diag& dg) {
   if (P.root_kind != kRootNode) {
-#pragma unroll
-    for (int k = 0; k < R; k++) {
-      float t;
-      occ[k] = active[k] && leaf_test<SPHERES>(prims, P.root_ref, r[k], t) && t < thr[k] &&
-               t > 0.0f;
-    }
-    return;
+    float t;
+    return active && leaf_test<SPHERES>(prims, P.root_ref, r, t) && t < thr && t > 0.0f;
   }
   const bool accel = FAST && P.accel_root >= 0;
-  const bool task = DN::kOn && start_node >= 0;
-  uint64_t m[R], alive[R];
-  if (task) {
-    m[0] = alive[0] = start_mask & ballot(active[0] && thr[0] > 0.0f);
-  } else {
-#pragma unroll
-    for (int k = 0; k < R; k++) {
-      float tn, tf;
-      bool acc, und;
-      // thr <= 0 (or NaN): nothing can satisfy 0 < t < thr
-      if (accel) {
-        slab_span<SKIP>(P.accel_box, r[k], tn, tf);
-        m[k] = ballot(active[k] && thr[k] > 0.0f && decide_cull(tn, tf));
-      } else {
-        slab_fast<SKIP>(P.root_box, r[k], tn, acc, und);
-        m[k] = ballot(active[k] && thr[k] > 0.0f &&
-                      (acc || (und && box_exact(P.root_box, r[k]))));
-      }
-      alive[k] = m[k];
+  uint64_t m;
+  {
+    float tn, tf;
+    bool acc, und;
+    // thr <= 0 (or NaN): nothing can satisfy 0 < t < thr
+    if (accel) {
+      slab_span<SKIP>(P.accel_box, r, tn, tf);
+      m = ballot(active && thr > 0.0f && decide_cull(tn, tf));
+    } else {
+      slab_fast<SKIP>(P.root_box, r, tn, acc, und);
+      m = ballot(active && thr > 0.0f && (acc || (und && box_exact(P.root_box, r))));
     }
   }
-  if (!any_of(m)) return;
+  if (!m) return false;
+  uint64_t alive = m;
   const int lane = lane_id();
-  WaveStack<DEEP, R> st;
+  WaveStack<DEEP> st;
   st.lds = spill;
-  constexpr bool batch = kBatchLeaves && R == 1;
   int pending = 0;
-  if (batch) L.key[lane] = 0ull;
-  int node = task ? start_node : (accel ? P.accel_root : P.root_ref);
+  L.key[lane] = 0ull;
+  int node = accel ? P.accel_root : P.root_ref;
   for (;;) {
-    if constexpr (batch) {  // between visits; a lane found occluded stops entering nodes
-      if (pending >= kShadowFlush) {
-        batch_flush<true, SPHERES>(L, pending, prims, r[0], thr[0]);
-        pending = 0;
-        occ[0] = L.key[lane] != 0ull;
-        alive[0] &= ~ballot(occ[0]);
-        m[0] &= alive[0];
-        if (!m[0] && !advance(st, 0, 0, m, m, thr, thr, node, m, alive)) break;
-      }
+    if (pending >= kShadowFlush) {  // between visits; a lane found occluded stops entering nodes
+      batch_flush<true, SPHERES>(L, pending, prims, r, thr);
+      pending = 0;
+      alive &= ~ballot(L.key[lane] != 0ull);
+      m &= alive;
+      if (!m && !st.pop_live(node, m, alive)) break;
     }
-    if constexpr (DN::kOn) {  // hand the oldest pending subtree (still-unoccluded lanes) over
-      if (dn.tick() && st.sp > 0) {
-        int n0;
-        uint64_t m0;
-        st.bottom(n0, m0);
-        m0 &= alive[0];
-        if (!m0 || dn.donate(n0, m0)) st.drop_bottom();
-      }
-    }
-    if constexpr (batch && FAST) {  // a wide culling node (WO: every node the walk meets is one)
+    if constexpr (FAST) {
       if (WO || (node & kWideTag)) {
-        uint64_t mm = m[0];
-        const bool more = visit_wide<SKIP, true, DEEP, SPHERES>(P, nodes, prims, L, pending, r[0],
-                                                               thr[0], node, mm, alive[0], st, dg);
-        m[0] = mm;
-        if (!more) break;
+        if (!visit_wide<SKIP, true, DEEP, SPHERES>(P, nodes, prims, L, pending, r, thr, node, m,
+                                                   alive, st, dg))
+          break;
         continue;
       }
     }
-    const DevNode N = load_node(nodes, node);
-    ChildPrefetch pf;
-    pf.issue(nodes, prims, N.child[0], N.child[1]);
-    bool h0[R], h1[R];
-    float t0[R], t1[R];
-#pragma unroll
-    for (int k = 0; k < R; k++)
-      visit_node<SKIP>(P, N, r[k], (m[k] >> lane) & 1, h0[k], h1[k], t0[k], t1[k]);
-    DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(any_of(m));
-         const int nl0 = N.child[0] < 0 ? 1 + ((N.pad & kAccelPair0) != 0) : 0;
-         const int nl1 = N.child[1] < 0 ? 1 + ((N.pad & kAccelPair1) != 0) : 0;
-         dg.leaves += nl0 + nl1;
-         dg.leaf_lanes += nl0 * __builtin_popcountll(ballot(h0[0])) +
-                          nl1 * __builtin_popcountll(ballot(h1[0])));
-    if constexpr (batch) {  // queue the still-unoccluded lanes' leaf tests
-      if (N.child[0] < 0) {
-        const uint64_t b = ballot(h0[0]) & alive[0];
-        batch_push(L, pending, ~N.child[0], b);
-        if (N.pad & kAccelPair0) batch_push(L, pending, ~N.child[0] + 1, b);
-      }
-      if (N.child[1] < 0) {
-        const uint64_t b = ballot(h1[0]) & alive[0];
-        batch_push(L, pending, ~N.child[1], b);
-        if (N.pad & kAccelPair1) batch_push(L, pending, ~N.child[1] + 1, b);
-      }
-    } else {
-#pragma unroll 1
-    for (int slot = 0; slot < 4; slot++) {  // (slot & 1: the second leaf of a leaf pair)
-      const int side = slot >> 1;
-      const int c = side ? N.child[1] : N.child[0];
-      if (c < 0 && (!(slot & 1) || (N.pad & (side ? kAccelPair1 : kAccelPair0)))) {
-        const int leaf = ~c + (slot & 1);
-#pragma unroll
-        for (int k = 0; k < R; k++) {
-          const bool tests = side ? h1[k] : h0[k];
-          float t = 0.0f;
-#ifndef RT_EXP_BRANCHY  // (RT_EXP_BRANCHY: the early-exit form, for A/B)
-          const bool want = tests & !occ[k];
-          if (ballot(want)) {
-            const bool hit = leaf_test<SPHERES>(prims, leaf, r[k], t);
-            occ[k] = occ[k] | (want & hit & (t > 0.0f) & (t < thr[k]));
-          }
-#else
-          if (tests && !occ[k] && leaf_test<SPHERES>(prims, leaf, r[k], t) && t > 0.0f &&
-              t < thr[k])
-            occ[k] = true;
-#endif
-        }
-      }
-    }
-    }
-    uint64_t m0[R], m1[R];
-#pragma unroll
-    for (int k = 0; k < R; k++) {
-      alive[k] &= ~ballot(occ[k]);
-      h0[k] &= N.child[0] >= 0;
-      h1[k] &= N.child[1] >= 0;
-      if (FAST && CULL) {
-        const float lim = cull_limit(thr[k]);
-        h0[k] = h0[k] && t0[k] <= lim;
-        h1[k] = h1[k] && t1[k] <= lim;
-      }
-      m0[k] = ballot(h0[k]) & alive[k];
-      m1[k] = ballot(h1[k]) & alive[k];
-    }
-    pf.retire();
-    if (!any_of(alive)) break;
+    const DevNode N = nodes[node];
+    bool h0, h1;
+    float t0, t1;
+    visit_node<SKIP>(P, N, r, (m >> lane) & 1, h0, h1, t0, t1);
+    DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m));
+    queue_binary_leaves(L, pending, N, h0, h1, alive, dg);  // the still-unoccluded lanes
+    const uint64_t m0 = N.child[0] >= 0 ? ballot(h0) & alive : 0ull;
+    const uint64_t m1 = N.child[1] >= 0 ? ballot(h1) & alive : 0ull;
     if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, alive)) break;
   }
-  if constexpr (batch) {
-    if (pending) batch_flush<true, SPHERES>(L, pending, prims, r[0], thr[0]);
-    occ[0] = L.key[lane] != 0ull;
-  }
+  if (pending) batch_flush<true, SPHERES>(L, pending, prims, r, thr);
+  return L.key[lane] != 0ull;
 }
 
 // The kernel's RenderParams (its FIRST argument, so at offset 0 of the kernarg segment) read
 // through a pointer the compiler cannot see through: loads from it are not hoisted above this
-// point, so the persistent packet loop does not pull every field it uses into SGPRs for the
-// whole kernel (they were spilled to VGPR lanes across the traversal and reloaded per visit).
+// point, so the packet code does not pull every field it uses into SGPRs for the whole kernel
+// (they were spilled to VGPR lanes across the traversal and reloaded per visit).
 typedef __attribute__((address_space(4))) const RenderParams KernargParams;
 __device__ __forceinline__ const RenderParams& fresh_params(const RenderParams& P) {
-#ifdef RT_EXP_NOLAUNDER
-  return P;
-#else
+  (void)P;
   KernargParams* p = (KernargParams*)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(p));
   return *(const RenderParams*)p;
-#endif
 }
 
 // ------------------------------------------------------------------ render kernels
-// Two launches per frame (wavefront style): `trace_primary` finds each pixel's closest hit and
-// writes an 8-byte {t, leaf} record; `shade` rebuilds the shading inputs from it and runs the
-// point-light loop with its shadow rays.  Splitting keeps each kernel's live state small
-// (occupancy is what hides the dependent node loads), at 16 B of HBM traffic per pixel.
+// Three launches per frame (wavefront style): `trace_primary` finds each pixel's closest hit
+// and writes an 8-byte {t, leaf} record; `trace_shadow` rebuilds the hit point from it and
+// traces the point-light shadow rays into occlusion bits; `shade` runs the point-light loop.
+// Splitting keeps each kernel's live state small (occupancy is what hides the dependent node
+// loads), at 16 B of HBM traffic per pixel.
 struct PacketPixel {
   int lane, px, py;
   bool valid;
@@ -1359,61 +810,39 @@ __device__ __forceinline__ unsigned long long* counter_row(const RenderParams& P
   return P.counters + kCounterWidth * (sel % kCounterSlots);
 }
 
-__device__ __forceinline__ unsigned long long hit_key(int2_t rec) {
-  return ((unsigned long long)(unsigned)rec.y << 32) | (unsigned)rec.x;
-}
 __device__ __forceinline__ float hit_t(int2_t rec) { return __int_as_float(rec.y); }
 __device__ __forceinline__ int hit_leaf(int2_t rec) { return rec.x; }
 
-// R selected tiles per wave (tile sel0 + k is ray k of every lane): one packet traversal
-// serves 64*R rays, so the per-visit overhead (node fetch, masks, stack) is shared.
-template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL, bool WO = false>
+// One wave = the 8x8 packet of selected tile `sel` (< num_sel_tiles): closest hit per pixel
+// into its 8-B record.
+template <bool FAST, bool DEEP, bool SPHERES, bool WO>
 __device__ __forceinline__ void primary_packet(const RenderParams& P,
                                                const DevNode* __restrict__ nodes,
-                                               const DevPrim* __restrict__ prims, int sel0,
+                                               const DevPrim* __restrict__ prims, int sel,
                                                int* spill, WaveLeafLds& L) {
-  PacketPixel q[R];
-  LaneRay ray[R];
-  bool valid[R];
-  bool any_skip = false;
-#pragma unroll
-  for (int k = 0; k < R; k++) {
-    q[k] = packet_pixel(P, sel0 + k);
-    valid[k] = q[k].valid && sel0 + k < P.num_sel_tiles;
-    ray[k] = make_ray(ld3(P.cam_e), primary_dir(P, q[k].px, q[k].py), P.quot_ok);
-#ifndef RT_EXP_UNIFORM_ORIGIN
-    // The camera origin is wave-uniform; left to itself the compiler keeps it in 3 SGPRs and
-    // copies it to VGPRs at every node visit (a VALU op takes one SGPR operand, the box
-    // coordinate already is one).  Pin it to VGPRs once.
-    asm volatile("" : "+v"(ray[k].o.x), "+v"(ray[k].o.y), "+v"(ray[k].o.z));
-#endif
-    any_skip |= valid[k] && (ray[k].skip0 || ray[k].skip1 || ray[k].skip2);
-  }
+  const PacketPixel q = packet_pixel(P, sel);
+  LaneRay ray = make_ray(ld3(P.cam_e), primary_dir(P, q.px, q.py), P.quot_ok);
+  // The camera origin is wave-uniform; left to itself the compiler keeps it in 3 SGPRs and
+  // copies it to VGPRs at every node visit (a VALU op takes one SGPR operand, the box
+  // coordinate already is one).  Pin it to VGPRs once.
+  asm volatile("" : "+v"(ray.o.x), "+v"(ray.o.y), "+v"(ray.o.z));
+  const bool any_skip = q.valid && (ray.skip0 || ray.skip1 || ray.skip2);
   Diag dg;
-  float t[R];
-  int leaf[R];
-  NoDonor nd;
+  float t;
+  int leaf;
   if (ballot(any_skip))
-    closest_hit<true, FAST, DEEP, SPHERES, R, CULL, NoDonor, WO>(P, nodes, prims, spill, L, ray, valid, t, leaf,
-                                                    dg, nd);
+    closest_hit<true, FAST, DEEP, SPHERES, WO>(P, nodes, prims, spill, L, ray, q.valid, t, leaf, dg);
   else
-    closest_hit<false, FAST, DEEP, SPHERES, R, CULL, NoDonor, WO>(P, nodes, prims, spill, L, ray, valid, t, leaf,
-                                                     dg, nd);
+    closest_hit<false, FAST, DEEP, SPHERES, WO>(P, nodes, prims, spill, L, ray, q.valid, t, leaf, dg);
   const RenderParams& Pw = fresh_params(P);  // post-traversal fields: not live across it
-  unsigned long long nvalid = 0, nhit = 0;
-#pragma unroll
-  for (int k = 0; k < R; k++) {
-    if (sel0 + k < Pw.num_sel_tiles) {
-      int2_t rec;  // key layout: leaf low, t bits high (rt_internal.h)
-      rec.x = valid[k] ? leaf[k] : -2;  // -1 miss, -2 outside the image
-      rec.y = __float_as_int(t[k]);
-      Pw.hits[(size_t)(sel0 + k) * (kTile * kTile) + q[k].lane] = rec;
-    }
-    nvalid += __builtin_popcountll(ballot(valid[k]));
-    nhit += __builtin_popcountll(ballot(valid[k] && leaf[k] >= 0));
-  }
-  if (Pw.counters && q[0].lane == 0) {  // spread over kCounterSlots rows: no hot address
-    unsigned long long* c = counter_row(Pw, sel0);
+  int2_t rec;  // key layout: leaf low, t bits high (rt_internal.h)
+  rec.x = q.valid ? leaf : -2;  // -1 miss, -2 outside the image
+  rec.y = __float_as_int(t);
+  Pw.hits[(size_t)sel * (kTile * kTile) + q.lane] = rec;
+  if (Pw.counters && q.lane == 0) {  // spread over kCounterSlots rows: no hot address
+    const unsigned long long nvalid = __builtin_popcountll(ballot(q.valid));
+    const unsigned long long nhit = __builtin_popcountll(ballot(q.valid && leaf >= 0));
+    unsigned long long* c = counter_row(Pw, sel);
     atomicAdd(&c[kCntPrimary], nvalid);
     atomicAdd(&c[kCntHits], nhit);
 #ifdef RT_DIAG
@@ -1426,33 +855,6 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
   }
 }
 
-// One piece of a packet in a sharing workgroup: the closest hit of tile sel's rays over the
-// whole tree (node < 0) or over the shared subtree (node, mask); returns this lane's key.
-template <bool FAST, bool SPHERES, bool CULL, int W>
-__device__ __forceinline__ unsigned long long primary_piece(const RenderParams& P,
-                                                            const DevNode* __restrict__ nodes,
-                                                            const DevPrim* __restrict__ prims,
-                                                            int sel, WaveLeafLds& L, Sharer<W>& sh,
-                                                            int node, uint64_t mask, Diag& dg) {
-  const PacketPixel q = packet_pixel(P, sel);
-  const bool valid[1] = {q.valid};
-  LaneRay ray[1] = {make_ray(ld3(P.cam_e), primary_dir(P, q.px, q.py), P.quot_ok)};
-  asm volatile("" : "+v"(ray[0].o.x), "+v"(ray[0].o.y), "+v"(ray[0].o.z));  // (primary_packet)
-  const bool any_skip = valid[0] && (ray[0].skip0 || ray[0].skip1 || ray[0].skip2);
-  float t[1];
-  int leaf[1];
-  if (ballot(any_skip))
-    closest_hit<true, FAST, false, SPHERES, 1, CULL>(P, nodes, prims, nullptr, L, ray, valid, t,
-                                                     leaf, dg, sh, node, mask);
-  else
-    closest_hit<false, FAST, false, SPHERES, 1, CULL>(P, nodes, prims, nullptr, L, ray, valid, t,
-                                                      leaf, dg, sh, node, mask);
-  int2_t rec;
-  rec.x = leaf[0];
-  rec.y = __float_as_int(t[0]);
-  return leaf[0] >= 0 ? hit_key(rec) : kNoHitKey;
-}
-
 // Hit point and normal of a primary hit, rebuilt from its {t, leaf} record exactly as
 // trace_ray computes them (HW2/Scene.cpp:101-105; Sphere.h:42,50 for sphere normals).
 __device__ __forceinline__ V3 hit_point(const RenderParams& P, const PacketPixel& q, float t) {
@@ -1460,18 +862,16 @@ __device__ __forceinline__ V3 hit_point(const RenderParams& P, const PacketPixel
 }
 
 // Shadow rays of HW2/Scene.cpp:113-127: one bit per point light, set when the light is
-// occluded for this pixel's primary hit.  R tiles per wave as in primary_packet.
-template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL, bool WO = false>
+// occluded for this pixel's primary hit.
+template <bool FAST, bool DEEP, bool SPHERES, bool WO>
 __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
                                               const DevNode* __restrict__ nodes,
                                               const DevPrim* __restrict__ prims,
-                                              const DevLight* __restrict__ lights, int sel0,
+                                              const DevLight* __restrict__ lights, int sel,
                                               int* spill, WaveLeafLds& L) {
   Diag dg;
   for (int w = 0; w < P0.occ_words; w++) {
-    unsigned bits[R];
-#pragma unroll
-    for (int k = 0; k < R; k++) bits[k] = 0;
+    unsigned bits = 0;
     const int lend = min(P0.num_lights, 32 * (w + 1));
     for (int li = 32 * w; li < lend; li++) {
       // per light: the pixel's hit record is re-read and its hit point rebuilt, so nothing but
@@ -1479,92 +879,40 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       // 8-B record is an L2 hit)
       const RenderParams& P = fresh_params(P0);
       const DevLight& lt = lights[li];
-      LaneRay sr[R];
-      float thr[R];
-      bool hit[R];
-      bool any_skip = false;
-#pragma unroll
-      for (int k = 0; k < R; k++) {
-        const PacketPixel q = packet_pixel(P, sel0 + k);
-        int2_t rec;
-        rec.x = -2;
-        rec.y = 0;
-        if (sel0 + k < P.num_sel_tiles) rec = P.hits[(size_t)(sel0 + k) * (kTile * kTile) + q.lane];
-        hit[k] = hit_leaf(rec) >= 0;
-        const V3 pk = hit[k] ? hit_point(P, q, hit_t(rec)) : v3(0, 0, 0);
-        const V3 ld = ld3(lt.position) - pk;
-        const V3 wi = normalize(ld);
-        const float dist = length(ld);
-        sr[k] = make_ray(pk + wi * P.eps, wi, P.quot_ok);  // p + eps * w_i
-        thr[k] = dist - P.eps;
-        any_skip |= hit[k] && (sr[k].skip0 || sr[k].skip1 || sr[k].skip2);
-      }
-      bool occ[R];
-      NoDonor nd;
-      if (ballot(any_skip))
-        occluded<true, FAST, DEEP, SPHERES, R, CULL, NoDonor, WO>(P, nodes, prims, spill, L, sr, hit, thr, occ, dg, nd);
-      else
-        occluded<false, FAST, DEEP, SPHERES, R, CULL, NoDonor, WO>(P, nodes, prims, spill, L, sr, hit, thr, occ, dg, nd);
-#pragma unroll
-      for (int k = 0; k < R; k++) bits[k] |= (occ[k] ? 1u : 0u) << (li - 32 * w);
+      const PacketPixel q = packet_pixel(P, sel);
+      const int2_t rec = P.hits[(size_t)sel * (kTile * kTile) + q.lane];
+      const bool hit = hit_leaf(rec) >= 0;
+      const V3 pk = hit ? hit_point(P, q, hit_t(rec)) : v3(0, 0, 0);
+      const V3 ld = ld3(lt.position) - pk;
+      const V3 wi = normalize(ld);
+      const float dist = length(ld);
+      const LaneRay sr = make_ray(pk + wi * P.eps, wi, P.quot_ok);  // p + eps * w_i
+      const float thr = dist - P.eps;
+      const bool any_skip = hit && (sr.skip0 || sr.skip1 || sr.skip2);
+      const bool occ = ballot(any_skip)
+                           ? occluded<true, FAST, DEEP, SPHERES, WO>(P, nodes, prims, spill, L, sr, hit, thr, dg)
+                           : occluded<false, FAST, DEEP, SPHERES, WO>(P, nodes, prims, spill, L, sr, hit, thr, dg);
+      bits |= (occ ? 1u : 0u) << (li - 32 * w);
     }
     const RenderParams& Pw = fresh_params(P0);
-#pragma unroll
-    for (int k = 0; k < R; k++)
-      if (sel0 + k < Pw.num_sel_tiles)
-        Pw.occ[((size_t)(sel0 + k) * (kTile * kTile) + lane_id()) * Pw.occ_words + w] = bits[k];
+    Pw.occ[((size_t)sel * (kTile * kTile) + lane_id()) * Pw.occ_words + w] = bits;
   }
   const RenderParams& Pc = fresh_params(P0);
-  unsigned long long nhit = 0;
-#pragma unroll
-  for (int k = 0; k < R; k++) {
-    const bool inside = sel0 + k < Pc.num_sel_tiles;
-    nhit += __builtin_popcountll(
-        ballot(inside && hit_leaf(Pc.hits[(size_t)(sel0 + k) * (kTile * kTile) + lane_id()]) >= 0));
-  }
-  if (Pc.counters && lane_id() == 0) {
-    unsigned long long* c = counter_row(Pc, sel0);
-    atomicAdd(&c[kCntShadow], nhit * (unsigned long long)Pc.num_lights);
+  if (Pc.counters) {
+    const bool hit = hit_leaf(Pc.hits[(size_t)sel * (kTile * kTile) + lane_id()]) >= 0;
+    const unsigned long long nhit = __builtin_popcountll(ballot(hit));
+    if (lane_id() == 0) {
+      unsigned long long* c = counter_row(Pc, sel);
+      atomicAdd(&c[kCntShadow], nhit * (unsigned long long)Pc.num_lights);
 #ifdef RT_DIAG
-    atomicAdd(&c[kCntShadNodes], dg.nodes);
-    atomicAdd(&c[kCntShadNodeLanes], dg.node_lanes);
-    atomicAdd(&c[kCntShadLeaves], dg.leaves);
-    atomicAdd(&c[kCntShadLeafLanes], dg.leaf_lanes);
-    atomicAdd(&c[kCntShadWide], dg.wide);
+      atomicAdd(&c[kCntShadNodes], dg.nodes);
+      atomicAdd(&c[kCntShadNodeLanes], dg.node_lanes);
+      atomicAdd(&c[kCntShadLeaves], dg.leaves);
+      atomicAdd(&c[kCntShadLeafLanes], dg.leaf_lanes);
+      atomicAdd(&c[kCntShadWide], dg.wide);
 #endif
+    }
   }
-}
-
-// One piece of a packet's shadow rays in a sharing workgroup: point light li for tile sel0
-// (HW2/Scene.cpp:113-127 as in shadow_packet), over the whole tree (start_node < 0) or over a
-// shared subtree.  Returns this lane's occlusion.
-template <bool FAST, bool SPHERES, bool CULL, class DN>
-__device__ __forceinline__ bool shadow_piece(const RenderParams& P0,
-                                            const DevNode* __restrict__ nodes,
-                                            const DevPrim* __restrict__ prims,
-                                            const DevLight* __restrict__ lights, int sel0, int li,
-                                            int* spill, WaveLeafLds& L, DN& dn, int start_node,
-                                            uint64_t start_mask, Diag& dg) {
-  const RenderParams& P = P0;
-  const DevLight& lt = lights[li];
-  const PacketPixel q = packet_pixel(P, sel0);
-  const int2_t rec = P.hits[(size_t)sel0 * (kTile * kTile) + q.lane];
-  bool hit[1] = {hit_leaf(rec) >= 0};
-  const V3 pk = hit[0] ? hit_point(P, q, hit_t(rec)) : v3(0, 0, 0);
-  const V3 ld = ld3(lt.position) - pk;
-  const V3 wi = normalize(ld);
-  const float dist = length(ld);
-  LaneRay sr[1] = {make_ray(pk + wi * P.eps, wi, P.quot_ok)};  // p + eps * w_i
-  float thr[1] = {dist - P.eps};
-  const bool any_skip = hit[0] && (sr[0].skip0 || sr[0].skip1 || sr[0].skip2);
-  bool occ[1];
-  if (ballot(any_skip))
-    occluded<true, FAST, false, SPHERES, 1, CULL>(P, nodes, prims, spill, L, sr, hit, thr, occ, dg,
-                                                  dn, start_node, start_mask);
-  else
-    occluded<false, FAST, false, SPHERES, 1, CULL>(P, nodes, prims, spill, L, sr, hit, thr, occ,
-                                                   dg, dn, start_node, start_mask);
-  return occ[0];
 }
 
 // Local shading of HW2/Scene.cpp:101-138 given the occlusion bits, in the reference's
@@ -1592,11 +940,11 @@ __device__ __forceinline__ void shade_pixel(const RenderParams& P,
     color = color + ld3(m.ambient) * ld3(P.ambient);
     for (int li = 0; li < P.num_lights; li++) {
       if ((P.occ[pix * P.occ_words + (li >> 5)] >> (li & 31)) & 1u) continue;
-      const DevLight& L = lights[li];
-      const V3 ld = ld3(L.position) - p;
+      const DevLight& Lt = lights[li];
+      const V3 ld = ld3(Lt.position) - p;
       const V3 wi = normalize(ld);
       const float dist = length(ld);
-      const V3 I = ld3(L.intensity);
+      const V3 I = ld3(Lt.intensity);
       const float d2 = dist * dist;
       const float cos_d = dot(n, wi);
       color = color + ((ld3(m.diffuse) * I) * cos_d) / d2;
@@ -1680,18 +1028,13 @@ __device__ __forceinline__ V3 local_color(const RenderParams& P, const DevNode* 
     const V3 ld = ld3(lt.position) - p;
     const V3 wi = normalize(ld);
     const float dist = length(ld);
-    const LaneRay sr[1] = {make_ray(p + wi * P.eps, wi, P.quot_ok)};
-    const float thr[1] = {dist - P.eps};
-    const bool act[1] = {shade};
-    const bool sskip = ballot(shade && (sr[0].skip0 || sr[0].skip1 || sr[0].skip2)) != 0;
-    bool occ[1];
-    NoDonor nd;
-    if (sskip)
-      occluded<true, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, L, sr, act, thr, occ, dg, nd);
-    else
-      occluded<false, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, L, sr, act, thr, occ, dg, nd);
+    const LaneRay sr = make_ray(p + wi * P.eps, wi, P.quot_ok);
+    const float thr = dist - P.eps;
+    const bool sskip = ballot(shade && (sr.skip0 || sr.skip1 || sr.skip2)) != 0;
+    const bool occ = sskip ? occluded<true, FAST, DEEP, SPHERES, false>(P, nodes, prims, spill, L, sr, shade, thr, dg)
+                           : occluded<false, FAST, DEEP, SPHERES, false>(P, nodes, prims, spill, L, sr, shade, thr, dg);
     shadow_rays += __builtin_popcountll(ballot(shade));
-    if (shade && !occ[0]) {
+    if (shade && !occ) {
       const V3 I = ld3(lt.intensity);
       const float d2 = dist * dist;
       color = color + ((ld3(m.diffuse) * I) * dot(n, wi)) / d2;
@@ -1729,19 +1072,14 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
   unsigned long long n_shadow = 0, n_secondary = 0;
   bool first = true;
   while (ballot(active)) {
-    const LaneRay rays[1] = {make_ray(ro, rd, P.quot_ok)};
-    const LaneRay& ray = rays[0];
-    const bool act[1] = {active};
+    const LaneRay ray = make_ray(ro, rd, P.quot_ok);
     const bool skip = ballot(active && (ray.skip0 || ray.skip1 || ray.skip2)) != 0;
-    float ts[1];
-    int leaves[1];
-    NoDonor nd;
+    float t;
+    int leaf;
     if (skip)
-      closest_hit<true, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, L, rays, act, ts, leaves, dg, nd);
+      closest_hit<true, FAST, DEEP, SPHERES, false>(P, nodes, prims, spill, L, ray, active, t, leaf, dg);
     else
-      closest_hit<false, FAST, DEEP, SPHERES, 1>(P, nodes, prims, spill, L, rays, act, ts, leaves, dg, nd);
-    const float t = ts[0];
-    const int leaf = leaves[0];
+      closest_hit<false, FAST, DEEP, SPHERES, false>(P, nodes, prims, spill, L, ray, active, t, leaf, dg);
     const bool hit = active && leaf >= 0;
     if (first) n_hits = __builtin_popcountll(ballot(hit));
     first = false;
@@ -1901,17 +1239,16 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
 }
 
 // Traversal kernels hide their dependent node loads with occupancy: hold them to 8 waves/SIMD
-// (<= 64 VGPRs, <= 100 SGPRs); the compiler otherwise settles at 7 on SGPR count.
-#ifndef RT_TRACE_MIN_WAVES  // (A/B: fewer waves per SIMD, more registers per wave)
+// (<= 64 VGPRs, <= 80 SGPRs); the primary kernel runs at 7, where the wide node's 32 SGPRs fit
+// without spills.  (Macros: A/B builds, `make exp EXTRA=-D...`.)
+#ifndef RT_TRACE_MIN_WAVES
 #define RT_TRACE_MIN_WAVES 8
 #endif
-#ifndef RT_PRIMARY_MIN_WAVES  // primary kernel only (A/B: RT_PRIMARY_MIN_WAVES=8)
-#define RT_PRIMARY_MIN_WAVES 7  // 32 more SGPRs for the wide node: frame 0.703 -> 0.691 ms
+#ifndef RT_PRIMARY_MIN_WAVES
+#define RT_PRIMARY_MIN_WAVES 7
 #endif
 #define RT_PRIMARY_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_PRIMARY_MIN_WAVES, 8)))
-#ifndef RT_TRAVERSAL_OCCUPANCY
 #define RT_TRAVERSAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_TRACE_MIN_WAVES, 8)))
-#endif
 
 // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so hand each
 // XCD a contiguous run of blocks — neighbouring packets share BVH nodes through its L2.
@@ -1926,37 +1263,25 @@ __device__ __forceinline__ int packet_index() {
 // Traversal workgroups: kTraceWaves packets, which the hardware keeps on ONE CU, so they share
 // its scalar cache.  With P.tile_block the workgroup's packets form a kBlockW x kBlockH block
 // of tiles (blocks row-major over the frame) instead of a run along a tile row: neighbouring
-// rays walk the same nodes, and the cache serves them once.  Deep trees keep 4-wave groups
-// (their LDS stack is 12 KB per wave).
-#ifndef RT_TRACE_BLOCK_W
-#define RT_TRACE_BLOCK_W 2
-#endif
-constexpr int kTraceWaves = RT_TRACE_WAVES;
-template <bool DEEP>
-constexpr int trace_waves() { return DEEP ? 4 : kTraceWaves; }
-
-template <int W>
-__host__ __device__ constexpr int block_w() { return W >= RT_TRACE_BLOCK_W ? RT_TRACE_BLOCK_W : W; }
+// rays walk the same nodes, and the cache serves them once.
+constexpr int kTraceWaves = 4;
+constexpr int kBlockW = 2, kBlockH = kTraceWaves / kBlockW;
 
 // Tile (= sel, tile_step 1) of logical packet p; -1 for a padding packet of an edge block.
-template <int W>
 __device__ __forceinline__ int packet_sel(const RenderParams& P, int p) {
   if (!P.tile_block) return p;
-  constexpr int BW = block_w<W>(), BH = W / BW;
-  const int w = p % W, b = p / W;
-  const int nbx = (P.tiles_x + BW - 1) / BW;
-  const int tx = (b % nbx) * BW + w % BW, ty = (b / nbx) * BH + w / BW;
+  const int w = p % kTraceWaves, b = p / kTraceWaves;
+  const int nbx = (P.tiles_x + kBlockW - 1) / kBlockW;
+  const int tx = (b % nbx) * kBlockW + w % kBlockW, ty = (b / nbx) * kBlockH + w / kBlockW;
   const int tiles_y = P.tiles_total / P.tiles_x;
   return (tx < P.tiles_x && ty < tiles_y) ? ty * P.tiles_x + tx : -1;
 }
 
-// Logical packets of a traversal launch (R tiles each; with tile_block, padded to whole blocks).
-template <int W, int R>
+// Logical packets of a traversal launch (with tile_block, padded to whole blocks).
 __host__ __device__ __forceinline__ int trace_packets(const RenderParams& P) {
-  if (!P.tile_block) return (P.num_sel_tiles + R - 1) / R;
-  constexpr int BW = block_w<W>(), BH = W / BW;
+  if (!P.tile_block) return P.num_sel_tiles;
   const int tiles_y = P.tiles_total / P.tiles_x;
-  return ((P.tiles_x + BW - 1) / BW) * ((tiles_y + BH - 1) / BH) * W;
+  return ((P.tiles_x + kBlockW - 1) / kBlockW) * ((tiles_y + kBlockH - 1) / kBlockH) * kTraceWaves;
 }
 
 // RT_TIMELINE (experiment builds only): every traversal wave records its start and end on the
@@ -1984,199 +1309,51 @@ __device__ unsigned long long g_timeline[2][kTimelineWaves][3];
 #define TL_END(k)
 #endif
 
-// Sharing workgroups (RT_EXP_SHARE, R == 1, lane stack; see "subtree sharing"): each wave
-// starts with its own packet, and every piece of work, own or shared, goes through the one call
-// site in the loop.  Bit-identical, but slower on C3, so off by default: every
-// wave traverses its own packet alone.
-#ifdef RT_EXP_SHARE
-constexpr bool kShare = true;
-#else
-constexpr bool kShare = false;
-#endif
-
-template <bool FAST, bool SPHERES, bool CULL, int W>
-__device__ __forceinline__ void share_primary(const RenderParams& P, const DevNode* __restrict__ nodes,
-                                              const DevPrim* __restrict__ prims, int sel,
-                                              WaveLeafLds& L, BlockShare<W>& SH) {
-  const int wv = (int)threadIdx.x >> 6, lane = lane_id();
-  if (threadIdx.x == 0) SH.want = 0;
-  if (lane == 0) {
-    SH.sel[wv] = sel;
-    SH.flag[wv] = 0;
-  }
-  SH.res[wv][lane] = kNoHitKey;
-  __syncthreads();
-  Sharer<W> sh;
-  sh.S = &SH;
-  sh.light = 0;
-  Diag dg;
-  int owner = wv, node = -1, light = 0;
-  uint64_t mask = 0;
-  bool have = sel >= 0;
-  unsigned long long shared = 0;
-  for (;;) {
-    if (!have && !share_next(SH, owner, node, mask, light)) break;
-    const int tsel = uniform(SH.sel[owner]);
-    sh.owner = owner;
-    sh.visits = 0;
-    const unsigned long long key =
-        primary_piece<FAST, SPHERES, CULL, W>(fresh_params(P), nodes, prims, tsel, L, sh,
-                                               have ? -1 : node, mask, dg);
-    if (key != kNoHitKey) atomicMin(&SH.res[owner][lane], key);
-    shared += have ? 0 : 1;
-    have = false;
-  }
-  __syncthreads();  // every piece of every packet of the workgroup has merged
-  const RenderParams& Pw = fresh_params(P);
-  if (sel >= 0) {
-    const PacketPixel q = packet_pixel(Pw, sel);
-    const unsigned long long key = SH.res[wv][lane];
-    int2_t rec;  // key layout: leaf low, t bits high (rt_internal.h)
-    rec.x = q.valid ? (int)(unsigned)key : -2;  // -1 miss, -2 outside the image
-    rec.y = (int)(unsigned)(key >> 32);
-    Pw.hits[(size_t)sel * (kTile * kTile) + q.lane] = rec;
-    const unsigned long long nvalid = __builtin_popcountll(ballot(q.valid));
-    const unsigned long long nhit = __builtin_popcountll(ballot(q.valid && rec.x >= 0));
-    if (Pw.counters && lane == 0) {
-      unsigned long long* c = counter_row(Pw, sel);
-      atomicAdd(&c[kCntPrimary], nvalid);
-      atomicAdd(&c[kCntHits], nhit);
-    }
-  }
-  if (Pw.counters && lane == 0) {
-    unsigned long long* c = counter_row(Pw, (int)blockIdx.x);
-    if (shared) atomicAdd(&c[kCntShared], shared);
-#ifdef RT_DIAG
-    atomicAdd(&c[kCntPrimNodes], dg.nodes);
-    atomicAdd(&c[kCntPrimNodeLanes], dg.node_lanes);
-    atomicAdd(&c[kCntPrimLeaves], dg.leaves);
-    atomicAdd(&c[kCntPrimLeafLanes], dg.leaf_lanes);
-    atomicAdd(&c[kCntPrimWide], dg.wide);
-#endif
-  }
-}
-
-// Shadow rays in a sharing workgroup, 32 lights (one occlusion word) at a time: the waves split
-// the word's (packet, light) traversals, merge the occlusion bits per packet in LDS, and write
-// the word after a workgroup barrier.
-template <bool FAST, bool SPHERES, bool CULL, int W>
-__device__ __forceinline__ void share_shadow(const RenderParams& P, const DevNode* __restrict__ nodes,
-                                             const DevPrim* __restrict__ prims,
-                                             const DevLight* __restrict__ lights, int sel,
-                                             WaveLeafLds& L, BlockShare<W>& SH) {
-  const int wv = (int)threadIdx.x >> 6, lane = lane_id();
-  const int nl = P.num_lights, words = P.occ_words;
-  if (lane == 0) SH.sel[wv] = sel;
-  Sharer<W> sh;
-  sh.S = &SH;
-  Diag dg;
-  unsigned long long shared = 0;
-  for (int w = 0; w < words; w++) {
-    if (threadIdx.x == 0) SH.want = 0;
-    if (lane == 0) SH.flag[wv] = 0;
-    SH.res[wv][lane] = 0ull;
-    __syncthreads();
-    const int lend = min(nl, 32 * (w + 1));
-    int li = 32 * w, owner = wv, node = -1, light = 0;
-    uint64_t mask = 0;
-    for (;;) {
-      const bool have = sel >= 0 && li < lend;
-      if (have) {
-        owner = wv;
-        light = li++;
-      } else if (!share_next(SH, owner, node, mask, light)) {
-        break;
-      }
-      sh.owner = owner;
-      sh.light = light;
-      sh.visits = 0;
-      const bool occ = shadow_piece<FAST, SPHERES, CULL>(fresh_params(P), nodes, prims, lights,
-                                                         uniform(SH.sel[owner]), light, nullptr, L,
-                                                         sh, have ? -1 : node, mask, dg);
-      if (occ) atomicOr(&SH.res[owner][lane], 1ull << (light & 31));
-      shared += have ? 0 : 1;
-    }
-    __syncthreads();  // every piece of this word has merged
-    if (sel >= 0) {
-      const RenderParams& Pw = fresh_params(P);
-      Pw.occ[((size_t)sel * (kTile * kTile) + lane) * words + w] = (unsigned)SH.res[wv][lane];
-    }
-  }
-  const RenderParams& Pc = fresh_params(P);
-  if (sel >= 0) {
-    const bool hit = hit_leaf(Pc.hits[(size_t)sel * (kTile * kTile) + lane]) >= 0;
-    const unsigned long long nhit = __builtin_popcountll(ballot(hit));
-    if (Pc.counters && lane == 0)
-      atomicAdd(&counter_row(Pc, sel)[kCntShadow], nhit * (unsigned long long)nl);
-  }
-  if (Pc.counters && lane == 0) {
-    unsigned long long* c = counter_row(Pc, (int)blockIdx.x);
-    if (shared) atomicAdd(&c[kCntShared], shared);
-#ifdef RT_DIAG
-    atomicAdd(&c[kCntShadNodes], dg.nodes);
-    atomicAdd(&c[kCntShadNodeLanes], dg.node_lanes);
-    atomicAdd(&c[kCntShadLeaves], dg.leaves);
-    atomicAdd(&c[kCntShadLeafLanes], dg.leaf_lanes);
-    atomicAdd(&c[kCntShadWide], dg.wide);
-#endif
-  }
-}
-
 // Traversal kernels: one packet per wave, XCD-remapped blocks of 2-D tile blocks.
-template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL, bool WO = false>
-__global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_PRIMARY_OCCUPANCY void trace_primary_kernel(
+template <bool FAST, bool DEEP, bool SPHERES, bool WO>
+__global__ __launch_bounds__(kTraceWaves * 64) RT_PRIMARY_OCCUPANCY void trace_primary_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
-  constexpr int W = trace_waves<DEEP>();
-  __shared__ WaveLeafLds leaf_lds[W];  // 2 KiB per wave
-  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * (1 + 2 * R) * kDeepStack : nullptr;
+  __shared__ WaveLeafLds leaf_lds[kTraceWaves];  // 2.5 KiB per wave
+  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * kDeepWords * kDeepStack : nullptr;
   WaveLeafLds& L = leaf_lds[threadIdx.x >> 6];
   TL_BEGIN;
   const RenderParams& Q = fresh_params(P);
-  const int p = packet_index<W>();
-  int sel = p < trace_packets<W, R>(Q) ? (R == 1 ? packet_sel<W>(Q, p) : p * R) : -1;
+  const int p = packet_index<kTraceWaves>();
+  int sel = p < trace_packets(Q) ? packet_sel(Q, p) : -1;
   if (sel >= Q.num_sel_tiles) sel = -1;
   TL_SEL(sel);
-  if constexpr (kShare && R == 1 && !DEEP) {
-    __shared__ BlockShare<W> SH;
-    share_primary<FAST, SPHERES, CULL, W>(P, nodes, prims, sel, L, SH);
-  } else if (sel >= 0) {
+  if (sel >= 0) {
     const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
-    primary_packet<FAST, DEEP, SPHERES, R, CULL, WO>(Q, nodes, prims, sel, spill, L);
+    primary_packet<FAST, DEEP, SPHERES, WO>(Q, nodes, prims, sel, spill, L);
     const RenderParams& Pw = fresh_params(P);
-    if (R == 1 && Pw.tile_cost && lane_id() == 0)  // the shadow kernel's dispatch order
+    if (Pw.tile_cost && lane_id() == 0)  // the shadow kernel's dispatch order
       Pw.tile_cost[sel] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - c0, 0xffffffffull);
   }
   TL_END(0);
 }
 
-template <bool FAST, bool DEEP, bool SPHERES, int R, bool CULL, bool WO = false>
-__global__ __launch_bounds__(trace_waves<DEEP>() * 64) RT_TRAVERSAL_OCCUPANCY void trace_shadow_kernel(
+template <bool FAST, bool DEEP, bool SPHERES, bool WO>
+__global__ __launch_bounds__(kTraceWaves * 64) RT_TRAVERSAL_OCCUPANCY void trace_shadow_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims,
     const DevLight* __restrict__ lights) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
-  constexpr int W = trace_waves<DEEP>();
-  __shared__ WaveLeafLds leaf_lds[W];  // 2 KiB per wave
-  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * (1 + 2 * R) * kDeepStack : nullptr;
+  __shared__ WaveLeafLds leaf_lds[kTraceWaves];
+  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * kDeepWords * kDeepStack : nullptr;
   WaveLeafLds& L = leaf_lds[threadIdx.x >> 6];
   TL_BEGIN;
   const RenderParams& Q = fresh_params(P);
   int sel;
-  if (R == 1 && Q.tile_order) {  // slowest primary tiles first, in plain block order
-    const int p = uniform((int)blockIdx.x * W + ((int)threadIdx.x >> 6));
+  if (Q.tile_order) {  // slowest primary tiles first, in plain block order
+    const int p = uniform((int)blockIdx.x * kTraceWaves + ((int)threadIdx.x >> 6));
     sel = p < Q.num_sel_tiles ? uniform(Q.tile_order[p]) : -1;
   } else {
-    const int p = packet_index<W>();
-    sel = p < trace_packets<W, R>(Q) ? (R == 1 ? packet_sel<W>(Q, p) : p * R) : -1;
+    const int p = packet_index<kTraceWaves>();
+    sel = p < trace_packets(Q) ? packet_sel(Q, p) : -1;
   }
   if (sel >= Q.num_sel_tiles) sel = -1;
   TL_SEL(sel);
-  if constexpr (kShare && R == 1 && !DEEP) {
-    __shared__ BlockShare<W> SH;
-    share_shadow<FAST, SPHERES, CULL, W>(P, nodes, prims, lights, sel, L, SH);
-  } else if (sel >= 0) {
-    shadow_packet<FAST, DEEP, SPHERES, R, CULL, WO>(Q, nodes, prims, lights, sel, spill, L);
-  }
+  if (sel >= 0) shadow_packet<FAST, DEEP, SPHERES, WO>(Q, nodes, prims, lights, sel, spill, L);
   TL_END(1);
 }
 
@@ -2189,8 +1366,9 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void recursive_kernel(
   __shared__ WaveLeafLds leaf_lds[kWavesPerBlock];
   const int sel = packet_index<kWavesPerBlock>();
   if (sel >= P.num_sel_tiles) return;
-  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * 3 * kDeepStack : nullptr;
-  recursive_packet<FAST, DEEP, SPHERES>(P, nodes, prims, normals, mats, lights, sel, spill, leaf_lds[threadIdx.x >> 6]);
+  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * kDeepWords * kDeepStack : nullptr;
+  recursive_packet<FAST, DEEP, SPHERES>(P, nodes, prims, normals, mats, lights, sel, spill,
+                                        leaf_lds[threadIdx.x >> 6]);
 }
 
 __global__ __launch_bounds__(kWavesPerBlock * 64) void shade_kernel(
@@ -2240,13 +1418,13 @@ static inline void mark(const hipEvent_t* marks, int k, hipStream_t stream) {
   if (marks) (void)hipEventRecord(marks[k], stream);
 }
 
-template <bool FAST, bool DEEP, bool SPHERES, bool CULL, bool WO = false>
+template <bool FAST, bool DEEP, bool SPHERES, bool WO>
 static void launch_variant(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                            const float* normals, const DevMaterial* mats,
                            const DevLight* lights, int blocks, const hipEvent_t* marks,
                            hipStream_t stream) {
-  const size_t lds = DEEP ? sizeof(int) * 3 * kDeepStack * kWavesPerBlock : 0;
   if (P.frames) {  // recursive scenes: one kernel walks each pixel's ray tree
+    const size_t lds = DEEP ? sizeof(int) * kDeepWords * kDeepStack * kWavesPerBlock : 0;
     mark(marks, 0, stream);
     mark(marks, 1, stream);
     mark(marks, 2, stream);
@@ -2256,27 +1434,25 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
     mark(marks, 3, stream);
     return;
   }
-  constexpr int R = kRaysPerLane;
-  constexpr int W = trace_waves<DEEP>();
   RenderParams T = P;
-  T.tile_block = R == 1 && P.tile_begin == 0 && P.tile_step == 1;
-  int tblocks = (trace_packets<W, R>(T) + W - 1) / W;
-  const size_t tlds = DEEP ? sizeof(int) * (1 + 2 * R) * kDeepStack * W : 0;
+  T.tile_block = P.tile_begin == 0 && P.tile_step == 1;
+  const int tblocks = (trace_packets(T) + kTraceWaves - 1) / kTraceWaves;
+  const size_t tlds = DEEP ? sizeof(int) * kDeepWords * kDeepStack * kTraceWaves : 0;
   RenderParams S = T;
   S.tile_cost = nullptr;  // (read by the shadow kernel through tile_order only)
-  const bool ordered = R == 1 && P.num_lights > 0 && T.tile_order != nullptr;
+  const bool ordered = P.num_lights > 0 && T.tile_order != nullptr;
   if (!ordered) T.tile_cost = S.tile_cost = nullptr, T.tile_order = S.tile_order = nullptr;
   mark(marks, 0, stream);
-  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, R, CULL, WO>), dim3(tblocks),
-                     dim3(W * 64), tlds, stream, T, nodes, prims);
+  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, WO>), dim3(tblocks),
+                     dim3(kTraceWaves * 64), tlds, stream, T, nodes, prims);
   mark(marks, 1, stream);
   if (ordered)
     hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, stream, T.tile_cost, T.tile_order,
                        T.num_sel_tiles);
-  const int sblocks = ordered ? (T.num_sel_tiles + W - 1) / W : tblocks;
+  const int sblocks = ordered ? (T.num_sel_tiles + kTraceWaves - 1) / kTraceWaves : tblocks;
   if (P.num_lights > 0)
-    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, R, CULL, WO>), dim3(sblocks),
-                       dim3(W * 64), tlds, stream, S, nodes, prims, lights);
+    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, WO>), dim3(sblocks),
+                       dim3(kTraceWaves * 64), tlds, stream, S, nodes, prims, lights);
   mark(marks, 2, stream);
   hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
                      prims, normals, mats, lights);
@@ -2337,6 +1513,29 @@ hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// The gathered tiles of a multi-device frame back into rows (UntileParams): one wave per tile,
+// one lane per pixel; each 8-pixel row of a tile is 96 contiguous bytes in both layouts.
+__global__ __launch_bounds__(256) void untile_kernel(UntileParams U) {
+  const int t = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
+  if (t >= U.tiles_total) return;
+  const int lane = lane_id();
+  const int tx = t % U.tiles_x, ty = t / U.tiles_x;
+  const int px = tx * kTile + (lane & 7), lr = ty * kTile + (lane >> 3);
+  if (px >= U.width || lr >= U.rows) return;
+  const float* src =
+      U.recv + ((size_t)((t % U.devices) * U.slot + t / U.devices) * (kTile * kTile) + lane) * 3;
+  float* dst = U.out + ((size_t)(U.row0 + lr * U.row_stride) * U.width + px) * 3;
+  dst[0] = src[0];
+  dst[1] = src[1];
+  dst[2] = src[2];
+}
+
+hipError_t launch_untile(const UntileParams& U, hipStream_t stream) {
+  if (U.tiles_total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(untile_kernel, dim3((U.tiles_total + 3) / 4), dim3(256), 0, stream, U);
+  return hipGetLastError();
+}
+
 int max_supported_depth() { return kDeepStack; }
 
 // Self-check of tri_quotients against `/` on random operands spanning the whole fast range:
@@ -2386,34 +1585,29 @@ hipError_t launch_quot_check(unsigned long long seed, long long count, unsigned 
 
 hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                          const float* normals, const DevMaterial* mats, const DevLight* lights,
-                         bool fast, bool deep, bool spheres, bool cull, bool wide_only,
+                         bool fast, bool deep, bool spheres, bool wide_only,
                          const hipEvent_t* marks, hipStream_t stream) {
   if (P.num_sel_tiles <= 0) return hipSuccess;
   const int blocks = (P.num_sel_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
   // wide_only (the culling tree is 4-wide and reaches no binary node): kernels without the
   // binary visit path, which costs the wide walk registers when compiled in
-  const bool wo = wide_only && fast && !deep && !cull && kRaysPerLane == 1 && kBatchLeaves;
-  const int v = (wo ? 16 : 0) | (fast && cull ? 8 : 0) | (fast ? 4 : 0) | (deep ? 2 : 0) |
-                (spheres ? 1 : 0);
+  const bool wo = wide_only && fast && !deep;
+  const int v = (wo ? 8 : 0) | (fast ? 4 : 0) | (deep ? 2 : 0) | (spheres ? 1 : 0);
   switch (v) {
-#define RT_CASE(F, D, S, C, W)                                                                    \
-  case (W ? 16 : 0) | (C ? 8 : 0) | (F ? 4 : 0) | (D ? 2 : 0) | (S ? 1 : 0):                      \
-    launch_variant<F, D, S, C, W>(P, nodes, prims, normals, mats, lights, blocks, marks, stream); \
+#define RT_CASE(F, D, S, W)                                                                    \
+  case (W ? 8 : 0) | (F ? 4 : 0) | (D ? 2 : 0) | (S ? 1 : 0):                                  \
+    launch_variant<F, D, S, W>(P, nodes, prims, normals, mats, lights, blocks, marks, stream); \
     break;
-    RT_CASE(true, false, false, false, true)
-    RT_CASE(true, false, true, false, true)
-    RT_CASE(true, false, false, false, false)
-    RT_CASE(true, false, true, false, false)
-    RT_CASE(true, true, false, false, false)
-    RT_CASE(true, true, true, false, false)
-    RT_CASE(false, false, false, false, false)
-    RT_CASE(false, false, true, false, false)
-    RT_CASE(false, true, false, false, false)
-    RT_CASE(false, true, true, false, false)
-    RT_CASE(true, false, false, true, false)
-    RT_CASE(true, false, true, true, false)
-    RT_CASE(true, true, false, true, false)
-    RT_CASE(true, true, true, true, false)
+    RT_CASE(true, false, false, true)
+    RT_CASE(true, false, true, true)
+    RT_CASE(true, false, false, false)
+    RT_CASE(true, false, true, false)
+    RT_CASE(true, true, false, false)
+    RT_CASE(true, true, true, false)
+    RT_CASE(false, false, false, false)
+    RT_CASE(false, false, true, false)
+    RT_CASE(false, true, false, false)
+    RT_CASE(false, true, true, false)
 #undef RT_CASE
   }
   return hipGetLastError();
@@ -2431,7 +1625,8 @@ unsigned long long read_reset_exact_fallbacks() {
 }
 
 // Copies (and clears) the RT_TIMELINE wave records: out[2][kTimelineWaves][3] start/end
-// ticks of the 100 MHz clock and tile (sel, -1 for none).  Returns the number of values written, 0 in other builds.
+// ticks of the 100 MHz clock and tile (sel, -1 for none).  Returns the number of values
+// written, 0 in other builds.
 long long read_reset_timeline(unsigned long long* out, long long max_values) {
 #ifdef RT_TIMELINE
   const long long n = 2ll * kTimelineWaves * 3;

@@ -1,4 +1,4 @@
-"""Image-tile sharding over GPUs + framebuffer gather.
+"""Image-tile sharding over GPUs + framebuffer gather, one process per GPU.
 
 The reference splits a frame over host threads by interleaved rows (HW2/main.cpp:33-36,
 HW2/Scene.cpp:25).  Here the 8x8-pixel tiles (one wavefront each) of every camera's frame are
@@ -10,18 +10,22 @@ Buffer layout.  Each rank's HBM buffer holds one fixed-size SLOT per camera
 (ceil(tiles / world) tiles, the largest share any rank gets), and the rank's tiles of that
 camera are written back to back (tile-major) at the slot's start.  Every rank's slot c has the
 same size, so camera c's shares are gathered to rank 0 by one equal-size collective
-(torch.distributed "nccl" = RCCL send/recv over xGMI), and the gather of camera c runs on a
-communication stream while the rank renders camera c + 1: only the last camera's gather of a
-step is exposed.  Rank 0 then untiles camera c with ONE index_select of 8-pixel tile rows
-(96 B, contiguous in both layouts) straight into the row-major framebuffer.
+(torch.distributed "nccl" = RCCL over xGMI).  Rank 0 then untiles camera c with ONE
+index_select of 8-pixel tile rows (96 B, contiguous in both layouts) straight into the
+row-major framebuffer.
 
-TileLayout and the untile index are pure bookkeeping (numpy / torch CPU) so the N>1 logic is
-testable with the gloo backend on CPU; FrameRenderer drives the GPU.
+TileGatherRenderer pipelines consecutive steps (frames) over `inflight` buffer sets and render
+streams, the way the one-GPU bench keeps frames in flight: step k renders into set k mod F
+while the gathers of earlier steps run on the communication stream.
+
+TileLayout and the untile index are pure bookkeeping (numpy / torch CPU), and the renderers
+take the tile renderer as a callable, so the N>1 logic is testable with the gloo backend on
+CPU.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Optional, Sequence, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -105,155 +109,160 @@ def untile_camera(gathered_c, layout: TileLayout, c: int, index=None, out=None):
     return out[:h, :w]
 
 
+def scene_tile_renderer(scene) -> Callable:
+    """The GPU tile renderer: rt_render_device of camera c's share, tile-major into `slot`."""
+    def render(sh: CameraShare, slot, stream):
+        scene.render_device(sh.camera, slot.data_ptr(), tile_begin=sh.tile_begin,
+                            tile_step=sh.tile_step, tile_major=True, stream=stream.cuda_stream)
+    return render
+
+
 class FrameRenderer:
-    """One step = render every camera of `scene`; with gather=True, gather to rank 0 and untile.
+    """One GPU, no exchange: one step = every camera of `scene` rendered in place into
+    row-major frames.  Consecutive steps go to `inflight` streams in turn (each with its own
+    frames and, in the library, its own scratch), so a frame's last, sparsely occupied waves
+    overlap the next frame's work; finish() joins them back into `stream`."""
 
-    world == 1 and gather == False renders each camera in place into a row-major frame.  With
-    inflight = F > 1 consecutive steps go to F streams in turn (each with its own frames and,
-    in the library, its own scratch), so a frame's last, sparsely occupied waves overlap the
-    next frame's work; finish() joins them back into `stream`.
-
-    gather=True (one process per GPU): camera c's share is rendered on `stream` in `chunks`
-    pieces (rt_render_device_range); an event hands each piece to a communication stream that
-    gathers it to rank 0 (RCCL) while `stream` renders the next piece, and rank 0 untiles
-    camera c on the comm stream after its last piece.  Only the last piece of the last camera
-    of a step is exposed.  Every rank's slot has the same size, so piece j of camera c is
-    slot tiles [j*cs, (j+1)*cs) on every rank (cs = ceil(slot / chunks)); a rank whose share
-    ends earlier sends its untouched (zero) padding, which the untile index never reads.
-    The rank buffer alternates between two copies per step, and a slot is rendered again only
-    after its gather two steps earlier has finished (per-slot events), so consecutive steps
-    pipeline too.  Rank 0's receive buffer and frames are only touched on the comm stream, in
-    order.  host_staging=True (the gloo rehearsal) does the same exchange synchronously via
-    host copies.
-    """
-
-    def __init__(self, scene, layout_or_none: Optional[TileLayout], stream, gather: bool,
-                 host_staging: bool = False, chunks: int = 1, inflight: int = 1):
+    def __init__(self, scene, stream, inflight: int = 1):
         import torch
-        import torch.distributed as dist
-        self.torch, self.dist = torch, dist
         self.scene = scene
         self.stream = stream
-        self.gather = gather
-        self.host_staging = host_staging
         self.sizes = [(scene.camera(c).width, scene.camera(c).height)
                       for c in range(scene.num_cameras)]
-        self.layout = layout_or_none
         dev = torch.device("cuda", torch.cuda.current_device())
-        if not gather:
-            self.inflight = max(1, int(inflight))
-            self.streams = [stream] + [torch.cuda.Stream(device=dev)
-                                       for _ in range(self.inflight - 1)]
-            self.frame_sets = [[torch.empty((h, w, 3), dtype=torch.float32, device=dev)
-                                for (w, h) in self.sizes] for _ in range(self.inflight)]
-            self.frames = self.frame_sets[0]
-            self.k = 0
-            return
-        L = self.layout
-        assert L.sizes == self.sizes, "tile layout built for other frame sizes"
-        self.rank = L.rank
-        self.pieces = [chunk_ranges(sh.slot, chunks) for sh in L.shares]
-        # two rank buffers, alternating per step: step k + 1 renders while step k's last
-        # slot is still being gathered
-        self.local = [torch.zeros((L.buffer_tiles, TILE_FLOATS), dtype=torch.float32, device=dev)
-                      for _ in range(2)]
-        self.buf = 0
-        self.comm = torch.cuda.Stream(device=dev)
-        # pieces alternate between two render streams (the library gives each its own scratch),
-        # so one piece's last, sparsely occupied waves overlap the next piece
-        self.pstreams = [stream, torch.cuda.Stream(device=dev)]
-        self.rendered = [[torch.cuda.Event() for _ in p] for p in self.pieces]
-        self.slot_free = [[torch.cuda.Event() for _ in L.shares] for _ in range(2)]
-        self.slot_used = [[False] * len(L.shares) for _ in range(2)]
-        if L.rank == 0:
-            self.gathered = [torch.empty((L.world, s.slot, TILE_FLOATS), dtype=torch.float32,
-                                         device=dev) for s in L.shares]
-            self.index = [torch.as_tensor(L.row_index(c).reshape(-1), device=dev)
-                          for c in range(len(L.shares))]
-            self.padded = []
-            for (w, h) in self.sizes:
-                tx, ty = tiles_of((w, h))
-                self.padded.append(torch.empty((ty * TILE, tx * TILE, 3), dtype=torch.float32,
-                                               device=dev))
-            self.frames = [p[:h, :w] for p, (w, h) in zip(self.padded, self.sizes)]
-        else:
-            self.frames = None
-
-    def _slot(self, sh: CameraShare):
-        return self.local[self.buf][sh.offset:sh.offset + sh.slot]
-
-    def _exchange(self, c: int, sh: CameraShare, j: int):
-        torch, dist, L = self.torch, self.dist, self.layout
-        root = self.rank == 0
-        lo, hi = self.pieces[c][j]
-        last = j == len(self.pieces[c]) - 1
-        if self.host_staging:  # gloo: host copies, synchronous
-            self.stream.synchronize()
-            host = self._slot(sh)[lo:hi].cpu()
-            glist = list(torch.empty((L.world, hi - lo, TILE_FLOATS))) if root else None
-            dist.gather(host, glist, dst=0)
-            if root:
-                self.gathered[c][:, lo:hi].copy_(torch.stack(glist))
-                if last:
-                    untile_camera(self.gathered[c].view(-1, TILE_FLOATS), L, c, self.index[c],
-                                  self.padded[c])
-            return
-        with torch.cuda.stream(self.comm):
-            self.comm.wait_event(self.rendered[c][j])
-            outs = [self.gathered[c][r, lo:hi] for r in range(L.world)] if root else None
-            work = dist.gather(self._slot(sh)[lo:hi], outs, dst=0, async_op=True)
-            work.wait()  # the comm stream waits for the collective (host does not block)
-            if last:
-                if root:
-                    untile_camera(self.gathered[c].view(-1, TILE_FLOATS), L, c, self.index[c],
-                                  self.padded[c])
-                self.slot_free[self.buf][c].record(self.comm)
+        self.inflight = max(1, int(inflight))
+        self.streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(self.inflight - 1)]
+        self.frame_sets = [[torch.empty((h, w, 3), dtype=torch.float32, device=dev)
+                            for (w, h) in self.sizes] for _ in range(self.inflight)]
+        self.frames = self.frame_sets[0]
+        self.k = 0
 
     def step(self, events=None):
-        s = self.stream.cuda_stream
+        slot = self.k % self.inflight
+        self.k += 1
+        st = self.streams[slot]
         if events is not None:
-            events[0].record(self.stream)
-        if not self.gather:
-            slot = self.k % self.inflight
-            self.k += 1
-            st = self.streams[slot]
-            if events is not None and slot:
-                events[0].record(st)
-            self.frames = self.frame_sets[slot]
-            for c, f in enumerate(self.frames):
-                self.scene.render_device(c, f.data_ptr(), stream=st.cuda_stream)
-            if events is not None:
-                events[1].record(st)
-            return self.frames
-        self.buf ^= 1
-        k = 0
-        for c, sh in enumerate(self.layout.shares):
-            if self.slot_used[self.buf][c]:  # this slot's gather two steps ago
-                for ps in self.pstreams:
-                    ps.wait_event(self.slot_free[self.buf][c])
-            slot = self._slot(sh)
-            for j, (lo, begin, n) in enumerate(piece_calls(sh, self.pieces[c])):
-                ps = self.pstreams[k % 2] if not self.host_staging else self.stream
-                k += 1
-                if n > 0:
-                    self.scene.render_device(sh.camera, slot[lo].data_ptr(), tile_begin=begin,
-                                             tile_step=sh.tile_step, tile_count=n,
-                                             tile_major=True, stream=ps.cuda_stream)
-                self.rendered[c][j].record(ps)
-                self._exchange(c, sh, j)
-            self.slot_used[self.buf][c] = True
+            events[0].record(st)
+        self.frames = self.frame_sets[slot]
+        for c, f in enumerate(self.frames):
+            self.scene.render_device(c, f.data_ptr(), stream=st.cuda_stream)
         if events is not None:
-            events[1].record(self.stream)
+            events[1].record(st)
         return self.frames
 
     def finish(self):
-        """Make `stream` wait for every outstanding gather / untile of this renderer."""
-        if self.gather and not self.host_staging:
-            self.stream.wait_stream(self.pstreams[1])
-            self.stream.wait_stream(self.comm)
-        elif not self.gather:
-            for st in self.streams[1:]:
-                self.stream.wait_stream(st)
+        for st in self.streams[1:]:
+            self.stream.wait_stream(st)
+
+
+class TileGatherRenderer:
+    """One step = every camera of the job split over the ranks by tiles (TileLayout), gathered
+    to rank 0 and untiled there: strong scaling of one frame over the N GPUs.
+
+    render(share, slot, stream) writes the rank's tiles of camera share.camera tile-major into
+    `slot` (a [slot tiles, 192] view) on `stream` (scene_tile_renderer on the GPU).  Step k uses
+    buffer set s = k mod F (F = inflight): its render stream renders every share into set s,
+    an event hands the set to the communication stream, which gathers each camera's slots to
+    rank 0 (one equal-size dist.gather per camera: RCCL send / receive pairs over xGMI with
+    backend "nccl") and, on rank 0, untiles them into set s's frames.  A set is rendered again
+    only after its gather F steps earlier has finished (per-set events), so up to F frames are
+    in flight per rank and a rank's render streams never wait on the exchange of the frame
+    before.  host_staging=True (gloo, CPU tensors): the same exchange synchronously through the
+    host, one buffer set.  frames: rank 0's frames of the last step (complete after finish())."""
+
+    def __init__(self, layout: TileLayout, stream, render: Callable, inflight: int = 2,
+                 host_staging: bool = False, device=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.layout = L = layout
+        self.stream = stream
+        self.render = render
+        self.host_staging = host_staging
+        self.inflight = 1 if host_staging else max(1, int(inflight))
+        F = self.inflight
+        dev = device if device is not None else (
+            "cpu" if host_staging else torch.device("cuda", torch.cuda.current_device()))
+        self.rank = L.rank
+        if host_staging:
+            self.rstreams = [stream]
+            self.comm = None
+        else:
+            self.rstreams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(F - 1)]
+            self.comm = torch.cuda.Stream(device=dev)
+        self.local = [torch.zeros((L.buffer_tiles, TILE_FLOATS), dtype=torch.float32, device=dev)
+                      for _ in range(F)]
+        self.done = [torch.cuda.Event() if not host_staging else None for _ in range(F)]
+        self.handoff = [torch.cuda.Event() if not host_staging else None for _ in range(F)]
+        self.used = [False] * F
+        self.k = 0
+        self.frames = None
+        if self.rank == 0:
+            self.gathered = [[torch.empty((L.world, sh.slot, TILE_FLOATS), dtype=torch.float32,
+                                          device=dev) for sh in L.shares] for _ in range(F)]
+            self.index = [torch.as_tensor(L.row_index(c).reshape(-1), device=dev)
+                          for c in range(len(L.shares))]
+            self.padded = []
+            for _ in range(F):
+                row = []
+                for (w, h) in L.sizes:
+                    tx, ty = tiles_of((w, h))
+                    row.append(torch.empty((ty * TILE, tx * TILE, 3), dtype=torch.float32,
+                                           device=dev))
+                self.padded.append(row)
+
+    def _slot(self, s: int, sh: CameraShare):
+        return self.local[s][sh.offset:sh.offset + sh.slot]
+
+    def _gather(self, s: int):
+        torch, dist, L = self.torch, self.dist, self.layout
+        root = self.rank == 0
+        for c, sh in enumerate(L.shares):
+            if self.host_staging:
+                glist = list(torch.empty((L.world, sh.slot, TILE_FLOATS))) if root else None
+                dist.gather(self._slot(s, sh).cpu(), glist, dst=0)
+                if root:
+                    self.gathered[s][c].copy_(torch.stack(glist))
+            else:
+                outs = list(self.gathered[s][c]) if root else None
+                dist.gather(self._slot(s, sh), outs, dst=0, async_op=True).wait()
+            if root:
+                untile_camera(self.gathered[s][c].view(-1, TILE_FLOATS), L, c, self.index[c],
+                              self.padded[s][c])
+
+    def step(self, events=None):
+        s = self.k % self.inflight
+        self.k += 1
+        st = self.rstreams[s]
+        if not self.host_staging and self.used[s]:  # its gather `inflight` steps ago
+            st.wait_event(self.done[s])
+        if events is not None:
+            events[0].record(st)
+        for sh in self.layout.shares:
+            if sh.count > 0:
+                self.render(sh, self._slot(s, sh), st)
+        if events is not None:
+            events[1].record(st)
+        if self.host_staging:
+            self._gather(s)
+        else:
+            self.handoff[s].record(st)
+            with self.torch.cuda.stream(self.comm):
+                self.comm.wait_event(self.handoff[s])
+                self._gather(s)
+                self.done[s].record(self.comm)
+            self.used[s] = True
+        if self.rank == 0:
+            self.frames = [p[:h, :w] for p, (w, h) in zip(self.padded[s], self.layout.sizes)]
+        return self.frames
+
+    def finish(self):
+        """Make `stream` wait for every render stream and every outstanding gather / untile."""
+        if self.host_staging:
+            return
+        for st in self.rstreams[1:]:
+            self.stream.wait_stream(st)
+        self.stream.wait_stream(self.comm)
 
 
 class FrameOwners:
@@ -273,12 +282,12 @@ class FrameOwners:
 class FrameGatherRenderer:
     """One step = every rank renders its own whole frames (FrameOwners) in place and rank 0
     gathers them: per round j, one equal-size collective of full row-major frames (RCCL over
-    xGMI with backend "nccl", host copies with gloo).  Unlike the tile deal of FrameRenderer,
-    a rank's frame is one launch of a full frame, so per-launch work does not shrink as the
-    world grows.  Consecutive steps alternate over `inflight` render streams, each with its own
-    send / receive buffers; a buffer set is rendered again only after its gathers `inflight`
-    steps earlier have finished (events), and rank 0's frames of a step are complete once
-    finish() has joined the streams.
+    xGMI with backend "nccl", host copies with gloo).  Unlike the tile deal of
+    TileGatherRenderer, a rank's frame is one launch of a full frame, so per-launch work does
+    not shrink as the world grows (weak scaling).  Consecutive steps alternate over `inflight`
+    render streams, each with its own send / receive buffers; a buffer set is rendered again
+    only after its gathers `inflight` steps earlier have finished (events), and rank 0's frames
+    of a step are complete once finish() has joined the streams.
 
     render(c, out, stream) writes camera c's [h, w, 3] frame into tensor `out` on `stream`
     (None: the scene's rt_render_device), so the same bookkeeping runs in the gloo tests."""
@@ -359,26 +368,8 @@ class FrameGatherRenderer:
         self.stream.wait_stream(self.comm)
 
 
-def chunk_ranges(slot: int, chunks: int) -> List[Tuple[int, int]]:
-    """Pieces [lo, hi) of a slot of `slot` tiles, ceil(slot / chunks) tiles each (the last may
-    be shorter); the same on every rank, since every rank's slot has the same size."""
-    chunks = max(1, min(int(chunks), max(1, slot)))
-    cs = (slot + chunks - 1) // chunks
-    return [(lo, min(slot, lo + cs)) for lo in range(0, max(slot, 1), cs)] if slot else [(0, 0)]
-
-
-def piece_calls(sh: CameraShare, pieces: List[Tuple[int, int]]) -> List[Tuple[int, int, int]]:
-    """The rt_render_device_range call of each piece of a rank's share: (first slot tile,
-    first camera tile, tile count).  Slot tile k holds camera tile tile_begin + k*tile_step."""
-    return [(lo, sh.tile_begin + lo * sh.tile_step, max(0, min(hi, sh.count) - lo))
-            for lo, hi in pieces]
-
-
-def TilePlan(scene, world: int, rank: int, force: bool = False) -> Optional[TileLayout]:
-    """Tile layout for every camera of `scene` (None when a single rank renders in place,
-    unless `force`: the one-rank rehearsal of the gather pipeline)."""
-    if world == 1 and not force:
-        return None
+def TilePlan(scene, world: int, rank: int) -> TileLayout:
+    """Tile layout for every camera of `scene`, checked against the library's tile count."""
     sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
     L = TileLayout(sizes, world, rank)
     for c in range(scene.num_cameras):

@@ -31,11 +31,21 @@ class Scene:
     ``result`` (an ``(h, w, 3)`` float32 array standing for ``Pixel[w*h]``) receive the fp32
     radiance ``Pixel::color``; other rows are untouched.  Errors raise ``RTError`` (the
     reference throws ``std::runtime_error`` from the loader, HW2/Scene.cpp:204,208).
+
+    ``devices`` (a list of GPU ordinals) makes one scene over several GPUs of this process
+    (rt_scene_load_xml_multi): every frame's tiles are dealt over them and gathered onto
+    ``devices[0]`` with RCCL.
     """
 
-    def __init__(self, file_name: str, device: int = -1, traversal: str = "fast"):
+    def __init__(self, file_name: str, device: int = -1, traversal: str = "fast",
+                 devices: Optional[list] = None):
         h = C.c_void_p()
-        check(lib().rt_scene_load_xml(str(file_name).encode(), device, C.byref(h)))
+        if devices is not None:
+            arr = (C.c_int * len(devices))(*devices)
+            check(lib().rt_scene_load_xml_multi(str(file_name).encode(), len(devices), arr,
+                                                C.byref(h)))
+        else:
+            check(lib().rt_scene_load_xml(str(file_name).encode(), device, C.byref(h)))
         self._h = h
         self.set_traversal(traversal)
 
@@ -77,6 +87,10 @@ class Scene:
         return lib().rt_scene_num_lights(self._h)
 
     @property
+    def device_count(self) -> int:
+        return lib().rt_scene_device_count(self._h)
+
+    @property
     def bvh_depth(self) -> int:
         return lib().rt_scene_bvh_depth(self._h)
 
@@ -88,8 +102,7 @@ class Scene:
                           tuple(c.top_left), tuple(c.s_u), tuple(c.s_v))
 
     def set_traversal(self, mode: str) -> None:
-        m = {"fast": _lib.RT_TRAVERSAL_FAST, "reference": _lib.RT_TRAVERSAL_REFERENCE,
-             "cull": _lib.RT_TRAVERSAL_CULL}[mode]
+        m = {"fast": _lib.RT_TRAVERSAL_FAST, "reference": _lib.RT_TRAVERSAL_REFERENCE}[mode]
         check(lib().rt_set_traversal(self._h, m))
 
     def set_msaa_seed(self, seed: int) -> None:
@@ -132,6 +145,10 @@ class Scene:
         check(lib().rt_render_device_range(self._h, camera_index, starting_row, row_stride,
                                            tile_begin, tile_step, tile_count, int(tile_major),
                                            C.c_void_p(out_ptr), C.c_void_p(stream)))
+
+    def release_stream(self, stream: int) -> None:
+        """Frees the scratch the library keeps for HIP stream ``stream`` (after waiting for it)."""
+        check(lib().rt_release_stream_scratch(self._h, C.c_void_p(stream)))
 
     def set_kernel_timing(self, enable: bool) -> None:
         check(lib().rt_set_kernel_timing(self._h, int(enable)))

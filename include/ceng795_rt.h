@@ -12,6 +12,7 @@
  * seam stays on the host, as in the reference: XML ingest (HW2/Scene.cpp:198-451), the
  * Camera basis (HW2/Camera.h:10-29) and the BVH build (HW2/Bounding_volume_hierarchy.cpp:3-29)
  * happen in rt_scene_create / rt_scene_load_xml, untimed like the reference's Scene ctor.
+ * rt_scene_create_multi spreads one scene's frames over several GPUs of the process.
  *
  * Plain C types only: no torch, no HIP types in signatures (streams are void*).
  * Every function returns 0 on success or a negative RT_E* code; the message of the last
@@ -23,8 +24,9 @@
 extern "C" {
 #endif
 
-#define CENG795_RT_ABI_VERSION 3  /* 2: MSAA cameras + rt_set_msaa_seed; 3: tile ranges,
-                                      kernel timing */
+#define CENG795_RT_ABI_VERSION 4  /* 2: MSAA cameras + rt_set_msaa_seed; 3: tile ranges,
+                                      kernel timing; 4: multi-device scenes, stream scratch
+                                      release, no CULL mode */
 
 enum {
   RT_OK = 0,
@@ -106,16 +108,11 @@ typedef struct rt_stats {
   double kernel_ms;             /* HIP-event time of the render kernel(s)  */
 } rt_stats;
 
-/* Traversal modes.  FAST and REFERENCE give the reference's result on every input (DESIGN.md
- * §4.1); CULL is faster on some scenes but rests on an unproven numerical assumption. */
+/* Traversal modes.  Both give the reference's result on every input. */
 enum {
   RT_TRAVERSAL_FAST = 0,        /* culling tree over reference treelets, near-first order,
-                                   batched leaf tests (default; exact)                        */
-  RT_TRAVERSAL_REFERENCE = 1,   /* visits every box the reference visits, in its order        */
-  RT_TRAVERSAL_CULL = 2         /* FAST + distance culling: skips a child whose entry distance
-                                   exceeds best_t (1 + 2^-8) — exact unless a triangle's fp32 t
-                                   undershoots its true distance by that much (rays within
-                                   ~1e-5 rad of its plane); opt-in, never the default        */
+                                   batched leaf tests (default)                               */
+  RT_TRAVERSAL_REFERENCE = 1    /* visits every box the reference visits, in its order        */
 };
 typedef struct rt_scene rt_scene;
 
@@ -127,6 +124,21 @@ void rt_scene_destroy(rt_scene* scene);
 
 /* Host convenience: HW2/Scene.cpp:198-451's XML ingest, then rt_scene_create. */
 int rt_scene_load_xml(const char* xml_path, int device, rt_scene** out);
+
+/* One scene over several GPUs of this process (the reference's T render
+ * threads, HW2/main.cpp:33-36, become the devices of one node).  The scene is built once on
+ * the host and replicated on devices[0 .. device_count-1] (NULL: devices 0 .. device_count-1);
+ * devices[0] holds the output.  rt_render / rt_render_device on such a scene deal the frame's
+ * 8x8 tiles round-robin over the devices (tile t -> device t mod device_count), render every
+ * share on its own device, gather the shares onto devices[0] with RCCL (one communicator per
+ * device, ncclCommInitAll; send / receive pairs in one group, over xGMI) and untile them there.
+ * Pixels are the single-device ones bit for bit.  MSAA cameras render on devices[0] alone.
+ * Frames of one multi-device scene are serialised (its RCCL communicators are shared). */
+int rt_scene_create_multi(const rt_scene_desc* desc, int device_count, const int* devices,
+                          rt_scene** out);
+int rt_scene_load_xml_multi(const char* xml_path, int device_count, const int* devices,
+                            rt_scene** out);
+int rt_scene_device_count(const rt_scene* scene);
 
 int rt_scene_num_cameras(const rt_scene* scene);
 int rt_scene_camera(const rt_scene* scene, int camera_index, rt_camera* out);
@@ -166,7 +178,8 @@ int rt_set_traversal(rt_scene* scene, int mode);
 int rt_render(rt_scene* scene, int camera_index, int starting_row, int row_stride,
               float* out_rgb, rt_stats* stats);
 
-/* Device-resident variant for multi-GPU image tiling.  The image (rows starting_row +
+/* Device-resident variant (the building block of the one-process-per-GPU image tiling, and
+ * of frames kept in HBM).  The image (rows starting_row +
  * k*row_stride) is cut into 8x8 tiles numbered row-major; this call renders tiles
  * tile_begin, tile_begin + tile_step, ... into d_out (device memory):
  *   tile_major == 0: d_out is a full w*h*3 frame, written in place;
@@ -177,7 +190,10 @@ int rt_render(rt_scene* scene, int camera_index, int starting_row, int row_strid
  * accumulate on the device until rt_collect_stats.  Calls on one stream run in order and share
  * that stream's scratch buffers (hit records, occlusion bits, tile schedule); each further
  * stream a scene renders on gets scratch of its own, so frames on different streams may be
- * in flight at the same time (their outputs must not overlap). */
+ * in flight at the same time (their outputs must not overlap); host threads may enqueue
+ * concurrently.  A stream's scratch lives until rt_release_stream_scratch or the scene's
+ * destruction.  Multi-device scenes: whole frames only (tile_begin 0, tile_step 1,
+ * tile_major 0; row subsets allowed), d_out and hip_stream on devices[0]. */
 int rt_render_device(rt_scene* scene, int camera_index, int starting_row, int row_stride,
                      int tile_begin, int tile_step, int tile_major, float* d_out,
                      void* hip_stream);
@@ -189,6 +205,9 @@ int rt_render_device(rt_scene* scene, int camera_index, int starting_row, int ro
 int rt_render_device_range(rt_scene* scene, int camera_index, int starting_row, int row_stride,
                            int tile_begin, int tile_step, int tile_count, int tile_major,
                            float* d_out, void* hip_stream);
+/* Waits for `hip_stream` and frees the scratch rt_render_device keeps for it (no-op for a
+ * stream the scene never rendered on).  Streams that come and go should release theirs. */
+int rt_release_stream_scratch(rt_scene* scene, void* hip_stream);
 /* Per-kernel timing of render launches: while enabled, every launch records HIP events around
  * its traversal kernels on the launch's stream.  rt_read_kernel_times returns (and resets)
  * the summed milliseconds ms4 = {primary-ray kernel, shadow-ray kernel, shade kernel (or the
@@ -206,8 +225,8 @@ int rt_collect_stats(rt_scene* scene, rt_stats* stats);
  * [2] secondary rays [3] primary hits; RT_DIAG builds (libceng795_rt_diag.so) add packet-level
  * work: [4..7] primary node visits / active lanes summed over visits / leaf visits / leaf
  * lane tests, [8..11] the same for shadow rays, [12] lanes that fell back to the exact slab
- * test, [13] subtree pieces handed between waves (RT_EXP_SHARE experiment builds only),
- * [14] / [15] the primary / shadow node visits that were 4-wide nodes (included in [4] / [8]).
+ * test, [13] unused, [14] / [15] the primary / shadow node visits that were 4-wide nodes
+ * (included in [4] / [8]).
  * Returns 1 for a diagnostic build, 0 otherwise (columns 4..15 then read 0). */
 int rt_debug_counters(rt_scene* scene, long long* out16);
 

@@ -1,7 +1,9 @@
 """Multi-rank tile sharding + framebuffer gather (ceng795_amd/dist_tiles.py), exercised with
-the gloo backend on CPU.  The GPU path (bench.py, FrameRenderer) uses the same TileLayout,
-per-camera slots and untile_camera(); only the tile renderer differs (here: tiles cut out of
-known frames) and the collective runs on host tensors."""
+the gloo backend on CPU.  The GPU path (bench.py, TileGatherRenderer) uses the same
+TileLayout, per-camera slots and untile_camera(); only the tile renderer differs (here: tiles
+cut out of known frames) and the collective runs on host tensors.  The last tests run bench.py
+itself: `--gpus N` without a launcher starts N ranks, and `--cpu-rehearsal` drives the default
+N>1 path (tile deal, pipelined gather, untile, check) with synthetic tiles."""
 import os
 import socket
 
@@ -11,8 +13,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from ceng795_amd.dist_tiles import (TILE, TILE_FLOATS, TileLayout, chunk_ranges, piece_calls,
-                                    untile_camera)
+from ceng795_amd.dist_tiles import TILE, TILE_FLOATS, TileLayout, untile_camera
 
 SIZES = [(37, 21), (64, 40), (5, 9), (96, 64)]  # (w, h): ragged edges, tiny frames
 
@@ -115,73 +116,75 @@ def test_every_tile_rendered_exactly_once(world):
         assert idx.max() < world * L0.slots[c] * TILE
 
 
-def _render_pieces(L, frames, c, pieces):
-    """What FrameRenderer's rt_render_device_range calls write into camera c's slot."""
-    sh = L.shares[c]
-    slot = torch.zeros((sh.slot, TILE_FLOATS))
-    for lo, begin, n in piece_calls(sh, pieces):
-        for k in range(n):
-            slot[lo + k] = torch.from_numpy(_tile(frames[c], begin + k * sh.tile_step))
-    return slot
-
-
-def _split_worker(rank, world, port, outdir, size, chunks):
-    """One frame split over the ranks (C4's strong-scaling mode), gathered piece by piece."""
+def _pipeline_worker(rank, world, port, outdir, sizes, steps):
+    """TileGatherRenderer over gloo: several cameras per step, several steps (buffers reused);
+    every rank renders exactly its tiles, and rank 0's frames equal the truth each step."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    rng = np.random.default_rng(11)
-    w, h = size
-    frames = [rng.standard_normal((h, w, 3)).astype(np.float32)]
-    L = TileLayout([size], world, rank)
-    sh = L.shares[0]
-    pieces = chunk_ranges(sh.slot, chunks)
-    slot = _render_pieces(L, frames, 0, pieces)
-    gathered = torch.full((world, sh.slot, TILE_FLOATS), float("nan"))
-    for lo, hi in pieces:
-        outs = [gathered[r, lo:hi] for r in range(world)] if rank == 0 else None
+    from ceng795_amd.dist_tiles import TileGatherRenderer
+    L = TileLayout(sizes, world, rank)
+    done = []
+
+    def truth(step):
+        return _frames(100 + step)[:len(sizes)] if sizes == SIZES else \
+            [np.random.default_rng(100 + step).standard_normal((h, w, 3)).astype(np.float32)
+             for (w, h) in sizes]
+
+    state = {"step": 0}
+
+    def render(sh, slot, stream):  # what rt_render_device(tile_major=True) writes
+        frame = truth(state["step"])[sh.camera]
+        for k in range(sh.count):
+            slot[k] = torch.from_numpy(_tile(frame, sh.tile_begin + k * sh.tile_step))
+        done.append((sh.camera, sh.count))
+
+    R = TileGatherRenderer(L, None, render, host_staging=True, device="cpu")
+    ok = True
+    for step in range(steps):
+        state["step"] = step
+        frames = R.step()
         if rank == 0:
-            tmp = [torch.empty(hi - lo, TILE_FLOATS) for _ in range(world)]
-            dist.gather(slot[lo:hi].contiguous(), tmp, dst=0)
-            for o, t in zip(outs, tmp):
-                o.copy_(t)
-        else:
-            dist.gather(slot[lo:hi].contiguous(), None, dst=0)
+            ok &= all(_same(frames[c].contiguous().numpy(), truth(step)[c])
+                      for c in range(len(sizes)))
+    R.finish()
+    assert sorted(done) == sorted([(sh.camera, sh.count) for sh in L.shares if sh.count] * steps)
     if rank == 0:
-        got = untile_camera(gathered.view(-1, TILE_FLOATS), L, 0)
-        ok = _same(got.contiguous().numpy(), frames[0])
         with open(os.path.join(outdir, "result"), "w") as fh:
             fh.write("ok" if ok else "mismatch")
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,size,chunks", [(2, (3840 // 8, 2160 // 8), 4), (2, (37, 21), 3),
-                                               (3, (64, 40), 1), (3, (21, 13), 5)])
-def test_single_frame_split_in_pieces(tmp_path, world, size, chunks):
-    mp.spawn(_split_worker, args=(world, _free_port(), str(tmp_path), size, chunks),
+@pytest.mark.parametrize("world,sizes,steps", [(2, [(1920 // 8, 1080 // 8)], 3),
+                                               (3, SIZES, 2), (2, [(5, 9)], 2)])
+def test_tile_gather_renderer_pipeline(tmp_path, world, sizes, steps):
+    mp.spawn(_pipeline_worker, args=(world, _free_port(), str(tmp_path), sizes, steps),
              nprocs=world, join=True)
     assert (tmp_path / "result").read_text() == "ok"
 
 
-@pytest.mark.parametrize("slot,chunks", [(0, 4), (1, 4), (7, 3), (8, 4), (130, 4), (5, 1)])
-def test_chunk_ranges_cover_slot(slot, chunks):
-    pieces = chunk_ranges(slot, chunks)
-    covered = [t for lo, hi in pieces for t in range(lo, hi)]
-    assert covered == list(range(slot))
-    assert len(pieces) <= max(1, chunks)
-
-
-def test_piece_calls_cover_share():
-    for world in (1, 2, 3, 8):
-        for size in [(37, 21), (3840 // 8, 2160 // 8)]:
-            for r in range(world):
-                L = TileLayout([size], world, r)
-                sh = L.shares[0]
-                tiles = []
-                for lo, begin, n in piece_calls(sh, chunk_ranges(sh.slot, 4)):
-                    tiles += [begin + k * sh.tile_step for k in range(n)]
-                assert tiles == [sh.tile_begin + k * world for k in range(sh.count)]
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_self_launches_ranks(tmp_path, world):
+    """`python bench.py --gpus N` with no launcher: bench.py starts N ranks itself (before
+    any GPU call) and rank 0 prints one JSON line with n_gpus == N; the default N>1 path (tile
+    deal, TileGatherRenderer exchange, untile) reassembles the frame bit for bit."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world),
+                        "--cpu-rehearsal", "--workload", "c2", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, env=env, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == world and line["scaling"] == "strong"
+    assert line["config"]["parallelism"] == f"tiles{world}+gloo_gather"
+    assert line["config"]["gather_verified"] is True
 
 
 # --------------------------------------------------------------------------- whole frames per rank

@@ -29,7 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("xml")
     ap.add_argument("--camera", type=int, default=0)
-    ap.add_argument("--traversal", default="fast", choices=["fast", "reference", "cull"])
+    ap.add_argument("--traversal", default="fast", choices=["fast", "reference"])
     a = ap.parse_args()
     if "diag" not in os.environ.get("CENG795_LIB", ""):
         raise SystemExit("run with CENG795_LIB=diag (an RT_DIAG build)")
