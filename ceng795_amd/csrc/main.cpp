@@ -1,7 +1,9 @@
-// `raytracer <scene.xml>` — the host driver of HW2/main.cpp:10-70 on top of the C ABI:
-// parse the scene, then for every <Camera> render (timed), quantise and write <ImageName>.
-// The reference spawns hardware_concurrency() threads on render_image (main.cpp:33-36); here
-// one rt_render call renders every row on the GPU.
+// `raytracer [--gpus N] [--reference-traversal] <scene.xml>` — the host driver of
+// HW2/main.cpp:10-70 on top of the C ABI: parse the scene, then for every <Camera> render
+// (timed), quantise and write <ImageName>.  The reference spawns hardware_concurrency()
+// threads on render_image (main.cpp:33-36); here one rt_render call renders every row on the
+// GPU, or with --gpus N on N GPUs of the node (rt_scene_load_xml_multi: tiles dealt over the
+// devices, RCCL gather onto the first).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -11,15 +13,26 @@
 #include "../../include/ceng795_rt.h"
 
 int main(int argc, char** argv) {
-  if (argc < 2) {
+  int mode = RT_TRAVERSAL_FAST, gpus = 0;
+  const char* xml = nullptr;
+  for (int i = 1; i < argc; i++) {
+    const std::string a = argv[i];
+    if (a == "--reference-traversal") {
+      mode = RT_TRAVERSAL_REFERENCE;
+    } else if (a == "--gpus" && i + 1 < argc) {
+      gpus = std::atoi(argv[++i]);
+    } else {
+      xml = argv[i];
+    }
+  }
+  if (!xml) {
     std::fprintf(stderr, "Please provide scene file as argument\n");
     return 1;
   }
-  const int mode = (argc > 2 && std::string(argv[2]) == "--reference-traversal")
-                       ? RT_TRAVERSAL_REFERENCE
-                       : RT_TRAVERSAL_FAST;
   rt_scene* scene = nullptr;
-  if (rt_scene_load_xml(argv[1], -1, &scene) != RT_OK) {
+  const int rc = gpus > 0 ? rt_scene_load_xml_multi(xml, gpus, nullptr, &scene)
+                          : rt_scene_load_xml(xml, -1, &scene);
+  if (rc != RT_OK) {
     std::fprintf(stderr, "%s\n", rt_last_error());
     return 1;
   }
@@ -31,7 +44,7 @@ int main(int argc, char** argv) {
     rt_camera cam;
     rt_scene_camera(scene, c, &cam);
     std::vector<float> rgb((size_t)cam.width * cam.height * 3, 0.0f);
-    std::printf("Starting rendering on the GPU\n");
+    std::printf("Starting rendering on %d GPU(s)\n", rt_scene_device_count(scene));
     const auto t0 = std::chrono::steady_clock::now();
     rt_stats st;
     if (rt_render(scene, c, 0, 1, rgb.data(), &st) != RT_OK) {

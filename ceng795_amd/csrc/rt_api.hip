@@ -275,19 +275,33 @@ int occ_words(const HostScene& h) { return std::max(1, ((int)h.lights.size() + 3
 
 // A counter buffer: kCounterRows x kCounterWidth ray counters.
 constexpr size_t kCounterAlloc = (size_t)kCounterWidth * kCounterRows;
-// CENG795_RT_ORDER=0 turns the heavy-first shadow dispatch off (A/B experiments); the
-// order cannot change any result, only which tiles start first.
-bool order_enabled() {
-  static const bool on = [] {
+// Dispatch order of the traversal kernels: CENG795_RT_ORDER=0 off, 1 heavy
+// first over the whole frame, 2 (default) heavy first within each XCD's part of the frame;
+// CENG795_RT_PROBE=0 orders the shadow kernel only (no probe pass before the primary).  The
+// order never changes a result, only which tiles start first.
+int order_regions() {
+  static const int r = [] {
     const char* e = std::getenv("CENG795_RT_ORDER");
+    if (e && e[0] == '0') return 0;
+    if (e && e[0] == '1') return 1;
+    return 8;
+  }();
+  return r;
+}
+bool probe_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CENG795_RT_PROBE");
     return !(e && e[0] == '0');
   }();
   return on;
 }
+// sched: sched_words_for(num_sel_tiles) words — tile costs, then the unit order lists
 void set_schedule(RenderParams& P, unsigned* sched) {
-  // (the buffer holds 2 x the camera's tiles; a launch uses its first 2 x num_sel_tiles)
-  P.tile_cost = order_enabled() ? sched : nullptr;
-  P.tile_order = order_enabled() ? reinterpret_cast<int*>(sched) + P.num_sel_tiles : nullptr;
+  const int regions = order_regions();
+  P.tile_cost = regions ? sched : nullptr;
+  P.unit_order = regions ? reinterpret_cast<int*>(sched) + P.num_sel_tiles : nullptr;
+  P.order_regions = regions;
+  P.order_probe = probe_enabled() ? 1 : 0;
 }
 
 // True when the culling tree is 4-wide and no slot leads to a binary node (every guarded slot
@@ -602,7 +616,8 @@ void bind_ctx(rt_scene* s, RenderCtx* x, RenderParams& P, const rt_camera& c) {
   P.hits = x->d_hits;
   ensure(x->d_occ, x->occ_words, (size_t)P.occ_words * lanes, "alloc occlusion bits");
   P.occ = x->d_occ;
-  ensure(x->d_sched, x->sched_words, 2 * lanes / (kTile * kTile), "alloc tile schedule");
+  ensure(x->d_sched, x->sched_words, (size_t)sched_words_for(lanes / (kTile * kTile)),
+         "alloc tile schedule");
   set_schedule(P, x->d_sched);
   if (s->needs_recursion) {
     ensure(x->d_frames, x->frames_floats, frame_floats(s->host, P.num_sel_tiles),
@@ -709,7 +724,7 @@ StreamScratch* scratch_for(rt_scene* s, Replica& r, void* stream) {
     hip_check(hipMalloc(&x->hits, most * sizeof(int2_t)), "alloc hit records");
     hip_check(hipMalloc(&x->occ, most * sizeof(unsigned) * occ_words(s->host)),
               "alloc occlusion bits");
-    hip_check(hipMalloc(&x->sched, 2 * (most / (kTile * kTile)) * sizeof(unsigned)),
+    hip_check(hipMalloc(&x->sched, sched_words_for(most / (kTile * kTile)) * sizeof(unsigned)),
               "alloc tile schedule");
   } catch (...) {
     free_scratch(*x);

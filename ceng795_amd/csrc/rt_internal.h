@@ -28,8 +28,7 @@ enum : int {
   kCntPrimNodes = 4, kCntPrimNodeLanes = 5, kCntPrimLeaves = 6, kCntPrimLeafLanes = 7,
   kCntShadNodes = 8, kCntShadNodeLanes = 9, kCntShadLeaves = 10, kCntShadLeafLanes = 11,
   kCntExactBox = 12,
-  // subtree sharing: pieces run by a wave other than the packet's owner
-  kCntShared = 13,
+  kCntUnused13 = 13,
   // RT_DIAG builds: the node visits above that were 4-wide culling nodes (128 B each)
   kCntPrimWide = 14, kCntShadWide = 15
 };
@@ -148,6 +147,10 @@ struct UntileParams {
   int width, row0, row_stride, rows, tiles_x, tiles_total, devices, slot;
 };
 
+// Words of the per-stream schedule buffer for a launch of `tiles` selected tiles: tile costs
+// + the unit order lists (order_layout in rt_kernels.hip stays within this).
+inline unsigned long long sched_words_for(unsigned long long tiles) { return 10 * tiles + 64; }
+
 struct RenderParams {
   const DevNode* nodes;
   const DevPrim* prims;
@@ -189,11 +192,20 @@ struct RenderParams {
   int2_t* hits;   // num_sel_tiles * 64 records {t bits, leaf}: trace_primary -> shadow, shade
   unsigned* occ;  // num_sel_tiles * 64 * occ_words light-occlusion bits: trace_shadow -> shade
   int occ_words;  // ceil(num_lights / 32)
-  // heavy-first shadow dispatch (null: off): trace_primary stores each tile's traversal time
-  // (100 MHz ticks) in tile_cost[sel]; order_kernel sorts the tiles by it, slowest first, into
-  // tile_order, which trace_shadow walks instead of the frame's block order
+  // heavy-first dispatch (null: off).  tile_cost[sel] holds each selected
+  // tile's cost: the probe kernel's estimate before the primary kernel, the primary kernel's
+  // measured time (100 MHz ticks) before the shadow kernel.  order_kernel sorts the traversal
+  // workgroups' units (kTraceWaves packets each) heaviest first within each of order_regions
+  // regions into unit_order[region * order_stride + i] (-1 pads); region r holds the chunks of
+  // order_chunk consecutive units c with c mod order_regions == r, and block b of an ordered
+  // launch takes unit_order[(b mod regions) * stride + b / regions] — with 8 regions, the
+  // blocks the hardware deals to one XCD walk one spatially coherent part of the frame,
+  // heaviest first, so its L2 serves neighbouring packets.  use_order: this launch reads it.
   unsigned* tile_cost;
-  int* tile_order;
+  int* unit_order;
+  int order_regions, order_chunk, order_stride, order_units;
+  int order_probe;  // estimate the primary kernel's tile costs with probe_kernel first
+  int use_order;
   float* frames;  // recursive scenes only: (max_depth+1) * 28 * lanes ray-tree frames, else null
   // kCounterRows rows of kCounterWidth u64 (columns: kCnt*)
   unsigned long long* counters;

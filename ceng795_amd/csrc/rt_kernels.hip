@@ -1284,6 +1284,154 @@ __host__ __device__ __forceinline__ int trace_packets(const RenderParams& P) {
   return ((P.tiles_x + kBlockW - 1) / kBlockW) * ((tiles_y + kBlockH - 1) / kBlockH) * kTraceWaves;
 }
 
+// ------------------------------------------------------------------ dispatch order
+// Traversal kernels are LPT-scheduled: a packet's cost varies ~5x over a C3 frame (rays that
+// graze the height field walk far more nodes), and a kernel's tail is set by the heavy packets
+// that start last.  The hardware dispatcher hands out workgroups in block order as slots free
+// up, so launching the units (one workgroup's kTraceWaves packets) heaviest first is a
+// longest-processing-time schedule.  Orders never change results: every tile is written by
+// exactly one wave.
+//
+// Unit u = the kTraceWaves packets of logical packets u*kTraceWaves .. (a 2x2 tile block in
+// tile_block mode).  Wave w's selected tile, or -1.
+__device__ __forceinline__ int unit_sel(const RenderParams& P, int unit, int w) {
+  const int p = unit * kTraceWaves + w;
+  if (p >= trace_packets(P)) return -1;
+  const int sel = packet_sel(P, p);
+  return sel < P.num_sel_tiles ? sel : -1;
+}
+
+// Selected tile of this wave in a traversal launch: ordered (block b of the grid takes the
+// b / regions-th heaviest unit of region b mod regions), else the XCD-remapped block order.
+__device__ __forceinline__ int dispatch_sel(const RenderParams& Q) {
+  const int w = (int)threadIdx.x >> 6;
+  if (Q.use_order) {
+    const int b = (int)blockIdx.x;
+    const int u = uniform(Q.unit_order[(b % Q.order_regions) * Q.order_stride + b / Q.order_regions]);
+    return u < 0 ? -1 : uniform(unit_sel(Q, u, w));
+  }
+  const int p = packet_index<kTraceWaves>();
+  const int sel = p < trace_packets(Q) ? packet_sel(Q, p) : -1;
+  return sel < Q.num_sel_tiles ? sel : -1;
+}
+
+// Cost estimate of each selected tile before its primary traversal: ONE ray per tile (the
+// pixel nearest the tile's centre) walks the culling tree on its own lane, with its own stack
+// in LDS, counting node visits and leaf tests (8 : 1, roughly their cost in the packet
+// kernels).  Conservative box decisions only (a culling node's !sure_out; a guard's too): it is
+// an estimate, so no exact fallback.  Lanes diverge; a wave runs as long as its longest ray,
+// about 30 dependent 128-B fetches — a few microseconds for the whole frame.
+constexpr int kProbeStack = 48;
+__global__ __launch_bounds__(256) void probe_kernel(RenderParams P, const DevNode* __restrict__ nodes) {
+  __shared__ int stack[kTraceWaves][kProbeStack][64];
+  const int sel = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  const int wv = (int)threadIdx.x >> 6, lane = lane_id();
+  if (sel >= P.num_sel_tiles) return;
+  const int tile = P.tile_begin + sel * P.tile_step;
+  const int px = min((tile % P.tiles_x) * kTile + kTile / 2, P.width - 1);
+  const int lr = min((tile / P.tiles_x) * kTile + kTile / 2, P.rows - 1);
+  const LaneRay r = make_ray(ld3(P.cam_e), primary_dir(P, px, P.row0 + lr * P.row_stride), 0);
+  unsigned cost = 1;
+  float tn, tf;
+  slab_span<true>(P.accel_box, r, tn, tf);
+  int node = decide_cull(tn, tf) ? P.accel_root : -1;
+  int sp = 0;
+  while (node >= 0) {
+    cost += 8;
+    int next = -1;
+    if (node & kWideTag) {
+      const DevNode4& N = *reinterpret_cast<const DevNode4*>(nodes + (node & ~kWideTag));
+      const int fl = N.flags;
+      for (int c = 0; c < 4; c++) {
+        if (!(fl & (kWideValid << c))) continue;
+        const float b[6] = {N.lo[0][c], N.lo[1][c], N.lo[2][c], N.hi[0][c], N.hi[1][c], N.hi[2][c]};
+        slab_span<true>(b, r, tn, tf);
+        if (!decide_cull(tn, tf)) continue;
+        const int ch = N.child[c];
+        if ((fl & (kWideGuard << c)) && ch < 0) {
+          cost += (fl & (kWidePair << c)) ? 2 : 1;
+        } else if (next < 0) {
+          next = ch;
+        } else if (sp < kProbeStack) {
+          stack[wv][sp++][lane] = ch;
+        }
+      }
+    } else {
+      const DevNode& N = nodes[node];
+      for (int c = 0; c < 2; c++) {
+        const float b[6] = {N.lo[0][c], N.lo[1][c], N.lo[2][c], N.hi[0][c], N.hi[1][c], N.hi[2][c]};
+        slab_span<true>(b, r, tn, tf);
+        if (!decide_cull(tn, tf)) continue;
+        const int ch = N.child[c];
+        if (ch < 0) {
+          cost += (N.pad & (c ? kAccelPair1 : kAccelPair0)) ? 2 : 1;
+        } else if (next < 0) {
+          next = ch;
+        } else if (sp < kProbeStack) {
+          stack[wv][sp++][lane] = ch;
+        }
+      }
+    }
+    node = next >= 0 ? next : (sp > 0 ? stack[wv][--sp][lane] : -1);
+  }
+  P.tile_cost[sel] = cost;
+}
+
+// Units of region x: chunks c = x, x + regions, ... of order_chunk consecutive units.
+__device__ __forceinline__ int region_units(const RenderParams& P, int x) {
+  const int full = P.order_units / P.order_chunk, rem = P.order_units % P.order_chunk;
+  int n = x < full ? ((full - 1 - x) / P.order_regions + 1) * P.order_chunk : 0;
+  if (rem && full % P.order_regions == x) n += rem;
+  return n;
+}
+__device__ __forceinline__ int region_unit(const RenderParams& P, int x, int i) {
+  return (x + (i / P.order_chunk) * P.order_regions) * P.order_chunk + i % P.order_chunk;
+}
+
+constexpr int kOrderBuckets = 256;
+__device__ __forceinline__ int cost_bucket(unsigned c) {  // 8 steps per octave
+  c = c ? c : 1u;
+  const int msb = 31 - __builtin_clz(c);
+  const int frac = msb >= 3 ? (int)((c >> (msb - 3)) & 7u) : (int)((c << (3 - msb)) & 7u);
+  return min(kOrderBuckets - 1, msb * 8 + frac);
+}
+
+__device__ __forceinline__ unsigned unit_cost(const RenderParams& P, int u) {
+  unsigned c = 0;
+  for (int w = 0; w < kTraceWaves; w++) {
+    const int sel = unit_sel(P, u, w);
+    if (sel >= 0) c += P.tile_cost[sel];
+  }
+  return c;
+}
+
+// One workgroup per region: a bucket sort of the region's units by cost, heaviest first (order
+// inside a bucket is free), into unit_order[x * stride ..]; -1 pads the list to `stride`.
+__global__ __launch_bounds__(1024) void order_kernel(RenderParams P) {
+  __shared__ int hist[kOrderBuckets];
+  const int tid = (int)threadIdx.x, x = (int)blockIdx.x;
+  const int n = region_units(P, x);
+  int* out = P.unit_order + (size_t)x * P.order_stride;
+  for (int i = tid; i < kOrderBuckets; i += 1024) hist[i] = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += 1024) atomicAdd(&hist[cost_bucket(unit_cost(P, region_unit(P, x, i)))], 1);
+  __syncthreads();
+  if (tid == 0) {  // exclusive offsets, heaviest bucket first
+    int run = 0;
+    for (int b = kOrderBuckets - 1; b >= 0; b--) {
+      const int c = hist[b];
+      hist[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += 1024) {
+    const int u = region_unit(P, x, i);
+    out[atomicAdd(&hist[cost_bucket(unit_cost(P, u))], 1)] = u;
+  }
+  for (int i = n + tid; i < P.order_stride; i += 1024) out[i] = -1;
+}
+
 // RT_TIMELINE (experiment builds only): every traversal wave records its start and end on the
 // 100 MHz clock and its own tile, so tools/timeline.py can draw the occupancy curve of a launch.
 #ifdef RT_TIMELINE
@@ -1319,9 +1467,7 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_PRIMARY_OCCUPANCY void trace_p
   WaveLeafLds& L = leaf_lds[threadIdx.x >> 6];
   TL_BEGIN;
   const RenderParams& Q = fresh_params(P);
-  const int p = packet_index<kTraceWaves>();
-  int sel = p < trace_packets(Q) ? packet_sel(Q, p) : -1;
-  if (sel >= Q.num_sel_tiles) sel = -1;
+  const int sel = dispatch_sel(Q);
   TL_SEL(sel);
   if (sel >= 0) {
     const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
@@ -1343,15 +1489,7 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_TRAVERSAL_OCCUPANCY void trace
   WaveLeafLds& L = leaf_lds[threadIdx.x >> 6];
   TL_BEGIN;
   const RenderParams& Q = fresh_params(P);
-  int sel;
-  if (Q.tile_order) {  // slowest primary tiles first, in plain block order
-    const int p = uniform((int)blockIdx.x * kTraceWaves + ((int)threadIdx.x >> 6));
-    sel = p < Q.num_sel_tiles ? uniform(Q.tile_order[p]) : -1;
-  } else {
-    const int p = packet_index<kTraceWaves>();
-    sel = p < trace_packets(Q) ? packet_sel(Q, p) : -1;
-  }
-  if (sel >= Q.num_sel_tiles) sel = -1;
+  const int sel = dispatch_sel(Q);
   TL_SEL(sel);
   if (sel >= 0) shadow_packet<FAST, DEEP, SPHERES, WO>(Q, nodes, prims, lights, sel, spill, L);
   TL_END(1);
@@ -1377,38 +1515,6 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void shade_kernel(
   const int sel = uniform((int)blockIdx.x * kWavesPerBlock + ((int)threadIdx.x >> 6));
   if (sel >= P.num_sel_tiles) return;
   shade_pixel(P, prims, normals, mats, lights, sel);
-}
-
-// Heavy-first dispatch order for the shadow kernel: the tiles sorted by their primary traversal
-// time, slowest first (a bucket sort on 8 steps per octave; order inside a bucket is free).
-// The slow primary tiles are where the slow shadow tiles are (tools/timeline.py tile maps), and
-// a kernel's tail is set by the slow tiles that start last.  One workgroup.
-constexpr int kOrderBuckets = 256;
-__device__ __forceinline__ int cost_bucket(unsigned c) {
-  c = c ? c : 1u;
-  const int msb = 31 - __builtin_clz(c);
-  const int frac = msb >= 3 ? (int)((c >> (msb - 3)) & 7u) : (int)((c << (3 - msb)) & 7u);
-  return min(kOrderBuckets - 1, msb * 8 + frac);
-}
-
-__global__ __launch_bounds__(1024) void order_kernel(const unsigned* __restrict__ cost,
-                                                     int* __restrict__ order, int n) {
-  __shared__ int hist[kOrderBuckets];
-  const int tid = (int)threadIdx.x;
-  for (int i = tid; i < kOrderBuckets; i += 1024) hist[i] = 0;
-  __syncthreads();
-  for (int i = tid; i < n; i += 1024) atomicAdd(&hist[cost_bucket(cost[i])], 1);
-  __syncthreads();
-  if (tid == 0) {  // exclusive offsets, heaviest bucket first
-    int run = 0;
-    for (int b = kOrderBuckets - 1; b >= 0; b--) {
-      const int c = hist[b];
-      hist[b] = run;
-      run += c;
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < n; i += 1024) order[atomicAdd(&hist[cost_bucket(cost[i])], 1)] = i;
 }
 
 // marks (nullable): 4 events recorded before the primary kernel, after it, after the shadow
@@ -1438,21 +1544,46 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
   T.tile_block = P.tile_begin == 0 && P.tile_step == 1;
   const int tblocks = (trace_packets(T) + kTraceWaves - 1) / kTraceWaves;
   const size_t tlds = DEEP ? sizeof(int) * kDeepWords * kDeepStack * kTraceWaves : 0;
+  // dispatch order: units of one traversal workgroup, `regions` regions of
+  // `chunk`-unit chunks (tile_block: half a row of 2x2 blocks), LPT within each region
+  T.use_order = 0;
+  bool ordered = T.tile_cost != nullptr && T.unit_order != nullptr && T.order_regions > 0;
+  if (ordered) {
+    T.order_units = tblocks;
+    const int nbx = (T.tiles_x + kBlockW - 1) / kBlockW;
+    T.order_chunk = T.tile_block ? max(1, (nbx + 1) / 2) : 64;
+    const int chunks = (T.order_units + T.order_chunk - 1) / T.order_chunk;
+    T.order_stride = ((chunks + T.order_regions - 1) / T.order_regions) * T.order_chunk;
+    ordered = (unsigned long long)T.num_sel_tiles +
+                  (unsigned long long)T.order_regions * T.order_stride <=
+              sched_words_for((unsigned long long)T.num_sel_tiles);
+  }
+  const int oblocks = ordered ? T.order_regions * T.order_stride : tblocks;
+  // probe -> order -> primary: the primary kernel LPT-scheduled by the probe's estimates
+  const bool probe = ordered && FAST && T.accel_root >= 0 && T.root_kind == kRootNode &&
+                     T.order_probe;
   RenderParams S = T;
-  S.tile_cost = nullptr;  // (read by the shadow kernel through tile_order only)
-  const bool ordered = P.num_lights > 0 && T.tile_order != nullptr;
-  if (!ordered) T.tile_cost = S.tile_cost = nullptr, T.tile_order = S.tile_order = nullptr;
   mark(marks, 0, stream);
-  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, WO>), dim3(tblocks),
+  if (probe) {
+    hipLaunchKernelGGL(probe_kernel, dim3((T.num_sel_tiles + 255) / 256), dim3(256), 0, stream,
+                       T, nodes);
+    hipLaunchKernelGGL(order_kernel, dim3(T.order_regions), dim3(1024), 0, stream, T);
+    T.use_order = 1;
+  }
+  if (!ordered) T.tile_cost = nullptr;
+  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, WO>), dim3(T.use_order ? oblocks : tblocks),
                      dim3(kTraceWaves * 64), tlds, stream, T, nodes, prims);
   mark(marks, 1, stream);
-  if (ordered)
-    hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, stream, T.tile_cost, T.tile_order,
-                       T.num_sel_tiles);
-  const int sblocks = ordered ? (T.num_sel_tiles + kTraceWaves - 1) / kTraceWaves : tblocks;
-  if (P.num_lights > 0)
-    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, WO>), dim3(sblocks),
+  S.tile_cost = T.tile_cost;
+  if (P.num_lights > 0) {
+    if (ordered) {  // the shadow kernel LPT-scheduled by the primary kernel's measured times
+      hipLaunchKernelGGL(order_kernel, dim3(S.order_regions), dim3(1024), 0, stream, S);
+      S.use_order = 1;
+    }
+    S.tile_cost = nullptr;  // (the shadow kernel reads the order only)
+    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, WO>), dim3(S.use_order ? oblocks : tblocks),
                        dim3(kTraceWaves * 64), tlds, stream, S, nodes, prims, lights);
+  }
   mark(marks, 2, stream);
   hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
                      prims, normals, mats, lights);
