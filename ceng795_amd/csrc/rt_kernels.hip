@@ -839,9 +839,9 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
   rec.x = q.valid ? leaf : -2;  // -1 miss, -2 outside the image
   rec.y = __float_as_int(t);
   Pw.hits[(size_t)sel * (kTile * kTile) + q.lane] = rec;
+  const unsigned long long nvalid = __builtin_popcountll(ballot(q.valid));  // (all lanes)
+  const unsigned long long nhit = __builtin_popcountll(ballot(q.valid && leaf >= 0));
   if (Pw.counters && q.lane == 0) {  // spread over kCounterSlots rows: no hot address
-    const unsigned long long nvalid = __builtin_popcountll(ballot(q.valid));
-    const unsigned long long nhit = __builtin_popcountll(ballot(q.valid && leaf >= 0));
     unsigned long long* c = counter_row(Pw, sel);
     atomicAdd(&c[kCntPrimary], nvalid);
     atomicAdd(&c[kCntHits], nhit);
