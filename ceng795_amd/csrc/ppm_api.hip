@@ -48,7 +48,7 @@ hipError_t launch_group_update(const PScene&, const PHitPoint*, const int*, cons
                                const int2*, int, const int*, const int*, const float4*,
                                const PDeposit*, const float*, int, float4*, unsigned*,
                                const long long*, float4*, unsigned long long*, hipStream_t);
-hipError_t launch_tile_compact_need(const int2*, int, const int*, const int*, long long, int,
+hipError_t launch_tile_compact_need(const int2*, int, const int*, const int*, long long, int, int,
                                     long long*, hipStream_t);
 hipError_t launch_density(const PHitPoint*, const float4*, const int*, int, double, float*,
                           hipStream_t);
@@ -197,17 +197,52 @@ struct ppm_scene {
   DevBuf<unsigned long long> wide;  // 64-bit scratch scalar (expansion total)
   DevBuf<unsigned long long> stats_keep;  // stats before a batch (restored when it is split)
   DevBuf<float> image;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> upd_events;  // update-kernel launches since the last collection
+  // update-kernel launches since the last collection: event pairs (reused from upd_spare),
+  // completed ones beyond kMaxUpdEvents folded into upd_ms_folded / upd_folded
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> upd_events, upd_spare;
+  double upd_ms_folded = 0;
+  long long upd_folded = 0;
   long long photons = 0;
   size_t slot_bytes = 0;          // ppm_set_batching (0: default_slot_bytes())
   long long max_updates = INT_MAX;  // ppm_set_batching: (group, deposit) pairs per batch
 
-  void drop_update_events() {
-    for (auto& ev : upd_events) (void)hipEventDestroy(ev.first), (void)hipEventDestroy(ev.second);
+  void drop_update_events() {  // (back to the pool)
+    upd_spare.insert(upd_spare.end(), upd_events.begin(), upd_events.end());
     upd_events.clear();
+    upd_ms_folded = 0;
+    upd_folded = 0;
+  }
+  // an event pair for one update launch; the pending list stays bounded while nobody collects
+  std::pair<hipEvent_t, hipEvent_t> update_event_pair() {
+    static constexpr size_t kMaxUpdEvents = 64;
+    if (upd_events.size() >= kMaxUpdEvents) {
+      size_t k = 0;
+      for (; k < upd_events.size(); k++) {
+        float ms = 0;
+        if (hipEventQuery(upd_events[k].second) != hipSuccess ||
+            hipEventElapsedTime(&ms, upd_events[k].first, upd_events[k].second) != hipSuccess)
+          break;
+        upd_ms_folded += ms;
+        upd_folded++;
+        upd_spare.push_back(upd_events[k]);
+      }
+      upd_events.erase(upd_events.begin(), upd_events.begin() + (long)k);
+    }
+    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+    if (!upd_spare.empty()) {
+      ev = upd_spare.back();
+      upd_spare.pop_back();
+    } else {
+      hip_check(hipEventCreate(&ev.first), "event");
+      hip_check(hipEventCreate(&ev.second), "event");
+    }
+    upd_events.push_back(ev);
+    return ev;
   }
   void free_all() {
     drop_update_events();
+    for (auto& ev : upd_spare) (void)hipEventDestroy(ev.first), (void)hipEventDestroy(ev.second);
+    upd_spare.clear();
     for (void* p : owned) (void)hipFree(p);
     owned.clear();
     hp.release(), state.release(), nupd.release(), pix_cnt.release(), pix_off.release();
@@ -245,6 +280,7 @@ bool lpt_order() {
 // on it (the copy is a superset of every window's candidates, in order).
 // CENG795_PPM_COMPACT sets the default (0: off); ppm_set_update_compaction sets it per scene.
 constexpr int kCompactShift = 2;  // scratch per compacted tile: a quarter of its list
+constexpr int kDefaultCompactSeg = 32768;  // deposits per compaction segment
 long long default_compact_min() {
   static const long long v = [] {
     const char* e = std::getenv("CENG795_PPM_COMPACT");
@@ -278,6 +314,7 @@ void create_device(ppm_scene* s, int device) {
   S.max_depth = h.max_depth;
   S.eps = h.eps;
   if (const char* d = std::getenv("CENG795_PPM_DIAG")) S.diag = std::atoi(d);  // experiments
+  S.compact_seg = kDefaultCompactSeg;
   std::memcpy(S.light_pos, h.lights.data(), 12);  // lights[0] (Scene.cpp:97)
   std::memcpy(S.light_intensity, h.lights.data() + 3, 12);
   s->stats.reserve(kStatSlots, "alloc counters");
@@ -559,7 +596,8 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
             s->cneed.reserve(s->n_tiles + 1, "alloc compaction sizes");
             s->cofs.reserve(s->n_tiles + 1, "alloc compaction offsets");
             hip_check(launch_tile_compact_need(tiles, s->n_tiles, s->list_start.p, s->list_end.p,
-                                               cmin, kCompactShift, s->cneed.p, s->stream),
+                                               cmin, kCompactShift, s->S.compact_seg,
+                                               s->cneed.p, s->stream),
                       "compaction sizes");
             bytes = 0;
             hip_check(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, s->cneed.p, s->cofs.p,
@@ -581,10 +619,8 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
               cofs = s->cofs.p;
             }
           }
-          hipEvent_t e0, e1;
-          hip_check(hipEventCreate(&e0), "event");
-          hip_check(hipEventCreate(&e1), "event");
-          s->upd_events.emplace_back(e0, e1);
+          const auto ev = s->update_event_pair();
+          const hipEvent_t e0 = ev.first, e1 = ev.second;
           hip_check(hipEventRecord(e0, s->stream), "event");
           hip_check(launch_group_update(s->S, s->hp.p, s->perm.p, s->gstart.p, tiles,
                                         s->n_tiles, s->list_start.p, s->list_end.p, s->gpos.p,
@@ -677,6 +713,13 @@ int ppm_settings(const ppm_scene* s, int* per_iteration, int* iterations, int* m
 int ppm_set_update_compaction(ppm_scene* s, long long min_list) {
   if (!s || min_list < -1) return set_error(RT_E_INVALID, "ppm_set_update_compaction: bad argument");
   s->compact_min = min_list;
+  return RT_OK;
+}
+
+int ppm_set_update_segment(ppm_scene* s, int seg_len) {
+  if (!s || seg_len < 0 || (seg_len > 0 && seg_len < 64))
+    return set_error(RT_E_INVALID, "ppm_set_update_segment: bad argument (0, or >= 64)");
+  s->S.compact_seg = seg_len ? seg_len : kDefaultCompactSeg;
   return RT_OK;
 }
 
@@ -815,11 +858,11 @@ int ppm_collect_stats(ppm_scene* s, ppm_stats* st) {
     st->hit_points = s->n_hp;
     st->update_deposit_visits = (long long)c[6];
     st->update_candidates = (long long)c[16];
-    st->update_launches = (long long)s->upd_events.size();
-    st->update_compacted_tiles = (long long)c[20];
+    st->update_launches = s->upd_folded + (long long)s->upd_events.size();
+    st->update_compacted_segments = (long long)c[20];
     st->update_compaction_fallbacks = (long long)c[21];
     st->update_compacted_deposits = (long long)c[22];
-    st->update_ms = 0;
+    st->update_ms = s->upd_ms_folded;
     for (auto& ev : s->upd_events) {
       float ms = 0;
       hip_check(hipEventElapsedTime(&ms, ev.first, ev.second), "update time");
@@ -830,7 +873,7 @@ int ppm_collect_stats(ppm_scene* s, ppm_stats* st) {
                                      "longest tile %llu ticks phases(max) stage+filter %llu "
                                      "counts %llu scan %llu scatter %llu color %llu gate %llu max-window-updates %llu "
                                      "unstaged-rr %llu candidates %llu max-tile-candidates %llu max-wave-updates %llu max-tile-windows %llu "
-                                     "compacted-tiles %llu fallbacks %llu compacted-deposits %llu\n",
+                                     "compacted-segments %llu fallbacks %llu compacted-deposits %llu\n",
                                      c[5], c[6], s->n_tiles, s->n_groups, c[7], c[8], c[9],
                                      c[10], c[11], c[12], c[13], c[14], c[15], c[16], c[17], c[18], c[19],
                                      c[20], c[21], c[22]);

@@ -90,6 +90,7 @@ struct PScene {  // device pointers + scalars, passed by value to every kernel
   float eps;
   float light_pos[3], light_intensity[3];
   int diag;  // timing experiments only (CENG795_PPM_DIAG): 1 = skip the update recurrence
+  int compact_seg;  // update pass: deposits per compaction segment (ppm_set_update_segment)
 };
 
 struct PCamera {

@@ -852,23 +852,20 @@ __device__ __forceinline__ float radius_reduction(unsigned n) {
 }
 
 // Tile-list compaction (group_update_kernel phase (0) for long lists): a tile whose group
-// list holds at least `min_len` deposits takes it in segments of kCompactSeg and gets a scratch
-// range of kCompactSeg >> shift records; per segment the kernel copies into it, in photon
+// list holds at least `min_len` deposits takes it in segments of `seg` (S.compact_seg,
+// default 32768) and gets a scratch range of seg >> shift records; per segment the
+// kernel copies into it, in photon
 // order, the deposits within the radius any of its hit points has at the segment start, and
 // streams its windows over that copy (over the segment itself when the copy overflows).
 // need[ntiles] = 0 closes the exclusive scan that turns the sizes into offsets.
-#ifndef PPM_SEG
-#define PPM_SEG 32768
-#endif
 #ifndef PPM_CPER
 #define PPM_CPER 4
 #endif
-constexpr int kCompactSeg = PPM_SEG;
 __global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tiles, int ntiles,
                                                                 const int* list_start,
                                                                 const int* list_end,
                                                                 long long min_len, int shift,
-                                                                long long* need) {
+                                                                int seg, long long* need) {
   const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (t > ntiles) return;
   if (t == ntiles) {
@@ -877,7 +874,7 @@ __global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tile
   }
   const int g = tiles[t].x;
   const long long L = list_end[g] - list_start[g];
-  need[t] = L >= min_len ? ((L < kCompactSeg ? L : (long long)kCompactSeg) >> shift) : 0;
+  need[t] = L >= min_len ? ((L < seg ? L : (long long)seg) >> shift) : 0;
 }
 
 __global__ __launch_bounds__(256) void rr_table_kernel(float* rr, int n) {
@@ -985,11 +982,11 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     tp0 = t1;                                                     \
   }
   if (S.diag == 2 && tid == 0) tp0 = wall_clock64();
-  // A compacted tile takes its list in segments of kCompactSeg; each segment is first copied,
+  // A compacted tile takes its list in segments of S.compact_seg; each segment is first copied,
   // in photon order, down to the deposits within the radius its hit points have at the
   // segment start (its windows' filters could pass no others: the radius only shrinks).
   const bool compact = cofs && cofs[blockIdx.x + 1] > cofs[blockIdx.x];
-  const int seg_len = compact ? kCompactSeg : max(1, list_e - list_s);
+  const int seg_len = compact ? S.compact_seg : max(1, list_e - list_s);
   for (int seg = list_s; seg < list_e; seg += seg_len) {
   const int seg_e = min(seg + seg_len, list_e);
   int ls = seg, le = seg_e;
@@ -1470,10 +1467,10 @@ hipError_t launch_group_update(const PScene& S, const PHitPoint* hps, const int*
   return hipGetLastError();
 }
 hipError_t launch_tile_compact_need(const int2* tiles, int ntiles, const int* list_start,
-                                    const int* list_end, long long min_len, int shift,
+                                    const int* list_end, long long min_len, int shift, int seg,
                                     long long* need, hipStream_t st) {
   hipLaunchKernelGGL(tile_compact_need_kernel, dim3(blocks_for(ntiles + 1)), dim3(kThreads), 0, st,
-                     tiles, ntiles, list_start, list_end, min_len, shift, need);
+                     tiles, ntiles, list_start, list_end, min_len, shift, seg, need);
   return hipGetLastError();
 }
 hipError_t launch_density(const PHitPoint* hps, const float4* state, const int* pix_offsets,

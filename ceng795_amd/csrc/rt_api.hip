@@ -277,8 +277,9 @@ int occ_words(const HostScene& h) { return std::max(1, ((int)h.lights.size() + 3
 constexpr size_t kCounterAlloc = (size_t)kCounterWidth * kCounterRows;
 // Dispatch order of the traversal kernels: CENG795_RT_ORDER=0 off, 1 heavy
 // first over the whole frame, 2 (default) heavy first within each XCD's part of the frame;
-// CENG795_RT_PROBE=0 orders the shadow kernel only (no probe pass before the primary).  The
-// order never changes a result, only which tiles start first.
+// CENG795_RT_PROBE=1 also orders the primary kernel, by a probe pass's estimates (off by
+// default: measured no faster).  The order never changes a result, only which
+// tiles start first.
 int order_regions() {
   static const int r = [] {
     const char* e = std::getenv("CENG795_RT_ORDER");
@@ -291,9 +292,13 @@ int order_regions() {
 bool probe_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("CENG795_RT_PROBE");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
+}
+int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e && *e ? std::atoi(e) : dflt;
 }
 // sched: sched_words_for(num_sel_tiles) words — tile costs, then the unit order lists
 void set_schedule(RenderParams& P, unsigned* sched) {
@@ -302,6 +307,10 @@ void set_schedule(RenderParams& P, unsigned* sched) {
   P.unit_order = regions ? reinterpret_cast<int*>(sched) + P.num_sel_tiles : nullptr;
   P.order_regions = regions;
   P.order_probe = probe_enabled() ? 1 : 0;
+  static const int depth = env_int("CENG795_RT_PROBE_DEPTH", 5);
+  static const int visits = env_int("CENG795_RT_PROBE_VISITS", 48);
+  P.probe_depth = depth;
+  P.probe_visits = visits;
 }
 
 // True when the culling tree is 4-wide and no slot leads to a binary node (every guarded slot

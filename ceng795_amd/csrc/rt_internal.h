@@ -205,6 +205,7 @@ struct RenderParams {
   int* unit_order;
   int order_regions, order_chunk, order_stride, order_units;
   int order_probe;  // estimate the primary kernel's tile costs with probe_kernel first
+  int probe_depth, probe_visits;  // probe_kernel: levels walked, visits per ray
   int use_order;
   float* frames;  // recursive scenes only: (max_depth+1) * 28 * lanes ray-tree frames, else null
   // kCounterRows rows of kCounterWidth u64 (columns: kCnt*)

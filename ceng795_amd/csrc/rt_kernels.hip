@@ -1315,66 +1315,104 @@ __device__ __forceinline__ int dispatch_sel(const RenderParams& Q) {
   return sel < Q.num_sel_tiles ? sel : -1;
 }
 
-// Cost estimate of each selected tile before its primary traversal: ONE ray per tile (the
-// pixel nearest the tile's centre) walks the culling tree on its own lane, with its own stack
-// in LDS, counting node visits and leaf tests (8 : 1, roughly their cost in the packet
-// kernels).  Conservative box decisions only (a culling node's !sure_out; a guard's too): it is
-// an estimate, so no exact fallback.  Lanes diverge; a wave runs as long as its longest ray,
-// about 30 dependent 128-B fetches — a few microseconds for the whole frame.
-constexpr int kProbeStack = 48;
+// Cost estimate of each selected tile before its primary traversal: kProbeRays rays per tile
+// (a 2x2 grid of its pixels), each walking the TOP probe_depth levels of the culling tree on
+// its own lane, with its own stack in LDS, and counting the nodes and leaves it enters there
+// (a node one level deeper counts as entered, not visited); the tile's cost is the sum over
+// its rays.  Rays that graze the geometry — the expensive packets — enter many boxes at every
+// level, so the top levels rank the tiles; and the top levels are the hot part of the tree
+// (L2 hits), which keeps this latency-bound kernel short: a wave runs as long as its longest
+// ray, one round trip per visit (the whole 128-B record in eight 16-B loads issued together).
+// Conservative box decisions only (a culling node's !sure_out; a guard's too): it is an
+// estimate, so no exact fallback.
+constexpr int kProbeStack = 40;
+constexpr int kProbeRays = 4;
+
 __global__ __launch_bounds__(256) void probe_kernel(RenderParams P, const DevNode* __restrict__ nodes) {
   __shared__ int stack[kTraceWaves][kProbeStack][64];
-  const int sel = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  __shared__ unsigned char sdepth[kTraceWaves][kProbeStack][64];
+  const int gid = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  const int sel = gid / kProbeRays, k = gid % kProbeRays;
   const int wv = (int)threadIdx.x >> 6, lane = lane_id();
-  if (sel >= P.num_sel_tiles) return;
-  const int tile = P.tile_begin + sel * P.tile_step;
-  const int px = min((tile % P.tiles_x) * kTile + kTile / 2, P.width - 1);
-  const int lr = min((tile / P.tiles_x) * kTile + kTile / 2, P.rows - 1);
-  const LaneRay r = make_ray(ld3(P.cam_e), primary_dir(P, px, P.row0 + lr * P.row_stride), 0);
-  unsigned cost = 1;
-  float tn, tf;
-  slab_span<true>(P.accel_box, r, tn, tf);
-  int node = decide_cull(tn, tf) ? P.accel_root : -1;
-  int sp = 0;
-  while (node >= 0) {
-    cost += 8;
-    int next = -1;
-    if (node & kWideTag) {
-      const DevNode4& N = *reinterpret_cast<const DevNode4*>(nodes + (node & ~kWideTag));
-      const int fl = N.flags;
-      for (int c = 0; c < 4; c++) {
-        if (!(fl & (kWideValid << c))) continue;
-        const float b[6] = {N.lo[0][c], N.lo[1][c], N.lo[2][c], N.hi[0][c], N.hi[1][c], N.hi[2][c]};
-        slab_span<true>(b, r, tn, tf);
-        if (!decide_cull(tn, tf)) continue;
-        const int ch = N.child[c];
-        if ((fl & (kWideGuard << c)) && ch < 0) {
-          cost += (fl & (kWidePair << c)) ? 2 : 1;
-        } else if (next < 0) {
-          next = ch;
-        } else if (sp < kProbeStack) {
-          stack[wv][sp++][lane] = ch;
+  unsigned cost = 0;
+  if (sel < P.num_sel_tiles) {
+    const int tile = P.tile_begin + sel * P.tile_step;
+    const int px = min((tile % P.tiles_x) * kTile + 2 + 4 * (k & 1), P.width - 1);
+    const int lr = min((tile / P.tiles_x) * kTile + 2 + 4 * (k >> 1), P.rows - 1);
+    const LaneRay r = make_ray(ld3(P.cam_e), primary_dir(P, px, P.row0 + lr * P.row_stride), 0);
+    float tn, tf;
+    slab_span<true>(P.accel_box, r, tn, tf);
+    int node = decide_cull(tn, tf) ? P.accel_root : -1;
+    int depth = 0, sp = 0, visits = 0;
+    cost = 1;
+    while (node >= 0) {
+      cost += 4;
+      if (depth >= P.probe_depth || visits >= P.probe_visits) {  // entered, not visited
+        node = sp > 0 ? stack[wv][--sp][lane] : -1;
+        depth = sp >= 0 && node >= 0 ? sdepth[wv][sp][lane] : 0;
+        continue;
+      }
+      visits++;
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      const v4f* q = reinterpret_cast<const v4f*>(nodes + (node & ~kWideTag));
+      v4f w[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) w[i] = q[i];  // (a binary node reads its neighbour too: unused)
+      int next = -1;
+      if (node & kWideTag) {  // DevNode4: lo[3][4] = w0..2, hi[3][4] = w3..5, child = w6, flags
+        const int fl = __float_as_int(w[7].x);
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          if (!(fl & (kWideValid << c))) continue;
+          const float b[6] = {w[0][c], w[1][c], w[2][c], w[3][c], w[4][c], w[5][c]};
+          slab_span<true>(b, r, tn, tf);
+          if (!decide_cull(tn, tf)) continue;
+          const int ch = __float_as_int(w[6][c]);
+          if ((fl & (kWideGuard << c)) && ch < 0) {
+            cost += (fl & (kWidePair << c)) ? 2 : 1;
+          } else if (next < 0) {
+            next = ch;
+          } else if (sp < kProbeStack) {
+            stack[wv][sp][lane] = ch;
+            sdepth[wv][sp++][lane] = (unsigned char)(depth + 1);
+          }
+        }
+      } else {  // DevNode: lo[3][2], hi[3][2] = w0..2, child[2] = w3.xy, pad = w3.w
+        const float f[12] = {w[0].x, w[0].y, w[0].z, w[0].w, w[1].x, w[1].y,
+                             w[1].z, w[1].w, w[2].x, w[2].y, w[2].z, w[2].w};
+        const int pad = __float_as_int(w[3].w);
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+          const float b[6] = {f[c], f[2 + c], f[4 + c], f[6 + c], f[8 + c], f[10 + c]};
+          slab_span<true>(b, r, tn, tf);
+          if (!decide_cull(tn, tf)) continue;
+          const int ch = __float_as_int(c ? w[3].y : w[3].x);
+          if (ch < 0) {
+            cost += (pad & (c ? kAccelPair1 : kAccelPair0)) ? 2 : 1;
+          } else if (next < 0) {
+            next = ch;
+          } else if (sp < kProbeStack) {
+            stack[wv][sp][lane] = ch;
+            sdepth[wv][sp++][lane] = (unsigned char)(depth + 1);
+          }
         }
       }
-    } else {
-      const DevNode& N = nodes[node];
-      for (int c = 0; c < 2; c++) {
-        const float b[6] = {N.lo[0][c], N.lo[1][c], N.lo[2][c], N.hi[0][c], N.hi[1][c], N.hi[2][c]};
-        slab_span<true>(b, r, tn, tf);
-        if (!decide_cull(tn, tf)) continue;
-        const int ch = N.child[c];
-        if (ch < 0) {
-          cost += (N.pad & (c ? kAccelPair1 : kAccelPair0)) ? 2 : 1;
-        } else if (next < 0) {
-          next = ch;
-        } else if (sp < kProbeStack) {
-          stack[wv][sp++][lane] = ch;
-        }
+      if (next >= 0) {
+        node = next;
+        depth++;
+      } else if (sp > 0) {
+        sp--;
+        node = stack[wv][sp][lane];
+        depth = sdepth[wv][sp][lane];
+      } else {
+        node = -1;
       }
     }
-    node = next >= 0 ? next : (sp > 0 ? stack[wv][--sp][lane] : -1);
   }
-  P.tile_cost[sel] = cost;
+  // a tile's rays are kProbeRays consecutive lanes: sum them
+#pragma unroll
+  for (int o = 1; o < kProbeRays; o <<= 1) cost += (unsigned)__shfl_xor((int)cost, o, 64);
+  if (k == 0 && sel < P.num_sel_tiles) P.tile_cost[sel] = cost;
 }
 
 // Units of region x: chunks c = x, x + regions, ... of order_chunk consecutive units.
@@ -1396,11 +1434,14 @@ __device__ __forceinline__ int cost_bucket(unsigned c) {  // 8 steps per octave
   return min(kOrderBuckets - 1, msb * 8 + frac);
 }
 
+// A unit holds its workgroup slot until its slowest packet ends, so it is ranked by its
+// most expensive tile (ranking by the sum measured 14 % worse in a replay of measured
+// per-tile times).
 __device__ __forceinline__ unsigned unit_cost(const RenderParams& P, int u) {
   unsigned c = 0;
   for (int w = 0; w < kTraceWaves; w++) {
     const int sel = unit_sel(P, u, w);
-    if (sel >= 0) c += P.tile_cost[sel];
+    if (sel >= 0) c = max(c, P.tile_cost[sel]);
   }
   return c;
 }
@@ -1439,8 +1480,10 @@ constexpr int kTimelineWaves = 1 << 18;
 __device__ unsigned long long g_timeline[2][kTimelineWaves][3];
 #define TL_BEGIN                                                   \
   int tl_sel = -1;                                                  \
+  unsigned tl_est = 0;                                              \
   const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime()
 #define TL_SEL(x) tl_sel = (x)
+#define TL_EST(x) tl_est = (x)
 #define TL_END(k)                                                                         \
   do {                                                                                    \
     const unsigned long long tl1 = __builtin_amdgcn_s_memrealtime();                      \
@@ -1448,12 +1491,13 @@ __device__ unsigned long long g_timeline[2][kTimelineWaves][3];
     if (lane_id() == 0 && wid < kTimelineWaves) {                                         \
       g_timeline[k][wid][0] = tl0;                                                        \
       g_timeline[k][wid][1] = tl1;                                                        \
-      g_timeline[k][wid][2] = (unsigned long long)(long long)tl_sel;                       \
+      g_timeline[k][wid][2] = ((unsigned long long)tl_est << 32) | (unsigned)tl_sel;      \
     }                                                                                     \
   } while (0)
 #else
 #define TL_BEGIN
 #define TL_SEL(x)
+#define TL_EST(x)
 #define TL_END(k)
 #endif
 
@@ -1469,6 +1513,7 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_PRIMARY_OCCUPANCY void trace_p
   const RenderParams& Q = fresh_params(P);
   const int sel = dispatch_sel(Q);
   TL_SEL(sel);
+  TL_EST(sel >= 0 && Q.use_order ? Q.tile_cost[sel] : 0u);  // the probe's estimate
   if (sel >= 0) {
     const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
     primary_packet<FAST, DEEP, SPHERES, WO>(Q, nodes, prims, sel, spill, L);
@@ -1565,8 +1610,8 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
   RenderParams S = T;
   mark(marks, 0, stream);
   if (probe) {
-    hipLaunchKernelGGL(probe_kernel, dim3((T.num_sel_tiles + 255) / 256), dim3(256), 0, stream,
-                       T, nodes);
+    hipLaunchKernelGGL(probe_kernel, dim3((T.num_sel_tiles * kProbeRays + 255) / 256), dim3(256),
+                       0, stream, T, nodes);
     hipLaunchKernelGGL(order_kernel, dim3(T.order_regions), dim3(1024), 0, stream, T);
     T.use_order = 1;
   }
@@ -1756,7 +1801,7 @@ unsigned long long read_reset_exact_fallbacks() {
 }
 
 // Copies (and clears) the RT_TIMELINE wave records: out[2][kTimelineWaves][3] start/end
-// ticks of the 100 MHz clock and tile (sel, -1 for none).  Returns the number of values
+// ticks of the 100 MHz clock and (estimated cost << 32 | tile sel, -1 for none).  Returns the number of values
 // written, 0 in other builds.
 long long read_reset_timeline(unsigned long long* out, long long max_values) {
 #ifdef RT_TIMELINE

@@ -25,7 +25,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _VARIANT = os.environ.get("CENG795_PPM_LIB", "")
 LIB_PATH = os.path.join(_HERE, "lib", f"libceng795_ppm_{_VARIANT}.so" if _VARIANT else
                         "libceng795_ppm.so")
-ABI_VERSION = 4  # CENG795_PPM_ABI_VERSION
+ABI_VERSION = 5  # CENG795_PPM_ABI_VERSION
 
 _lib = None
 
@@ -37,7 +37,7 @@ class ppm_stats(C.Structure):
                 ("eye_ms", C.c_double), ("grid_ms", C.c_double), ("photon_ms", C.c_double),
                 ("density_ms", C.c_double), ("update_deposit_visits", C.c_longlong),
                 ("update_candidates", C.c_longlong), ("update_launches", C.c_longlong),
-                ("update_ms", C.c_double), ("update_compacted_tiles", C.c_longlong),
+                ("update_ms", C.c_double), ("update_compacted_segments", C.c_longlong),
                 ("update_compaction_fallbacks", C.c_longlong),
                 ("update_compacted_deposits", C.c_longlong)]
 
@@ -58,6 +58,7 @@ SIGNATURES = {
     "ppm_set_seed": (_I, [_VP, C.c_ulonglong]),
     "ppm_set_batching": (_I, [_VP, C.c_longlong, C.c_longlong]),
     "ppm_set_update_compaction": (_I, [_VP, C.c_longlong]),
+    "ppm_set_update_segment": (_I, [_VP, _I]),
     "ppm_eye_pass": (_I, [_VP, _I]),
     "ppm_build_hash_grid": (_I, [_VP, _I, _I, C.POINTER(C.c_double)]),
     "ppm_num_hit_points": (_I, [_VP]),
@@ -156,6 +157,11 @@ class PhotonScene:
         """Update-pass tile-list compaction threshold (results do not depend on it):
         -1 = default, 0 = off, n = compact tiles whose deposit list holds >= n deposits."""
         check(lib().ppm_set_update_compaction(self._h, int(min_list)))
+
+    def set_update_segment(self, seg_len: int = 0) -> None:
+        """Deposits per compaction segment of the update pass (results do not depend on it):
+        0 = default (32768)."""
+        check(lib().ppm_set_update_segment(self._h, int(seg_len)))
 
     # ------------------------------------------------------------------ reference passes
     def reset_hash_grid(self) -> None:

@@ -26,8 +26,9 @@
 extern "C" {
 #endif
 
-#define CENG795_PPM_ABI_VERSION 4  /* 2: ppm_set_batching; 3: update-pass work in ppm_stats;
-                                     4: tile-list compaction (setter + counters) */
+#define CENG795_PPM_ABI_VERSION 5  /* 2: ppm_set_batching; 3: update-pass work in ppm_stats;
+                                     4: tile-list compaction (setter + counters); 5: compaction
+                                     segment length, counters per segment */
 
 typedef struct ppm_scene ppm_scene;
 
@@ -44,10 +45,10 @@ typedef struct ppm_stats {
    * kernel summed over the photon batches since the last collection */
   long long update_deposit_visits, update_candidates, update_launches;
   double update_ms;
-  /* tiles whose deposit list was compacted before the windows (ppm_set_update_compaction),
-   * tiles whose copy did not fit its scratch range (they ran over the full list), and the
-   * deposits the compacted tiles kept */
-  long long update_compacted_tiles, update_compaction_fallbacks, update_compacted_deposits;
+  /* list segments (of ppm_set_update_segment deposits) that compacted tiles copied before
+   * their windows (ppm_set_update_compaction), segments whose copy did not fit the tile's
+   * scratch range (they ran over the segment itself), and the deposits the copies kept */
+  long long update_compacted_segments, update_compaction_fallbacks, update_compacted_deposits;
 } ppm_stats;
 
 int ppm_abi_version(void);
@@ -77,6 +78,10 @@ int ppm_set_batching(ppm_scene* scene, long long slot_bytes, long long max_updat
  * within the radius its hit points have when the pass starts, then streams that copy.
  * min_list: -1 = the default (65536, or CENG795_PPM_COMPACT), 0 = off. */
 int ppm_set_update_compaction(ppm_scene* scene, long long min_list);
+/* Segment length of that compaction (no effect on results): a compacted tile takes its list
+ * in segments of seg_len deposits, each copied with the radii its hit points have at the
+ * segment's start, into a scratch range of seg_len / 4.  0 = the default (32768). */
+int ppm_set_update_segment(ppm_scene* scene, int seg_len);
 /* reset_hash_grid + eye_trace_lines over all rows: builds the hit points. */
 int ppm_eye_pass(ppm_scene* scene, int camera);
 /* build_hash_grid; info8 (nullable) receives {initial radius, hash scale, grid bbox min xyz,

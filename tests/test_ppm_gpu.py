@@ -122,16 +122,19 @@ def test_batching_arguments_are_checked(ppm, scene_dir):
 
 
 @pytest.mark.parametrize("name", list(scenes.PPM))
-@pytest.mark.parametrize("min_list", [1, 256, 0])
-def test_update_compaction_matches_oracle(ppm, scene_dir, name, min_list):
+@pytest.mark.parametrize("min_list,seg", [(1, 0), (256, 0), (0, 0), (1, 64), (1, 300)])
+def test_update_compaction_matches_oracle(ppm, scene_dir, name, min_list, seg):
     """Tile-list compaction (update-pass phase (0)): tiles whose group list holds >= min_list
-    deposits stream a photon-order copy of the deposits their hit points can reach; tiles
-    whose copy overflows its scratch range (a quarter of the list) fall back to the full list.
-    Either way the bits are the oracle's.  min_list 0 is the uncompacted pass."""
+    deposits stream a photon-order copy of the deposits their hit points can reach, segment by
+    segment (seg deposits each; 64 and 300 split these scenes' lists into many segments, each
+    copied with the radii its hit points have at its start); a copy that overflows its scratch
+    range (a quarter of the segment) falls back to the segment itself.  Either way the bits are
+    the oracle's.  min_list 0 is the uncompacted pass."""
     xml = scenes.write_ppm(name, scene_dir)
     o = OraclePPM(xml)
     with ppm.PhotonScene(xml, seed=4) as g:
         g.set_update_compaction(min_list)
+        g.set_update_segment(seg)
         g.set_batching(256 << 10, 0)  # several batches: later ones start from shrunken radii
         c = g.camera(0)
         g.eye_trace_lines(0)
@@ -146,8 +149,10 @@ def test_update_compaction_matches_oracle(ppm, scene_dir, name, min_list):
         st = g.collect_stats()
         assert st.updates == ost.updates
         if min_list == 0:
-            assert st.update_compacted_tiles == st.update_compaction_fallbacks == 0
+            assert st.update_compacted_segments == st.update_compaction_fallbacks == 0
         if min_list == 1:
-            assert st.update_compacted_tiles > 0, "no tile took the compacted path"
+            assert st.update_compacted_segments > 0, "no tile took the compacted path"
         with pytest.raises(ppm.RTError):
             g.set_update_compaction(-2)
+        with pytest.raises(ppm.RTError):
+            g.set_update_segment(8)

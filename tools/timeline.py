@@ -52,10 +52,19 @@ def main():
         t = tl[k]
         t = t[t[:, 0] > 0]
         m = np.zeros(((cam.height + 7) // 8, tiles_x), np.float32)
-        ok = t[:, 2] >= 0
-        m.flat[t[ok, 2]] = (t[ok, 1] - t[ok, 0]) * 0.01  # us per tile
+        sel = (t[:, 2] & 0xffffffff).astype(np.uint32).astype(np.int32)
+        est = (t[:, 2] >> 32) & 0xffffffff
+        ok = sel >= 0
+        m.flat[sel[ok]] = (t[ok, 1] - t[ok, 0]) * 0.01  # us per tile
         maps[name] = m
         t0 = t[:, 0].min()
+        smap = np.zeros_like(m)
+        smap.flat[sel[ok]] = (t[ok, 0] - t0) * 0.01  # start, us
+        maps[name + "_start"] = smap
+        if est[ok].any():  # the probe's cost estimates (ordered primary launches)
+            emap = np.zeros_like(m)
+            emap.flat[sel[ok]] = est[ok]
+            maps[name + "_estimate"] = emap
         st, en = (t[:, 0] - t0) * 10, (t[:, 1] - t0) * 10  # ns
         span = en.max()
         dur = en - st
