@@ -307,6 +307,11 @@ void set_schedule(RenderParams& P, unsigned* sched) {
   P.unit_order = regions ? reinterpret_cast<int*>(sched) + P.num_sel_tiles : nullptr;
   P.order_regions = regions;
   P.order_probe = probe_enabled() ? 1 : 0;
+  // chunks per region: 1 = each XCD walks one contiguous band of the frame (its L2 then holds
+  // that band's part of the tree: shadow kernel reads 91 vs 130 MB per C3 frame with
+  // interleaved half-row chunks, CENG795_RT_ORDER_CHUNKS=0; profiles/r03/ab_order_chunks.jsonl)
+  static const int chunks = env_int("CENG795_RT_ORDER_CHUNKS", 1);
+  P.order_chunk = chunks;
   static const int depth = env_int("CENG795_RT_PROBE_DEPTH", 5);
   static const int visits = env_int("CENG795_RT_PROBE_VISITS", 48);
   P.probe_depth = depth;

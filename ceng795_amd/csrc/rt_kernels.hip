@@ -502,6 +502,9 @@ __device__ __forceinline__ DevNode4 load_node4(const DevNode* __restrict__ nodes
   return N;
 }
 
+#ifndef RT_MASK_SLOTS  // slot decisions as wave masks (0: as per-lane booleans, for A/B)
+#define RT_MASK_SLOTS 1
+#endif
 // One packet visit of a wide culling node, slot by slot with the binary tree's rules
 // (visit_node): a guarded slot accepts on a decided guard test (else guard_exact), and its
 // leaf or leaf pair goes straight to the leaf queue; an inner slot culls only on a sure
@@ -517,7 +520,9 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
                                            uint64_t& m, uint64_t alive, WaveStack<DEEP>& st,
                                            Diag& dg) {
   const DevNode4 N = load_node4(nodes, node & ~kWideTag);
+#if !RT_MASK_SLOTS
   const bool in = (m >> lane_id()) & 1;
+#endif
   const int fl = N.flags;
   DIAG(dg.nodes++; dg.wide++; dg.node_lanes += __builtin_popcountll(m));
   int nxt = -1;
@@ -529,10 +534,30 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
     const float b[6] = {N.lo[0][c], N.lo[1][c], N.lo[2][c], N.hi[0][c], N.hi[1][c], N.hi[2][c]};
     float tn, tf;
     slab_span<SKIP>(b, r, tn, tf);
-    bool sin, sout;
-    decide_sure(tn, tf, sin, sout);
     const int ch = N.child[c];
     const bool guard = (fl & (kWideGuard << c)) != 0;
+#if RT_MASK_SLOTS
+    // the slot's decisions as wave masks straight from the compares (decide_sure's rules)
+    const float band = __builtin_fmaf(__builtin_fabsf(tn) + __builtin_fabsf(tf), 0x1p-20f, 0x1p-120f);
+    const float d = tn - tf;
+    const uint64_t out_m = ballot((tf < 0.0f) | (d > band));
+    uint64_t hm;
+    if (guard) {
+      const uint64_t in_m = ballot((d < -band) & (tf >= 0.0f));
+      hm = m & in_m;
+      const uint64_t um = m & ~(in_m | out_m);
+      if (um) {
+        const bool ok = ((um >> lane_id()) & 1) && guard_exact(P, ch, r);
+        hm |= ballot(ok);
+        DIAG(if ((um >> lane_id()) & 1) atomicAdd(&g_exact_fallbacks, 1ull));
+      }
+    } else {
+      hm = m & ~out_m;
+    }
+    hm &= alive;
+#else
+    bool sin, sout;
+    decide_sure(tn, tf, sin, sout);
     bool h;
     if (guard) {
       h = in & sin;
@@ -545,6 +570,7 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
       h = in & !sout;
     }
     const uint64_t hm = ballot(h) & alive;
+#endif
     if (!hm) continue;
     if (guard && ch < 0) {  // a leaf, or a leaf pair
       const bool pair = (fl & (kWidePair << c)) != 0;
@@ -1264,7 +1290,10 @@ __device__ __forceinline__ int packet_index() {
 // its scalar cache.  With P.tile_block the workgroup's packets form a kBlockW x kBlockH block
 // of tiles (blocks row-major over the frame) instead of a run along a tile row: neighbouring
 // rays walk the same nodes, and the cache serves them once.
-constexpr int kTraceWaves = 4;
+#ifndef RT_TRACE_WAVES  // (A/B builds: 2 = 1x2-tile workgroups)
+#define RT_TRACE_WAVES 4
+#endif
+constexpr int kTraceWaves = RT_TRACE_WAVES;
 constexpr int kBlockW = 2, kBlockH = kTraceWaves / kBlockW;
 
 // Tile (= sel, tile_step 1) of logical packet p; -1 for a padding packet of an edge block.
@@ -1329,8 +1358,8 @@ constexpr int kProbeStack = 40;
 constexpr int kProbeRays = 4;
 
 __global__ __launch_bounds__(256) void probe_kernel(RenderParams P, const DevNode* __restrict__ nodes) {
-  __shared__ int stack[kTraceWaves][kProbeStack][64];
-  __shared__ unsigned char sdepth[kTraceWaves][kProbeStack][64];
+  __shared__ int stack[4][kProbeStack][64];  // 256 threads
+  __shared__ unsigned char sdepth[4][kProbeStack][64];
   const int gid = (int)blockIdx.x * 256 + (int)threadIdx.x;
   const int sel = gid / kProbeRays, k = gid % kProbeRays;
   const int wv = (int)threadIdx.x >> 6, lane = lane_id();
@@ -1596,7 +1625,10 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
   if (ordered) {
     T.order_units = tblocks;
     const int nbx = (T.tiles_x + kBlockW - 1) / kBlockW;
-    T.order_chunk = T.tile_block ? max(1, (nbx + 1) / 2) : 64;
+    if (T.order_chunk > 0)  // host-set: that many chunks per region
+      T.order_chunk = max(1, (tblocks + T.order_regions * T.order_chunk - 1) / (T.order_regions * T.order_chunk));
+    else
+      T.order_chunk = T.tile_block ? max(1, (nbx + 1) / 2) : 64;
     const int chunks = (T.order_units + T.order_chunk - 1) / T.order_chunk;
     T.order_stride = ((chunks + T.order_regions - 1) / T.order_regions) * T.order_chunk;
     ordered = (unsigned long long)T.num_sel_tiles +
