@@ -84,6 +84,13 @@ __device__ __forceinline__ LaneRay make_ray(V3 o, V3 d, int scene_quot_ok) {
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+// Lane masks of one fp32 compare, straight from the v_cmp (ballot of a combined boolean makes
+// the compiler round-trip it through a VGPR: v_cndmask + v_cmp per mask).  LLVM FCmp
+// predicates; ordered, so NaN gives false as the C++ operators do.
+enum : int { kFcmpOGT = 2, kFcmpOGE = 3, kFcmpOLT = 4 };
+__device__ __forceinline__ uint64_t lanes_gt(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, kFcmpOGT); }
+__device__ __forceinline__ uint64_t lanes_ge(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, kFcmpOGE); }
+__device__ __forceinline__ uint64_t lanes_lt(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, kFcmpOLT); }
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // ------------------------------------------------------------------ slab test
@@ -540,10 +547,10 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
     // the slot's decisions as wave masks straight from the compares (decide_sure's rules)
     const float band = __builtin_fmaf(__builtin_fabsf(tn) + __builtin_fabsf(tf), 0x1p-20f, 0x1p-120f);
     const float d = tn - tf;
-    const uint64_t out_m = ballot((tf < 0.0f) | (d > band));
+    const uint64_t out_m = lanes_lt(tf, 0.0f) | lanes_gt(d, band);
     uint64_t hm;
     if (guard) {
-      const uint64_t in_m = ballot((d < -band) & (tf >= 0.0f));
+      const uint64_t in_m = lanes_lt(d, -band) & lanes_ge(tf, 0.0f);
       hm = m & in_m;
       const uint64_t um = m & ~(in_m | out_m);
       if (um) {
