@@ -262,6 +262,11 @@ struct Scene {
   float hash_scale = 0, r0 = 0;
   unsigned num_hash = 0;
   int eye_cam = -1;  // camera of the last eye pass (sizes density_estimation's image)
+  // analysis log (ppmref_trace_photons_logged, tools/ppm_list_study.py): per deposit x, normal,
+  // photon index; per update (hit point, deposit number)
+  std::vector<float>* log_dep = nullptr;
+  std::vector<long long>* log_upd = nullptr;
+  long long log_photon = 0;
 
   // ---------------------------------------------------------------- intersection
   bool tri_intersect(const Shape& s, const Ray& r, Isect& h, bool culling) const {
@@ -965,6 +970,10 @@ void photon_trace(Scene& sc, Ray ray, V3 flux, ppm_math::Rng& rng, ppmref_stats*
     const Material& m = sc.material_of(h);
     if (m.type == kDiffuse) {
       if (st) st->deposits++;
+      if (sc.log_dep) {
+        const float rec[8] = {x.x, x.y, x.z, normal.x, normal.y, normal.z, (float)sc.log_photon, 0.0f};
+        sc.log_dep->insert(sc.log_dep->end(), rec, rec + 8);
+      }
       if (sc.num_hash) {
         const V3 hh = (x - sc.hp_box.lo) * sc.hash_scale;
         const int ix = std::abs(int(hh.x)), iy = std::abs(int(hh.y)), iz = std::abs(int(hh.z));
@@ -977,6 +986,10 @@ void photon_trace(Scene& sc, Ray ray, V3 flux, ppm_math::Rng& rng, ppmref_stats*
             hp.radius_squared = hp.radius_squared * rr;
             hp.n++;
             if (st) st->updates++;
+            if (sc.log_upd) {
+              sc.log_upd->push_back(id);
+              sc.log_upd->push_back((long long)(sc.log_dep->size() / 8) - 1);
+            }
             V3 color(0.0f);
             const Material& hm = sc.materials[hp.material];
             if (hm.brdf_id == -1) {
@@ -1175,6 +1188,35 @@ int ppmref_trace_photons(ppmref_scene* s, unsigned long long seed, long long fir
     photon_trace(sc, ray, flux, rng, st);
   }
   return 0;
+}
+
+// Analysis only (tools/ppm_list_study.py): ppmref_trace_photons that also logs every deposit
+// (x, normal, photon index: 8 floats) and every update (hit point, deposit number).  Returns the
+// deposit count; *n_upd = the update count; outputs truncated to their capacities.
+long long ppmref_trace_photons_logged(ppmref_scene* s, unsigned long long seed, long long first,
+                                      long long count, float* dep8, long long dep_cap,
+                                      long long* upd2, long long upd_cap, long long* n_upd) {
+  Scene& sc = s->sc;
+  if (sc.lights.empty()) return -1;
+  std::vector<float> dep;
+  std::vector<long long> upd;
+  sc.log_dep = &dep;
+  sc.log_upd = &upd;
+  for (long long p = first; p < first + count; p++) {
+    ppm_math::Rng rng(seed, (unsigned long long)p);
+    Ray ray;
+    V3 flux;
+    generate_photon(sc, rng, ray, flux);
+    sc.log_photon = p;
+    photon_trace(sc, ray, flux, rng, nullptr);
+  }
+  sc.log_dep = nullptr;
+  sc.log_upd = nullptr;
+  const long long nd = (long long)dep.size() / 8, nu = (long long)upd.size() / 2;
+  std::copy(dep.begin(), dep.begin() + 8 * std::min(nd, dep_cap), dep8);
+  std::copy(upd.begin(), upd.begin() + 2 * std::min(nu, upd_cap), upd2);
+  *n_upd = nu;
+  return nd;
 }
 
 int ppmref_density(const ppmref_scene* s, long long total, float* out) {

@@ -55,6 +55,10 @@ int ppmref_hit_state(const ppmref_scene* s, float* out5);
 /* Photons [first, first+count) of the photon sequence (trace_n_photons, Scene.cpp:95-104). */
 int ppmref_trace_photons(ppmref_scene* s, unsigned long long seed, long long first,
                          long long count, ppmref_stats* st);
+/* analysis only (tools/ppm_list_study.py): the same photons, logging deposits and updates */
+long long ppmref_trace_photons_logged(ppmref_scene* s, unsigned long long seed, long long first,
+                                      long long count, float* dep8, long long dep_cap,
+                                      long long* upd2, long long upd_cap, long long* n_upd);
 /* density_estimation (Scene.cpp:363-371) + Pixel::get_color: out w*h*3. */
 int ppmref_density(const ppmref_scene* s, long long total_num_of_photons, float* out_rgb);
 
