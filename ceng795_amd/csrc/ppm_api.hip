@@ -873,10 +873,11 @@ int ppm_collect_stats(ppm_scene* s, ppm_stats* st) {
                                      "longest tile %llu ticks phases(max) stage+filter %llu "
                                      "counts %llu scan %llu scatter %llu color %llu gate %llu max-window-updates %llu "
                                      "unstaged-rr %llu candidates %llu max-tile-candidates %llu max-wave-updates %llu max-tile-windows %llu "
-                                     "compacted-segments %llu fallbacks %llu compacted-deposits %llu\n",
+                                     "compacted-segments %llu fallbacks %llu compacted-deposits %llu "
+                                     "tile-ticks-sum %llu phases(sum) %llu %llu %llu %llu %llu %llu gate0(RK, all) %llu %llu\n",
                                      c[5], c[6], s->n_tiles, s->n_groups, c[7], c[8], c[9],
                                      c[10], c[11], c[12], c[13], c[14], c[15], c[16], c[17], c[18], c[19],
-                                     c[20], c[21], c[22]);
+                                     c[20], c[21], c[22], c[23], c[24], c[25], c[26], c[27], c[28], c[29], c[30], c[31]);
     s->photons = 0;
     return RT_OK;
   });

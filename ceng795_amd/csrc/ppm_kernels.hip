@@ -877,6 +877,197 @@ __global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tile
   need[t] = L >= min_len ? ((L < seg ? L : (long long)seg) >> shift) : 0;
 }
 
+#ifndef PPM_LATE_FETCH  // 1: the next window's records are fetched after its rounds (registers)
+#define PPM_LATE_FETCH 0
+#endif
+#ifndef PPM_PHASE_TIMERS  // 1: per-phase wall-clock timers for CENG795_PPM_DIAG=2 (tools/ppm_diag.sh)
+#define PPM_PHASE_TIMERS 0
+#endif
+#ifndef PPM_WAVE_GATE  // 1: the recurrence of a tile's hit point run by its own wave (gate_round)
+#define PPM_WAVE_GATE 1
+#endif
+
+__device__ __forceinline__ float rr_at(const float* rrtab, int nrr, unsigned n) {
+  return n < (unsigned)nrr ? rrtab[n] : radius_reduction(n);
+}
+
+// The exact recurrence of ONE hit point over its n candidates of a round (Scene.cpp:137-166,
+// photon order), run by the hit point's wave; state (fx, fy, fz, r2, cnt) is wave-uniform.
+// rec[k] = candidate k's record: color * photon_flux, and in w its distance^2 (negated when
+// the deposit's multiplicity exceeds 1, +inf when its normal test failed).
+// With a the number of accepts so far, the radius^2 is R(a) = (((r2 * rr(cnt)) * rr(cnt+1))
+// ... * rr(cnt+a-1)) — the float products the sequential loop makes, in its order — and R only
+// shrinks (rr < 1), so candidate k, tested against R(a_k), is accepted iff a_k <= K_k with
+// K_k = max{a : d2_k <= R(a)} (-1: none).  So:
+//   (R) lane 0 tabulates R(0..n) — one dependent multiply per entry;
+//   (K) every lane binary-searches R for its candidates' K_k (lane l holds k = l + 64u);
+//   (A) the acceptance sequence a_{k+1} = a_k + [a_k <= K_k] in RUNS: from k with a accepts,
+//       candidates keep being accepted up to the first j with K_j - j < a - k (one ballot per
+//       64 candidates finds it), then rejected up to the first j with K_j >= a; a round costs
+//       one search per run, not one dependent step per candidate;
+//   (C) the accepted records are compacted in order into acc[] (ranks by popcount / mbcnt);
+//   (B) flux = (flux + c) * rr(cnt + i) over the i-th accepted record: lanes 0, 1, 2 each run
+//       one colour component's chain (two dependent operations per accept).
+// Bit-identical to the one-candidate-at-a-time loop, which remains for rounds holding a
+// deposit of multiplicity > 1 (lane 0, rr from the table).  rrb[i] = rr(cnt + i), i < n.
+[[maybe_unused]] constexpr int kGateK = 6;    // candidates per lane (n <= 64 * kGateK)
+[[maybe_unused]] constexpr int kGatePad = 8;  // rr cache / R rows: slack for read-ahead
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// lanes [lo, hi) of a 64-lane chunk as a mask (0 <= lo <= hi <= 64)
+__device__ __forceinline__ uint64_t lane_range(int lo, int hi) {
+  const uint64_t upto_hi = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+  const uint64_t below_lo = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
+  return upto_hi & ~below_lo;
+}
+__device__ void gate_round(float4* __restrict__ rec, float4* __restrict__ acc, int n, bool multi,
+                           const unsigned* __restrict__ ck, const float* __restrict__ rrtab,
+                           int nrr, const float* __restrict__ rrb, float* __restrict__ R,
+                           float& fx, float& fy, float& fz, float& r2, unsigned& cnt,
+                           unsigned long long* tick) {
+  const int lane = (int)__lane_id();
+  if (n <= 0) return;
+  const unsigned long long t0 = tick ? wall_clock64() : 0;
+  if (multi) {  // exact serial loop (multiplicity: retested while inside)
+    if (lane == 0) {
+      for (int k = 0; k < n; k++) {
+        const float4 c = rec[k];
+        const float d2 = __builtin_fabsf(c.w);
+        const unsigned reps = (__float_as_uint(c.w) >> 31) ? (ck[k] & kRepMask) : 1u;
+        for (unsigned i = 0; i < reps && d2 <= r2; i++) {
+          const float rr = rr_at(rrtab, nrr, cnt);
+          cnt++;
+          fx = (fx + c.x) * rr;
+          fy = (fy + c.y) * rr;
+          fz = (fz + c.z) * rr;
+          r2 = r2 * rr;
+        }
+      }
+    }
+    fx = __shfl(fx, 0, 64), fy = __shfl(fy, 0, 64), fz = __shfl(fz, 0, 64);
+    r2 = __shfl(r2, 0, 64);
+    cnt = (unsigned)__shfl((int)cnt, 0, 64);
+    return;
+  }
+  if (lane == 0) {  // (R): the next 4 factors are read before this block's entries are stored
+    float r = r2;
+    R[0] = r;
+    float q0 = rrb[0], q1 = rrb[1], q2 = rrb[2], q3 = rrb[3];
+    for (int i = 0; i < n; i += 4) {
+      const float p0 = rrb[i + 4], p1 = rrb[i + 5], p2 = rrb[i + 6], p3 = rrb[i + 7];
+      r = r * q0;
+      R[i + 1] = r;
+      r = r * q1;
+      R[i + 2] = r;
+      r = r * q2;
+      R[i + 3] = r;
+      r = r * q3;
+      R[i + 4] = r;
+      q0 = p0, q1 = p1, q2 = p2, q3 = p3;
+    }
+  }
+  wave_sync_lds();
+  // (K): #{a : d2 <= R(a)} - 1 (R non-increasing), a lane's candidates searched together
+  int K[kGateK];
+  {
+    int steps = 0;  // ceil(log2(n + 1)): the branch-free search's trip count (uniform)
+    while ((1 << steps) < n + 1) steps++;
+    float d2[kGateK];
+    int len = n + 1;
+#pragma unroll
+    for (int u = 0; u < kGateK; u++) {
+      const int k = lane + 64 * u;
+      d2[u] = k < n ? rec[k].w : kInf;
+      K[u] = 0;
+    }
+    for (int t = 0; t < steps; t++) {
+      const int half = len >> 1;
+#pragma unroll
+      for (int u = 0; u < kGateK; u++) K[u] = d2[u] <= R[K[u] + half] ? K[u] + half : K[u];
+      len -= half;
+    }
+#pragma unroll
+    for (int u = 0; u < kGateK; u++) K[u] = K[u] + (d2[u] <= R[K[u]] ? 1 : 0) - 1;
+  }
+  // (A): runs of accepts and of rejects
+  uint64_t accm[kGateK];
+#pragma unroll
+  for (int u = 0; u < kGateK; u++) accm[u] = 0;
+  int k = 0, a = 0;
+  while (k < n) {
+    int j = n;  // first j >= k with K_j - j < a - k
+    {
+      bool found = false;
+#pragma unroll
+      for (int u = 0; u < kGateK; u++) {
+        if (found || 64 * u + 64 <= k || 64 * u >= n) continue;
+        const int kk = 64 * u + lane;
+        const uint64_t m = __ballot(kk >= k && kk < n && K[u] - kk < a - k);
+        if (m) {
+          j = 64 * u + (int)__builtin_ctzll(m);
+          found = true;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kGateK; u++) {  // candidates [k, j) are accepted
+      const int lo = max(k, 64 * u) - 64 * u, hi = min(j, 64 * u + 64) - 64 * u;
+      if (lo < hi) accm[u] |= lane_range(lo, hi);
+    }
+    a += j - k;
+    k = j;
+    if (k >= n) break;
+    j = n;  // rejected from k up to the first j with K_j >= a
+    {
+      bool found = false;
+#pragma unroll
+      for (int u = 0; u < kGateK; u++) {
+        if (found || 64 * u + 64 <= k || 64 * u >= n) continue;
+        const int kk = 64 * u + lane;
+        const uint64_t m = __ballot(kk >= k && kk < n && K[u] >= a);
+        if (m) {
+          j = 64 * u + (int)__builtin_ctzll(m);
+          found = true;
+        }
+      }
+    }
+    k = j;
+  }
+  // (C): the accepted records in order
+  {
+    int base = 0;
+#pragma unroll
+    for (int u = 0; u < kGateK; u++) {
+      const uint64_t m = accm[u];
+      if ((m >> lane) & 1ull) {
+        const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        acc[base + below] = rec[64 * u + lane];
+      }
+      base += __builtin_popcountll(m);
+    }
+  }
+  wave_sync_lds();
+  if (tick) tick[0] += wall_clock64() - t0;  // diag: (R) .. (C)
+  // (B): lane c < 3 runs colour component c's chain
+  if (lane < 3) {
+    float f = lane == 0 ? fx : (lane == 1 ? fy : fz);
+    const float* cf = reinterpret_cast<const float*>(acc) + lane;
+#pragma unroll 8
+    for (int i = 0; i < a; i++) f = (f + cf[4 * i]) * rrb[i];
+    if (lane == 0) fx = f;
+    if (lane == 1) fy = f;
+    if (lane == 2) fz = f;
+  }
+  fx = __shfl(fx, 0, 64), fy = __shfl(fy, 1, 64), fz = __shfl(fz, 2, 64);
+  r2 = R[a];
+  cnt += (unsigned)a;
+  if (tick) tick[1] += wall_clock64() - t0;
+}
+
 __global__ __launch_bounds__(256) void rr_table_kernel(float* rr, int n) {
   const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (i < n) rr[i] = radius_reduction((unsigned)i);
@@ -934,14 +1125,25 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   __shared__ int s_wc[kTileHP * kWords + 1];
   __shared__ int s_wtot[kUpdThreads / 64];
   __shared__ unsigned s_ck[kTileHP * kWinMax];  // photon-order index << kRepBits | multiplicity
-  __shared__ float s_cd2[kTileHP * kWinMax];
   // color * photon_flux, and in w the candidate's distance^2 for the gate: negated when its
   // multiplicity exceeds 1 (sign bit: the gate's scalar path), +inf when its normal fails
-  __shared__ float4 s_ccf[kChunk];
+  __shared__ float4 s_ccf[kChunk + 4];  // (+4: gate_round reads two records ahead)
   constexpr int kRRStage = PPM_RR_STAGE;  // rr(n) staged per hit point per window (more: computed inline)
+#if PPM_WAVE_GATE
+  constexpr int kRRCache = 2 * kPerHp;
+  static_assert(kPerHp <= 64 * kGateK, "gate_round: candidates per lane");
+  __shared__ float s_grr[kTileHP][kRRCache + kGatePad];  // gate_round: rr(grrb + i), i < kRRCache
+  __shared__ float s_gR[kTileHP][kPerHp + 1 + kGatePad];  // gate_round: R(a)
+  __shared__ int s_gmulti[kTileHP];  // a candidate of this round has multiplicity > 1
+  __shared__ float4 s_gacc[kTileHP][kPerHp + 4];  // gate_round: the accepted records
+  __shared__ __attribute__((aligned(16))) float s_rr[1][4];
+#else
   __shared__ __attribute__((aligned(16))) float s_rr[kTileHP][kRRStage];
+#endif
   const int tid = (int)threadIdx.x, lane = tid & 63;
+#if PPM_PHASE_TIMERS
   const unsigned long long t_start = S.diag == 2 ? wall_clock64() : 0;
+#endif
   const int2 tile = tiles[blockIdx.x];
   const int g = tile.x, first = tile.y;
   const int nh = min(kTileHP, gstart[g + 1] - first);
@@ -968,12 +1170,33 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   const int list_s = list_start[g], list_e = list_end[g];
   unsigned long long visits = 0, windows = 0;  // 16-B records the filters read; windows run
   __syncthreads();
-  V tp[kTileHP], tn[kTileHP];
+#if PPM_WAVE_GATE
+  // wave j runs hit point j's recurrence (wave_gate) and keeps its state for the whole tile
+  const int gw = tid >> 6;
+  float gfx = 0.0f, gfy = 0.0f, gfz = 0.0f, gr2 = 0.0f;
+  unsigned gcnt = 0;
+  if (gw < nh) {
+    const int hg = perm[first + gw];
+    const float4 st = state[hg];
+    gfx = st.x, gfy = st.y, gfz = st.z, gr2 = st.w;
+    gcnt = s_cnt[gw];
+    if (lane == 0) s_gmulti[gw] = 0;
+  }
+  unsigned grrb = gcnt;  // the wave's rr cache holds rr(grrb + i), i < kRRCache
+#if PPM_PHASE_TIMERS
+  unsigned long long gtick[2] = {0, 0};  // diag: wave 0's gate_round ticks, (R)..(C) and total
+#endif
+  if (gw < nh) {
+    for (int i = lane; i < kRRCache; i += 64) s_grr[gw][i] = rr_at(rrtab, nrr, grrb + (unsigned)i);
+  }
+  const unsigned cnt0 = cnt;  // this thread's hit point's count at the start (tid < nh)
+#endif
+  V tp[kTileHP];
 #pragma unroll
   for (int j = 0; j < kTileHP; j++) {
     tp[j] = mk(s_hp[j][0], s_hp[j][1], s_hp[j][2]);
-    tn[j] = mk(s_hp[j][3], s_hp[j][4], s_hp[j][5]);
   }
+#if PPM_PHASE_TIMERS
   unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tp0 = 0;
 #define PPM_PHASE(i)                                              \
   if (S.diag == 2 && tid == 0) {                                  \
@@ -982,6 +1205,9 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     tp0 = t1;                                                     \
   }
   if (S.diag == 2 && tid == 0) tp0 = wall_clock64();
+#else
+#define PPM_PHASE(i)
+#endif
   // A compacted tile takes its list in segments of S.compact_seg; each segment is first copied,
   // in photon order, down to the deposits within the radius its hit points have at the
   // segment start (its windows' filters could pass no others: the radius only shrinks).
@@ -1083,7 +1309,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     const int total = min(kWinMax, le - base);
     const int nwords = (total + 31) >> 5;
     // stage rr(n) for the updates this window can make
-    for (int e = tid; e < nh * kRRStage; e += kUpdThreads) {
+    for (int e = tid; !PPM_WAVE_GATE && e < nh * kRRStage; e += kUpdThreads) {
       const int j = e / kRRStage, t = e % kRRStage;
       const unsigned n = s_cnt[j] + (unsigned)t;
       s_rr[j][t] = n < (unsigned)nrr ? rrtab[n] : radius_reduction(n);
@@ -1114,7 +1340,9 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         }
       }
     }
+#if !PPM_LATE_FETCH
     fetch(base + kWinMax);  // next window in flight
+#endif
     __syncthreads();
     PPM_PHASE(0)
     // (2) candidates per hit point, in photon order: exclusive scan of the per-word counts,
@@ -1146,17 +1374,20 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         const int w = k >> 5;
         const int idx = s_wc[j * nwords + w] + __builtin_popcount(s_mask[j][w] & ((1u << (k & 31)) - 1u));
         s_ck[idx] = rp[q];
-        s_cd2[idx] = d2r[q][j];
       }
     }
     __syncthreads();
     PPM_PHASE(3)
     const int ncand = s_wc[nh * nwords];
     cands += (unsigned)ncand;
+#if !PPM_WAVE_GATE
     const int my_beg = h >= 0 ? s_wc[tid * nwords] : 0;
     const int my_end = h >= 0 ? (tid + 1 < nh ? s_wc[(tid + 1) * nwords] : ncand) : 0;
+#endif
     const unsigned cnt_w = cnt;  // count at the window start: rr(n) is staged from there
+#if !PPM_WAVE_GATE
     unsigned rbase = cnt_w;      // the gate lane's staged rr(n) start (restaged in the gate)
+#endif
     // Rounds of up to kPerHp candidates of EVERY hit point, so that the gate lanes run side by
     // side however the window's candidates are spread over the tile's hit points.
     int most = 0;
@@ -1169,12 +1400,11 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         const int e = s_wc[j * nwords] + c0 + (x - j * kPerHp);
         if (e >= (j + 1 < nh ? s_wc[(j + 1) * nwords] : ncand)) continue;
         const PDeposit d = dense[s_ck[e] >> kRepBits];
-        const V hn = tn[j], w_i = ld(d.w_i), pf = ld(d.flux);
+        const V hn = mk(s_hp[j][3], s_hp[j][4], s_hp[j][5]), w_i = ld(d.w_i), pf = ld(d.flux);
         const PMaterial& m = S.materials[s_mat[j]];
         V color = mk(0.0f, 0.0f, 0.0f);
         // Scene.cpp:136: a deposit whose normal fails the test never updates the hit point
         const bool normal_ok = dot(hn, ld(d.normal)) > 1e-3f;
-        if (!normal_ok) s_cd2[e] = kInf;
         if (normal_ok && m.brdf_id == -1) {
           const float cos_i = dot(hn, w_i);
           if (!(cos_i > 1.0f || cos_i <= 0.0f)) {
@@ -1185,7 +1415,14 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
           }
         }
         const V cf = color * pf;
-        const float d2c = !normal_ok ? kInf : ((s_ck[e] & kRepMask) > 1u ? -s_cd2[e] : s_cd2[e]);
+        // distance^2 as the filter computed it (same operands, same arithmetic)
+        const V dv = mk(s_hp[j][0], s_hp[j][1], s_hp[j][2]) - ld(d.x);
+        const float d2 = dot(dv, dv);
+        const bool multi = normal_ok && (s_ck[e] & kRepMask) > 1u;
+        const float d2c = !normal_ok ? kInf : (multi ? -d2 : d2);
+#if PPM_WAVE_GATE
+        if (multi) s_gmulti[j] = 1;
+#endif
         s_ccf[x] = make_float4(cf.x, cf.y, cf.z, d2c);
       }
       __syncthreads();
@@ -1201,6 +1438,31 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
       // batch (it changes nothing; the ones after it are redone with the right rr).  A batch
       // holding a multiplicity > 1, or reaching past the staged rr(n), takes the scalar path
       // for its first candidate.
+#if PPM_WAVE_GATE
+      if (gw < nh && S.diag != 1) {
+        const int gb = s_wc[gw * nwords];
+        const int ge = gw + 1 < nh ? s_wc[(gw + 1) * nwords] : ncand;
+        const int n = min(ge, gb + c0 + kPerHp) - (gb + c0);
+        __builtin_amdgcn_s_setprio(3);
+        if (gcnt + (unsigned)n > grrb + (unsigned)kRRCache) {  // slide the rr cache to cnt
+          grrb = gcnt;
+          for (int i = lane; i < kRRCache; i += 64) s_grr[gw][i] = rr_at(rrtab, nrr, grrb + (unsigned)i);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        const bool multi = s_gmulti[gw] != 0;
+        gate_round(s_ccf + gw * kPerHp, s_gacc[gw], n, multi, s_ck + gb + c0, rrtab, nrr,
+                   s_grr[gw] + (gcnt - grrb), s_gR[gw], gfx, gfy, gfz, gr2, gcnt,
+#if PPM_PHASE_TIMERS
+                   S.diag == 2 && gw == 0 ? gtick : nullptr);
+#else
+                   nullptr);
+#endif
+        __builtin_amdgcn_s_setprio(0);
+        if (lane == 0) s_r2[gw] = gr2, s_cnt[gw] = gcnt, s_gmulti[gw] = 0;
+      }
+#else
 #if PPM_PRIO
       if (tid < 64) __builtin_amdgcn_s_setprio(3);  // the gate wave is the tile's critical path
 #endif
@@ -1278,10 +1540,11 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
 #if PPM_PRIO
       if (tid < 64) __builtin_amdgcn_s_setprio(0);
 #endif
+#endif  // PPM_WAVE_GATE
       __syncthreads();
       PPM_PHASE(5)
     }
-    if (h >= 0) {
+    if (h >= 0 && !PPM_WAVE_GATE) {
       if (S.diag == 2) {  // experiment counters: most updates in one window, unstaged rr(n)
         const unsigned t_rr = cnt - cnt_w;  // updates made by this hit point in this window
         d_max = max(d_max, (unsigned long long)t_rr);
@@ -1290,11 +1553,22 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
       applied += cnt - s_cnt[tid];
       s_r2[tid] = r2, s_cnt[tid] = cnt;
     }
+#if PPM_LATE_FETCH
+    fetch(base + kWinMax);  // next window in flight (issued here: nothing is live across the rounds)
+#endif
     __syncthreads();
     PPM_PHASE(5)
   }
   }  // segments
-  if (h >= 0) {
+#if PPM_WAVE_GATE
+  if (gw < nh && lane == 0) {
+    state[perm[first + gw]] = make_float4(gfx, gfy, gfz, gr2);
+    nupd[perm[first + gw]] = gcnt;
+  }
+  __syncthreads();
+  if (h >= 0) applied = s_cnt[tid] - cnt0;
+#endif
+  if (h >= 0 && !PPM_WAVE_GATE) {
     state[h] = make_float4(flux.x, flux.y, flux.z, r2);
     nupd[h] = cnt;
     if (stats && S.diag == 2) {
@@ -1310,8 +1584,17 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   }
   if (stats && S.diag == 2 && tid == 0) {  // experiment counters: windows, longest tile
     atomicAdd(&stats[5], windows);
-    atomicMax(&stats[7], wall_clock64() - t_start);  // longest tile, in wall-clock ticks
+#if PPM_PHASE_TIMERS
+    const unsigned long long dur = wall_clock64() - t_start;
+    atomicMax(&stats[7], dur);  // longest tile, in wall-clock ticks
+    atomicAdd(&stats[23], dur);  // sum over tiles, and of each phase (23..29)
+#if PPM_WAVE_GATE
+    atomicAdd(&stats[30], gtick[0]);  // hit point 0's gate_round: (R)+(K), all phases
+    atomicAdd(&stats[31], gtick[1]);
+#endif
+    for (int i = 0; i < 6; i++) atomicAdd(&stats[24 + i], ph[i]);
     for (int i = 0; i < 6; i++) atomicMax(&stats[8 + i], ph[i]);
+#endif
     atomicMax(&stats[17], cands);  // most candidates in one tile
     atomicMax(&stats[19], windows);
   }
