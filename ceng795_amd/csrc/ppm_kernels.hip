@@ -877,6 +877,12 @@ __global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tile
   need[t] = L >= min_len ? ((L < seg ? L : (long long)seg) >> shift) : 0;
 }
 
+#ifndef PPM_GATE_RUNS  // gate_round (A1): candidates per accept/reject run pair below which (A2) takes over
+#define PPM_GATE_RUNS 32
+#endif
+#ifndef PPM_GATE_PRIO  // wave priority of the gate waves while they run gate_round
+#define PPM_GATE_PRIO 3
+#endif
 #ifndef PPM_LATE_FETCH  // 1: the next window's records are fetched after its rounds (registers)
 #define PPM_LATE_FETCH 0
 #endif
@@ -912,6 +918,7 @@ __device__ __forceinline__ float rr_at(const float* rrtab, int nrr, unsigned n) 
 // deposit of multiplicity > 1 (lane 0, rr from the table).  rrb[i] = rr(cnt + i), i < n.
 [[maybe_unused]] constexpr int kGateK = 6;    // candidates per lane (n <= 64 * kGateK)
 [[maybe_unused]] constexpr int kGatePad = 8;  // rr cache / R rows: slack for read-ahead
+[[maybe_unused]] constexpr int kGateMinRun = PPM_GATE_RUNS;  // (A1) while runs average this
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -992,12 +999,14 @@ __device__ void gate_round(float4* __restrict__ rec, float4* __restrict__ acc, i
 #pragma unroll
     for (int u = 0; u < kGateK; u++) K[u] = K[u] + (d2[u] <= R[K[u]] ? 1 : 0) - 1;
   }
-  // (A): runs of accepts and of rejects
   uint64_t accm[kGateK];
 #pragma unroll
   for (int u = 0; u < kGateK; u++) accm[u] = 0;
-  int k = 0, a = 0;
-  while (k < n) {
+  int a = 0, k = 0;
+  // (A1): runs of accepts and of rejects, while they average kGateMinRun candidates or more
+  // (high acceptance: the hot hit points); a round whose runs turn out short falls through to
+  // (A2) from where it stands
+  for (int runs = 0; k < n && (runs < 2 || k >= kGateMinRun * runs); runs++) {
     int j = n;  // first j >= k with K_j - j < a - k
     {
       bool found = false;
@@ -1035,6 +1044,20 @@ __device__ void gate_round(float4* __restrict__ rec, float4* __restrict__ acc, i
       }
     }
     k = j;
+  }
+  // (A2): the rest one candidate at a time on the scalar unit (K_k by readlane)
+#pragma unroll
+  for (int u = 0; u < kGateK; u++) {
+    if (64 * u + 64 <= k || 64 * u >= n) continue;
+    const int cu = min(64, n - 64 * u);
+    uint64_t m = accm[u];
+    for (int l = max(k - 64 * u, 0); l < cu; l++) {
+      const int Kk = __builtin_amdgcn_readlane(K[u], l);
+      const int acc = a <= Kk ? 1 : 0;
+      m |= (uint64_t)acc << l;
+      a += acc;
+    }
+    accm[u] = m;
   }
   // (C): the accepted records in order
   {
@@ -1443,7 +1466,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         const int gb = s_wc[gw * nwords];
         const int ge = gw + 1 < nh ? s_wc[(gw + 1) * nwords] : ncand;
         const int n = min(ge, gb + c0 + kPerHp) - (gb + c0);
-        __builtin_amdgcn_s_setprio(3);
+        __builtin_amdgcn_s_setprio(PPM_GATE_PRIO);
         if (gcnt + (unsigned)n > grrb + (unsigned)kRRCache) {  // slide the rr cache to cnt
           grrb = gcnt;
           for (int i = lane; i < kRRCache; i += 64) s_grr[gw][i] = rr_at(rrtab, nrr, grrb + (unsigned)i);

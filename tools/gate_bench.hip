@@ -2,7 +2,7 @@
 // ceng795_amd/csrc/ppm_kernels.hip) on synthetic rounds, one wave per workgroup.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-slp-vectorize \
 //         -I ceng795_amd/csrc tools/gate_bench.hip -o build/gate_bench
-//   build/gate_bench [n=341] [blocks=1] [reps=200]
+//   build/gate_bench [n=341] [blocks=1] [reps=200] [dmax=0.9]
 // Prints core-clock cycles per candidate of (R)+(K) and of the whole round (diag ticks are
 // 100 MHz; clock64 here is the shader clock).  Development tool; not part of the product.
 #include "ppm_kernels.hip"
@@ -15,7 +15,7 @@ namespace ppm {
 namespace {
 constexpr int kGateKMaxBench = 64 * kGateK;
 __global__ __launch_bounds__(64) void gate_bench_kernel(int n, int reps, const float* rr_table,
-                                                         int nrr, float* out,
+                                                         int nrr, float dmax, float* out,
                                                          unsigned long long* ticks) {
   __shared__ float4 rec[kGateKMaxBench + 4];
   __shared__ float4 acc[kGateKMaxBench + 4];
@@ -28,7 +28,7 @@ __global__ __launch_bounds__(64) void gate_bench_kernel(int n, int reps, const f
   unsigned s = 12345u + 77u * blockIdx.x;
   for (int k = lane; k < n; k += 64) {
     s = s * 1664525u + 1013904223u + (unsigned)k * 2654435761u;
-    d2s[k] = (float)(s >> 8) * (1.0f / 16777216.0f) * 0.9f;
+    d2s[k] = (float)(s >> 8) * (1.0f / 16777216.0f) * dmax;
   }
   __syncthreads();
   float fx = 0, fy = 0, fz = 0, r2 = 1.0f;
@@ -60,6 +60,7 @@ int main(int argc, char** argv) {
   const int n = argc > 1 ? std::atoi(argv[1]) : 341;
   const int blocks = argc > 2 ? std::atoi(argv[2]) : 1;
   const int reps = argc > 3 ? std::atoi(argv[3]) : 200;
+  const float dmax = argc > 4 ? (float)std::atof(argv[4]) : 0.9f;  // d2 ~ U(0, dmax): 1.8 ~ half accepted
   if (n > ppm::kGateKMaxBench) return 2;
   const int nrr = 1 << 16;
   std::vector<float> rr(nrr);
@@ -73,13 +74,13 @@ int main(int argc, char** argv) {
   hipMalloc(&d_out, blocks * 4);
   hipMalloc(&d_t, blocks * 24);
   hipMemcpy(d_rr, rr.data(), nrr * 4, hipMemcpyHostToDevice);
-  hipLaunchKernelGGL(ppm::gate_bench_kernel, dim3(blocks), dim3(64), 0, 0, n, 2, d_rr, nrr, d_out, d_t);
+  hipLaunchKernelGGL(ppm::gate_bench_kernel, dim3(blocks), dim3(64), 0, 0, n, 2, d_rr, nrr, dmax, d_out, d_t);
   hipDeviceSynchronize();
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   hipEventRecord(e0);
-  hipLaunchKernelGGL(ppm::gate_bench_kernel, dim3(blocks), dim3(64), 0, 0, n, reps, d_rr, nrr, d_out, d_t);
+  hipLaunchKernelGGL(ppm::gate_bench_kernel, dim3(blocks), dim3(64), 0, 0, n, reps, d_rr, nrr, dmax, d_out, d_t);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms = 0;
@@ -87,9 +88,9 @@ int main(int argc, char** argv) {
   std::vector<unsigned long long> t(3 * blocks);
   hipMemcpy(t.data(), d_t, blocks * 24, hipMemcpyDeviceToHost);
   const double per = (double)reps * n;
-  std::printf("{\"n\": %d, \"blocks\": %d, \"reps\": %d, \"kernel_ms\": %.3f, "
+  std::printf("{\"dmax\": %.2f, \"n\": %d, \"blocks\": %d, \"reps\": %d, \"kernel_ms\": %.3f, "
               "\"cycles_per_candidate\": %.1f, \"RK_ns_per_candidate\": %.1f, "
               "\"all_ns_per_candidate\": %.1f}\n",
-              n, blocks, reps, ms, t[0] / per, t[1] * 10.0 / per, t[2] * 10.0 / per);
+              dmax, n, blocks, reps, ms, t[0] / per, t[1] * 10.0 / per, t[2] * 10.0 / per);
   return 0;
 }
