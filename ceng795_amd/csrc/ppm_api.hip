@@ -11,7 +11,9 @@
 #include <cstring>
 #include <memory>
 #include <stdexcept>
+#include <exception>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ceng795_ppm.h"
@@ -41,6 +43,10 @@ hipError_t launch_group_starts(const int*, const int*, int, int*, hipStream_t);
 hipError_t launch_group_tiles(const int*, int, int*, hipStream_t);
 hipError_t launch_tile_table(const int*, const int*, int, int2*, hipStream_t);
 hipError_t launch_tile_work(const int2*, int, const int*, const int*, unsigned*, hipStream_t);
+hipError_t launch_tile_shard(const int2*, int, int, int, const int*, const int*, int2*, int*,
+                             hipStream_t);
+hipError_t launch_merge_state(const int*, int, int, const float4*, const unsigned*, float4*,
+                              unsigned*, hipStream_t);
 hipError_t launch_rr_table(float*, int, hipStream_t);
 hipError_t launch_materialize(const unsigned*, const unsigned*, int, const float4*, float4*,
                               hipStream_t);
@@ -205,6 +211,18 @@ struct ppm_scene {
   long long photons = 0;
   size_t slot_bytes = 0;          // ppm_set_batching (0: default_slot_bytes())
   long long max_updates = INT_MAX;  // ppm_set_batching: (group, deposit) pairs per batch
+  // update-pass shard (ppm_set_update_shard; replica d of a multi-device scene is shard d):
+  // the update kernel runs only the tiles t with t mod shards == shard (build_grid)
+  int shard = 0, shards = 1;
+  DevBuf<int> owner;  // per hit point: the shard whose tiles update it (shards > 1)
+  // multi-device scene (ppm_scene_load_xml_multi): this object is replica 0 on the first
+  // device; peers[d - 1] is replica d.  Every replica runs the eye pass, the grid and the
+  // whole photon sequence; each applies the update pass to its own tiles; `merged` is false
+  // until the peers' hit-point state has been gathered here (merge_peers).
+  std::vector<std::unique_ptr<ppm_scene>> peers;
+  DevBuf<float4> peer_state;  // gathered peer state, shards x n_hp
+  DevBuf<unsigned> peer_nupd;
+  bool merged = true;
 
   void drop_update_events() {  // (back to the pool)
     upd_spare.insert(upd_spare.end(), upd_events.begin(), upd_events.end());
@@ -247,6 +265,7 @@ struct ppm_scene {
     owned.clear();
     hp.release(), state.release(), nupd.release(), pix_cnt.release(), pix_off.release();
     grid.release(), bstart.release(), bend.release(), slots.release(), ndep.release();
+    owner.release(), peer_state.release(), peer_nupd.release();
     gkeys.release(), gkeys2.release(), gidx.release(), perm.release(), gflags.release();
     gid.release(), gstart.release(), ntile.release(), tile_off.release(), tiles.release();
     tiles_lpt.release(), tkey.release(), tkey2.release();
@@ -424,6 +443,16 @@ void build_grid(ppm_scene* s, int width, int height) {
     hip_check(launch_tile_table(s->gstart.p, s->tile_off.p, groups, s->tiles.p, s->stream),
               "tile table");
     s->n_tiles = ntiles;
+    if (s->shards > 1) {  // this shard's tiles (table order), and every hit point's shard
+      s->owner.reserve(n, "alloc hit-point shards");
+      s->tiles_lpt.reserve(std::max(1, ntiles), "alloc shard tiles");
+      hip_check(launch_tile_shard(s->tiles.p, ntiles, s->shard, s->shards, s->gstart.p, s->perm.p,
+                                  s->tiles_lpt.p, s->owner.p, s->stream), "tile shard");
+      s->n_tiles = ntiles > s->shard ? (ntiles - s->shard + s->shards - 1) / s->shards : 0;
+      if (s->n_tiles > 0)
+        hip_check(hipMemcpyAsync(s->tiles.p, s->tiles_lpt.p, s->n_tiles * sizeof(int2),
+                                 hipMemcpyDeviceToDevice, s->stream), "shard tiles");
+    }
     // each group's buckets, and the bucket -> groups map the expansion uses
     s->gb.reserve((size_t)groups * kMaxCells, "alloc group buckets");
     s->gm.reserve((size_t)groups * kMaxCells, "alloc group multiplicities");
@@ -653,6 +682,125 @@ void density(ppm_scene* s, long long total, float* out) {
   hip_check(hipStreamSynchronize(s->stream), "density estimation");
 }
 
+// Runs f on every replica of a multi-device scene — replica 0 on the calling thread, each peer
+// on a thread of its own with its device current — and rethrows the first failure once all
+// have finished.  A single-device scene runs f(s) alone.
+template <typename F>
+void each_replica(ppm_scene* s, F&& f) {
+  if (s->peers.empty()) {
+    f(s);
+    return;
+  }
+  std::vector<std::exception_ptr> err(s->peers.size() + 1);
+  std::vector<std::thread> th;
+  th.reserve(s->peers.size());
+  for (size_t d = 0; d < s->peers.size(); d++) {
+    ppm_scene* p = s->peers[d].get();
+    th.emplace_back([&f, &err, p, d] {
+      try {
+        DeviceGuard g(p->device);
+        f(p);
+      } catch (...) {
+        err[d + 1] = std::current_exception();
+      }
+    });
+  }
+  try {
+    DeviceGuard g(s->device);
+    f(s);
+  } catch (...) {
+    err[0] = std::current_exception();
+  }
+  for (auto& t : th) t.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+}
+
+// Gathers a multi-device scene's sharded update results onto replica 0: each peer's (state,
+// count) arrays are copied device to device (xGMI peer copies; the peers' passes have ended
+// with a stream synchronisation), then every hit point takes the values of the replica whose
+// tiles own it (merge_state_kernel).  Ordered on replica 0's stream.
+void merge_peers(ppm_scene* s) {
+  if (s->merged || s->peers.empty() || !s->grid_ready || s->n_hp == 0) {
+    s->merged = true;
+    return;
+  }
+  const int n = s->n_hp;
+  const size_t D = s->peers.size() + 1;
+  DeviceGuard g(s->device);
+  s->peer_state.reserve(D * n, "alloc gathered hit-point state");
+  s->peer_nupd.reserve(D * n, "alloc gathered hit-point counts");
+  for (size_t d = 1; d < D; d++) {
+    const ppm_scene* p = s->peers[d - 1].get();
+    if (p->n_hp != n) throw std::runtime_error("multi-device PPM: replicas disagree on the hit points");
+    hip_check(hipMemcpyPeerAsync(s->peer_state.p + d * n, s->device, p->state.p, p->device,
+                                 (size_t)n * sizeof(float4), s->stream), "gather state");
+    hip_check(hipMemcpyPeerAsync(s->peer_nupd.p + d * n, s->device, p->nupd.p, p->device,
+                                 (size_t)n * sizeof(unsigned), s->stream), "gather counts");
+  }
+  hip_check(launch_merge_state(s->owner.p, n, 0, s->peer_state.p, s->peer_nupd.p, s->state.p,
+                               s->nupd.p, s->stream), "merge state");
+  s->merged = true;
+}
+
+// Device counters of one replica's passes since the last collection (and resets them).
+void collect(ppm_scene* s, ppm_stats* st) {
+  DeviceGuard g(s->device);
+  unsigned long long c[kStatSlots];
+  hip_check(hipMemcpyAsync(c, s->stats.p, sizeof c, hipMemcpyDeviceToHost, s->stream), "read counters");
+  hip_check(hipMemsetAsync(s->stats.p, 0, sizeof c, s->stream), "reset counters");
+  hip_check(hipStreamSynchronize(s->stream), "counters");
+  std::memset(st, 0, sizeof *st);
+  st->photons = s->photons;
+  st->photon_rays = (long long)c[1];
+  st->deposits = (long long)c[2];
+  st->updates = (long long)c[3];
+  st->eye_rays = (long long)c[4];
+  st->hit_points = s->n_hp;
+  st->update_deposit_visits = (long long)c[6];
+  st->update_candidates = (long long)c[16];
+  st->update_launches = s->upd_folded + (long long)s->upd_events.size();
+  st->update_compacted_segments = (long long)c[20];
+  st->update_compaction_fallbacks = (long long)c[21];
+  st->update_compacted_deposits = (long long)c[22];
+  st->update_ms = s->upd_ms_folded;
+  for (auto& ev : s->upd_events) {
+    float ms = 0;
+    hip_check(hipEventElapsedTime(&ms, ev.first, ev.second), "update time");
+    st->update_ms += ms;
+  }
+  s->drop_update_events();
+  if (s->S.diag == 2) std::fprintf(stderr, "ppm diag: windows %llu deposit-visits %llu tiles %d groups %d "
+                                   "longest tile %llu ticks phases(max) stage+filter %llu "
+                                   "counts %llu scan %llu scatter %llu color %llu gate %llu max-window-updates %llu "
+                                   "unstaged-rr %llu candidates %llu max-tile-candidates %llu max-wave-updates %llu max-tile-windows %llu "
+                                   "compacted-segments %llu fallbacks %llu compacted-deposits %llu "
+                                   "tile-ticks-sum %llu phases(sum) %llu %llu %llu %llu %llu %llu gate0(RK, all) %llu %llu\n",
+                                   c[5], c[6], s->n_tiles, s->n_groups, c[7], c[8], c[9],
+                                   c[10], c[11], c[12], c[13], c[14], c[15], c[16], c[17], c[18], c[19],
+                                   c[20], c[21], c[22], c[23], c[24], c[25], c[26], c[27], c[28], c[29], c[30], c[31]);
+  s->photons = 0;
+}
+
+// The counters of every replica: the photon sequence, eye pass and grid are replicated, so
+// those counts are replica 0's; the update pass is sharded, so its work is summed, and its
+// device time is the longest replica's (they run concurrently).
+void collect_all(ppm_scene* s, ppm_stats* st) {
+  collect(s, st);
+  for (auto& p : s->peers) {
+    ppm_stats q;
+    collect(p.get(), &q);
+    st->updates += q.updates;
+    st->update_deposit_visits += q.update_deposit_visits;
+    st->update_candidates += q.update_candidates;
+    st->update_launches += q.update_launches;
+    st->update_compacted_segments += q.update_compacted_segments;
+    st->update_compaction_fallbacks += q.update_compaction_fallbacks;
+    st->update_compacted_deposits += q.update_compacted_deposits;
+    st->update_ms = std::max(st->update_ms, q.update_ms);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -677,13 +825,100 @@ int ppm_scene_load_xml(const char* xml_path, int device, ppm_scene** out) {
   return RT_OK;
 }
 
+int ppm_scene_load_xml_multi(const char* xml_path, int device_count, const int* devices,
+                             ppm_scene** out) {
+  if (!xml_path || !out || device_count < 1 || !devices)
+    return set_error(RT_E_INVALID, "ppm_scene_load_xml_multi: bad argument");
+  *out = nullptr;
+  auto s = std::make_unique<ppm_scene>();
+  const int rc = guarded([&] {
+    load_ppm_xml(xml_path, s->host);
+    create_device(s.get(), devices[0]);
+    s->shards = device_count;
+    for (int d = 1; d < device_count; d++) {
+      s->peers.push_back(std::make_unique<ppm_scene>());
+      ppm_scene* p = s->peers.back().get();
+      p->host = s->host;
+      create_device(p, devices[d]);
+      p->shard = d;
+      p->shards = device_count;
+    }
+    return RT_OK;
+  });
+  if (rc != RT_OK) {
+    ppm_scene_destroy(s.release());
+    return rc;
+  }
+  *out = s.release();
+  return RT_OK;
+}
+
 void ppm_scene_destroy(ppm_scene* s) {
   if (!s) return;
+  for (auto& p : s->peers) ppm_scene_destroy(p.release());
+  s->peers.clear();
   int cur = -1;
   if (hipGetDevice(&cur) == hipSuccess && cur != s->device) (void)hipSetDevice(s->device);
   s->free_all();
   if (cur >= 0 && cur != s->device) (void)hipSetDevice(cur);
   delete s;
+}
+
+int ppm_scene_device_count(const ppm_scene* s) { return s ? 1 + (int)s->peers.size() : 0; }
+
+int ppm_set_update_shard(ppm_scene* s, int shard, int shards) {
+  if (!s || shards < 1 || shard < 0 || shard >= shards)
+    return set_error(RT_E_INVALID, "ppm_set_update_shard: bad argument (0 <= shard < shards)");
+  if (!s->peers.empty())
+    return set_error(RT_E_INVALID, "ppm_set_update_shard: a multi-device scene shards its own update pass");
+  s->shard = shard;
+  s->shards = shards;
+  s->grid_ready = false;  // the tile table is the grid's: build_hash_grid again
+  return RT_OK;
+}
+
+int ppm_hit_point_shards(ppm_scene* s, int* out) {
+  return guarded([&] {
+    check_scene(s);
+    if (!out) throw std::invalid_argument("ppm_hit_point_shards: NULL output");
+    if (!s->grid_ready) throw std::invalid_argument("no hash grid yet");
+    DeviceGuard g(s->device);
+    if (s->shards == 1 || s->n_hp == 0) {
+      std::fill(out, out + s->n_hp, 0);
+      return RT_OK;
+    }
+    hip_check(hipMemcpyAsync(out, s->owner.p, (size_t)s->n_hp * sizeof(int), hipMemcpyDeviceToHost,
+                             s->stream), "read hit-point shards");
+    hip_check(hipStreamSynchronize(s->stream), "read hit-point shards");
+    return RT_OK;
+  });
+}
+
+int ppm_write_hit_state(ppm_scene* s, const float* in) {
+  return guarded([&] {
+    check_scene(s);
+    if (!in) throw std::invalid_argument("ppm_write_hit_state: NULL input");
+    if (!s->grid_ready) throw std::invalid_argument("no hash grid yet");
+    const int n = s->n_hp;
+    std::vector<float4> st(n);
+    std::vector<unsigned> cnt(n);
+    for (int k = 0; k < n; k++) {
+      const float* r = in + 5 * (size_t)k;
+      if (!(r[4] >= 0.0f && r[4] < 4294967296.0f)) throw std::invalid_argument("bad update count");
+      st[k] = make_float4(r[0], r[1], r[2], r[3]);
+      cnt[k] = (unsigned)r[4];
+    }
+    each_replica(s, [&](ppm_scene* r) {
+      if (n == 0) return;
+      hip_check(hipMemcpyAsync(r->state.p, st.data(), n * sizeof(float4), hipMemcpyHostToDevice,
+                               r->stream), "write state");
+      hip_check(hipMemcpyAsync(r->nupd.p, cnt.data(), n * sizeof(unsigned), hipMemcpyHostToDevice,
+                               r->stream), "write counts");
+      hip_check(hipStreamSynchronize(r->stream), "write state");
+    });
+    s->merged = true;
+    return RT_OK;
+  });
 }
 
 int ppm_num_cameras(const ppm_scene* s) { return s ? (int)s->host.cameras.size() : 0; }
@@ -713,6 +948,7 @@ int ppm_settings(const ppm_scene* s, int* per_iteration, int* iterations, int* m
 int ppm_set_update_compaction(ppm_scene* s, long long min_list) {
   if (!s || min_list < -1) return set_error(RT_E_INVALID, "ppm_set_update_compaction: bad argument");
   s->compact_min = min_list;
+  for (auto& p : s->peers) p->compact_min = min_list;
   return RT_OK;
 }
 
@@ -720,6 +956,7 @@ int ppm_set_update_segment(ppm_scene* s, int seg_len) {
   if (!s || seg_len < 0 || (seg_len > 0 && seg_len < 64))
     return set_error(RT_E_INVALID, "ppm_set_update_segment: bad argument (0, or >= 64)");
   s->S.compact_seg = seg_len ? seg_len : kDefaultCompactSeg;
+  for (auto& p : s->peers) p->S.compact_seg = s->S.compact_seg;
   return RT_OK;
 }
 
@@ -728,21 +965,24 @@ int ppm_set_batching(ppm_scene* s, long long slot_bytes, long long max_updates) 
     return set_error(RT_E_INVALID, "ppm_set_batching: bad argument");
   s->slot_bytes = (size_t)slot_bytes;
   s->max_updates = max_updates ? std::min<long long>(max_updates, INT_MAX) : INT_MAX;
+  for (auto& p : s->peers) p->slot_bytes = s->slot_bytes, p->max_updates = s->max_updates;
   return RT_OK;
 }
 
 int ppm_set_seed(ppm_scene* s, unsigned long long seed) {
   if (!s) return set_error(RT_E_INVALID, "ppm_set_seed: NULL scene");
   s->seed = seed;
+  for (auto& p : s->peers) p->seed = seed;
   return RT_OK;
 }
 
 int ppm_eye_pass(ppm_scene* s, int cam) {
   return guarded([&] {
     check_scene(s);
-    DeviceGuard g(s->device);
-    eye_pass(s, cam);
-    hip_check(hipStreamSynchronize(s->stream), "eye pass");
+    each_replica(s, [&](ppm_scene* r) {
+      eye_pass(r, cam);
+      hip_check(hipStreamSynchronize(r->stream), "eye pass");
+    });
     return RT_OK;
   });
 }
@@ -751,8 +991,12 @@ int ppm_build_hash_grid(ppm_scene* s, int width, int height, double* info) {
   return guarded([&] {
     check_scene(s);
     if (width <= 0 || height <= 0) throw std::invalid_argument("bad image size");
+    each_replica(s, [&](ppm_scene* r) {
+      build_grid(r, width, height);
+      hip_check(hipStreamSynchronize(r->stream), "build hash grid");
+    });
+    s->merged = true;
     DeviceGuard g(s->device);
-    build_grid(s, width, height);
     PGrid G;
     hip_check(hipMemcpyAsync(&G, s->grid.p, sizeof G, hipMemcpyDeviceToHost, s->stream), "read grid");
     hip_check(hipStreamSynchronize(s->stream), "build hash grid");
@@ -771,6 +1015,7 @@ int ppm_read_hit_points(ppm_scene* s, float* out) {
   return guarded([&] {
     check_scene(s);
     if (!out) throw std::invalid_argument("ppm_read_hit_points: NULL output");
+    merge_peers(s);
     DeviceGuard g(s->device);
     std::vector<PHitPoint> hp(s->n_hp);
     std::vector<float4> st(s->n_hp);
@@ -803,6 +1048,7 @@ int ppm_read_hit_state(ppm_scene* s, float* out) {
     check_scene(s);
     if (!out) throw std::invalid_argument("ppm_read_hit_state: NULL output");
     if (!s->grid_ready) throw std::invalid_argument("no hash grid yet");
+    merge_peers(s);
     DeviceGuard g(s->device);
     std::vector<float4> st(s->n_hp);
     std::vector<unsigned> n(s->n_hp);
@@ -824,8 +1070,8 @@ int ppm_read_hit_state(ppm_scene* s, float* out) {
 int ppm_trace_photons(ppm_scene* s, long long first, long long count) {
   return guarded([&] {
     check_scene(s);
-    DeviceGuard g(s->device);
-    trace_photons(s, first, count);
+    each_replica(s, [&](ppm_scene* r) { trace_photons(r, first, count); });
+    if (!s->peers.empty()) s->merged = false;
     return RT_OK;
   });
 }
@@ -834,6 +1080,7 @@ int ppm_density_estimation(ppm_scene* s, long long total, float* out) {
   return guarded([&] {
     check_scene(s);
     if (!out) throw std::invalid_argument("ppm_density_estimation: NULL output");
+    merge_peers(s);
     DeviceGuard g(s->device);
     density(s, total, out);
     return RT_OK;
@@ -844,41 +1091,7 @@ int ppm_collect_stats(ppm_scene* s, ppm_stats* st) {
   return guarded([&] {
     check_scene(s);
     if (!st) throw std::invalid_argument("ppm_collect_stats: NULL output");
-    DeviceGuard g(s->device);
-    unsigned long long c[kStatSlots];
-    hip_check(hipMemcpyAsync(c, s->stats.p, sizeof c, hipMemcpyDeviceToHost, s->stream), "read counters");
-    hip_check(hipMemsetAsync(s->stats.p, 0, sizeof c, s->stream), "reset counters");
-    hip_check(hipStreamSynchronize(s->stream), "counters");
-    std::memset(st, 0, sizeof *st);
-    st->photons = s->photons;
-    st->photon_rays = (long long)c[1];
-    st->deposits = (long long)c[2];
-    st->updates = (long long)c[3];
-    st->eye_rays = (long long)c[4];
-    st->hit_points = s->n_hp;
-    st->update_deposit_visits = (long long)c[6];
-    st->update_candidates = (long long)c[16];
-    st->update_launches = s->upd_folded + (long long)s->upd_events.size();
-    st->update_compacted_segments = (long long)c[20];
-    st->update_compaction_fallbacks = (long long)c[21];
-    st->update_compacted_deposits = (long long)c[22];
-    st->update_ms = s->upd_ms_folded;
-    for (auto& ev : s->upd_events) {
-      float ms = 0;
-      hip_check(hipEventElapsedTime(&ms, ev.first, ev.second), "update time");
-      st->update_ms += ms;
-    }
-    s->drop_update_events();
-    if (s->S.diag == 2) std::fprintf(stderr, "ppm diag: windows %llu deposit-visits %llu tiles %d groups %d "
-                                     "longest tile %llu ticks phases(max) stage+filter %llu "
-                                     "counts %llu scan %llu scatter %llu color %llu gate %llu max-window-updates %llu "
-                                     "unstaged-rr %llu candidates %llu max-tile-candidates %llu max-wave-updates %llu max-tile-windows %llu "
-                                     "compacted-segments %llu fallbacks %llu compacted-deposits %llu "
-                                     "tile-ticks-sum %llu phases(sum) %llu %llu %llu %llu %llu %llu gate0(RK, all) %llu %llu\n",
-                                     c[5], c[6], s->n_tiles, s->n_groups, c[7], c[8], c[9],
-                                     c[10], c[11], c[12], c[13], c[14], c[15], c[16], c[17], c[18], c[19],
-                                     c[20], c[21], c[22], c[23], c[24], c[25], c[26], c[27], c[28], c[29], c[30], c[31]);
-    s->photons = 0;
+    collect_all(s, st);
     return RT_OK;
   });
 }
@@ -899,19 +1112,27 @@ int ppm_render(ppm_scene* s, int cam, int threads, float* out, ppm_stats* stats)
         for (int k = 0; k < 5; k++) (void)hipEventDestroy(e[k]);
       }
     } guard{ev};
-    hip_check(hipMemsetAsync(s->stats.p, 0, kStatSlots * sizeof(unsigned long long), s->stream), "zero counters");
-    s->photons = 0;
-    s->drop_update_events();
+    // a multi-device scene runs each pass on every replica (update pass sharded), then
+    // gathers the hit-point state onto replica 0 for the density estimation
+    each_replica(s, [&](ppm_scene* r) {
+      hip_check(hipMemsetAsync(r->stats.p, 0, kStatSlots * sizeof(unsigned long long), r->stream),
+                "zero counters");
+      r->photons = 0;
+      r->drop_update_events();
+    });
     hip_check(hipEventRecord(ev[0], s->stream), "event");
-    eye_pass(s, cam);
+    each_replica(s, [&](ppm_scene* r) { eye_pass(r, cam); });
     hip_check(hipEventRecord(ev[1], s->stream), "event");
-    build_grid(s, C.width, C.height);
+    each_replica(s, [&](ppm_scene* r) { build_grid(r, C.width, C.height); });
+    s->merged = true;
     hip_check(hipEventRecord(ev[2], s->stream), "event");
     const long long P = s->host.per_iteration, I = s->host.iterations;
     const long long per_thread = P / threads;
     const long long traced = C.height < threads ? P * I : per_thread * I * threads;
-    trace_photons(s, 0, traced);
+    each_replica(s, [&](ppm_scene* r) { trace_photons(r, 0, traced); });
+    if (!s->peers.empty()) s->merged = false;
     hip_check(hipEventRecord(ev[3], s->stream), "event");
+    merge_peers(s);
     const int normalizer = (int)(P * per_thread * threads);  // main.cpp:94, int arithmetic
     density(s, normalizer, out);
     hip_check(hipEventRecord(ev[4], s->stream), "event");

@@ -830,6 +830,37 @@ __global__ __launch_bounds__(256) void tile_table_kernel(const int* gstart, cons
     tiles[t] = make_int2(g, gstart[g] + (t - tile_off[g]) * kTileHP);
 }
 
+// Update-pass sharding (ppm_set_update_shard, multi-device scenes): tile t of the group-order
+// table belongs to shard t mod shards.  `mine` receives this shard's tiles in table order;
+// `owner` (nullable) the shard of every hit point.  Tiles own disjoint hit points, so a shard
+// applies the complete photon-order recurrence of each of its hit points.
+__global__ __launch_bounds__(256) void tile_shard_kernel(const int2* all, int ntiles, int shard,
+                                                         int shards, const int* gstart,
+                                                         const int* perm, int2* mine, int* owner) {
+  const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (t >= ntiles) return;
+  const int2 tile = all[t];
+  if (t % shards == shard) mine[t / shards] = tile;
+  if (owner) {
+    const int e = min(tile.y + kTileHP, gstart[tile.x + 1]);
+    for (int k = tile.y; k < e; k++) owner[perm[k]] = t % shards;
+  }
+}
+
+// Merge of a sharded update pass: hit point h takes (state, count) from the shard that owns
+// it; `self`'s own values are already in place, the others' come from `peer` (shards x n).
+__global__ __launch_bounds__(256) void merge_state_kernel(const int* owner, int n, int self,
+                                                          const float4* peer_state,
+                                                          const unsigned* peer_nupd,
+                                                          float4* state, unsigned* nupd) {
+  const int h = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (h >= n) return;
+  const int o = owner[h];
+  if (o == self) return;
+  state[h] = peer_state[(size_t)o * n + h];
+  nupd[h] = peer_nupd[(size_t)o * n + h];
+}
+
 
 // Longest-first launch order for the update pass: a tile's work is its group's deposit-list
 // length in this batch; the complemented length sorts the heaviest tiles to the front, so the
@@ -1742,6 +1773,21 @@ hipError_t launch_tile_table(const int* gstart, const int* tile_off, int groups,
                              hipStream_t st) {
   hipLaunchKernelGGL(tile_table_kernel, dim3(blocks_for(groups)), dim3(kThreads), 0, st, gstart,
                      tile_off, groups, tiles);
+  return hipGetLastError();
+}
+hipError_t launch_tile_shard(const int2* all, int ntiles, int shard, int shards, const int* gstart,
+                             const int* perm, int2* mine, int* owner, hipStream_t st) {
+  if (ntiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tile_shard_kernel, dim3(blocks_for(ntiles)), dim3(kThreads), 0, st, all,
+                     ntiles, shard, shards, gstart, perm, mine, owner);
+  return hipGetLastError();
+}
+hipError_t launch_merge_state(const int* owner, int n, int self, const float4* peer_state,
+                              const unsigned* peer_nupd, float4* state, unsigned* nupd,
+                              hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(merge_state_kernel, dim3(blocks_for(n)), dim3(kThreads), 0, st, owner, n,
+                     self, peer_state, peer_nupd, state, nupd);
   return hipGetLastError();
 }
 hipError_t launch_tile_work(const int2* tiles, int ntiles, const int* list_start,

@@ -465,6 +465,16 @@ RenderParams make_params(const rt_scene* s, const Replica& r, int cam, int row0,
   return P;
 }
 
+// P restricted to its first `rows` selected rows (rows row0 .. row0 + rows - 1 at stride 1):
+// the band launches of a multi-device MSAA frame.
+void limit_rows(RenderParams& P, int rows) {
+  P.rows = std::min(P.rows, rows);
+  P.tiles_total = P.tiles_x * ((P.rows + kTile - 1) / kTile);
+  P.num_sel_tiles = P.tile_begin < P.tiles_total
+                        ? (P.tiles_total - P.tile_begin + P.tile_step - 1) / P.tile_step
+                        : 0;
+}
+
 void check_render_args(const rt_scene* s, int cam, int row0, int row_stride) {
   if (!s) throw std::invalid_argument("scene is NULL");
   if (cam < 0 || cam >= (int)s->host.cameras.size())
@@ -523,20 +533,11 @@ const hipEvent_t* timing_marks(rt_scene* s, const RenderParams& P) {
   return t.pending.back().data();
 }
 
-// One frame (or a tile subset of one) of camera `cam` into P.out.  Pixel-centre cameras: the
-// render kernels write P.out directly.  MSAA cameras (HW2/Scene.cpp:32-69): one render pass per
-// sample index into d_samples[s], then the resolve kernel's splat + colour / weight into P.out
-// (row-major).  `timed`: this launch may take kernel-timing events (the first device only).
-void enqueue_frame(rt_scene* s, const Replica& r, const RenderParams& P, int samples,
-                   float* d_samples, hipStream_t stream, bool timed) {
+// The sample passes of an MSAA camera (HW2/Scene.cpp:32-69) over P's rows: pass k renders
+// sample k of every selected pixel into d_samples[k] (row-major, full-frame positions).
+void enqueue_samples(rt_scene* s, const Replica& r, const RenderParams& P, int samples,
+                     float* d_samples, hipStream_t stream, bool timed) {
   const bool fast = s->mode != RT_TRAVERSAL_REFERENCE;
-  if (samples <= 1) {
-    hip_check(launch_render(P, r.d_nodes, r.d_prims, r.d_normals, r.d_mats, r.d_lights, fast,
-                            s->deep, s->has_spheres, s->wide_only,
-                            timed ? timing_marks(s, P) : nullptr, stream),
-              "render launch");
-    return;
-  }
   const size_t frame = (size_t)P.width * P.height * 3;
   for (int k = 0; k < samples * samples; k++) {
     RenderParams Q = P;
@@ -552,14 +553,39 @@ void enqueue_frame(rt_scene* s, const Replica& r, const RenderParams& P, int sam
                             timed ? timing_marks(s, Q) : nullptr, stream),
               "render launch");
   }
+}
+
+// The splat + colour / weight of rows [row_lo, row_hi) into out (row-major, full frame).
+void enqueue_resolve(rt_scene* s, int width, int height, int samples, const float* d_samples,
+                     float* out, int row_lo, int row_hi, hipStream_t stream) {
   MsaaResolveParams M;
   M.samples = d_samples;
-  M.out = P.out;
-  M.width = P.width;
-  M.height = P.height;
+  M.out = out;
+  M.width = width;
+  M.height = height;
   M.n = samples;
   M.seed = s->msaa_seed;
+  M.row_lo = row_lo;
+  M.row_hi = row_hi;
   hip_check(launch_msaa_resolve(M, stream), "msaa resolve launch");
+}
+
+// One frame (or a tile subset of one) of camera `cam` into P.out.  Pixel-centre cameras: the
+// render kernels write P.out directly.  MSAA cameras (HW2/Scene.cpp:32-69): one render pass per
+// sample index into d_samples[s], then the resolve kernel's splat + colour / weight into P.out
+// (row-major).  `timed`: this launch may take kernel-timing events (the first device only).
+void enqueue_frame(rt_scene* s, const Replica& r, const RenderParams& P, int samples,
+                   float* d_samples, hipStream_t stream, bool timed) {
+  const bool fast = s->mode != RT_TRAVERSAL_REFERENCE;
+  if (samples <= 1) {
+    hip_check(launch_render(P, r.d_nodes, r.d_prims, r.d_normals, r.d_mats, r.d_lights, fast,
+                            s->deep, s->has_spheres, s->wide_only,
+                            timed ? timing_marks(s, P) : nullptr, stream),
+              "render launch");
+    return;
+  }
+  enqueue_samples(s, r, P, samples, d_samples, stream, timed);
+  enqueue_resolve(s, P.width, P.height, samples, d_samples, P.out, 0, P.height, stream);
 }
 
 size_t sample_floats(const rt_camera& c) {
@@ -647,6 +673,92 @@ void add_counters(const std::vector<unsigned long long>& cnt, rt_stats* stats) {
     stats->shadow_rays += (long long)cnt[kCounterWidth * r + kCntShadow];
     stats->secondary_rays += (long long)cnt[kCounterWidth * r + kCntSecondary];
     stats->primary_hits += (long long)cnt[kCounterWidth * r + kCntHits];
+  }
+}
+
+// One frame of an MSAA camera over every device of a multi-device scene (the
+// Gaussian splat of HW2/Scene.cpp:51-63 reaches the 3x3 neighbours, so pixels do not shard as
+// independent tiles).  Device d owns the band of rows [H*d/D, H*(d+1)/D) and renders every
+// sample pass over its band plus a one-row halo on each side (the halo rows' samples are
+// recomputed, bit for bit: each pixel's generators depend only on the seed and the pixel, §7),
+// resolves its band, and one RCCL group of send / receive pairs lands the bands in d_frame on
+// the first device.  Halo launches carry no counters, so the ray counts are one frame's.
+// Caller holds s->multi_mu.
+void render_multi_msaa(rt_scene* s, CtxSet& cx, int cam, float* d_frame, hipStream_t s0,
+                       bool per_call) {
+  const int D = (int)s->rep.size();
+  const rt_camera& c = s->host.cameras[cam];
+  const int H = c.height, W = c.width, n = c.num_samples;
+  const size_t frame = (size_t)W * H * 3;
+  RenderCtx* x0 = cx.x[0];
+  {
+    DeviceGuard g(s->rep[0]->device);
+    hip_check(hipEventRecord(x0->ev_in, s0), "event record");  // d_frame's earlier work
+    hip_check(hipStreamWaitEvent(x0->stream, x0->ev_in, 0), "wait event");
+  }
+  for (int d = 0; d < D; d++) {
+    const int lo = (int)((long long)H * d / D), hi = (int)((long long)H * (d + 1) / D);
+    if (hi <= lo) continue;
+    Replica& r = *s->rep[d];
+    RenderCtx* x = cx.x[d];
+    DeviceGuard g(r.device);
+    float* dst = d_frame;
+    if (d > 0) {
+      ensure(x->d_image, x->image_floats, frame, "alloc band frame");
+      dst = x->d_image;
+    }
+    RenderParams P = make_params(s, r, cam, lo, 1, 0, 1, 0, dst, per_call ? x->d_cnt : r.d_counters);
+    limit_rows(P, hi - lo);
+    bind_ctx(s, x, P, c);
+    enqueue_samples(s, r, P, n, x->d_samples, x->stream, d == 0);
+    for (const int row : {lo - 1, hi}) {  // the halo rows the splat of the band's edges reads
+      if (row < 0 || row >= H) continue;
+      RenderParams Q = make_params(s, r, cam, row, 1, 0, 1, 0, dst, nullptr);
+      limit_rows(Q, 1);
+      Q.hits = P.hits;
+      Q.occ = P.occ;
+      Q.frames = P.frames;
+      set_schedule(Q, x->d_sched);
+      enqueue_samples(s, r, Q, n, x->d_samples, x->stream, false);
+    }
+    enqueue_resolve(s, W, H, n, x->d_samples, dst, lo, hi, x->stream);
+  }
+  DeviceGuard g(s->rep[0]->device);
+  if (D > 1) {
+    auto band = [&](int d, float* base) {
+      const int lo = (int)((long long)H * d / D), hi = (int)((long long)H * (d + 1) / D);
+      return std::make_pair(base + (size_t)lo * W * 3, (size_t)(hi - lo) * W * 3);
+    };
+    if (s->copy_gather) {
+      for (int d = 1; d < D; d++) {
+        const auto src = band(d, cx.x[d]->d_image);
+        if (!src.second) continue;
+        {
+          DeviceGuard gd(s->rep[d]->device);
+          hip_check(hipEventRecord(cx.x[d]->ev_out, cx.x[d]->stream), "event record");
+        }
+        hip_check(hipStreamWaitEvent(x0->stream, cx.x[d]->ev_out, 0), "wait event");
+        hip_check(hipMemcpyPeerAsync(band(d, d_frame).first, s->rep[0]->device, src.first,
+                                     s->rep[d]->device, src.second * sizeof(float), x0->stream),
+                  "gather copy");
+      }
+    } else {
+      nccl_check(ncclGroupStart(), "ncclGroupStart");
+      for (int d = 1; d < D; d++) {
+        const auto src = band(d, cx.x[d]->d_image);
+        if (!src.second) continue;
+        nccl_check(ncclSend(src.first, src.second, ncclFloat, 0, s->comms[d], cx.x[d]->stream),
+                   "ncclSend");
+        nccl_check(ncclRecv(band(d, d_frame).first, src.second, ncclFloat, d, s->comms[0],
+                            x0->stream),
+                   "ncclRecv");
+      }
+      nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    }
+  }
+  if (s0 != x0->stream) {
+    hip_check(hipEventRecord(x0->ev_out, x0->stream), "event record");
+    hip_check(hipStreamWaitEvent(s0, x0->ev_out, 0), "wait event");
   }
 }
 
@@ -953,13 +1065,16 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
     if (tile_begin < 0 || tile_step < 1 || !d_out)
       throw std::invalid_argument("rt_render_device: bad tile selection / output");
     const rt_camera& c = s->host.cameras[cam];
-    if (s->multi && c.num_samples <= 1) {
+    if (s->multi) {
       // a multi-device scene renders whole frames (rows subsets allowed) split over its devices
       if (tile_begin != 0 || tile_step != 1 || tile_major || tile_count >= 0)
         throw std::domain_error("multi-device scenes render whole row-major frames only");
       std::lock_guard<std::mutex> lk(s->multi_mu);
       CtxSet cx(s, s->rep.size());
-      render_multi(s, cx, cam, row0, row_stride, d_out, (hipStream_t)stream, false);
+      if (c.num_samples > 1)
+        render_multi_msaa(s, cx, cam, d_out, (hipStream_t)stream, false);
+      else
+        render_multi(s, cx, cam, row0, row_stride, d_out, (hipStream_t)stream, false);
       return RT_OK;
     }
     Replica& r = *s->rep[0];
@@ -1085,7 +1200,7 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
     const rt_camera& c = s->host.cameras[cam];
     const TilePlan tp = plan(c, row0, row_stride);
     if (tp.rows == 0) return RT_OK;
-    const bool multi = s->multi && c.num_samples <= 1;
+    const bool multi = s->multi;
     std::unique_lock<std::mutex> multi_lock(s->multi_mu, std::defer_lock);
     if (multi) multi_lock.lock();
     CtxSet cx(s, multi ? s->rep.size() : 1);
@@ -1110,7 +1225,9 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
                 "zero counters");
     }
     hip_check(hipEventRecord(x->e0, x->stream), "event record");
-    if (multi) {
+    if (multi && c.num_samples > 1) {
+      render_multi_msaa(s, cx, cam, d_frame, x->stream, true);
+    } else if (multi) {
       render_multi(s, cx, cam, row0, row_stride, d_frame, x->stream, true);
     } else {
       RenderParams P = make_params(s, r, cam, row0, row_stride, 0, 1, 0, d_frame, x->d_cnt);

@@ -135,6 +135,7 @@ struct MsaaResolveParams {
   float* out;
   int width, height, n;
   unsigned long long seed;
+  int row_lo, row_hi;  // the rows resolved: [row_lo, row_hi) (a multi-device band)
 };
 
 // Untile of a multi-device frame (rt_api.hip render_multi): the frame's tiles were dealt

@@ -1686,8 +1686,8 @@ __device__ __forceinline__ float gaussian_filter(float x, float y, float sigma) 
 
 __global__ __launch_bounds__(256) void msaa_resolve_kernel(MsaaResolveParams M) {
   const int ai = (int)(blockIdx.x * 16 + (threadIdx.x & 15));
-  const int aj = (int)(blockIdx.y * 16 + (threadIdx.x >> 4));
-  if (ai >= M.width || aj >= M.height) return;
+  const int aj = M.row_lo + (int)(blockIdx.y * 16 + (threadIdx.x >> 4));
+  if (ai >= M.width || aj >= M.row_hi) return;
   const int n = M.n, S = n * n;
   const size_t frame = (size_t)M.width * M.height * 3;
   float cr = 0.0f, cg = 0.0f, cb = 0.0f, wsum = 0.0f;
@@ -1723,7 +1723,8 @@ __global__ __launch_bounds__(256) void msaa_resolve_kernel(MsaaResolveParams M) 
 }
 
 hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream) {
-  const dim3 grid((M.width + 15) / 16, (M.height + 15) / 16);
+  if (M.row_hi <= M.row_lo) return hipSuccess;
+  const dim3 grid((M.width + 15) / 16, (M.row_hi - M.row_lo + 15) / 16);
   hipLaunchKernelGGL(msaa_resolve_kernel, grid, dim3(256), 0, stream, M);
   return hipGetLastError();
 }

@@ -25,7 +25,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _VARIANT = os.environ.get("CENG795_PPM_LIB", "")
 LIB_PATH = os.path.join(_HERE, "lib", f"libceng795_ppm_{_VARIANT}.so" if _VARIANT else
                         "libceng795_ppm.so")
-ABI_VERSION = 5  # CENG795_PPM_ABI_VERSION
+ABI_VERSION = 6  # CENG795_PPM_ABI_VERSION
 
 _lib = None
 
@@ -69,6 +69,11 @@ SIGNATURES = {
     "ppm_render": (_I, [_VP, _I, _I, _VP, C.POINTER(ppm_stats)]),
     "ppm_collect_stats": (_I, [_VP, C.POINTER(ppm_stats)]),
     "ppm_write_png": (_I, [C.c_char_p, _VP, _I, _I]),
+    "ppm_scene_load_xml_multi": (_I, [C.c_char_p, _I, _IP, C.POINTER(_VP)]),
+    "ppm_scene_device_count": (_I, [_VP]),
+    "ppm_set_update_shard": (_I, [_VP, _I, _I]),
+    "ppm_hit_point_shards": (_I, [_VP, _VP]),
+    "ppm_write_hit_state": (_I, [_VP, _VP]),
 }
 
 
@@ -106,11 +111,18 @@ class PPMCamera:
 
 
 class PhotonScene:
-    """PPM Scene on one GPU (device index ``device``)."""
+    """PPM Scene on one GPU (device index ``device``), or — ``devices=[...]`` — one scene over
+    several GPUs of this process: every pass runs on each, the update pass is sharded by hit
+    point and the shards' state is gathered onto ``devices[0]`` (ppm_scene_load_xml_multi)."""
 
-    def __init__(self, xml_path: str, device: int = 0, seed: int = 0):
+    def __init__(self, xml_path: str, device: int = 0, seed: int = 0, devices=None):
         h = C.c_void_p()
-        check(lib().ppm_scene_load_xml(str(xml_path).encode(), device, C.byref(h)))
+        if devices is None:
+            check(lib().ppm_scene_load_xml(str(xml_path).encode(), device, C.byref(h)))
+        else:
+            ids = (C.c_int * len(devices))(*[int(d) for d in devices])
+            check(lib().ppm_scene_load_xml_multi(str(xml_path).encode(), len(devices), ids,
+                                                 C.byref(h)))
         self._h = h
         self.set_seed(seed)
 
@@ -163,6 +175,28 @@ class PhotonScene:
         0 = default (32768)."""
         check(lib().ppm_set_update_segment(self._h, int(seg_len)))
 
+    @property
+    def device_count(self) -> int:
+        return lib().ppm_scene_device_count(self._h)
+
+    def set_update_shard(self, shard: int, shards: int) -> None:
+        """Apply only update shard ``shard`` of ``shards`` (one process per GPU); takes effect
+        at the next build_hash_grid."""
+        check(lib().ppm_set_update_shard(self._h, int(shard), int(shards)))
+
+    def hit_point_shards(self) -> np.ndarray:
+        """Per hit point, the shard whose update tiles own it (after build_hash_grid)."""
+        out = np.zeros(lib().ppm_num_hit_points(self._h), np.int32)
+        check(lib().ppm_hit_point_shards(self._h, out.ctypes.data))
+        return out
+
+    def write_hit_state(self, state: np.ndarray) -> None:
+        """Overwrite the hit-point state (n x 5: flux xyz, radius^2, n)."""
+        st = np.ascontiguousarray(state, np.float32)
+        if st.shape != (lib().ppm_num_hit_points(self._h), 5):
+            raise ValueError(f"hit state must be ({lib().ppm_num_hit_points(self._h)}, 5)")
+        check(lib().ppm_write_hit_state(self._h, st.ctypes.data))
+
     # ------------------------------------------------------------------ reference passes
     def reset_hash_grid(self) -> None:
         """Scene::reset_hash_grid — folded into eye_trace_lines (which rebuilds the points)."""
@@ -212,6 +246,17 @@ class PhotonScene:
         check(lib().ppm_render(self._h, camera_index, reference_threads, out.ctypes.data,
                                C.byref(st)))
         return out, st
+
+
+def merge_shard_states(states, owners: np.ndarray) -> np.ndarray:
+    """The merged hit-point state of a sharded update pass: hit point h takes row h of the
+    state of the shard that owns it (``owners`` = hit_point_shards())."""
+    states = np.stack([np.asarray(s, np.float32) for s in states])
+    owners = np.asarray(owners)
+    if owners.shape != states.shape[1:2] or (owners.size and (owners.min() < 0 or
+                                                              owners.max() >= len(states))):
+        raise ValueError("owners must name one of the shards for every hit point")
+    return states[owners, np.arange(owners.size)]
 
 
 def write_ppm_png(path: str, rgb: np.ndarray) -> None:

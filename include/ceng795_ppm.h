@@ -26,9 +26,10 @@
 extern "C" {
 #endif
 
-#define CENG795_PPM_ABI_VERSION 5  /* 2: ppm_set_batching; 3: update-pass work in ppm_stats;
+#define CENG795_PPM_ABI_VERSION 6  /* 2: ppm_set_batching; 3: update-pass work in ppm_stats;
                                      4: tile-list compaction (setter + counters); 5: compaction
-                                     segment length, counters per segment */
+                                     segment length, counters per segment; 6: multi-device
+                                     scenes, update-pass shards, hit-state write */
 
 typedef struct ppm_scene ppm_scene;
 
@@ -103,8 +104,39 @@ int ppm_density_estimation(ppm_scene* scene, long long total_num_of_photons, flo
  * normalises by P*(P/T)*T (main.cpp:74, 94).  Synchronous; stats nullable. */
 int ppm_render(ppm_scene* scene, int camera, int reference_threads, float* out_rgb,
                ppm_stats* stats);
-/* Reads (and resets) the device counters of the passes run since the last call. */
+/* Reads (and resets) the device counters of the passes run since the last call.  On a
+ * multi-device scene the photon / eye counts are replica 0's (every replica traces the whole
+ * sequence), the update-pass work is summed over the replicas and update_ms is the longest
+ * replica's. */
 int ppm_collect_stats(ppm_scene* scene, ppm_stats* stats);
+
+/* ---- several GPUs ("PPM photons shard freely, but the hit-point flux state is
+ * shared").  The reference's T threads share every hit point under a mutex
+ * (PPM/src/Scene.cpp:131-168, PPM/include/Hit_point.h:22).  Here the update pass is split by
+ * hit point instead: the grid's update tiles (hit points of one hash-cell range, <= 3 each)
+ * are dealt round-robin over S shards, a shard applies the complete photon-order recurrence
+ * of its own hit points, and the shards' results are merged by hit point.  Results are
+ * bit-identical to the one-device scene for any S. */
+
+/* One process over several GPUs: replica d (on devices[d]) runs the eye pass, grid and the
+ * whole photon sequence, and the update pass of shard d of device_count; density estimation,
+ * ppm_read_hit_state and ppm_read_hit_points first gather the replicas' hit-point state onto
+ * devices[0] (device-to-device copies + a merge kernel).  The same device may be listed more
+ * than once.  Every other call of this header accepts the scene and fans out to the replicas
+ * (passes run concurrently, one host thread per replica). */
+int ppm_scene_load_xml_multi(const char* xml_path, int device_count, const int* devices,
+                             ppm_scene** out);
+int ppm_scene_device_count(const ppm_scene* scene);
+/* One process per GPU: this scene applies only the update tiles of shard `shard` of
+ * `shards` (0 <= shard < shards; 0 of 1 = all, the default).  Takes effect at the next
+ * ppm_build_hash_grid (call it again).  Not for multi-device scenes, which shard themselves. */
+int ppm_set_update_shard(ppm_scene* scene, int shard, int shards);
+/* The shard owning each hit point (ppm_num_hit_points ints), after ppm_build_hash_grid. */
+int ppm_hit_point_shards(ppm_scene* scene, int* out);
+/* Overwrites the hit-point state with 5 floats per hit point (the ppm_read_hit_state layout:
+ * flux xyz, radius_squared, n) — e.g. the merge of the shards' states before
+ * ppm_density_estimation.  After ppm_build_hash_grid. */
+int ppm_write_hit_state(ppm_scene* scene, const float* in5);
 
 /* main.cpp:142-156 (no tone-mapping operator): c -> int(pow(1 - exp(-c), 1/2.2f)*255 + 0.5f),
  * clamped to [0, 255], RGBA8 PNG. */

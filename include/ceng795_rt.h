@@ -132,7 +132,10 @@ int rt_scene_load_xml(const char* xml_path, int device, rt_scene** out);
  * 8x8 tiles round-robin over the devices (tile t -> device t mod device_count), render every
  * share on its own device, gather the shares onto devices[0] with RCCL (one communicator per
  * device, ncclCommInitAll; send / receive pairs in one group, over xGMI) and untile them there.
- * Pixels are the single-device ones bit for bit.  MSAA cameras render on devices[0] alone.
+ * Pixels are the single-device ones bit for bit.  MSAA cameras (whose 3x3 splat crosses tile
+ * borders, HW2/Scene.cpp:51-63) split by bands of rows instead: device d owns rows
+ * [H*d/n, H*(d+1)/n), renders every sample pass over its band plus a one-row halo each side,
+ * resolves its band, and the bands are gathered the same way.
  * Frames of one multi-device scene are serialised (its RCCL communicators are shared). */
 int rt_scene_create_multi(const rt_scene_desc* desc, int device_count, const int* devices,
                           rt_scene** out);

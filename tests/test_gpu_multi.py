@@ -51,6 +51,51 @@ def test_multi_device_scene_matches_oracle(scene_dir, name, devices):
             assert gst.secondary_rays == st.secondary_rays
 
 
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0], [0] * 8])
+@pytest.mark.parametrize("name", ["msaa4", "msaa5", "msaa9_depth2", "msaa16"])
+def test_multi_device_msaa_matches_single_device(scene_dir, name, devices):
+    """MSAA over several devices (the Gaussian splat of HW2/Scene.cpp:51-63
+    crosses tile borders): each device renders the samples of its band of rows plus a one-row
+    halo, resolves its band, and the bands are gathered.  Every frame must be the one-device
+    frame bit for bit (which test_msaa_matches_oracle pins to the oracle), with the same ray
+    counts — halo rows are not counted twice."""
+    import ceng795_amd
+    xml = scenes.write(name, scene_dir)
+    for seed in (0, 12345):
+        with ceng795_amd.Scene(xml) as one:
+            one.set_msaa_seed(seed)
+            refs = [one.render_image(c) for c in range(one.num_cameras)]
+        with ceng795_amd.Scene(xml, devices=devices) as s:
+            s.set_msaa_seed(seed)
+            for cam, (ref, st) in enumerate(refs):
+                got, gst = s.render_image(cam)
+                assert same(got, ref), (name, devices, cam, seed)
+                assert (gst.primary_rays, gst.shadow_rays, gst.secondary_rays, gst.primary_hits) == \
+                    (st.primary_rays, st.shadow_rays, st.secondary_rays, st.primary_hits)
+
+
+def test_multi_device_msaa_on_caller_stream(scene_dir):
+    """rt_render_device of an MSAA camera on a multi-device scene: bands gathered into the
+    caller's HBM frame, ordered on the caller's stream."""
+    import torch
+    import ceng795_amd
+    xml = scenes.write("msaa4", scene_dir)
+    o = OracleScene(xml)
+    ref, _ = o.render_msaa(0, seed=7, threads=THREADS)
+    with ceng795_amd.Scene(xml, devices=[0, 0, 0]) as s:
+        s.set_msaa_seed(7)
+        st = torch.cuda.Stream()
+        bufs = []
+        for _ in range(2):
+            b = torch.full(ref.shape, -1.0, dtype=torch.float32, device="cuda")
+            st.wait_stream(torch.cuda.current_stream())
+            s.render_device(0, b.data_ptr(), stream=st.cuda_stream)
+            bufs.append(b)
+        torch.cuda.synchronize()
+        for b in bufs:
+            assert same(b.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
 @pytest.mark.parametrize("start,stride", [(3, 5), (0, 64), (47, 1)])
 def test_multi_device_row_subsets(scene_dir, devices, start, stride):

@@ -156,3 +156,85 @@ def test_update_compaction_matches_oracle(ppm, scene_dir, name, min_list, seg):
             g.set_update_compaction(-2)
         with pytest.raises(ppm.RTError):
             g.set_update_segment(8)
+
+
+# ---------------------------------------------------------------- several GPUs
+# The reference shares every hit point between its T threads under a mutex
+# (PPM/src/Scene.cpp:131-168); the GPU path shards the update pass by hit point instead.  On
+# the one-GPU test box the multi-device scene lists device 0 several times: each replica is a
+# complete scene on its own stream, so the shard, gather and merge code is the multi-GPU one.
+@pytest.mark.parametrize("name", list(scenes.PPM))
+@pytest.mark.parametrize("replicas", [2, 3])
+def test_multi_device_scene_matches_oracle(ppm, scene_dir, name, replicas):
+    xml = scenes.write_ppm(name, scene_dir)
+    o = OraclePPM(xml)
+    with ppm.PhotonScene(xml, seed=4, devices=[0] * replicas) as g:
+        assert g.device_count == replicas
+        g.set_batching(256 << 10, 0)  # several batches: each shard keeps its hit points' state
+        c = g.camera(0)
+        g.eye_trace_lines(0)
+        g.build_hash_grid(c.width, c.height)
+        o.eye_pass(0, seed=4)
+        o.build_hash_grid(c.width, c.height)
+        g.trace_photons(0, 7000)
+        g.trace_photons(7000, 13000)
+        ost = o.trace_photons(4, 0, 20000)
+        got, want = g.hit_state(), o.hit_state()
+        assert np.array_equal(bits(got), bits(want)), \
+            f"{(bits(got) != bits(want)).any(1).sum()} of {len(want)} hit points differ"
+        owners = g.hit_point_shards()
+        assert owners.min() >= 0 and owners.max() < replicas
+        assert len(set(owners.tolist())) == min(replicas, len(owners))  # every shard has work
+        st = g.collect_stats()
+        assert (st.photons, st.photon_rays, st.deposits, st.updates) == \
+            (20000, ost.photon_rays, ost.deposits, ost.updates)
+
+
+@pytest.mark.parametrize("replicas", [2, 3])
+def test_multi_device_render_matches_oracle(ppm, scene_dir, replicas):
+    xml = scenes.write_ppm("ppm_box", scene_dir)
+    o = OraclePPM(xml)
+    with ppm.PhotonScene(xml, seed=21, devices=[0] * replicas) as g:
+        img, st = g.render(0, reference_threads=8)
+        want, ost = o.render(0, seed=21, threads=8)
+        assert np.array_equal(bits(img), bits(want))
+        assert (st.photons, st.hit_points, st.eye_rays) == (ost.photons, ost.hit_points, ost.eye_rays)
+        assert st.updates == ost.updates
+        img2, _ = g.render(0, reference_threads=8)  # again on the same scene: same bits
+        assert np.array_equal(bits(img2), bits(want))
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_update_shards_merge_to_oracle(ppm, scene_dir, shards):
+    """One process per GPU: S scenes, each applying update shard s of S, merged by hit-point
+    owner (ppm.merge_shard_states) and written back for the density estimation."""
+    xml = scenes.write_ppm("ppm_box", scene_dir)
+    o = OraclePPM(xml)
+    states, owners, gs = [], None, []
+    try:
+        for s in range(shards):
+            g = ppm.PhotonScene(xml, seed=21)
+            gs.append(g)
+            g.set_update_shard(s, shards)
+            c = g.camera(0)
+            g.eye_trace_lines(0)
+            g.build_hash_grid(c.width, c.height)
+            g.trace_photons(0, 20000)
+            states.append(g.hit_state())
+            own = g.hit_point_shards()
+            assert owners is None or np.array_equal(own, owners)
+            owners = own
+        o.eye_pass(0, seed=21)
+        o.build_hash_grid(c.width, c.height)
+        o.trace_photons(21, 0, 20000)
+        merged = ppm.merge_shard_states(states, owners)
+        assert np.array_equal(bits(merged), bits(o.hit_state()))
+        gs[0].write_hit_state(merged)
+        assert np.array_equal(bits(gs[0].hit_state()), bits(merged))
+        img = gs[0].density_estimation(20000)
+        assert np.array_equal(bits(img), bits(o.density(20000)))
+        with pytest.raises(ppm.RTError):
+            gs[0].set_update_shard(shards, shards)
+    finally:
+        for g in gs:
+            g.close()
