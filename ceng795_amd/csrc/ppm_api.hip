@@ -425,7 +425,7 @@ void build_grid(ppm_scene* s, int width, int height) {
     hip_check(hipStreamSynchronize(s->stream), "group hit points");
     if (err) throw std::domain_error("a hit point's radius box spans more hash cells than supported");
     s->n_groups = groups;
-    // tiles of <= kTileHP (3) hit points per group (group_update_kernel)
+    // tiles of <= kTileHP (5) hit points per group (group_update_kernel)
     s->ntile.reserve(groups + 1, "alloc tile counts");
     s->tile_off.reserve(groups + 1, "alloc tile offsets");
     hip_check(launch_group_tiles(s->gstart.p, groups, s->ntile.p, s->stream), "group tiles");
@@ -775,10 +775,12 @@ void collect(ppm_scene* s, ppm_stats* st) {
                                    "counts %llu scan %llu scatter %llu color %llu gate %llu max-window-updates %llu "
                                    "unstaged-rr %llu candidates %llu max-tile-candidates %llu max-wave-updates %llu max-tile-windows %llu "
                                    "compacted-segments %llu fallbacks %llu compacted-deposits %llu "
-                                   "tile-ticks-sum %llu phases(sum) %llu %llu %llu %llu %llu %llu gate0(RK, all) %llu %llu\n",
+                                   "tile-ticks-sum %llu phases(sum) %llu %llu %llu %llu %llu %llu gate0(RK, all) %llu %llu "
+                                   "compaction(sum, max) %llu %llu\n",
                                    c[5], c[6], s->n_tiles, s->n_groups, c[7], c[8], c[9],
                                    c[10], c[11], c[12], c[13], c[14], c[15], c[16], c[17], c[18], c[19],
-                                   c[20], c[21], c[22], c[23], c[24], c[25], c[26], c[27], c[28], c[29], c[30], c[31]);
+                                   c[20], c[21], c[22], c[23], c[24], c[25], c[26], c[27], c[28], c[29], c[30], c[31],
+                                   c[32], c[33]);
   s->photons = 0;
 }
 

@@ -12,7 +12,7 @@ constexpr int kObjSphere = 0, kObjInstance = 1;
 constexpr int kTopStack = 48;   // per-lane traversal stacks (host checks the BVH depths)
 constexpr int kMeshStack = 64;
 constexpr int kEyeStack = 24;   // eye-ray tree: <= MaxRecursionDepth (<= 20) + 1 pending
-constexpr int kStatSlots = 32;  // device counter words (ppm_collect_stats)
+constexpr int kStatSlots = 36;  // device counter words (ppm_collect_stats)
 constexpr int kMaxCells = 27;
 constexpr int kGroupBits = 27;  // expansion keys: group | multiplicity << kGroupBits
 constexpr int kRepBits = 5;  // multiplicity bits next to a deposit index (kMaxCells < 32)

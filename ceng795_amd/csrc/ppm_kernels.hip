@@ -717,10 +717,10 @@ __global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, con
 }
 
 #ifndef PPM_TILE
-#define PPM_TILE 3
+#define PPM_TILE 5  // hit points per update tile (round 3: 5 with 1,024-deposit windows, C5 update 9.58 -> 8.60 ms)
 #endif
 #ifndef PPM_WIN
-#define PPM_WIN 2048
+#define PPM_WIN 1024
 #endif
 #ifndef PPM_GATE_B
 #define PPM_GATE_B 3
@@ -1251,7 +1251,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     tp[j] = mk(s_hp[j][0], s_hp[j][1], s_hp[j][2]);
   }
 #if PPM_PHASE_TIMERS
-  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tp0 = 0;
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tp0 = 0, ctick = 0;  // ctick: compaction
 #define PPM_PHASE(i)                                              \
   if (S.diag == 2 && tid == 0) {                                  \
     const unsigned long long t1 = wall_clock64();                 \
@@ -1286,6 +1286,10 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     float r2c[kTileHP];
 #pragma unroll
     for (int j = 0; j < kTileHP; j++) r2c[j] = j < nh ? s_r2[j] : -1.0f;
+#if PPM_PHASE_TIMERS
+    const unsigned long long t_c0 = S.diag == 2 && tid == 0 ? wall_clock64() : 0;
+#endif
+    int kept = 0;
     float4 cd[kCPer];
     auto cfetch = [&](int base) {
 #pragma unroll
@@ -1295,7 +1299,6 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
       }
     };
     cfetch(ls);
-    int kept = 0;
     for (int base = ls; base < le; base += kCPer * kUpdThreads) {
       float4 cw[kCPer];
       unsigned rank[kCPer];
@@ -1339,6 +1342,9 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
       kept += s_cp[64];
     }
     __syncthreads();  // the copy is read by other threads of the workgroup below
+#if PPM_PHASE_TIMERS
+    if (S.diag == 2 && tid == 0) ctick += wall_clock64() - t_c0;
+#endif
     if (kept <= cap) {
       src = dst, ls = 0, le = kept;
       visits += (unsigned long long)kept;
@@ -1647,6 +1653,8 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     atomicAdd(&stats[31], gtick[1]);
 #endif
     for (int i = 0; i < 6; i++) atomicAdd(&stats[24 + i], ph[i]);
+    atomicAdd(&stats[32], ctick);
+    atomicMax(&stats[33], ctick);
     for (int i = 0; i < 6; i++) atomicMax(&stats[8 + i], ph[i]);
 #endif
     atomicMax(&stats[17], cands);  // most candidates in one tile

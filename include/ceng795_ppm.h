@@ -113,7 +113,7 @@ int ppm_collect_stats(ppm_scene* scene, ppm_stats* stats);
 /* ---- several GPUs ("PPM photons shard freely, but the hit-point flux state is
  * shared").  The reference's T threads share every hit point under a mutex
  * (PPM/src/Scene.cpp:131-168, PPM/include/Hit_point.h:22).  Here the update pass is split by
- * hit point instead: the grid's update tiles (hit points of one hash-cell range, <= 3 each)
+ * hit point instead: the grid's update tiles (hit points of one hash-cell range, <= 5 each)
  * are dealt round-robin over S shards, a shard applies the complete photon-order recurrence
  * of its own hit points, and the shards' results are merged by hit point.  Results are
  * bit-identical to the one-device scene for any S. */
