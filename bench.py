@@ -399,7 +399,11 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS) + ["c5"],
-                    help="c5: the photon-mapping Cornell box alone (tools/bench_ppm.py), 1 GPU")
+                    help="c5: the photon-mapping Cornell box alone (tools/bench_ppm.py); "
+                         "--gpus N: one multi-device scene over devices 0..N-1 of this process")
+    ap.add_argument("--devices", default="",
+                    help="c5: comma-separated device list of the multi-device scene (e.g. 0,0 "
+                         "rehearses two replicas on one GPU)")
     ap.add_argument("--traversal", default="fast", choices=["fast", "reference"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true",
@@ -428,11 +432,18 @@ def main() -> int:
                          "its gather) overlap the next frame; 1 = one frame at a time")
     args = ap.parse_args()
     if args.workload == "c5":
-        if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.gpus > 1:
-            log("c5 (photon mapping) is a one-GPU configuration (BASELINE.json configs[4])")
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            log("c5 over several GPUs runs as ONE process (a multi-device scene): "
+                "bench.py --workload c5 --gpus N, without a launcher")
             return 2
         import bench_ppm
-        print(json.dumps(bench_ppm.run(args.steps, args.warmup, not args.no_cpu_baseline)))
+        devices = None
+        if args.devices:
+            devices = [int(d) for d in args.devices.split(",")]
+        elif args.gpus > 1:
+            devices = list(range(args.gpus))
+        print(json.dumps(bench_ppm.run(args.steps, args.warmup,
+                                       not args.no_cpu_baseline and devices is None, devices)))
         return 0
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return relaunch(args.gpus)

@@ -100,12 +100,16 @@ def update_roofline(st, launches_per_step: int, ms_per_launch: float):
             "traffic_source": "profiles/traffic_c5.json" if traffic is not None else None}
 
 
-def run(steps: int, warmup: int, with_cpu: bool) -> dict:
+def run(steps: int, warmup: int, with_cpu: bool, devices=None) -> dict:
+    """devices: None = one GPU (device 0); a list = one multi-device scene over those GPUs of
+    this process (ppm_scene_load_xml_multi: every pass on each, the update pass sharded by hit
+    point, the state gathered on devices[0])."""
     import torch  # noqa: F401  (shares the HIP runtime; see ceng795_amd/_lib.py)
     from ceng795_amd import ppm
 
     xml = scene_path()
-    scene = ppm.PhotonScene(xml, device=0, seed=1)
+    scene = ppm.PhotonScene(xml, device=0, seed=1, devices=devices)
+    n_gpus = 1 if devices is None else len(devices)
     for k in range(warmup):
         img, st = scene.render(0, reference_threads=REFERENCE_THREADS)
     times, photon_ms, phases, upd_ms = [], [], [], []
@@ -122,9 +126,10 @@ def run(steps: int, warmup: int, with_cpu: bool) -> dict:
     avg = [sum(p[i] for p in phases) / len(phases) for i in range(4)]
     value = st.photons / (ph_ms / 1e3) / 1e6
     line = {
-        "metric": METRIC, "value": round(value, 2), "unit": "Mphotons/s", "n_gpus": 1,
+        "metric": METRIC, "value": round(value, 2), "unit": "Mphotons/s", "n_gpus": n_gpus,
         "steps": steps, "warmup": warmup, "ms_per_step": round(ms_step, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "higher_is_better": True, "scaling": "strong" if n_gpus > 1 else "weak",
+        "vs_baseline": None, "dtype": "f32",
         "data": "synthetic",
         "config": {"workload": "C5: PPM Cornell box (10 tris + mirror + glass sphere), 256x256, "
                                "10000 photons x 1000 iterations (BASELINE.json configs[4])",
@@ -135,6 +140,12 @@ def run(steps: int, warmup: int, with_cpu: bool) -> dict:
                                 "photon": round(avg[2], 3), "density": round(avg[3], 3)},
                    "frame_photons_per_s": round(st.photons / (ms_step / 1e3) / 1e6, 2)},
     }
+    if devices is not None:
+        line["config"]["devices"] = list(devices)
+        line["config"]["parallelism"] = (f"ppm_multi{n_gpus}: photon pass replicated, update pass "
+                                         "sharded by hit point, state gathered on devices[0]")
+        if len(set(devices)) < len(devices):
+            line["config"]["rehearsal"] = "a device is listed more than once: replicas share a GPU"
     launches = max(1, st.update_launches)  # one per photon batch (one at this size)
     line["roofline"] = update_roofline(st, launches, sum(upd_ms) / len(upd_ms) / launches)
     if with_cpu:
