@@ -396,8 +396,8 @@ def cpu_rehearsal(args) -> int:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS) + ["c5"],
                     help="c5: the photon-mapping Cornell box alone (tools/bench_ppm.py); "
                          "--gpus N: one multi-device scene over devices 0..N-1 of this process")
