@@ -230,9 +230,9 @@ int collapse_wide(std::vector<DevNode>& nodes, int nref, int root, int& stack) {
     return dx * dy + dy * dz + dz * dx;
   };
   struct Job {
-    int bnode, parent, slot;
+    int bnode, parent, slot, depth;
   };
-  std::vector<Job> todo{{root, -1, 0}};
+  std::vector<Job> todo{{root, -1, 0, 0}};
   int wroot = -1;
   std::vector<int> order;  // wide nodes in preorder
   while (!todo.empty()) {
@@ -259,6 +259,7 @@ int collapse_wide(std::vector<DevNode>& nodes, int nref, int root, int& stack) {
     nodes.resize(w + 2);
     DevNode4 W;
     std::memset(&W, 0, sizeof W);
+    if (j.depth < kWideTopLevels) W.flags |= kWideTop;
     for (int k = 0; k < 4; k++) {
       for (int a = 0; a < 3; a++) {  // (empty slots: an inverted box, never read)
         W.lo[a][k] = k < n ? sl[k].box[a] : 1.0f;
@@ -283,7 +284,7 @@ int collapse_wide(std::vector<DevNode>& nodes, int nref, int root, int& stack) {
     }
     order.push_back(w);
     for (int k = n - 1; k >= 0; k--)
-      if (!sl[k].guard) todo.push_back({sl[k].ref, w, k});
+      if (!sl[k].guard) todo.push_back({sl[k].ref, w, k, j.depth + 1});
   }
   // stack bound, bottom-up: a visit pushes at most (slots - 1) entries
   std::vector<int> need(nodes.size(), 0);

@@ -103,6 +103,9 @@ struct Replica {
   DevMaterial* d_mats = nullptr;
   DevLight* d_lights = nullptr;
   unsigned long long* d_counters = nullptr;
+  // per camera: the wide nodes relative to the camera origin (RenderParams::rel_nodes); the
+  // allocation holds the wide part only, d_rel[c] is that minus the first wide slot's index
+  std::vector<DevNode*> d_rel_alloc, d_rel;
   std::mutex mu;  // ctx pool and stream table
   std::vector<RenderCtx*> ctx_free, ctx_all;
   std::vector<std::unique_ptr<StreamScratch>> streams;
@@ -231,6 +234,9 @@ void free_replica(Replica& r) {
   (void)hipFree(r.d_mats);
   (void)hipFree(r.d_lights);
   (void)hipFree(r.d_counters);
+  for (DevNode* p : r.d_rel_alloc) (void)hipFree(p);
+  r.d_rel_alloc.clear();
+  r.d_rel.clear();
   if (cur != r.device) (void)hipSetDevice(cur);
 }
 
@@ -343,6 +349,30 @@ void upload_replica(const rt_scene* s, Replica& r) {
   r.d_lights = upload(h.lights, "upload lights");
   hip_check(hipMalloc(&r.d_counters, sizeof(unsigned long long) * kCounterAlloc), "alloc counters");
   hip_check(hipMemset(r.d_counters, 0, sizeof(unsigned long long) * kCounterAlloc), "zero counters");
+  // camera-relative wide nodes for the primary kernel: RN(b - e) per slot coordinate, the very
+  // operation the kernel's slab test would do first (IEEE fp32 on both sides, no contraction)
+  if (s->wide_only && h.accel_root >= 0 && h.root_kind == kRootNode) {
+    const size_t w0 = (size_t)(h.accel_root & ~kWideTag), n = h.nodes.size() - w0;
+    std::vector<DevNode> rel(h.nodes.begin() + (long)w0, h.nodes.end());
+    for (const rt_camera& c : h.cameras) {
+      for (size_t k = 0; k + 1 < n; k += 2) {
+        DevNode4 W;
+        std::memcpy(&W, &rel[k], sizeof W);
+        DevNode4 A;
+        std::memcpy(&A, &h.nodes[w0 + k], sizeof A);
+        for (int a = 0; a < 3; a++)
+          for (int q = 0; q < 4; q++) {
+            W.lo[a][q] = A.lo[a][q] - c.e[a];
+            W.hi[a][q] = A.hi[a][q] - c.e[a];
+          }
+        std::memcpy(&rel[k], &W, sizeof W);
+      }
+      DevNode* d = upload(rel, "upload camera-relative nodes");
+      r.d_rel_alloc.push_back(d);
+      r.d_rel.push_back(reinterpret_cast<DevNode*>(reinterpret_cast<uintptr_t>(d) -
+                                                   w0 * sizeof(DevNode)));
+    }
+  }
 }
 
 // Builds the culling tree once on the host, then uploads the scene to every device.  Several
@@ -426,6 +456,10 @@ RenderParams make_params(const rt_scene* s, const Replica& r, int cam, int row0,
   RenderParams P;
   std::memset(&P, 0, sizeof P);
   P.nodes = r.d_nodes;
+  static const bool no_rel = env_int("CENG795_RT_NOREL", 0) != 0;  // A/B switch
+  P.rel_nodes = s->mode != RT_TRAVERSAL_REFERENCE && cam < (int)r.d_rel.size() && !no_rel
+                    ? r.d_rel[cam]
+                    : nullptr;
   P.prims = r.d_prims;
   P.normals = r.d_normals;
   P.materials = r.d_mats;

@@ -28,7 +28,7 @@ enum : int {
   kCntPrimNodes = 4, kCntPrimNodeLanes = 5, kCntPrimLeaves = 6, kCntPrimLeafLanes = 7,
   kCntShadNodes = 8, kCntShadNodeLanes = 9, kCntShadLeaves = 10, kCntShadLeafLanes = 11,
   kCntExactBox = 12,
-  kCntUnused13 = 13,
+  kCntPrimTopWide = 13,  // RT_DIAG: primary visits of wide nodes in the top kWideTopLevels levels
   // RT_DIAG builds: the node visits above that were 4-wide culling nodes (128 B each)
   kCntPrimWide = 14, kCntShadWide = 15
 };
@@ -63,6 +63,10 @@ static_assert(sizeof(DevNode) == 64, "node must be one 64-byte scalar load");
 // (child = its tagged index) tested conservatively.
 constexpr int32_t kWideTag = 1 << 30;
 enum : int32_t { kWideGuard = 1, kWidePair = 16, kWideValid = 256 };
+// a wide node in the top kWideTopLevels levels of the tree (the RT_DIAG build counts the visits;
+// would those nodes pay for LDS residency?)
+constexpr int32_t kWideTop = 1 << 12;
+constexpr int kWideTopLevels = 3;
 struct alignas(16) DevNode4 {
   float lo[3][4];
   float hi[3][4];
@@ -154,6 +158,10 @@ inline unsigned long long sched_words_for(unsigned long long tiles) { return 10 
 
 struct RenderParams {
   const DevNode* nodes;
+  // the wide nodes again with every slot box relative to this camera's origin, RN(b - e) per
+  // coordinate (upload_replica), indexed like `nodes`; null when unavailable.  The primary
+  // kernel's wide visits read them: the slab test's b - o is then precomputed (same bits).
+  const DevNode* rel_nodes;
   const DevPrim* prims;
   const float* normals;  // float4 per leaf: nx ny nz material(bits)
   const DevMaterial* materials;

@@ -40,7 +40,7 @@ constexpr int kCounterSlots = kCounterRows;
 #define DIAG(stmt)
 #endif
 struct Diag {  // per-wave traversal work (RT_DIAG builds)
-  unsigned long long nodes = 0, node_lanes = 0, leaves = 0, leaf_lanes = 0, wide = 0;
+  unsigned long long nodes = 0, node_lanes = 0, leaves = 0, leaf_lanes = 0, wide = 0, top = 0;
 };
 
 // ------------------------------------------------------------------ vector helpers
@@ -128,11 +128,12 @@ __device__ unsigned long long g_exact_fallbacks;  // lanes that needed box_exact
 // accepts iff tmin <= tmax and tmax >= 0 (tmin, tmax finite here): the sign test is exact, and
 // the order test is decided here only outside a 2^-20 relative band; inside it the lane is
 // flagged for box_exact.  tnear (approximate entry distance) only orders.
-template <bool SKIP>
+// REL: b holds RN(box - o) already (RenderParams::rel_nodes, primary rays share o).
+template <bool SKIP, bool REL = false>
 __device__ __forceinline__ void slab_span(const float* b, const LaneRay& r, float& tn, float& tf) {
-  const float ax = (b[0] - r.o.x) * r.r.x, bx = (b[3] - r.o.x) * r.r.x;
-  const float ay = (b[1] - r.o.y) * r.r.y, by = (b[4] - r.o.y) * r.r.y;
-  const float az = (b[2] - r.o.z) * r.r.z, bz = (b[5] - r.o.z) * r.r.z;
+  const float ax = (REL ? b[0] : b[0] - r.o.x) * r.r.x, bx = (REL ? b[3] : b[3] - r.o.x) * r.r.x;
+  const float ay = (REL ? b[1] : b[1] - r.o.y) * r.r.y, by = (REL ? b[4] : b[4] - r.o.y) * r.r.y;
+  const float az = (REL ? b[2] : b[2] - r.o.z) * r.r.z, bz = (REL ? b[5] : b[5] - r.o.z) * r.r.z;
   float nx = __builtin_fminf(ax, bx), fx = __builtin_fmaxf(ax, bx);
   float ny = __builtin_fminf(ay, by), fy = __builtin_fmaxf(ay, by);
   float nz = __builtin_fminf(az, bz), fz = __builtin_fmaxf(az, bz);
@@ -520,7 +521,7 @@ __device__ __forceinline__ DevNode4 load_node4(const DevNode* __restrict__ nodes
 // `alive`: lanes still searching.  Up to 4 slots x 2 leaves x 64 lanes of leaf tests are
 // queued per visit, so the queue is run in between when it could overflow.  Returns false when
 // the walk is over.
-template <bool SKIP, bool SHADOW, bool DEEP, bool SPHERES>
+template <bool SKIP, bool SHADOW, bool DEEP, bool SPHERES, bool REL = false>
 __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode* __restrict__ nodes,
                                            const DevPrim* __restrict__ prims, WaveLeafLds& L,
                                            int& pending, const LaneRay& r, float thr, int& node,
@@ -531,7 +532,8 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
   const bool in = (m >> lane_id()) & 1;
 #endif
   const int fl = N.flags;
-  DIAG(dg.nodes++; dg.wide++; dg.node_lanes += __builtin_popcountll(m));
+  DIAG(dg.nodes++; dg.wide++; dg.node_lanes += __builtin_popcountll(m);
+       dg.top += (fl & kWideTop) != 0);
   int nxt = -1;
   uint64_t nm = 0;
   float nkey = 0.0f;
@@ -540,7 +542,7 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
     if (!(fl & (kWideValid << c))) continue;
     const float b[6] = {N.lo[0][c], N.lo[1][c], N.lo[2][c], N.hi[0][c], N.hi[1][c], N.hi[2][c]};
     float tn, tf;
-    slab_span<SKIP>(b, r, tn, tf);
+    slab_span<SKIP, REL>(b, r, tn, tf);
     const int ch = N.child[c];
     const bool guard = (fl & (kWideGuard << c)) != 0;
 #if RT_MASK_SLOTS
@@ -620,7 +622,7 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
 // The reference's (t, leaf) for every active ray: leaf < 0 = miss.  FAST: the culling tree
 // over reference treelets (WO: every node the fast walk meets is a 4-wide node); otherwise the
 // reference tree itself.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, bool WO>
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, bool WO, bool REL = false>
 __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode* __restrict__ nodes,
                                             const DevPrim* __restrict__ prims, int* spill,
                                             WaveLeafLds& L, const LaneRay& r, bool active,
@@ -662,8 +664,8 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
     }
     if constexpr (FAST) {
       if (WO || (node & kWideTag)) {
-        if (!visit_wide<SKIP, false, DEEP, SPHERES>(P, nodes, prims, L, pending, r, 0.0f, node, m,
-                                                    ~0ull, st, dg))
+        if (!visit_wide<SKIP, false, DEEP, SPHERES, REL>(P, nodes, prims, L, pending, r, 0.0f,
+                                                         node, m, ~0ull, st, dg))
           break;
         continue;
       }
@@ -848,7 +850,7 @@ __device__ __forceinline__ int hit_leaf(int2_t rec) { return rec.x; }
 
 // One wave = the 8x8 packet of selected tile `sel` (< num_sel_tiles): closest hit per pixel
 // into its 8-B record.
-template <bool FAST, bool DEEP, bool SPHERES, bool WO>
+template <bool FAST, bool DEEP, bool SPHERES, bool WO, bool REL = false>
 __device__ __forceinline__ void primary_packet(const RenderParams& P,
                                                const DevNode* __restrict__ nodes,
                                                const DevPrim* __restrict__ prims, int sel,
@@ -864,9 +866,9 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
   float t;
   int leaf;
   if (ballot(any_skip))
-    closest_hit<true, FAST, DEEP, SPHERES, WO>(P, nodes, prims, spill, L, ray, q.valid, t, leaf, dg);
+    closest_hit<true, FAST, DEEP, SPHERES, WO, REL>(P, nodes, prims, spill, L, ray, q.valid, t, leaf, dg);
   else
-    closest_hit<false, FAST, DEEP, SPHERES, WO>(P, nodes, prims, spill, L, ray, q.valid, t, leaf, dg);
+    closest_hit<false, FAST, DEEP, SPHERES, WO, REL>(P, nodes, prims, spill, L, ray, q.valid, t, leaf, dg);
   const RenderParams& Pw = fresh_params(P);  // post-traversal fields: not live across it
   int2_t rec;  // key layout: leaf low, t bits high (rt_internal.h)
   rec.x = q.valid ? leaf : -2;  // -1 miss, -2 outside the image
@@ -884,6 +886,7 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
     atomicAdd(&c[kCntPrimLeaves], dg.leaves);
     atomicAdd(&c[kCntPrimLeafLanes], dg.leaf_lanes);
     atomicAdd(&c[kCntPrimWide], dg.wide);
+    atomicAdd(&c[kCntPrimTopWide], dg.top);
 #endif
   }
 }
@@ -1538,7 +1541,8 @@ __device__ unsigned long long g_timeline[2][kTimelineWaves][3];
 #endif
 
 // Traversal kernels: one packet per wave, XCD-remapped blocks of 2-D tile blocks.
-template <bool FAST, bool DEEP, bool SPHERES, bool WO>
+// REL (FAST, WO): `nodes` is RenderParams::rel_nodes, the wide nodes relative to the camera.
+template <bool FAST, bool DEEP, bool SPHERES, bool WO, bool REL = false>
 __global__ __launch_bounds__(kTraceWaves * 64) RT_PRIMARY_OCCUPANCY void trace_primary_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
@@ -1552,7 +1556,7 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_PRIMARY_OCCUPANCY void trace_p
   TL_EST(sel >= 0 && Q.use_order ? Q.tile_cost[sel] : 0u);  // the probe's estimate
   if (sel >= 0) {
     const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
-    primary_packet<FAST, DEEP, SPHERES, WO>(Q, nodes, prims, sel, spill, L);
+    primary_packet<FAST, DEEP, SPHERES, WO, REL>(Q, nodes, prims, sel, spill, L);
     const RenderParams& Pw = fresh_params(P);
     if (Pw.tile_cost && lane_id() == 0)  // the shadow kernel's dispatch order
       Pw.tile_cost[sel] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - c0, 0xffffffffull);
@@ -1655,8 +1659,17 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
     T.use_order = 1;
   }
   if (!ordered) T.tile_cost = nullptr;
-  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, WO>), dim3(T.use_order ? oblocks : tblocks),
-                     dim3(kTraceWaves * 64), tlds, stream, T, nodes, prims);
+  bool rel = false;
+  if constexpr (FAST && WO) rel = T.rel_nodes != nullptr && T.accel_root >= 0 && T.root_kind == kRootNode;
+  if constexpr (FAST && WO) {
+    if (rel)
+      hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, WO, true>),
+                         dim3(T.use_order ? oblocks : tblocks), dim3(kTraceWaves * 64), tlds, stream,
+                         T, T.rel_nodes, prims);
+  }
+  if (!rel)
+    hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, WO>), dim3(T.use_order ? oblocks : tblocks),
+                       dim3(kTraceWaves * 64), tlds, stream, T, nodes, prims);
   mark(marks, 1, stream);
   S.tile_cost = T.tile_cost;
   if (P.num_lights > 0) {

@@ -52,7 +52,7 @@ def main():
         shad = (node_bytes(d["shad_node_visits"], d["shad_wide_visits"])
                 + 48 * d["shad_leaf_visits"] + (8 + 4 * words) * pixels) if s.num_lights else 0
         out = {"pixels": pixels, "packets": ((c.width + 7) // 8) * ((c.height + 7) // 8),
-               "counters": {k: v for k, v in d.items() if k != "shared_pieces"},
+               "counters": d,
                "primary_bytes": prim, "shadow_bytes": shad}
     print(json.dumps(out))
 
