@@ -400,7 +400,9 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS) + ["c5"],
                     help="c5: the photon-mapping Cornell box alone (tools/bench_ppm.py); "
-                         "--gpus N: one multi-device scene over devices 0..N-1 of this process")
+                         "--gpus N: one multi-device scene over devices 0..N-1 of this process; "
+                         "under a launcher (WORLD_SIZE > 1) or --gather-rehearsal: one process "
+                         "per GPU, update pass sharded, state gathered over RCCL")
     ap.add_argument("--devices", default="",
                     help="c5: comma-separated device list of the multi-device scene (e.g. 0,0 "
                          "rehearses two replicas on one GPU)")
@@ -431,11 +433,27 @@ def main() -> int:
                          "buffer sets, so one frame's sparsely occupied last waves (and, N>1, "
                          "its gather) overlap the next frame; 1 = one frame at a time")
     args = ap.parse_args()
+    if args.workload == "c5" and (int(os.environ.get("WORLD_SIZE", "1")) > 1
+                                  or args.gather_rehearsal):
+        # one process per GPU (launcher, or --gpus N relaunched below): the update pass
+        # sharded over the ranks, the hit-point state gathered to rank 0 (dist_ppm)
+        import torch
+        import torch.distributed as dist
+        import bench_ppm
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        device = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29577))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        line = bench_ppm.run_dist(args.steps, args.warmup, "cuda", not args.no_verify)
+        if line is not None:
+            print(json.dumps(line), flush=True)
+        dist.destroy_process_group()
+        return 0
     if args.workload == "c5":
-        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-            log("c5 over several GPUs runs as ONE process (a multi-device scene): "
-                "bench.py --workload c5 --gpus N, without a launcher")
-            return 2
         import bench_ppm
         devices = None
         if args.devices:

@@ -224,3 +224,39 @@ def test_whole_frames_per_rank_gather(tmp_path, world, n_cams):
     mp.spawn(_frame_worker, args=(world, _free_port(), str(tmp_path), n_cams), nprocs=world,
              join=True)
     assert open(os.path.join(tmp_path, "frames_ok")).read() == "1"
+
+
+def _ppm_merge_worker(rank, world, port, out_dir):
+    """gather_merged_state over gloo: rank r's state holds r+1 in the rows it owns and garbage
+    elsewhere; rank 0 must get every row from its owner."""
+    import numpy as np
+    import torch.distributed as dist
+    from ceng795_amd.dist_ppm import gather_merged_state
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 1001
+    owners = (np.arange(n) * 7 % world).astype(np.int32)
+    state = np.full((n, 5), -1.0, np.float32)
+    state[owners == rank] = rank + 1
+    got = gather_merged_state(state, owners)
+    if rank == 0:
+        assert got.shape == (n, 5)
+        assert np.array_equal(got[:, 0], owners + 1.0)
+        np.save(os.path.join(out_dir, "merged.npy"), got)
+    else:
+        assert got is None
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ppm_shard_state_gather(tmp_path, world):
+    mp.spawn(_ppm_merge_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    assert (tmp_path / "merged.npy").exists()
+
+
+def test_ppm_photon_budget_matches_reference_rule():
+    from ceng795_amd.dist_ppm import photons_and_normaliser
+    assert photons_and_normaliser(10000, 1000, 256, 8) == (10_000_000, 10000 * 1250 * 8)
+    assert photons_and_normaliser(10000, 1000, 256, 3) == (3333 * 1000 * 3, 10000 * 3333 * 3)
+    assert photons_and_normaliser(100, 10, 2, 8) == (1000, 100 * 12 * 8)  # height < T

@@ -155,6 +155,56 @@ def run(steps: int, warmup: int, with_cpu: bool, devices=None) -> dict:
     return line
 
 
+def run_dist(steps: int, warmup: int, device: str = "cuda", verify: bool = True) -> dict:
+    """C5 with one process per GPU (ceng795_amd.dist_ppm): every rank traces the whole photon
+    sequence and updates its shard of the hit points; rank 0 gathers the state (RCCL) and runs
+    the density estimation.  Timed: whole frames (eye pass, grid, photon pass, gather, density),
+    barrier + synchronize on both sides, max over ranks.  Rank 0 checks the last frame against
+    a one-GPU render of the same seed (gather_verified).  Returns the line on rank 0, else None."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from ceng795_amd import dist_ppm, ppm
+
+    rank, world = dist.get_rank(), dist.get_world_size()
+    xml = scene_path()
+    scene = ppm.PhotonScene(xml, device=torch.cuda.current_device(), seed=1)
+    for k in range(warmup):
+        dist_ppm.render_sharded(scene, 0, REFERENCE_THREADS, device)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    img = traced = None
+    for k in range(steps):
+        scene.set_seed(100 + k)
+        img, traced = dist_ppm.render_sharded(scene, 0, REFERENCE_THREADS, device)
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    ms_step = 1e3 * float(dt.item()) / steps
+    verified = None
+    if rank == 0 and verify:
+        scene.set_update_shard(0, 1)
+        want, _ = scene.render(0, reference_threads=REFERENCE_THREADS)
+        verified = bool(np.array_equal(np.asarray(img).view(np.uint32), want.view(np.uint32)))
+    scene.close()
+    if rank != 0:
+        return None
+    return {
+        "metric": METRIC + ", whole frames", "value": round(traced / (ms_step / 1e3) / 1e6, 2),
+        "unit": "Mphotons/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "C5: PPM Cornell box, 256x256, 10000 photons x 1000 iterations "
+                               "(BASELINE.json configs[4])",
+                   "photons_per_step": traced,
+                   "parallelism": f"ppm_shards{world}+{dist.get_backend()}_gather",
+                   "timed": "whole frame: eye pass, grid, photon pass (whole sequence on every "
+                            "rank, update pass sharded by hit point), state gather, density",
+                   "gather_verified": verified}}
+
+
 if __name__ == "__main__":
     import argparse
     ap = argparse.ArgumentParser()
