@@ -1,7 +1,8 @@
-// `ppm_render <scene.xml> [threads]` — the host driver of PPM/src/main.cpp:21-160 on top of the
-// photon-mapping C ABI: for every <Camera>, the eye pass, hash grid, photon pass and density
-// estimation (with the photon budget and normaliser the reference uses on `threads` host
+// `ppm_render [--gpus N] <scene.xml> [threads]` — the host driver of PPM/src/main.cpp:21-160 on
+// top of the photon-mapping C ABI: for every <Camera>, the eye pass, hash grid, photon pass and
+// density estimation (with the photon budget and normaliser the reference uses on `threads` host
 // threads, default 8), then the default tone curve and <ImageName> (extension replaced by .png).
+// --gpus N: one multi-device scene over GPUs 0..N-1 (update pass sharded by hit point).
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -10,13 +11,22 @@
 #include "../../include/ceng795_ppm.h"
 
 int main(int argc, char** argv) {
-  if (argc < 2) {
+  int gpus = 0, arg = 1;
+  if (argc > 2 && std::string(argv[1]) == "--gpus") {
+    gpus = std::atoi(argv[2]);
+    arg = 3;
+  }
+  if (argc <= arg) {
     std::fprintf(stderr, "Please provide scene file as argument\n");
     return 1;
   }
-  const int threads = argc > 2 ? std::atoi(argv[2]) : 8;
+  const int threads = argc > arg + 1 ? std::atoi(argv[arg + 1]) : 8;
   ppm_scene* scene = nullptr;
-  if (ppm_scene_load_xml(argv[1], 0, &scene) != RT_OK) {
+  std::vector<int> devices;
+  for (int d = 0; d < gpus; d++) devices.push_back(d);
+  const int rc = gpus > 0 ? ppm_scene_load_xml_multi(argv[arg], gpus, devices.data(), &scene)
+                          : ppm_scene_load_xml(argv[arg], 0, &scene);
+  if (rc != RT_OK) {
     std::fprintf(stderr, "%s\n", ppm_last_error());
     return 1;
   }

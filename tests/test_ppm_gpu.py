@@ -238,3 +238,29 @@ def test_update_shards_merge_to_oracle(ppm, scene_dir, shards):
     finally:
         for g in gs:
             g.close()
+
+
+def test_ppm_cli_single_and_multi_device_write_the_same_png(scene_dir, tmp_path):
+    """ceng795_amd/bin/ppm_render (the PPM/src/main.cpp driver on the C ABI): the PNG of a
+    one-device run and of `--gpus 1` (the multi-device scene with one device) are byte-identical."""
+    import os
+    import shutil
+    import subprocess
+    import xml.etree.ElementTree as ET
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "ceng795_amd", "bin", "ppm_render")
+    assert os.path.exists(cli), "build the product first (make -C ceng795_amd/csrc)"
+    xml = scenes.write_ppm("ppm_box", scene_dir)
+    name = ET.parse(xml).getroot().find(".//Camera/ImageName").text.strip()
+    png = os.path.splitext(name)[0] + ".png"
+    outs = []
+    for k, extra in enumerate([[], ["--gpus", "1"]]):
+        d = tmp_path / f"run{k}"
+        d.mkdir()
+        r = subprocess.run([cli, *extra, xml, "8"], cwd=d, capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert "Tracing photon rays is completed" in r.stdout
+        outs.append((d / png).read_bytes())
+    assert outs[0] == outs[1]
+    shutil.rmtree(tmp_path, ignore_errors=True)
