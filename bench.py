@@ -252,8 +252,8 @@ def roofline_line(xml, world, local_share, kt, launches, prof, kt_iso=None, n_is
             "kernel_timing": "one frame at a time after the timed region" if kt_iso is not None
                              and n_iso else "timed region",
             "algorithmic_bytes_per_launch": int(per_launch),
-            "bytes_model": "128 B x 4-wide node visits + 64 B x binary node visits + 48 B x leaf "
-                           "visits + 8 B hit record per pixel (tools/kernel_work.py, RT_DIAG "
+            "bytes_model": "128 B x 8-wide node visits + 64 B x leaf visits (DevLeaf: primitive "
+                           "+ guard box) + 8 B hit record per pixel (tools/kernel_work.py, RT_DIAG "
                            "build, same frame)",
             "work_per_frame": {"node_visits": c["prim_node_visits"],
                                "wide_node_visits": c.get("prim_wide_visits"),
@@ -329,6 +329,47 @@ def timed_steps(renderer, steps: int, world: int, coll_dev: str, events=None):
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     return float(el.item())
+
+
+def one_frame_ms(scene, stream, frames: int):
+    """Wall time per frame of camera 0 rendered ONE frame at a time (one stream, nothing else
+    in flight): the single-frame latency beside the pipelined `value`."""
+    import torch
+    from ceng795_amd import dist_tiles
+    R = dist_tiles.FrameRenderer(scene, stream, inflight=1)
+    for _ in range(3):
+        R.step()
+    R.finish()
+    ms = timed_steps(R, frames, 1, "cuda") / frames * 1e3
+    scene.collect_stats()
+    return round(ms, 4)
+
+
+def share_probe(scene, stream, steps: int, inflight: int, t1_ms: float, ns=(2, 4, 8)):
+    """Prediction of strong scaling on one GPU (no N-GPU node needed): for each N, every rank
+    r's share of the N-way tile deal (tile_begin r, tile_step N, tile-major, frames in flight
+    as in the N > 1 path) is rendered alone on this GPU and timed; the N-GPU step can be no
+    shorter than the slowest share, so t1 / (N * max_r t_share) bounds the efficiency from
+    above.  Excludes the gather to rank 0 and its untile (rehearsed by --gather-rehearsal)."""
+    from ceng795_amd import dist_tiles
+    out = {}
+    for n in ns:
+        per = []
+        for r in range(n):
+            R = dist_tiles.ShareRenderer(scene, n, r, stream, inflight=inflight)
+            for _ in range(3):
+                R.step()
+            R.finish()
+            per.append(timed_steps(R, steps, 1, "cuda") / steps * 1e3)
+            scene.collect_stats()
+        slow = max(per)
+        out[str(n)] = {"share_ms_max": round(slow, 4), "share_ms_min": round(min(per), 4),
+                       "predicted_efficiency": round(t1_ms / (n * slow), 4),
+                       "predicted_Mrays_s_factor": round(t1_ms / slow, 3)}
+    return {"t1_ms": round(t1_ms, 4), "frames_in_flight": inflight, "per_n": out,
+            "note": "PREDICTION from one GPU: each rank's tile share of one frame rendered alone "
+                    "(same frames in flight), t1 / (N * slowest share); the gather to rank 0 "
+                    "and its untile are not included"}
 
 
 def synthetic_frame(w: int, h: int, seed: int = 795):
@@ -425,6 +466,8 @@ def main() -> int:
     ap.add_argument("--no-weak", action="store_true",
                     help="N>1: skip the extra weak-scaling measurement (one frame per rank)")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-share-probe", action="store_true",
+                    help="N=1: skip the one-GPU prediction of strong scaling (share probe)")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="no GPU: the N>1 tile deal / gather / untile with synthetic tiles over "
                          "gloo (tests of the launcher and the exchange)")
@@ -613,6 +656,16 @@ def main() -> int:
                                            "make those fetches)")
             except Exception as e:  # the checker must never hide the measurement
                 log(f"roofline accounting failed: {e!r}")
+        single = None
+        probe = None
+        if world == 1 and not use_pg:
+            try:
+                single = one_frame_ms(scene, stream, max(10, args.steps // 2))
+                if not args.no_share_probe:
+                    probe = share_probe(scene, stream, max(10, args.steps // 2), args.inflight,
+                                        elapsed / args.steps * 1e3)
+            except Exception as e:
+                log(f"one-frame / share probe failed: {e!r}")
         host_rate = None
         if world == 1:
             try:
@@ -644,6 +697,11 @@ def main() -> int:
                        "render_ms_avg": round(sum(render_ms) / len(render_ms), 4)},
             "roofline": roof, "cpu_baseline": cpu, "pcie_inclusive": host_rate,
         }
+        if single is not None:
+            line["one_frame_ms"] = single
+            line["one_frame_Mrays_s"] = round(rays_step / n_cams / (single * 1e-3) / 1e6, 2)
+        if probe is not None:
+            line["predicted_strong_scaling"] = probe
         if strong and t1_ms is not None:
             line["strong_scaling"] = {"t1_ms": round(t1_ms, 4), "tN_ms": round(ms_step, 4),
                                       "efficiency_t1_over_N_tN": round(t1_ms / (world * ms_step), 4)}

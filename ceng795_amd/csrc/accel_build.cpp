@@ -3,24 +3,24 @@
 // The reference BVH (midpoint split cycling x -> y -> z, HW2/Bounding_volume_hierarchy.cpp:
 // 3-29) decides WHICH leaves a ray may test: a leaf is reachable iff every ancestor box
 // accepts the ray (BVH.cpp:31-55).  Its shape, though, makes a ray test ~146 boxes on C3.
-// Here the reference tree is cut into treelets (maximal subtrees with <= K leaves; a lone leaf
-// child of a larger node is a treelet of its own) and a binned-SAH tree is built over the
-// treelets.  The kernels walk the SAH tree to find treelets, then walk each treelet with the
-// reference's own semantics.  Reachability is preserved by a per-treelet guard:
-//   * the guard box is the innermost reference ancestor box a ray must pass to enter the
-//     treelet (the treelet root's own box, or for a lone leaf its parent's box);
-//   * the fast slab test decides "accept" only with a 2^-20 relative margin, and an accept
-//     with that margin implies every enclosing reference box accepts too (the boxes are
-//     unions, so the exact t-intervals nest; each computed bound is within 2^-22 of its exact
-//     value) — no need to test the ancestors;
-//   * inside the margin band the kernel walks the ancestor chain with the literal reference
-//     test (ref_parent / ref_box below).
-// SAH inner boxes are only culling bounds: they contain every guard box below them, and the
-// kernel tests them conservatively (only a sure reject culls), so a treelet the reference would
-// enter is never culled.  The SAH tree's nodes are appended to HostScene::nodes after the
-// reference nodes; DevNode::pad marks them (kAccelNode | guard bits per child).
+// Here the reference tree is cut into treelets — a lone leaf, or (K = 2) the two leaf children
+// of one reference node, a leaf PAIR — and an 8-wide SAH tree is built over them:
+//   * every leaf has a GUARD box, the box of the reference node holding it; the kernels take
+//     the exact decision per ray on that box in the leaf batch (accept with a 2^-20 relative
+//     margin implies every enclosing reference box accepts too, since the boxes are unions
+//     and each computed bound is within 2^-22 of its exact value; inside the band they walk
+//     the ancestry with the literal reference test);
+//   * the 8-wide nodes only FIND treelets: each slot holds a conservative fp16 box relative to
+//     the node's origin (DevNode8), containing every guard box below it with a per-axis
+//     margin (HostScene::cull_margin) that covers the rounding of the kernels' slab test, so
+//     a plain slab test never culls a treelet the reference would enter.
+// The wide nodes are appended to HostScene::nodes after the reference nodes; the leaves of
+// the culling tree are DevLeaf records in HostScene::leaves (each wide node's leaves
+// contiguous), the reference's leaf order and tie-break are untouched.
 #include <algorithm>
+#include <array>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -31,13 +31,6 @@
 
 namespace rt {
 namespace {
-
-struct Item {
-  int ref;        // treelet root: reference node index, or ~leaf
-  float box[6];   // guard box
-  float c[3];     // centroid (SAH binning)
-  int height;     // internal-node levels of the treelet (stack use inside it)
-};
 
 struct Box {
   float lo[3] = {std::numeric_limits<float>::infinity(), std::numeric_limits<float>::infinity(),
@@ -63,16 +56,22 @@ struct Box {
   }
 };
 
-// outward by a few ulps: a culling bound only, never compared with the reference's boxes
-float widen_down(float x) { return x - std::fabs(x) * 0x1p-20f - 0x1p-100f; }
-float widen_up(float x) { return x + std::fabs(x) * 0x1p-20f + 0x1p-100f; }
+struct Item {   // one treelet
+  int leaf;     // first DFS leaf
+  bool pair;    // with leaf + 1 (the two leaf children of one reference node)
+  float box[6]; // guard box (the holder's box)
+  float c[3];   // centroid (SAH binning)
+};
+
+// Binary SAH node: child >= 0 another node, < 0 ~item.
+struct BNode {
+  int child[2];
+  Box box[2];
+};
 
 struct SahBuilder {
   std::vector<Item>& items;
-  std::vector<DevNode>& nodes;
-  bool pairs = true;  // two-leaf treelets as leaf pairs (kAccelPair*)
-  int depth = 0;  // max over leaves of (SAH levels + treelet height)
-
+  std::vector<BNode> nodes;
   static constexpr int kBins = 32;
 
   // Splits items[b, e) (e - b >= 2); returns the split point.
@@ -134,181 +133,269 @@ struct SahBuilder {
     return (m == b || m == e) ? b + (e - b) / 2 : m;
   }
 
-  // Emits the SAH tree over items[b0, e0) (>= 2 items) in DFS preorder; returns its root.
+  // The SAH tree over items[b0, e0) (>= 2 items); returns its root.
   int build(int b0, int e0) {
     struct Task {
-      int b, e, parent, side, depth;
+      int b, e, parent, side;
     };
-    std::vector<Task> todo{{b0, e0, -1, 0, 0}};
+    std::vector<Task> todo{{b0, e0, -1, 0}};
     int root = -1;
     while (!todo.empty()) {
       const Task t = todo.back();
       todo.pop_back();
       const int idx = (int)nodes.size();
-      nodes.push_back(DevNode{});
+      nodes.push_back(BNode{});
       if (t.parent >= 0)
         nodes[t.parent].child[t.side] = idx;
       else
         root = idx;
-      DevNode& N = nodes[idx];
-      N.pad = kAccelNode;
       const int m = split(t.b, t.e);
       const int ranges[2][2] = {{t.b, m}, {m, t.e}};
       for (int side = 0; side < 2; side++) {
         const int b = ranges[side][0], e = ranges[side][1];
-        if (e - b == 1) {
-          const Item& it = items[b];
-          int ref = it.ref;
-          if (pairs && ref >= 0) {  // a reference node whose children are two consecutive leaves
-            const DevNode& R = nodes[ref];
-            if (R.pad == 0 && R.child[0] < 0 && R.child[1] < 0 && ~R.child[1] == ~R.child[0] + 1) {
-              ref = R.child[0];
-              N.pad |= side ? kAccelPair1 : kAccelPair0;
-            }
-          }
-          N.child[side] = ref;
-          N.pad |= side ? kAccelGuard1 : kAccelGuard0;
-          for (int a = 0; a < 3; a++) {
-            N.lo[a][side] = it.box[a];
-            N.hi[a][side] = it.box[a + 3];
-          }
-          depth = std::max(depth, t.depth + 1 + it.height);
-        } else {
-          Box u;
-          for (int i = b; i < e; i++) u.grow(items[i].box);
-          for (int a = 0; a < 3; a++) {
-            N.lo[a][side] = widen_down(u.lo[a]);
-            N.hi[a][side] = widen_up(u.hi[a]);
-          }
-        }
+        Box u;
+        for (int i = b; i < e; i++) u.grow(items[i].box);
+        nodes[idx].box[side] = u;
+        if (e - b == 1) nodes[idx].child[side] = ~b;
       }
-      // right pushed first: the left subtree is emitted first (preorder)
       for (int side = 1; side >= 0; side--)
         if (ranges[side][1] - ranges[side][0] >= 2)
-          todo.push_back({ranges[side][0], ranges[side][1], idx, side, t.depth + 1});
+          todo.push_back({ranges[side][0], ranges[side][1], idx, side});
     }
     return root;
   }
 };
 
-// Reference subtree height (internal-node levels): the stack a guarded treelet of more than
-// two leaves can need.
-int ref_height(const std::vector<DevNode>& nodes, int n) {
-  int h = 0;
-  for (int side = 0; side < 2; side++)
-    if (nodes[n].child[side] >= 0) h = std::max(h, ref_height(nodes, nodes[n].child[side]));
-  return h + 1;
+// fp16 bits of the largest half <= x (up = false) or the smallest half >= x (up = true), for
+// 0 <= x <= 32768; never a subnormal (a value below 2^-14 becomes 0 going down, 2^-14 going up).
+uint16_t half_dir(double x, bool up) {
+  if (!(x > 0.0)) return 0;
+  if (x < 0x1p-14) return up ? 0x0400 : 0;
+  int e;
+  std::frexp(x, &e);
+  int E = e - 1;  // x in [2^E, 2^(E + 1))
+  const double m = std::ldexp(x, 10 - E);  // in [1024, 2048)
+  double mi = up ? std::ceil(m) : std::floor(m);
+  if (mi >= 2048.0) {
+    mi = 1024.0;
+    E++;
+  }
+  return (uint16_t)(((E + 15) << 10) | ((int)mi - 1024));
 }
 
-// Collapses the binary culling tree (nodes[nref..], rooted at `root`) into 4-wide nodes that
-// replace it: each wide node takes a binary node's two slots and repeatedly opens the inner
-// slot with the largest box (surface area) into its two children, up to four slots.  Every
-// slot keeps its box, guard and pair flags, so the acceptance tests are the binary tree's.
-// Returns the tagged wide root; `stack` receives a bound on the traversal stack.
-int collapse_wide(std::vector<DevNode>& nodes, int nref, int root, int& stack) {
-  const std::vector<DevNode> bin(nodes.begin() + nref, nodes.end());
-  nodes.resize(nref);
-  struct Slot {
-    int ref;
-    bool guard, pair;
-    float box[6];
-  };
-  auto slot_of = [&](int bnode, int side) {
-    const DevNode& N = bin[bnode - nref];
-    Slot sl;
-    sl.ref = N.child[side];
-    sl.guard = (N.pad & (side ? kAccelGuard1 : kAccelGuard0)) != 0;
-    sl.pair = (N.pad & (side ? kAccelPair1 : kAccelPair0)) != 0;
+double half_value(uint16_t h) {
+  const int E = (h >> 10) & 31, M = h & 1023;
+  if (E == 0) return std::ldexp((double)M, -24);
+  return std::ldexp(1.0 + M / 1024.0, E - 15);
+}
+
+constexpr uint16_t kHalfNaN = 0x7e00;
+
+// Largest float <= x.
+float float_down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+  return f;
+}
+
+struct Slot {
+  int ref;  // BNode index (inner) or ~item (treelet)
+  Box box;  // exact union of the guard boxes below (a treelet's guard box)
+};
+
+// Writes one wide node's header and slot boxes: origin = the inflated union's lower corner
+// (rounded down to fp32), per-axis power-of-two scale with the largest offset <= 32768, each
+// plane rounded outward to fp16 after the margin is applied.
+void encode_node(DevNode8& W, const Slot* sl, int n, const double* margin) {
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int k = 0; k < n; k++)
     for (int a = 0; a < 3; a++) {
-      sl.box[a] = N.lo[a][side];
-      sl.box[a + 3] = N.hi[a][side];
+      lo[a] = std::min(lo[a], (double)sl[k].box.lo[a] - margin[a]);
+      hi[a] = std::max(hi[a], (double)sl[k].box.hi[a] + margin[a]);
     }
-    return sl;
-  };
-  auto area = [](const float* b) {
-    const double dx = (double)b[3] - b[0], dy = (double)b[4] - b[1], dz = (double)b[5] - b[2];
-    return dx * dy + dy * dz + dz * dx;
-  };
+  W.scale = 0;
+  int ka[3];
+  for (int a = 0; a < 3; a++) {
+    W.origin[a] = float_down(lo[a]);
+    const double ext = hi[a] - (double)W.origin[a];
+    int k = (int)std::ceil(std::log2(std::max(ext, 1e-300) / 32768.0));
+    k = std::min(std::max(k, -120), 120);
+    while (std::ldexp(ext, -k) > 32768.0) k++;  // (log2 rounding)
+    ka[a] = k;
+    W.scale |= (uint32_t)(k + 128) << (8 * a);
+  }
+  for (int c = 0; c < kWideSlots; c++)
+    for (int a = 0; a < 3; a++) {
+      if (c >= n) {
+        W.box[c][a] = (uint32_t)kHalfNaN | ((uint32_t)kHalfNaN << 16);
+        continue;
+      }
+      const double o = (double)W.origin[a];
+      const uint16_t l = half_dir(std::ldexp((double)sl[c].box.lo[a] - margin[a] - o, -ka[a]), false);
+      const uint16_t h = half_dir(std::ldexp((double)sl[c].box.hi[a] + margin[a] - o, -ka[a]), true);
+      W.box[c][a] = (uint32_t)l | ((uint32_t)h << 16);
+    }
+}
+
+// The decoded box of slot c (for the invariant check).
+void decode_slot(const DevNode8& W, int c, double* lo, double* hi) {
+  for (int a = 0; a < 3; a++) {
+    const int k = (int)((W.scale >> (8 * a)) & 255) - 128;
+    lo[a] = (double)W.origin[a] + std::ldexp(half_value((uint16_t)(W.box[c][a] & 0xffff)), k);
+    hi[a] = (double)W.origin[a] + std::ldexp(half_value((uint16_t)(W.box[c][a] >> 16)), k);
+  }
+}
+
+// SAH cost model of the wide collapse: visiting a wide node costs kNodeCost (one scalar fetch
+// and eight slot tests per packet, whatever its fill), a treelet's leaf tests kLeafCost per
+// leaf (they run in full-wave batches), each weighted by the surface area of the box that
+// leads there (the chance a ray reaches it).
+constexpr double kNodeCost = 1.0, kLeafCost = 0.3;
+
+// Optimal 8-wide collapse of the binary SAH tree (dynamic programme over (binary node, slots)):
+// F[n][k] = least cost of covering n's subtree with k slots (a slot is a treelet, or an inner
+// binary node that becomes a wide node of its own), T[n] = cost of n as a wide node.
+struct WideCollapse {
+  const SahBuilder& B;
+  std::vector<std::array<double, kWideSlots + 1>> F;
+  std::vector<std::array<signed char, kWideSlots + 1>> split;  // k of the left side
+  std::vector<double> T;
+  std::vector<signed char> tk;  // slots of n as a wide node
+
+  explicit WideCollapse(const SahBuilder& b, int root) : B(b) {
+    const size_t n = B.nodes.size();
+    F.assign(n, {});
+    split.assign(n, {});
+    T.assign(n, 0.0);
+    tk.assign(n, 2);
+    // children after parents in B.nodes (preorder emission): a reverse sweep is post-order
+    (void)root;
+    for (size_t i = n; i-- > 0;) solve((int)i);
+  }
+  // cost of one side of binary node n as k slots
+  double side(int n, int s, int k) const {
+    const int c = B.nodes[n].child[s];
+    if (c < 0) {
+      if (k != 1) return INFINITY;
+      return B.nodes[n].box[s].area() * kLeafCost * (B.items[~c].pair ? 2 : 1);
+    }
+    if (k == 1) return B.nodes[n].box[s].area() * kNodeCost + T[c];
+    return F[c][k];
+  }
+  void solve(int n) {
+    // F[n][k]: n's two sides covered by k slots together (k >= 2)
+    for (int k = 0; k <= kWideSlots; k++) F[n][k] = INFINITY;
+    for (int k = 2; k <= kWideSlots; k++)
+      for (int k1 = 1; k1 < k; k1++) {
+        const double c = side(n, 0, k1) + side(n, 1, k - k1);
+        if (c < F[n][k]) {
+          F[n][k] = c;
+          split[n][k] = (signed char)k1;
+        }
+      }
+    T[n] = INFINITY;
+    for (int k = 2; k <= kWideSlots; k++)
+      if (F[n][k] < T[n]) {
+        T[n] = F[n][k];
+        tk[n] = (signed char)k;
+      }
+  }
+  // the slots of binary node n's side s covered by k slots
+  void emit_side(int n, int s, int k, std::vector<Slot>& out) const {
+    const int c = B.nodes[n].child[s];
+    if (k == 1 || c < 0) {
+      out.push_back(Slot{c, B.nodes[n].box[s]});
+      return;
+    }
+    emit(c, k, out);
+  }
+  void emit(int n, int k, std::vector<Slot>& out) const {
+    const int k1 = split[n][k];
+    emit_side(n, 0, k1, out);
+    emit_side(n, 1, k - k1, out);
+  }
+};
+
+// Collapses the binary SAH tree into 8-wide nodes appended to s.nodes (WideCollapse), with
+// every node's inner children allocated contiguously and its treelets' leaves appended to
+// s.leaves in slot order.  Returns the tagged root; s.accel_depth receives the
+// traversal-stack bound.
+int collapse_wide(HostScene& s, const SahBuilder& B, int broot, const std::vector<int>& holder,
+                  const std::vector<float>& ref_box) {
+  const std::vector<Item>& items = B.items;
+  const WideCollapse W8(B, broot);
   struct Job {
-    int bnode, parent, slot, depth;
+    int bnode, wide;
   };
-  std::vector<Job> todo{{root, -1, 0, 0}};
-  int wroot = -1;
-  std::vector<int> order;  // wide nodes in preorder
+  const int w0 = (int)s.nodes.size();
+  s.nodes.resize(w0 + 2);
+  std::vector<Job> todo{{broot, w0}};
+  std::vector<int> order;           // wide nodes as processed (parents before children)
+  std::vector<std::vector<int>> kids;  // per processed node: its inner children (wide indices)
+  std::vector<Slot> slots;
   while (!todo.empty()) {
     const Job j = todo.back();
     todo.pop_back();
-    Slot sl[4];
-    int n = 2;
-    sl[0] = slot_of(j.bnode, 0);
-    sl[1] = slot_of(j.bnode, 1);
-    while (n < 4) {
-      int best = -1;
-      double ba = -1.0;
-      for (int k = 0; k < n; k++)
-        if (!sl[k].guard && area(sl[k].box) > ba) {
-          ba = area(sl[k].box);
-          best = k;
-        }
-      if (best < 0) break;
-      const int bn = sl[best].ref;
-      sl[best] = slot_of(bn, 0);
-      sl[n++] = slot_of(bn, 1);
-    }
-    const int w = (int)nodes.size();
-    nodes.resize(w + 2);
-    DevNode4 W;
+    slots.clear();
+    W8.emit(j.bnode, W8.tk[j.bnode], slots);
+    const int n = (int)slots.size();
+    const Slot* sl = slots.data();
+    DevNode8 W;
     std::memset(&W, 0, sizeof W);
-    if (j.depth < kWideTopLevels) W.flags |= kWideTop;
-    for (int k = 0; k < 4; k++) {
-      for (int a = 0; a < 3; a++) {  // (empty slots: an inverted box, never read)
-        W.lo[a][k] = k < n ? sl[k].box[a] : 1.0f;
-        W.hi[a][k] = k < n ? sl[k].box[a + 3] : -1.0f;
+    encode_node(W, sl, n, s.cull_margin);
+    int inner = 0;
+    for (int k = 0; k < n; k++) inner += sl[k].ref >= 0;
+    W.inner_base = inner ? (int)s.nodes.size() : 0;
+    s.nodes.resize(s.nodes.size() + 2 * (size_t)inner);
+    W.leaf_base = (int)s.leaves.size();
+    std::vector<int> mine;
+    int off = 0, r = 0;
+    for (int k = 0; k < n; k++) {
+      W.kinds |= kSlotValid << k;
+      if (sl[k].ref >= 0) {
+        mine.push_back(W.inner_base + 2 * r++);
+        continue;
       }
-      if (k >= n) continue;
-      W.flags |= kWideValid << k;
-      if (sl[k].guard) {
-        W.child[k] = sl[k].ref;
-        W.flags |= kWideGuard << k;
-        if (sl[k].pair) W.flags |= kWidePair << k;
+      const Item& it = items[~sl[k].ref];
+      W.kinds |= kSlotLeafy << k;
+      if (it.pair) W.kinds |= kSlotPair << k;
+      W.offs |= (uint32_t)off << (4 * k);  // <= 14: at most 7 pairs before the last slot
+      for (int q = 0; q < (it.pair ? 2 : 1); q++) {
+        const int l = it.leaf + q;
+        const DevPrim& p = s.prims[l];
+        DevLeaf L;
+        std::memcpy(L.v0, p.v0, sizeof L.v0);
+        std::memcpy(L.a1, p.a1, sizeof L.a1);
+        std::memcpy(L.a2, p.a2, sizeof L.a2);
+        L.dfs = l | (p.kind == kPrimSphere ? kLeafSphere : 0);
+        const float* g = &ref_box[(size_t)holder[l] * 6];
+        L.g0 = g[0], L.g1 = g[1], L.g2 = g[2], L.g3 = g[3], L.g4 = g[4], L.g5 = g[5];
+        s.leaves.push_back(L);
+        off++;
       }
     }
-    std::memcpy(&nodes[w], &W, sizeof W);
-    if (j.parent >= 0) {
-      DevNode4 P;
-      std::memcpy(&P, &nodes[j.parent], sizeof P);
-      P.child[j.slot] = w | kWideTag;
-      std::memcpy(&nodes[j.parent], &P, sizeof P);
-    } else {
-      wroot = w;
-    }
-    order.push_back(w);
-    for (int k = n - 1; k >= 0; k--)
-      if (!sl[k].guard) todo.push_back({sl[k].ref, w, k, j.depth + 1});
+    std::memcpy(&s.nodes[j.wide], &W, sizeof W);
+    order.push_back(j.wide);
+    kids.push_back(mine);
+    r = 0;
+    std::vector<Job> next;
+    for (int k = 0; k < n; k++)
+      if (sl[k].ref >= 0) next.push_back({sl[k].ref, mine[r++]});
+    for (auto it = next.rbegin(); it != next.rend(); ++it) todo.push_back(*it);
   }
-  // stack bound, bottom-up: a visit pushes at most (slots - 1) entries
-  std::vector<int> need(nodes.size(), 0);
-  for (auto it = order.rbegin(); it != order.rend(); ++it) {
-    DevNode4 W;
-    std::memcpy(&W, &nodes[*it], sizeof W);
-    int slots = 0, deepest = 0;
-    for (int k = 0; k < 4; k++) {
-      if (!(W.flags & (kWideValid << k))) continue;
-      slots++;
-      const int c = W.child[k];
-      if (!(W.flags & (kWideGuard << k)))
-        deepest = std::max(deepest, need[c & ~kWideTag]);
-      else if (c >= 0)
-        deepest = std::max(deepest, ref_height(nodes, c));
-    }
-    need[*it] = slots - 1 + deepest;
+  // stack bound, children before parents: a visit keeps one entered inner slot and pushes the
+  // others, then the deepest requirement below
+  std::vector<int> need(s.nodes.size(), 0);
+  for (size_t i = order.size(); i-- > 0;) {
+    int deepest = 0;
+    for (int c : kids[i]) deepest = std::max(deepest, need[c]);
+    need[order[i]] = kids[i].empty() ? 0 : (int)kids[i].size() - 1 + deepest;
   }
-  stack = need[wroot] + 1;
-  return wroot | kWideTag;
+  s.accel_depth = need[w0] + 1;
+  return w0 | kWideTag;
 }
 
 }  // namespace
-
 
 void build_accel(HostScene& s, int K) {
   if (s.accel_root >= 0) s.nodes.resize(s.accel_root & ~kWideTag);  // drop an earlier culling tree
@@ -316,10 +403,12 @@ void build_accel(HostScene& s, int K) {
   s.accel_depth = 0;
   s.accel_items = 0;
   s.ancestry.clear();
+  s.leaves.clear();
+  K = std::min(K, 2);
   if (K <= 0 || s.root_kind != kRootNode) return;
   const int nn = (int)s.nodes.size();
-  std::vector<int> leaves(nn, 0), height(nn, 1);
-  std::vector<int> parent(nn, -1), leaf_parent(s.prims.size(), -1);
+  std::vector<int> leaves(nn, 0);
+  std::vector<int> parent(nn, -1), holder(s.prims.size(), -1);
   std::vector<float> ref_box((size_t)nn * 6, 0.0f);
   std::memcpy(&ref_box[0], s.root_box, sizeof s.root_box);
   for (int n = 0; n < nn; n++) {  // preorder: a parent precedes its children
@@ -334,102 +423,82 @@ void build_accel(HostScene& s, int K) {
           b[a + 3] = N.hi[a][side];
         }
       } else {
-        leaf_parent[~c] = n;
+        holder[~c] = n;
       }
     }
   }
-  for (int n = nn - 1; n >= 0; n--) {
-    const DevNode& N = s.nodes[n];
-    int h = 0;
+  for (int n = nn - 1; n >= 0; n--)
     for (int side = 0; side < 2; side++) {
-      const int c = N.child[side];
-      if (c >= 0) {
-        leaves[n] += leaves[c];
-        h = std::max(h, height[c]);
-      } else {
-        leaves[n] += 1;
-      }
+      const int c = s.nodes[n].child[side];
+      leaves[n] += c >= 0 ? leaves[c] : 1;
     }
-    height[n] = h + 1;
-  }
   if (leaves[0] <= K) return;  // the whole tree is one treelet: nothing to cull
-  s.ancestry.assign(std::max<size_t>(nn, leaf_parent.size()), DevAncestry{});
+  s.ancestry.assign(std::max<size_t>(nn, holder.size()), DevAncestry{});
   for (size_t i = 0; i < s.ancestry.size(); i++) {
     DevAncestry& A = s.ancestry[i];
     if (i < (size_t)nn) {
       std::memcpy(A.box, &ref_box[i * 6], sizeof A.box);
       A.parent = parent[i];
     }
-    A.leaf_parent = i < leaf_parent.size() ? leaf_parent[i] : -1;
+    A.leaf_parent = i < holder.size() ? holder[i] : -1;
+  }
+  // culling margin: 2^-18 of the largest scene coordinate magnitude per axis
+  // (the kernels add the ray origin's share per ray)
+  for (int a = 0; a < 3; a++) {
+    const double m = std::max(std::fabs((double)s.root_box[a]), std::fabs((double)s.root_box[a + 3]));
+    s.cull_margin[a] = std::ldexp(m, -18) + 0x1p-100;
   }
   std::vector<Item> items;
-  std::vector<int> todo{0};
-  auto push_item = [&](int ref, const float* box, int h) {
+  auto push_item = [&](int leaf, bool pair, int hold) {
     Item it;
-    it.ref = ref;
-    std::memcpy(it.box, box, sizeof it.box);
-    for (int a = 0; a < 3; a++) it.c[a] = 0.5f * (box[a] + box[a + 3]);
-    it.height = h;
+    it.leaf = leaf;
+    it.pair = pair;
+    std::memcpy(it.box, &ref_box[(size_t)hold * 6], sizeof it.box);
+    for (int a = 0; a < 3; a++) it.c[a] = 0.5f * (it.box[a] + it.box[a + 3]);
     items.push_back(it);
   };
+  std::vector<int> todo{0};
   while (!todo.empty()) {
     const int n = todo.back();
     todo.pop_back();
     const DevNode& N = s.nodes[n];
+    if (K == 2 && N.child[0] < 0 && N.child[1] < 0) {  // both children leaves: a pair
+      if (~N.child[1] != ~N.child[0] + 1) throw std::logic_error("leaf children not consecutive");
+      push_item(~N.child[0], true, n);
+      continue;
+    }
     for (int side = 0; side < 2; side++) {
       const int c = N.child[side];
       if (c < 0)
-        push_item(c, &ref_box[(size_t)n * 6], 0);  // lone leaf: guarded by the parent's box
-      else if (leaves[c] <= K)
-        push_item(c, &ref_box[(size_t)c * 6], height[c]);
+        push_item(~c, false, n);  // lone leaf: guarded by its holder's box
       else
         todo.push_back(c);
     }
   }
-  // The node array is appended to; nothing else refers to the indices past the reference's.
-  SahBuilder B{items, s.nodes};
-  const char* pe = std::getenv("CENG795_RT_PAIRS");  // =0: visit two-leaf treelets (A/B)
-  B.pairs = !(pe && pe[0] == '0');
-  const int root = B.build(0, (int)items.size());
+  SahBuilder B{items, {}};
+  const int broot = B.build(0, (int)items.size());
   Box u;
   for (const Item& it : items) u.grow(it.box);
-  for (int a = 0; a < 3; a++) {
-    s.accel_box[a] = widen_down(u.lo[a]);
-    s.accel_box[a + 3] = widen_up(u.hi[a]);
+  for (int a = 0; a < 3; a++) {  // root box: outward by a few ulps, tested with the band
+    s.accel_box[a] = u.lo[a] - std::fabs(u.lo[a]) * 0x1p-20f - 0x1p-100f;
+    s.accel_box[a + 3] = u.hi[a] + std::fabs(u.hi[a]) * 0x1p-20f + 0x1p-100f;
   }
-  s.accel_root = root;
-  s.accel_depth = B.depth + 1;
   s.accel_items = (int)items.size();
-  const char* we = std::getenv("CENG795_RT_WIDE");  // =0: keep the binary culling tree (A/B)
-  if (!(we && we[0] == '0')) {
-    int stack = 0;
-    s.accel_root = collapse_wide(s.nodes, nn, root, stack);
-    s.accel_depth = stack;
-  }
+  s.accel_root = collapse_wide(s, B, broot, holder, ref_box);
 }
-
-int accel_treelet_leaves() {
-  const char* e = std::getenv("CENG795_RT_TREELET");
-  if (e && *e) return std::atoi(e);
-  return kDefaultTreeletLeaves;
-}
-
-}  // namespace rt
-
-namespace rt {
 
 // Structural invariants of the culling tree the kernels' exactness argument relies on
 // (DESIGN.md §4.2).  Returns "" when they hold, else a description of the first violation.
 std::string check_accel(const HostScene& s, int K, long long stats[4]) {
   for (int i = 0; i < 4; i++) stats[i] = 0;
   if (s.accel_root < 0) return "";
+  K = std::min(K, 2);
   const int nref = s.accel_root & ~kWideTag;  // culling nodes follow the reference's
   const size_t nleaf = s.prims.size();
-  auto box_of = [&](int ref_node) { return s.ancestry[ref_node].box; };
   // ancestry: each reference node's box is its parent's child slot; leaves point at holders
   for (int n = 0; n < nref; n++) {
     const DevNode& N = s.nodes[n];
-    if (N.pad != 0) return "reference node " + std::to_string(n) + " is flagged as culling";
+    if (N.pad != 0) return "reference node " + std::to_string(n) + " is flagged";
     for (int side = 0; side < 2; side++) {
       const int c = N.child[side];
       if (c >= 0) {
@@ -444,144 +513,116 @@ std::string check_accel(const HostScene& s, int K, long long stats[4]) {
   }
   for (int a = 0; a < 6; a++)
     if (s.ancestry[0].box[a] != s.root_box[a]) return "root box differs from ancestry";
-  // the slots of a culling node, binary (DevNode, kAccelNode) or wide (DevNode4, tagged)
-  struct Slot {
-    int ref;
-    bool guard, pair;
-    float box[6];
-  };
-  auto slots_of = [&](int node, std::vector<Slot>& out, std::string& err) {
-    out.clear();
-    const int idx = node & ~kWideTag;
-    if (idx < nref || (size_t)idx >= s.nodes.size()) {
-      err = "culling child is not a culling node";
-      return;
-    }
-    if (node & kWideTag) {
-      if ((size_t)idx + 1 >= s.nodes.size()) {
-        err = "wide node past the end";
-        return;
-      }
-      DevNode4 W;
-      std::memcpy(&W, &s.nodes[idx], sizeof W);
-      for (int k = 0; k < 4; k++) {
-        if (!(W.flags & (kWideValid << k))) continue;
-        Slot sl{W.child[k], (W.flags & (kWideGuard << k)) != 0, (W.flags & (kWidePair << k)) != 0, {}};
-        for (int a = 0; a < 3; a++) {
-          sl.box[a] = W.lo[a][k];
-          sl.box[a + 3] = W.hi[a][k];
-        }
-        if (!sl.guard && !(sl.ref & kWideTag)) err = "inner slot of a wide node is not wide";
-        out.push_back(sl);
-      }
-      if (out.size() < 2) err = "wide node with fewer than two slots";
-    } else {
-      const DevNode& N = s.nodes[idx];
-      if (!(N.pad & kAccelNode)) {
-        err = "culling child is not a culling node";
-        return;
-      }
-      for (int side = 0; side < 2; side++) {
-        Slot sl{N.child[side], (N.pad & (side ? kAccelGuard1 : kAccelGuard0)) != 0,
-                (N.pad & (side ? kAccelPair1 : kAccelPair0)) != 0, {}};
-        for (int a = 0; a < 3; a++) {
-          sl.box[a] = N.lo[a][side];
-          sl.box[a + 3] = N.hi[a][side];
-        }
-        out.push_back(sl);
-      }
-    }
-  };
+  if (s.leaves.size() != nleaf) return "culling leaves do not cover the leaves once";
   std::vector<int> seen(nleaf, 0);
-  long long lone = 0, items = 0;
+  long long lone = 0, items = 0, nodes = 0;
+  const double* mg = s.cull_margin;
+  // returns the union of the guard boxes below `node` (tagged) through lo/hi, or an error
   struct Frame {
     int node, depth;
   };
   std::vector<Frame> todo{{s.accel_root, 1}};
-  // leaves of a reference subtree, and the union of guard boxes under a culling node
-  auto ref_leaves = [&](int root, std::vector<int>& out) {
-    std::vector<int> st{root};
-    while (!st.empty()) {
-      const int n = st.back();
-      st.pop_back();
-      for (int side = 0; side < 2; side++) {
-        const int c = s.nodes[n].child[side];
-        if (c >= 0) st.push_back(c); else out.push_back(~c);
-      }
-    }
-  };
-  std::vector<float> lo(s.nodes.size() * 3), hi(s.nodes.size() * 3);
-  std::vector<int> order;  // culling nodes in preorder, for the bottom-up union pass
-  std::vector<Slot> sl;
-  std::string err;
+  std::vector<int> order;
+  std::vector<double> ulo(s.nodes.size() * 3, INFINITY), uhi(s.nodes.size() * 3, -INFINITY);
   while (!todo.empty()) {
     const Frame f = todo.back();
     todo.pop_back();
-    slots_of(f.node, sl, err);
-    if (!err.empty()) return err;
-    order.push_back(f.node);
+    if (!(f.node & kWideTag)) return "culling child is not a wide node";
+    const int idx = f.node & ~kWideTag;
+    if (idx < nref || (size_t)idx + 1 >= s.nodes.size()) return "wide node index out of range";
+    DevNode8 W;
+    std::memcpy(&W, &s.nodes[idx], sizeof W);
+    nodes++;
+    order.push_back(idx);
     stats[2] = std::max<long long>(stats[2], f.depth);
-    for (const Slot& x : sl) {
-      const int c = x.ref;
-      if (!x.guard) {
-        if (x.pair) return "pair flag on an inner slot";
-        todo.push_back({c, f.depth + 1});
+    int valid = 0, r = 0;
+    for (int c = 0; c < kWideSlots; c++) {
+      if (!(W.kinds & (kSlotValid << c))) {
+        if (W.box[c][0] != (0x7e00u | 0x7e000000u)) return "invalid slot without NaN planes";
         continue;
       }
-      items++;
-      const float* g = c >= 0 ? box_of(c) : box_of(s.ancestry[~c].leaf_parent);
-      for (int a = 0; a < 6; a++)
-        if (x.box[a] != g[a]) return "guard box differs from the reference box it stands for";
-      std::vector<int> lv;
-      if (c >= 0) {
-        if (x.pair) return "leaf pair stored as a node";
-        if (c >= nref) return "guarded child is not a reference node";
-        ref_leaves(c, lv);
-        if ((int)lv.size() > K) return "treelet larger than K";
-      } else if (x.pair) {  // the two leaf children, in DFS order, of the guard's reference node
-        if ((size_t)~c + 1 >= nleaf) return "leaf pair past the last leaf";
-        const int holder = s.ancestry[~c].leaf_parent;
-        if (holder < 0 || s.ancestry[~c + 1].leaf_parent != holder ||
-            s.nodes[holder].child[0] != c || s.nodes[holder].child[1] != ~(~c + 1))
-          return "leaf pair " + std::to_string(~c) + " is not one node's two leaves";
-        lv.push_back(~c);
-        lv.push_back(~c + 1);
-      } else {
-        lv.push_back(~c);
-        lone++;
+      valid++;
+      double lo[3], hi[3];
+      decode_slot(W, c, lo, hi);
+      if (!(W.kinds & (kSlotLeafy << c))) {
+        if (W.kinds & (kSlotPair << c)) return "pair flag on an inner slot";
+        const int child = W.inner_base + 2 * r++;
+        todo.push_back({child | kWideTag, f.depth + 1});
+        continue;  // containment checked bottom-up below
       }
-      for (int l : lv)
+      items++;
+      const bool pair = (W.kinds & (kSlotPair << c)) != 0;
+      const int first = W.leaf_base + (int)((W.offs >> (4 * c)) & 15);
+      if (first < 0 || (size_t)first + (pair ? 2 : 1) > s.leaves.size()) return "leaf range out of bounds";
+      if (!pair) lone++;
+      if (pair && K < 2) return "leaf pair with K = 1";
+      int hold = -1;
+      for (int q = 0; q < (pair ? 2 : 1); q++) {
+        const DevLeaf& L = s.leaves[first + q];
+        const int l = L.dfs & ~kLeafSphere;
+        if (l < 0 || (size_t)l >= nleaf) return "leaf index out of range";
         if (seen[l]++) return "leaf " + std::to_string(l) + " in two treelets";
+        const DevPrim& p = s.prims[l];
+        if ((p.kind == kPrimSphere) != ((L.dfs & kLeafSphere) != 0) ||
+            std::memcmp(L.v0, p.v0, 12) || std::memcmp(L.a1, p.a1, 12) || std::memcmp(L.a2, p.a2, 12))
+          return "leaf record differs from its primitive";
+        const int h = s.ancestry[l].leaf_parent;
+        const float g[6] = {L.g0, L.g1, L.g2, L.g3, L.g4, L.g5};
+        if (std::memcmp(g, s.ancestry[h].box, sizeof g)) return "guard box is not the holder's box";
+        if (q == 0) hold = h;
+        if (q == 1 && (h != hold || l != (s.leaves[first].dfs & ~kLeafSphere) + 1 ||
+                       s.nodes[h].child[0] != ~(l - 1) || s.nodes[h].child[1] != ~l))
+          return "leaf pair " + std::to_string(l - 1) + " is not one node's two leaves";
+        if (q == 0 && pair && s.nodes[h].child[0] != ~l) return "leaf pair does not start its holder";
+        for (int a = 0; a < 3; a++)  // the slot box holds the guard box with the margin
+          if (!(lo[a] <= (double)g[a] - mg[a] && hi[a] >= (double)g[a + 3] + mg[a]))
+            return "slot box does not hold its guard box with the margin";
+      }
     }
+    if (valid < 2) return "wide node with fewer than two slots";
   }
   for (size_t l = 0; l < nleaf; l++)
     if (!seen[l]) return "leaf " + std::to_string(l) + " in no treelet";
-  // containment: every inner slot box contains every guard box below it
+  // containment, bottom-up: every inner slot box holds every guard box below it, with the margin
   for (auto it = order.rbegin(); it != order.rend(); ++it) {
-    slots_of(*it, sl, err);
-    float ulo[3] = {INFINITY, INFINITY, INFINITY}, uhi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (const Slot& x : sl) {
-      const size_t ci = (size_t)(x.ref & ~kWideTag) * 3;
+    DevNode8 W;
+    std::memcpy(&W, &s.nodes[*it], sizeof W);
+    double nlo[3] = {INFINITY, INFINITY, INFINITY}, nhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    int r = 0;
+    for (int c = 0; c < kWideSlots; c++) {
+      if (!(W.kinds & (kSlotValid << c))) continue;
+      double lo[3], hi[3];
+      decode_slot(W, c, lo, hi);
+      double glo[3], ghi[3];
+      if (W.kinds & (kSlotLeafy << c)) {
+        const DevLeaf& L = s.leaves[W.leaf_base + ((W.offs >> (4 * c)) & 15)];
+        const float g[6] = {L.g0, L.g1, L.g2, L.g3, L.g4, L.g5};
+        for (int a = 0; a < 3; a++) glo[a] = g[a], ghi[a] = g[a + 3];
+      } else {
+        const size_t ci = (size_t)(W.inner_base + 2 * r++) * 3;
+        for (int a = 0; a < 3; a++) {
+          glo[a] = ulo[ci + a];
+          ghi[a] = uhi[ci + a];
+          if (!(lo[a] <= glo[a] - mg[a] && hi[a] >= ghi[a] + mg[a]))
+            return "culling box does not hold the guard boxes below it with the margin";
+        }
+      }
       for (int a = 0; a < 3; a++) {
-        const float l = x.guard ? x.box[a] : lo[ci + a], h = x.guard ? x.box[a + 3] : hi[ci + a];
-        if (!x.guard && (x.box[a] > l || x.box[a + 3] < h))
-          return "culling box does not contain the guard boxes below it";
-        ulo[a] = std::min(ulo[a], l);
-        uhi[a] = std::max(uhi[a], h);
+        nlo[a] = std::min(nlo[a], glo[a]);
+        nhi[a] = std::max(nhi[a], ghi[a]);
       }
     }
-    const size_t me = (size_t)(*it & ~kWideTag) * 3;
     for (int a = 0; a < 3; a++) {
-      lo[me + a] = ulo[a];
-      hi[me + a] = uhi[a];
+      ulo[(size_t)*it * 3 + a] = nlo[a];
+      uhi[(size_t)*it * 3 + a] = nhi[a];
     }
   }
   const size_t r0 = (size_t)nref * 3;
   for (int a = 0; a < 3; a++)
-    if (s.accel_box[a] > lo[r0 + a] || s.accel_box[a + 3] < hi[r0 + a])
+    if (s.accel_box[a] > ulo[r0 + a] || s.accel_box[a + 3] < uhi[r0 + a])
       return "culling root box does not contain the tree";
   stats[0] = items;
-  stats[1] = (long long)order.size();
+  stats[1] = nodes;
   stats[3] = lone;
   return "";
 }

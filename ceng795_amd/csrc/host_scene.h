@@ -38,20 +38,26 @@ struct HostScene {
   float root_box[6] = {0, 0, 0, 0, 0, 0};
   int depth = 0;  // internal-node levels
   // culling tree over reference treelets (accel_build.cpp), FAST traversal only
-  int accel_root = -1;   // index into nodes (SAH nodes follow the reference's), -1 = none
-  int accel_depth = 0;   // stack levels a traversal from accel_root can need
+  int accel_root = -1;   // tagged index into nodes (8-wide nodes follow the reference's), -1 = none
+  int accel_depth = 0;   // stack entries a traversal from accel_root can need
   int accel_items = 0;   // treelets
   float accel_box[6] = {0, 0, 0, 0, 0, 0};
+  // per-axis outward margin of every culling box: 2^-18 * the largest coordinate magnitude of
+  // the scene, its cameras and every ray origin; it lets the kernels cull on
+  // a plain slab test
+  double cull_margin[3] = {0, 0, 0};
+  std::vector<DevLeaf> leaves;        // culling-tree order (DevLeaf)
   std::vector<DevAncestry> ancestry;  // max(nodes, leaves) entries, see DevAncestry
   int quot_ok = 0;  // every triangle v0 coordinate passes quot_coord_ok (rt_internal.h)
 };
 
-// Cuts the reference tree into treelets of <= K leaves and appends a SAH tree over them
-// (K <= 0: none).  Leaves the reference nodes, leaves and tie-break order untouched.
+// Cuts the reference tree into treelets of <= K leaves (K = 1: lone leaves; 2: also leaf
+// pairs; K <= 0: no culling tree) and appends an 8-wide SAH tree over them.  Leaves the
+// reference nodes, leaves and tie-break order untouched.
 void build_accel(HostScene& s, int K);
-int accel_treelet_leaves();  // CENG795_RT_TREELET, else kDefaultTreeletLeaves
-// Invariants of the culling tree (coverage, guard boxes, containment, ancestry); "" if they
-// hold.  stats: treelets, culling nodes, culling depth, lone-leaf treelets.
+// Invariants of the culling tree (coverage, guard boxes, conservative containment with the
+// margin, child layout, ancestry); "" if they hold.  stats: treelets, culling nodes, culling
+// depth, lone-leaf treelets.
 std::string check_accel(const HostScene& s, int K, long long stats[4]);
 
 // Builds `out` from `desc`; throws std::invalid_argument on a bad description.

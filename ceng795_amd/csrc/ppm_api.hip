@@ -223,6 +223,9 @@ struct ppm_scene {
   DevBuf<float4> peer_state;  // gathered peer state, shards x n_hp
   DevBuf<unsigned> peer_nupd;
   bool merged = true;
+  // a single-device scene with shards > 1 (process per GPU) holds only its own tiles' results
+  // after ppm_trace_photons, until ppm_write_hit_state brings in the merged state
+  bool shard_partial = false;
 
   void drop_update_events() {  // (back to the pool)
     upd_spare.insert(upd_spare.end(), upd_events.begin(), upd_events.end());
@@ -385,6 +388,7 @@ void build_grid(ppm_scene* s, int width, int height) {
   if (s->eye_cam < 0) throw std::invalid_argument("build_hash_grid before the eye pass");
   const int n = s->n_hp;
   s->grid_ready = false;
+  s->shard_partial = false;  // the state is reset below
   // a failed earlier build may have left the device error flag set: every pass reads it
   hip_check(hipMemsetAsync(s->error.p, 0, sizeof(int), s->stream), "zero error flag");
   hip_check(launch_grid(s->hp.p, n, width, height, s->grid.p, s->state.p, s->nupd.p, s->stream),
@@ -688,6 +692,7 @@ void density(ppm_scene* s, long long total, float* out) {
 template <typename F>
 void each_replica(ppm_scene* s, F&& f) {
   if (s->peers.empty()) {
+    DeviceGuard g(s->device);  // the scene's buffers and stream live on its device
     f(s);
     return;
   }
@@ -875,6 +880,7 @@ int ppm_set_update_shard(ppm_scene* s, int shard, int shards) {
     return set_error(RT_E_INVALID, "ppm_set_update_shard: a multi-device scene shards its own update pass");
   s->shard = shard;
   s->shards = shards;
+  s->shard_partial = false;
   s->grid_ready = false;  // the tile table is the grid's: build_hash_grid again
   return RT_OK;
 }
@@ -906,7 +912,9 @@ int ppm_write_hit_state(ppm_scene* s, const float* in) {
     std::vector<unsigned> cnt(n);
     for (int k = 0; k < n; k++) {
       const float* r = in + 5 * (size_t)k;
-      if (!(r[4] >= 0.0f && r[4] < 4294967296.0f)) throw std::invalid_argument("bad update count");
+      // counts travel as float32 (the read_hit_state layout): exact up to 2^24
+      if (!(r[4] >= 0.0f && r[4] <= 16777216.0f && r[4] == (float)(unsigned)r[4]))
+        throw std::invalid_argument("bad update count (a whole number <= 2^24 expected)");
       st[k] = make_float4(r[0], r[1], r[2], r[3]);
       cnt[k] = (unsigned)r[4];
     }
@@ -919,6 +927,7 @@ int ppm_write_hit_state(ppm_scene* s, const float* in) {
       hip_check(hipStreamSynchronize(r->stream), "write state");
     });
     s->merged = true;
+    s->shard_partial = false;
     return RT_OK;
   });
 }
@@ -1074,6 +1083,7 @@ int ppm_trace_photons(ppm_scene* s, long long first, long long count) {
     check_scene(s);
     each_replica(s, [&](ppm_scene* r) { trace_photons(r, first, count); });
     if (!s->peers.empty()) s->merged = false;
+    if (s->peers.empty() && s->shards > 1) s->shard_partial = true;
     return RT_OK;
   });
 }
@@ -1082,6 +1092,11 @@ int ppm_density_estimation(ppm_scene* s, long long total, float* out) {
   return guarded([&] {
     check_scene(s);
     if (!out) throw std::invalid_argument("ppm_density_estimation: NULL output");
+    if (s->shard_partial)
+      throw std::invalid_argument("ppm_density_estimation: update shard " + std::to_string(s->shard) +
+                                  " of " + std::to_string(s->shards) +
+                                  " holds only its own hit points; write the merged state "
+                                  "(ppm_write_hit_state) first");
     merge_peers(s);
     DeviceGuard g(s->device);
     density(s, total, out);
@@ -1104,6 +1119,11 @@ int ppm_render(ppm_scene* s, int cam, int threads, float* out, ppm_stats* stats)
     if (threads < 1 || !out) throw std::invalid_argument("ppm_render: bad argument");
     if (cam < 0 || cam >= (int)s->host.cameras.size())
       throw std::invalid_argument("camera index out of range");
+    if (s->peers.empty() && s->shards > 1)
+      throw std::invalid_argument("ppm_render: the scene applies only update shard " +
+                                  std::to_string(s->shard) + " of " + std::to_string(s->shards) +
+                                  " (ppm_set_update_shard); reset it to 0 of 1 or render the "
+                                  "passes and merge the shards' states");
     DeviceGuard g(s->device);
     const PCamera& C = s->host.cameras[cam].cam;
     hipEvent_t ev[5];

@@ -23,8 +23,8 @@
 namespace rt {
 hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                          const float* normals, const DevMaterial* mats, const DevLight* lights,
-                         bool fast, bool deep, bool spheres, bool wide_only,
-                         const hipEvent_t* marks, hipStream_t stream);
+                         bool fast, bool deep, bool spheres, const hipEvent_t* marks,
+                         hipStream_t stream);
 int max_supported_depth();
 hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream);
 hipError_t launch_untile(const UntileParams& U, hipStream_t stream);
@@ -98,14 +98,12 @@ struct Replica {
   int device = 0;
   DevNode* d_nodes = nullptr;
   DevPrim* d_prims = nullptr;
+  DevLeaf* d_leaves = nullptr;
   float* d_normals = nullptr;
   DevAncestry* d_anc = nullptr;
   DevMaterial* d_mats = nullptr;
   DevLight* d_lights = nullptr;
   unsigned long long* d_counters = nullptr;
-  // per camera: the wide nodes relative to the camera origin (RenderParams::rel_nodes); the
-  // allocation holds the wide part only, d_rel[c] is that minus the first wide slot's index
-  std::vector<DevNode*> d_rel_alloc, d_rel;
   std::mutex mu;  // ctx pool and stream table
   std::vector<RenderCtx*> ctx_free, ctx_all;
   std::vector<std::unique_ptr<StreamScratch>> streams;
@@ -117,7 +115,6 @@ struct rt_scene {
   bool deep = false;
   bool needs_recursion = false;
   bool has_spheres = false;
-  bool wide_only = false;  // the fast walk meets 4-wide culling nodes only (launch_render)
   size_t most = 1;         // pixel records of the largest camera frame (whole tiles)
   unsigned long long msaa_seed = 0;
   std::vector<std::unique_ptr<Replica>> rep;  // rep[0]: the first (output) device
@@ -125,8 +122,8 @@ struct rt_scene {
   KernelTiming timing;
   // multi-device scenes: one RCCL communicator per device (single process, ncclCommInitAll);
   // multi_mu serialises the frames that use them.  copy_gather: the shares are gathered by
-  // peer copies instead (a device listed twice — the one-GPU rehearsal of the deal / gather /
-  // untile path — or CENG795_RT_GATHER=copy)
+  // peer copies instead (a device listed twice: the one-GPU rehearsal of the deal / gather /
+  // untile path)
   std::mutex multi_mu;
   std::vector<ncclComm_t> comms;
   bool multi = false;  // made by rt_scene_*_multi: frames go through render_multi (any count)
@@ -229,14 +226,12 @@ void free_replica(Replica& r) {
   r.streams.clear();
   (void)hipFree(r.d_nodes);
   (void)hipFree(r.d_prims);
+  (void)hipFree(r.d_leaves);
   (void)hipFree(r.d_normals);
   (void)hipFree(r.d_anc);
   (void)hipFree(r.d_mats);
   (void)hipFree(r.d_lights);
   (void)hipFree(r.d_counters);
-  for (DevNode* p : r.d_rel_alloc) (void)hipFree(p);
-  r.d_rel_alloc.clear();
-  r.d_rel.clear();
   if (cur != r.device) (void)hipSetDevice(cur);
 }
 
@@ -281,61 +276,25 @@ int occ_words(const HostScene& h) { return std::max(1, ((int)h.lights.size() + 3
 
 // A counter buffer: kCounterRows x kCounterWidth ray counters.
 constexpr size_t kCounterAlloc = (size_t)kCounterWidth * kCounterRows;
-// Dispatch order of the traversal kernels: CENG795_RT_ORDER=0 off, 1 heavy
-// first over the whole frame, 2 (default) heavy first within each XCD's part of the frame;
-// CENG795_RT_PROBE=1 also orders the primary kernel, by a probe pass's estimates (off by
-// default: measured no faster).  The order never changes a result, only which
-// tiles start first.
-int order_regions() {
-  static const int r = [] {
-    const char* e = std::getenv("CENG795_RT_ORDER");
-    if (e && e[0] == '0') return 0;
-    if (e && e[0] == '1') return 1;
-    return 8;
-  }();
-  return r;
-}
-bool probe_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("CENG795_RT_PROBE");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-int env_int(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e && *e ? std::atoi(e) : dflt;
-}
+// Dispatch order of the traversal kernels: heavy first within each XCD's
+// part of the frame (RT_ORDER_REGIONS regions, one per XCD; 0 = block order), each region one
+// contiguous band of the frame (RT_ORDER_CHUNKS chunks per region: its L2 then holds that
+// band's part of the tree — shadow kernel reads 91 vs 130 MB per C3 frame with interleaved
+// half-row chunks, profiles/r03/ab_order_chunks.jsonl).  The order never changes a result,
+// only which tiles start first.  (Macros: A/B builds, `make exp EXTRA=-D...`.)
+#ifndef RT_ORDER_REGIONS
+#define RT_ORDER_REGIONS 8
+#endif
+#ifndef RT_ORDER_CHUNKS
+#define RT_ORDER_CHUNKS 1
+#endif
 // sched: sched_words_for(num_sel_tiles) words — tile costs, then the unit order lists
 void set_schedule(RenderParams& P, unsigned* sched) {
-  const int regions = order_regions();
+  const int regions = RT_ORDER_REGIONS;
   P.tile_cost = regions ? sched : nullptr;
   P.unit_order = regions ? reinterpret_cast<int*>(sched) + P.num_sel_tiles : nullptr;
   P.order_regions = regions;
-  P.order_probe = probe_enabled() ? 1 : 0;
-  // chunks per region: 1 = each XCD walks one contiguous band of the frame (its L2 then holds
-  // that band's part of the tree: shadow kernel reads 91 vs 130 MB per C3 frame with
-  // interleaved half-row chunks, CENG795_RT_ORDER_CHUNKS=0; profiles/r03/ab_order_chunks.jsonl)
-  static const int chunks = env_int("CENG795_RT_ORDER_CHUNKS", 1);
-  P.order_chunk = chunks;
-  static const int depth = env_int("CENG795_RT_PROBE_DEPTH", 5);
-  static const int visits = env_int("CENG795_RT_PROBE_VISITS", 48);
-  P.probe_depth = depth;
-  P.probe_visits = visits;
-}
-
-// True when the culling tree is 4-wide and no slot leads to a binary node (every guarded slot
-// is a leaf or a leaf pair), so the fast walk never visits a binary node.
-bool wide_only_tree(const HostScene& h) {
-  if (h.accel_root < 0 || !(h.accel_root & kWideTag)) return false;
-  for (size_t n = (size_t)(h.accel_root & ~kWideTag); n + 1 < h.nodes.size(); n += 2) {
-    DevNode4 W;
-    std::memcpy(&W, &h.nodes[n], sizeof W);
-    for (int k = 0; k < 4; k++)
-      if ((W.flags & (kWideValid << k)) && (W.flags & (kWideGuard << k)) && W.child[k] >= 0)
-        return false;
-  }
-  return true;
+  P.order_chunk = RT_ORDER_CHUNKS;
 }
 
 void upload_replica(const rt_scene* s, Replica& r) {
@@ -343,54 +302,26 @@ void upload_replica(const rt_scene* s, Replica& r) {
   const HostScene& h = s->host;
   r.d_nodes = upload(h.nodes, "upload nodes");
   r.d_prims = upload(h.prims, "upload prims");
+  r.d_leaves = upload(h.leaves, "upload culling leaves");
   r.d_normals = upload(h.normals, "upload normals");
   r.d_anc = upload(h.ancestry, "upload ancestry");
   r.d_mats = upload(h.materials, "upload materials");
   r.d_lights = upload(h.lights, "upload lights");
   hip_check(hipMalloc(&r.d_counters, sizeof(unsigned long long) * kCounterAlloc), "alloc counters");
   hip_check(hipMemset(r.d_counters, 0, sizeof(unsigned long long) * kCounterAlloc), "zero counters");
-  // camera-relative wide nodes for the primary kernel: RN(b - e) per slot coordinate, the very
-  // operation the kernel's slab test would do first (IEEE fp32 on both sides, no contraction)
-  if (s->wide_only && h.accel_root >= 0 && h.root_kind == kRootNode) {
-    const size_t w0 = (size_t)(h.accel_root & ~kWideTag), n = h.nodes.size() - w0;
-    std::vector<DevNode> rel(h.nodes.begin() + (long)w0, h.nodes.end());
-    for (const rt_camera& c : h.cameras) {
-      for (size_t k = 0; k + 1 < n; k += 2) {
-        DevNode4 W;
-        std::memcpy(&W, &rel[k], sizeof W);
-        DevNode4 A;
-        std::memcpy(&A, &h.nodes[w0 + k], sizeof A);
-        for (int a = 0; a < 3; a++)
-          for (int q = 0; q < 4; q++) {
-            W.lo[a][q] = A.lo[a][q] - c.e[a];
-            W.hi[a][q] = A.hi[a][q] - c.e[a];
-          }
-        std::memcpy(&rel[k], &W, sizeof W);
-      }
-      DevNode* d = upload(rel, "upload camera-relative nodes");
-      r.d_rel_alloc.push_back(d);
-      r.d_rel.push_back(reinterpret_cast<DevNode*>(reinterpret_cast<uintptr_t>(d) -
-                                                   w0 * sizeof(DevNode)));
-    }
-  }
 }
 
 // Builds the culling tree once on the host, then uploads the scene to every device.  Several
 // devices: one RCCL communicator each, for the framebuffer gather (render_multi).
 int create_from_host(rt_scene* s, const std::vector<int>& devices, bool multi) {
-  build_accel(s->host, accel_treelet_leaves());
+  build_accel(s->host, kDefaultTreeletLeaves);
   if (s->host.accel_depth > max_supported_depth()) build_accel(s->host, 0);
-  if (std::getenv("CENG795_RT_VERBOSE"))
-    std::fprintf(stderr, "ceng795_rt: %zu nodes (reference depth %d), culling tree root %d over "
-                 "%d treelets, depth %d, %zu device(s)\n", s->host.nodes.size(), s->host.depth,
-                 s->host.accel_root, s->host.accel_items, s->host.accel_depth, devices.size());
   const HostScene& h = s->host;
   if (h.depth > max_supported_depth())
     throw std::invalid_argument("BVH deeper than " + std::to_string(max_supported_depth()) +
                                 " levels is not supported");
   s->deep = std::max(h.depth, h.accel_depth) > kLaneStack - 2;
   for (const DevPrim& p : h.prims) s->has_spheres |= p.kind == kPrimSphere;
-  s->wide_only = wide_only_tree(h);
   for (const DevMaterial& m : h.materials) {
     const bool mirror = m.mirror[0] != 0 || m.mirror[1] != 0 || m.mirror[2] != 0;
     const bool glass = m.transparency[0] != 0 || m.transparency[1] != 0 || m.transparency[2] != 0;
@@ -409,9 +340,7 @@ int create_from_host(rt_scene* s, const std::vector<int>& devices, bool multi) {
   if (multi) {
     std::vector<int> distinct = devices;
     std::sort(distinct.begin(), distinct.end());
-    const char* g = std::getenv("CENG795_RT_GATHER");
-    s->copy_gather = std::unique(distinct.begin(), distinct.end()) != distinct.end() ||
-                     (g && std::strcmp(g, "copy") == 0);
+    s->copy_gather = std::unique(distinct.begin(), distinct.end()) != distinct.end();
     if (!s->copy_gather) {
       s->comms.resize(devices.size());
       nccl_check(ncclCommInitAll(s->comms.data(), (int)devices.size(), devices.data()),
@@ -456,10 +385,7 @@ RenderParams make_params(const rt_scene* s, const Replica& r, int cam, int row0,
   RenderParams P;
   std::memset(&P, 0, sizeof P);
   P.nodes = r.d_nodes;
-  static const bool no_rel = env_int("CENG795_RT_NOREL", 0) != 0;  // A/B switch
-  P.rel_nodes = s->mode != RT_TRAVERSAL_REFERENCE && cam < (int)r.d_rel.size() && !no_rel
-                    ? r.d_rel[cam]
-                    : nullptr;
+  P.leaves = r.d_leaves;
   P.prims = r.d_prims;
   P.normals = r.d_normals;
   P.materials = r.d_mats;
@@ -583,8 +509,7 @@ void enqueue_samples(rt_scene* s, const Replica& r, const RenderParams& P, int s
     Q.tile_major = 0;
     Q.out = d_samples + (size_t)k * frame;
     hip_check(launch_render(Q, r.d_nodes, r.d_prims, r.d_normals, r.d_mats, r.d_lights, fast,
-                            s->deep, s->has_spheres, s->wide_only,
-                            timed ? timing_marks(s, Q) : nullptr, stream),
+                            s->deep, s->has_spheres, timed ? timing_marks(s, Q) : nullptr, stream),
               "render launch");
   }
 }
@@ -613,8 +538,7 @@ void enqueue_frame(rt_scene* s, const Replica& r, const RenderParams& P, int sam
   const bool fast = s->mode != RT_TRAVERSAL_REFERENCE;
   if (samples <= 1) {
     hip_check(launch_render(P, r.d_nodes, r.d_prims, r.d_normals, r.d_mats, r.d_lights, fast,
-                            s->deep, s->has_spheres, s->wide_only,
-                            timed ? timing_marks(s, P) : nullptr, stream),
+                            s->deep, s->has_spheres, timed ? timing_marks(s, P) : nullptr, stream),
               "render launch");
     return;
   }

@@ -28,53 +28,69 @@ enum : int {
   kCntPrimNodes = 4, kCntPrimNodeLanes = 5, kCntPrimLeaves = 6, kCntPrimLeafLanes = 7,
   kCntShadNodes = 8, kCntShadNodeLanes = 9, kCntShadLeaves = 10, kCntShadLeafLanes = 11,
   kCntExactBox = 12,
-  kCntPrimTopWide = 13,  // RT_DIAG: primary visits of wide nodes in the top kWideTopLevels levels
-  // RT_DIAG builds: the node visits above that were 4-wide culling nodes (128 B each)
+  kCntGuardTests = 13,  // RT_DIAG: leaf-batch guard tests (primary + shadow)
+  // RT_DIAG builds: the node visits above that were 8-wide culling nodes (128 B each)
   kCntPrimWide = 14, kCntShadWide = 15
 };
 
-// DevNode::pad of the culling-tree nodes (accel_build.cpp); reference nodes have pad == 0.
-// Guard bit set: that child is a treelet root (node index or ~leaf) behind a reachability
-// guard; clear: an inner culling node tested conservatively.
-// culling nodes (accel_build.cpp): pad = kAccelNode | guard bits | leaf-pair bits.  A guarded
-// child with its pair bit set is a treelet of two leaves, stored as ~first leaf (its second
-// leaf is the next one in DFS order): the kernels queue both leaf tests at once instead of
-// visiting the treelet's root, whose own box is the guard already tested.
-enum : int32_t { kAccelGuard0 = 1, kAccelGuard1 = 2, kAccelNode = 4, kAccelPair0 = 8, kAccelPair1 = 16 };
-constexpr int kDefaultTreeletLeaves = 2;
+constexpr int kDefaultTreeletLeaves = 2;  // culling-tree treelets: lone leaves and leaf pairs
 
 struct alignas(16) DevNode {
-  // Both CHILD boxes, interleaved per coordinate ([axis][child]) so one packed-fp32 op
-  // (v_pk_add_f32 / v_pk_mul_f32) works on both children.  Unused for a leaf child.
+  // Both CHILD boxes, interleaved per coordinate ([axis][child]).  Unused for a leaf child (a
+  // +-1e30 box every normalised ray accepts, scene_build.cpp).
   float lo[3][2];
   float hi[3][2];
   int32_t child[2];  // >= 0: internal node index; < 0: leaf index ~child
   int32_t axis;      // split dimension of THIS node (Bounding_volume_hierarchy.cpp:8)
-  int32_t pad;       // 0: reference node; else kAccelNode | guard bits | pair bits
+  int32_t pad;       // 0 (reference nodes; the culling tree has its own record, DevNode8)
 };
 static_assert(sizeof(DevNode) == 64, "node must be one 64-byte scalar load");
 
-// 4-wide culling node (accel_build.cpp, collapse of the binary SAH tree): two consecutive
-// DevNode slots of `nodes`, referred to as (index of the first slot) | kWideTag, so a stack
-// entry says which kind it holds before the fetch.  Slot c of a wide node is valid when
-// flags bit kWideValid << c is set; it is then either a guarded treelet (bit kWideGuard << c:
-// child = ~leaf, with kWidePair << c the leaf pair ~child, ~child + 1, or a reference node
-// for treelets of more than two leaves) tested with the guard rule, or an inner wide node
-// (child = its tagged index) tested conservatively.
+// 8-wide culling node (accel_build.cpp): two consecutive DevNode slots of
+// `nodes`, referred to as (index of the first slot) | kWideTag.  Slot c is valid when bit c of
+// `kinds` is set; it is then either LEAFY (bit 8 + c: one treelet = a lone leaf, or with bit
+// 16 + c a leaf pair; its leaves are DevLeaf records leaf_base + (offs >> 4c & 15) and the next
+// one) or INNER (a child node: inner_base + 2 * (number of inner slots before c)).  Every slot
+// carries a CONSERVATIVE box in fp16, relative to `origin` and scaled by 2^k per axis:
+//   plane = origin[a] + h * 2^(scale byte a - 128)
+// rounded outward and inflated by the scene's culling margin (HostScene::cull_margin), so a
+// plain slab test (no decision band) never culls a treelet the reference would enter; the
+// exact decision (the treelet's guard box) is taken per ray in the leaf batch.  An invalid
+// slot holds NaN planes, which every slab test rejects.
 constexpr int32_t kWideTag = 1 << 30;
-enum : int32_t { kWideGuard = 1, kWidePair = 16, kWideValid = 256 };
-// a wide node in the top kWideTopLevels levels of the tree (the RT_DIAG build counts the visits;
-// would those nodes pay for LDS residency?)
-constexpr int32_t kWideTop = 1 << 12;
-constexpr int kWideTopLevels = 3;
-struct alignas(16) DevNode4 {
-  float lo[3][4];
-  float hi[3][4];
-  int32_t child[4];
-  int32_t flags;  // kWideGuard << c | kWidePair << c | kWideValid << c
-  int32_t pad[3];
+constexpr int kWideSlots = 8;
+enum : int32_t { kSlotValid = 1, kSlotLeafy = 1 << 8, kSlotPair = 1 << 16 };
+struct alignas(16) DevNode8 {
+  float origin[3];
+  uint32_t scale;      // byte a: k_a + 128
+  int32_t inner_base;  // DevNode index of the first inner child (children contiguous, 2 slots each)
+  int32_t leaf_base;   // DevLeaf index of the first leafy slot's first leaf
+  int32_t kinds;       // kSlotValid << c | kSlotLeafy << c | kSlotPair << c
+  uint32_t offs;       // 4 bits per slot: its first leaf's offset from leaf_base (leafy slots)
+  uint32_t box[kWideSlots][3];  // per slot and axis: lo fp16 (bits 0-15), hi fp16 (16-31)
 };
-static_assert(sizeof(DevNode4) == 2 * sizeof(DevNode), "a wide node is two node slots");
+static_assert(sizeof(DevNode8) == 128, "a wide node is two s_load_dwordx16");
+static_assert(sizeof(DevNode8) == 2 * 64, "a wide node is two node slots");
+
+// A leaf as the fast traversal tests it, in culling-tree order (each wide node's leaves
+// contiguous): the primitive (as DevPrim), its DFS leaf index — the reference's tie-break key
+// and the index of every per-leaf array — and the GUARD box, the box of the reference node
+// holding the leaf.  A ray may test the leaf iff every reference ancestor box accepts it
+// (HW2/Bounding_volume_hierarchy.cpp:31-55); the guard accepting with margin implies that
+// (DESIGN.md §4.1), else the kernel walks the ancestry (guard_exact).
+//   q[0] = v0.xyz, dfs | kLeafSphere      q[1] = a1.xyz (sphere: radius, 0, 0), guard lo.x
+//   q[2] = a2.xyz, guard lo.y              q[3] = guard lo.z, hi.xyz
+constexpr int32_t kLeafSphere = 1 << 30;
+struct alignas(16) DevLeaf {
+  float v0[3];
+  int32_t dfs;  // | kLeafSphere for a sphere
+  float a1[3];
+  float g0;
+  float a2[3];
+  float g1;
+  float g2, g3, g4, g5;
+};
+static_assert(sizeof(DevLeaf) == 64, "leaf record is four 16-byte loads");
 
 enum PrimKind : int32_t { kPrimTriangle = 0, kPrimSphere = 1 };
 
@@ -158,10 +174,7 @@ inline unsigned long long sched_words_for(unsigned long long tiles) { return 10 
 
 struct RenderParams {
   const DevNode* nodes;
-  // the wide nodes again with every slot box relative to this camera's origin, RN(b - e) per
-  // coordinate (upload_replica), indexed like `nodes`; null when unavailable.  The primary
-  // kernel's wide visits read them: the slab test's b - o is then precomputed (same bits).
-  const DevNode* rel_nodes;
+  const DevLeaf* leaves;  // culling-tree order (DevLeaf), FAST traversal
   const DevPrim* prims;
   const float* normals;  // float4 per leaf: nx ny nz material(bits)
   const DevMaterial* materials;
@@ -202,8 +215,8 @@ struct RenderParams {
   unsigned* occ;  // num_sel_tiles * 64 * occ_words light-occlusion bits: trace_shadow -> shade
   int occ_words;  // ceil(num_lights / 32)
   // heavy-first dispatch (null: off).  tile_cost[sel] holds each selected
-  // tile's cost: the probe kernel's estimate before the primary kernel, the primary kernel's
-  // measured time (100 MHz ticks) before the shadow kernel.  order_kernel sorts the traversal
+  // tile's cost: the primary kernel's measured time (100 MHz ticks), read before the shadow
+  // kernel.  order_kernel sorts the traversal
   // workgroups' units (kTraceWaves packets each) heaviest first within each of order_regions
   // regions into unit_order[region * order_stride + i] (-1 pads); region r holds the chunks of
   // order_chunk consecutive units c with c mod order_regions == r, and block b of an ordered
@@ -213,8 +226,6 @@ struct RenderParams {
   unsigned* tile_cost;
   int* unit_order;
   int order_regions, order_chunk, order_stride, order_units;
-  int order_probe;  // estimate the primary kernel's tile costs with probe_kernel first
-  int probe_depth, probe_visits;  // probe_kernel: levels walked, visits per ray
   int use_order;
   float* frames;  // recursive scenes only: (max_depth+1) * 28 * lanes ray-tree frames, else null
   // kCounterRows rows of kCounterWidth u64 (columns: kCnt*)

@@ -40,7 +40,7 @@ constexpr int kCounterSlots = kCounterRows;
 #define DIAG(stmt)
 #endif
 struct Diag {  // per-wave traversal work (RT_DIAG builds)
-  unsigned long long nodes = 0, node_lanes = 0, leaves = 0, leaf_lanes = 0, wide = 0, top = 0;
+  unsigned long long nodes = 0, node_lanes = 0, leaves = 0, leaf_lanes = 0, wide = 0, guard = 0;
 };
 
 // ------------------------------------------------------------------ vector helpers
@@ -61,6 +61,7 @@ __device__ __forceinline__ V3 ld3(const float* p) { return {p[0], p[1], p[2]}; }
 struct LaneRay {
   V3 o, d;
   V3 r;       // v_rcp_f32 reciprocals (<= 1 ulp): the approximate slab test only
+  V3 m;       // 2^-18 |o| / d per axis: the ray's share of the culling margin (visit_wide)
   bool skip0, skip1, skip2;  // |d_i| < 1e-6: axis ignored (HW2/bounding_box.cpp:21)
   bool quot;  // origin and scene in the shared-reciprocal range (tri_quotients)
 };
@@ -75,6 +76,8 @@ __device__ __forceinline__ LaneRay make_ray(V3 o, V3 d, int scene_quot_ok) {
   r.o = o;
   r.d = d;
   r.r = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+  r.m = v3(0x1p-18f * __builtin_fabsf(o.x) * r.r.x, 0x1p-18f * __builtin_fabsf(o.y) * r.r.y,
+           0x1p-18f * __builtin_fabsf(o.z) * r.r.z);
   r.skip0 = __builtin_fabsf(d.x) < kEps;
   r.skip1 = __builtin_fabsf(d.y) < kEps;
   r.skip2 = __builtin_fabsf(d.z) < kEps;
@@ -87,10 +90,12 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 // Lane masks of one fp32 compare, straight from the v_cmp (ballot of a combined boolean makes
 // the compiler round-trip it through a VGPR: v_cndmask + v_cmp per mask).  LLVM FCmp
 // predicates; ordered, so NaN gives false as the C++ operators do.
-enum : int { kFcmpOGT = 2, kFcmpOGE = 3, kFcmpOLT = 4 };
+enum : int { kFcmpOGT = 2, kFcmpOGE = 3, kFcmpOLT = 4, kFcmpULT = 12 };
 __device__ __forceinline__ uint64_t lanes_gt(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, kFcmpOGT); }
 __device__ __forceinline__ uint64_t lanes_ge(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, kFcmpOGE); }
 __device__ __forceinline__ uint64_t lanes_lt(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, kFcmpOLT); }
+// !(a >= b): true for a NaN operand too
+__device__ __forceinline__ uint64_t lanes_nge(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, kFcmpULT); }
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // ------------------------------------------------------------------ slab test
@@ -128,12 +133,11 @@ __device__ unsigned long long g_exact_fallbacks;  // lanes that needed box_exact
 // accepts iff tmin <= tmax and tmax >= 0 (tmin, tmax finite here): the sign test is exact, and
 // the order test is decided here only outside a 2^-20 relative band; inside it the lane is
 // flagged for box_exact.  tnear (approximate entry distance) only orders.
-// REL: b holds RN(box - o) already (RenderParams::rel_nodes, primary rays share o).
-template <bool SKIP, bool REL = false>
+template <bool SKIP>
 __device__ __forceinline__ void slab_span(const float* b, const LaneRay& r, float& tn, float& tf) {
-  const float ax = (REL ? b[0] : b[0] - r.o.x) * r.r.x, bx = (REL ? b[3] : b[3] - r.o.x) * r.r.x;
-  const float ay = (REL ? b[1] : b[1] - r.o.y) * r.r.y, by = (REL ? b[4] : b[4] - r.o.y) * r.r.y;
-  const float az = (REL ? b[2] : b[2] - r.o.z) * r.r.z, bz = (REL ? b[5] : b[5] - r.o.z) * r.r.z;
+  const float ax = (b[0] - r.o.x) * r.r.x, bx = (b[3] - r.o.x) * r.r.x;
+  const float ay = (b[1] - r.o.y) * r.r.y, by = (b[4] - r.o.y) * r.r.y;
+  const float az = (b[2] - r.o.z) * r.r.z, bz = (b[5] - r.o.z) * r.r.z;
   float nx = __builtin_fminf(ax, bx), fx = __builtin_fmaxf(ax, bx);
   float ny = __builtin_fminf(ay, by), fy = __builtin_fmaxf(ay, by);
   float nz = __builtin_fminf(az, bz), fz = __builtin_fmaxf(az, bz);
@@ -320,8 +324,9 @@ __device__ __forceinline__ bool child_box_exact(const DevNode& N, int c, const L
   return box_exact(b, r);
 }
 
-// Treelet guard that the fast test could not decide: the reference's literal test on the
-// guard box and on every enclosing reference box (the ancestry of BVH.cpp:31-55).
+// A leaf's guard that the fast test could not decide: the reference's literal test on the
+// holder's box and on every enclosing reference box (the ancestry of BVH.cpp:31-55).
+// child: a reference node index, or ~leaf (its holder's box first).
 __device__ bool guard_exact(const RenderParams& P, int child, const LaneRay& r) {
   int v = child >= 0 ? child : P.anc[~child].leaf_parent;
   while (v >= 0) {
@@ -331,19 +336,13 @@ __device__ bool guard_exact(const RenderParams& P, int child, const LaneRay& r) 
   return true;
 }
 
-// One packet visit of a binary node of either tree, per child:
-//   * leaf of a reference node: every lane in the node tests it (leaves have no box; the slot
-//     holds a +-1e30 box that every normalised ray accepts, so no special case is needed);
-//   * inner child of a reference node: the reference's box test (fast, else box_exact);
-//   * guarded child of a culling node (treelet root or lone leaf): the reference's acceptance
-//     of its guard box, decided with margin — which implies every enclosing reference box
-//     accepts too (accel_build.cpp) — else guard_exact over the whole ancestry;
-//   * inner child of a culling node: the conservative cull test.
-// h0/h1: lanes that enter (inner) or test (leaf) each child.
+// One packet visit of a reference node (RT_TRAVERSAL_REFERENCE, or a scene without culling
+// tree), per child: a leaf child is tested by every lane in the node (leaves have no box; the
+// slot holds a +-1e30 box that every normalised ray accepts); an inner child's box takes the
+// reference's test (fast, else box_exact).  h0/h1: lanes that enter (inner) or test (leaf).
 template <bool SKIP>
-__device__ __forceinline__ void visit_node(const RenderParams& P, const DevNode& N,
-                                           const LaneRay& r, bool in, bool& h0, bool& h1,
-                                           float& t0, float& t1) {
+__device__ __forceinline__ void visit_node(const DevNode& N, const LaneRay& r, bool in, bool& h0,
+                                           bool& h1, float& t0, float& t1) {
   const float b0[6] = {N.lo[0][0], N.lo[1][0], N.lo[2][0], N.hi[0][0], N.hi[1][0], N.hi[2][0]};
   const float b1[6] = {N.lo[0][1], N.lo[1][1], N.lo[2][1], N.hi[0][1], N.hi[1][1], N.hi[2][1]};
   float f0, f1;
@@ -352,18 +351,13 @@ __device__ __forceinline__ void visit_node(const RenderParams& P, const DevNode&
   bool in0, out0, in1, out1;
   decide_sure(t0, f0, in0, out0);
   decide_sure(t1, f1, in1, out1);
-  const int pad = N.pad;  // wave-uniform
-  const bool an = (pad & kAccelNode) != 0;
-  const bool g0 = (pad & kAccelGuard0) != 0, g1 = (pad & kAccelGuard1) != 0;
-  // (a reference node's leaf slot holds a +-1e30 box, scene_build.cpp: every lane accepts it)
-  const bool cull0 = an & !g0, cull1 = an & !g1;
-  h0 = in & (in0 | (cull0 & !out0));
-  h1 = in & (in1 | (cull1 & !out1));
-  const bool u0 = in & !cull0 & !(in0 | out0);
-  const bool u1 = in & !cull1 & !(in1 | out1);
+  h0 = in & in0;
+  h1 = in & in1;
+  const bool u0 = in & !(in0 | out0);
+  const bool u1 = in & !(in1 | out1);
   if (ballot(u0 | u1)) {
-    if (u0) h0 = g0 ? guard_exact(P, N.child[0], r) : child_box_exact(N, 0, r);
-    if (u1) h1 = g1 ? guard_exact(P, N.child[1], r) : child_box_exact(N, 1, r);
+    if (u0) h0 = child_box_exact(N, 0, r);
+    if (u1) h1 = child_box_exact(N, 1, r);
     DIAG(if (u0 | u1) atomicAdd(&g_exact_fallbacks, 1ull));
   }
 }
@@ -407,20 +401,24 @@ __device__ __forceinline__ bool advance(WaveStack<DEEP>& st, int c0, int c1, uin
 // A packet reaches a leaf with only the few lanes whose rays pass over that triangle (C3:
 // ~14 of 64), so testing leaves one at a time runs the triangle test at ~20% SIMD efficiency.
 // The traversal instead queues (lane, leaf) pairs in a per-wave LDS list and runs them 64 at a
-// time, one pair per lane (the owner's ray fetched with ds_bpermute, the triangle with a
-// per-lane load), once kBatchFlush are pending and when the walk ends.  Results land per ray
-// by LDS atomics: closest hit = atomic min of the key (t bits << 32 | leaf), which for 0 < t
-// orders exactly like the reference's (t, DFS leaf) rule; shadow = a flag.  The queued tests
-// are the ones the reference makes, so the answer is unchanged.
+// time, one pair per lane (the owner's ray fetched with ds_bpermute, the leaf with a per-lane
+// load), once kBatchFlush are pending and when the walk ends.  Results land per ray by LDS
+// atomics: closest hit = atomic min of the key (t bits << 32 | DFS leaf), which for 0 < t
+// orders exactly like the reference's (t, DFS leaf) rule; shadow = a flag.
+// CULL (the culling tree): an entry is a DevLeaf, and its lane first takes the reference's
+// decision on the leaf's GUARD box — the fast slab test with the 2^-20 band, which on accept
+// implies every enclosing reference box accepts, else guard_exact over the
+// ancestry — so exactly the leaves the reference reaches are tested.  Without CULL (reference
+// walk) an entry is a DFS leaf whose boxes the walk has already decided.
 #ifndef RT_BATCH_FLUSH
 #define RT_BATCH_FLUSH 64
 #endif
 constexpr int kBatchFlush = RT_BATCH_FLUSH;   // run the queue once this many tests are pending
-constexpr int kBatchCap = kBatchFlush + 256;  // < kBatchFlush pending + 4 leaves x 64 per visit
+constexpr int kBatchCap = kBatchFlush + 256;  // a wide visit flushes before a slot could overflow
 constexpr int kShadowFlush = kBatchFlush;
 
 struct WaveLeafLds {
-  unsigned long long q[kBatchCap];  // lo 32: leaf index, hi 32: lane
+  unsigned long long q[kBatchCap];  // lo 32: leaf (DevLeaf or DFS index), hi 32: lane
   unsigned long long key[64];       // per lane: closest-hit key, or shadow flag
 };
 
@@ -437,28 +435,78 @@ __device__ __forceinline__ void batch_push(WaveLeafLds& L, int& n, int leaf, uin
   n += __builtin_popcountll(m);
 }
 
+// Queue leaves `leaf` and `leaf + 1` (a pair) for the lanes of `m`: each lane's two entries are
+// adjacent (one 16-B LDS write), the queue order does not matter.
+__device__ __forceinline__ void batch_push_pair(WaveLeafLds& L, int& n, int leaf, uint64_t m) {
+  const int lane = lane_id();
+  if ((m >> lane) & 1) {
+    const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    const unsigned long long hi = (unsigned long long)lane << 32;
+    L.q[n + 2 * below] = hi | (unsigned)leaf;
+    L.q[n + 2 * below + 1] = hi | (unsigned)(leaf + 1);
+  }
+  n += 2 * __builtin_popcountll(m);
+}
+
 __device__ __forceinline__ float lane_f(int src, float v) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
 }
 
+typedef float f4 __attribute__((ext_vector_type(4)));
+
 // Runs the n queued tests; SHADOW: 0 < t < thr of the owner sets its flag, else the owner's
 // key takes min(key, (t, leaf)) for 0 < t < inf.  All lanes of the wave take part.
-template <bool SHADOW, bool SPHERES>
-__device__ __forceinline__ void batch_flush(WaveLeafLds& L, int n, const DevPrim* __restrict__ prims,
-                                            const LaneRay& r, float thr) {
+template <bool SHADOW, bool SPHERES, bool CULL>
+__device__ __forceinline__ void batch_flush(const RenderParams& P, WaveLeafLds& L, int n,
+                                            const LaneRay& r, float thr, Diag& dg) {
   const int lane = lane_id();
   for (int base = 0; base < n; base += 64) {
     const int i = base + lane;
     const bool valid = i < n;
     const unsigned long long e = valid ? L.q[i] : 0ull;
-    const int src = (int)(e >> 32), leaf = (int)(unsigned)e;
+    const int src = (int)(e >> 32), idx = (int)(unsigned)e;
     LaneRay rr;
     rr.o = v3(lane_f(src, r.o.x), lane_f(src, r.o.y), lane_f(src, r.o.z));
     rr.d = v3(lane_f(src, r.d.x), lane_f(src, r.d.y), lane_f(src, r.d.z));
     rr.quot = __builtin_amdgcn_ds_bpermute(src << 2, (int)r.quot) != 0;
     const float othr = SHADOW ? lane_f(src, thr) : 0.0f;
     float t = 0.0f;
-    const bool hit = leaf_test<SPHERES>(prims, leaf, rr, t);  // leaf 0 for idle lanes: unused
+    bool hit;
+    int leaf;
+    if constexpr (CULL) {
+      const f4* q = reinterpret_cast<const f4*>(P.leaves + idx);  // idle lanes: record 0, unused
+      const f4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+      const int tag = __float_as_int(q0.w);
+      leaf = tag & ~kLeafSphere;
+      // the guard: the holder box {q1.w, q2.w, q3.x, q3.y, q3.z, q3.w}
+      rr.r = v3(__builtin_amdgcn_rcpf(rr.d.x), __builtin_amdgcn_rcpf(rr.d.y),
+                __builtin_amdgcn_rcpf(rr.d.z));
+      rr.skip0 = __builtin_fabsf(rr.d.x) < kEps;
+      rr.skip1 = __builtin_fabsf(rr.d.y) < kEps;
+      rr.skip2 = __builtin_fabsf(rr.d.z) < kEps;
+      const float g[6] = {q1.w, q2.w, q3.x, q3.y, q3.z, q3.w};
+      float tn, tf;
+      slab_span<true>(g, rr, tn, tf);
+      bool in, out;
+      decide_sure(tn, tf, in, out);
+      bool ok = valid & in;
+      const bool und = valid & !(in | out);
+      if (ballot(und)) {
+        if (und) ok = guard_exact(P, ~leaf, rr);
+        DIAG(if (und) atomicAdd(&g_exact_fallbacks, 1ull));
+      }
+      DIAG(dg.guard += __builtin_popcountll(ballot(valid)));
+      const V3 v0 = v3(q0.x, q0.y, q0.z);
+      if (!SPHERES || !(tag & kLeafSphere))
+        hit = tri_test(v0, v3(q1.x, q1.y, q1.z), v3(q2.x, q2.y, q2.z), rr, t);
+      else
+        hit = sphere_test(v0, q1.x, rr, t);
+      hit &= ok;
+    } else {
+      hit = leaf_test<SPHERES>(P.prims, idx, rr, t);  // leaf 0 for idle lanes: unused
+      leaf = idx;
+    }
     if (SHADOW) {
       if (valid & hit & (t > 0.0f) & (t < othr)) L.key[src] = 1ull;  // any writer: same value
     } else if (valid & hit & (t > 0.0f) & (t < RT_INF)) {
@@ -467,134 +515,115 @@ __device__ __forceinline__ void batch_flush(WaveLeafLds& L, int n, const DevPrim
   }
 }
 
-// Queues the leaf tests of a visited binary node's leaf children for the lanes of h0 / h1.
+// Queues the leaf tests of a visited reference node's leaf children for the lanes of h0 / h1.
 __device__ __forceinline__ void queue_binary_leaves(WaveLeafLds& L, int& pending, const DevNode& N,
                                                     bool h0, bool h1, uint64_t alive, Diag& dg) {
   if (N.child[0] < 0) {
     const uint64_t b = ballot(h0) & alive;
     batch_push(L, pending, ~N.child[0], b);
-    if (N.pad & kAccelPair0) batch_push(L, pending, ~N.child[0] + 1, b);
-    DIAG(const int nl = 1 + ((N.pad & kAccelPair0) != 0); dg.leaves += nl;
-         dg.leaf_lanes += nl * __builtin_popcountll(b));
+    DIAG(dg.leaves++; dg.leaf_lanes += __builtin_popcountll(b));
   }
   if (N.child[1] < 0) {
     const uint64_t b = ballot(h1) & alive;
     batch_push(L, pending, ~N.child[1], b);
-    if (N.pad & kAccelPair1) batch_push(L, pending, ~N.child[1] + 1, b);
-    DIAG(const int nl = 1 + ((N.pad & kAccelPair1) != 0); dg.leaves += nl;
-         dg.leaf_lanes += nl * __builtin_popcountll(b));
+    DIAG(dg.leaves++; dg.leaf_lanes += __builtin_popcountll(b));
   }
 }
 
-// ------------------------------------------------------------------ wide culling nodes
-// The whole 128-B node in one round trip: two s_load_dwordx16 and one wait.  Left to itself
-// the compiler splits the record into ~14 loads of 1-8 dwords in three dependent rounds (and,
-// short of SGPRs, reloads the first slot's box after the flags test).
+// ------------------------------------------------------------------ 8-wide culling nodes
+// The whole 128-B node (DevNode8) in one round trip: two s_load_dwordx16 and one wait.
 typedef int v16i __attribute__((ext_vector_type(16)));
-__device__ __forceinline__ DevNode4 load_node4(const DevNode* __restrict__ nodes, int idx) {
-  v16i a, b;
+__device__ __forceinline__ void load_node8(const DevNode* __restrict__ nodes, int idx, v16i& a,
+                                           v16i& b) {
   const void* p = nodes + idx;
   asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
                : "=s"(a), "=s"(b) : "s"(p) : "memory");
-  DevNode4 N;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-#pragma unroll
-    for (int x = 0; x < 3; x++) {
-      N.lo[x][k] = __int_as_float(a[4 * x + k]);
-      N.hi[x][k] = __int_as_float(k + 4 * x < 4 ? a[12 + 4 * x + k] : b[4 * x + k - 4]);
-    }
-    N.child[k] = b[8 + k];
-  }
-  N.flags = b[12];
-  return N;
 }
 
-#ifndef RT_MASK_SLOTS  // slot decisions as wave masks (0: as per-lane booleans, for A/B)
-#define RT_MASK_SLOTS 1
-#endif
-// One packet visit of a wide culling node, slot by slot with the binary tree's rules
-// (visit_node): a guarded slot accepts on a decided guard test (else guard_exact), and its
-// leaf or leaf pair goes straight to the leaf queue; an inner slot culls only on a sure
-// reject.  Of the entered inner slots one becomes `node` (SHADOW: the nearest by the entry
-// distance of the first entering lane, so occluders turn up early) and the others are pushed.
-// `alive`: lanes still searching.  Up to 4 slots x 2 leaves x 64 lanes of leaf tests are
-// queued per visit, so the queue is run in between when it could overflow.  Returns false when
-// the walk is over.
-template <bool SKIP, bool SHADOW, bool DEEP, bool SPHERES, bool REL = false>
+// fp16 halves of a slot word: the compiler feeds them to v_fma_mix_f32 straight from the SGPR
+__device__ __forceinline__ float half_lo(int w) {
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)((unsigned)w & 0xffffu));
+}
+__device__ __forceinline__ float half_hi(int w) {
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)((unsigned)w >> 16));
+}
+
+#define RT_NODE_WORD(k) ((k) < 16 ? a[(k)] : b[(k) - 16])
+
+// One packet visit of an 8-wide culling node.  Every slot takes a plain slab test on its
+// conservative box (plane t = fma(h, 2^k / d, (origin - o) / d), the lo planes moved down and
+// the hi planes up by the ray's own margin 2^-18 |o| — DESIGN.md §4.2: with the host's margin
+// the test never culls a treelet the reference would enter, so no decision band is needed);
+// an invalid slot's NaN planes fail it.  A leafy slot's leaves go to the leaf queue (the exact
+// guard decision is taken there); of the entered inner slots one becomes `node` (SHADOW: the
+// nearest by the entry distance of the first entering lane, so occluders turn up early) and the
+// others are pushed.  `alive`: lanes still searching.  Returns false when the walk is over.
+template <bool SKIP, bool SHADOW, bool DEEP, bool SPHERES>
 __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode* __restrict__ nodes,
-                                           const DevPrim* __restrict__ prims, WaveLeafLds& L,
-                                           int& pending, const LaneRay& r, float thr, int& node,
-                                           uint64_t& m, uint64_t alive, WaveStack<DEEP>& st,
-                                           Diag& dg) {
-  const DevNode4 N = load_node4(nodes, node & ~kWideTag);
-#if !RT_MASK_SLOTS
-  const bool in = (m >> lane_id()) & 1;
-#endif
-  const int fl = N.flags;
-  DIAG(dg.nodes++; dg.wide++; dg.node_lanes += __builtin_popcountll(m);
-       dg.top += (fl & kWideTop) != 0);
+                                           WaveLeafLds& L, int& pending, const LaneRay& r, float thr,
+                                           int& node, uint64_t& m, uint64_t alive,
+                                           WaveStack<DEEP>& st, Diag& dg) {
+  v16i a, b;
+  load_node8(nodes, node & ~kWideTag, a, b);
+  const unsigned scale = (unsigned)a[3];
+  const int inner_base = a[4], leaf_base = a[5], kinds = a[6];
+  const unsigned offs = (unsigned)a[7];
+  const unsigned inner = (unsigned)kinds & ~((unsigned)kinds >> 8) & 0xffu;
+  DIAG(dg.nodes++; dg.wide++; dg.node_lanes += __builtin_popcountll(m));
+  const float o[3] = {r.o.x, r.o.y, r.o.z}, rc[3] = {r.r.x, r.r.y, r.r.z}, mg[3] = {r.m.x, r.m.y, r.m.z};
+  float S[3], Alo[3], Ahi[3];
+#pragma unroll
+  for (int x = 0; x < 3; x++) {
+    S[x] = __builtin_amdgcn_ldexpf(rc[x], (int)((scale >> (8 * x)) & 255u) - 128);
+    const float A = (__int_as_float(a[x]) - o[x]) * rc[x];
+    Alo[x] = A - mg[x];
+    Ahi[x] = A + mg[x];
+  }
   int nxt = -1;
   uint64_t nm = 0;
-  float nkey = 0.0f;
+  unsigned nkey = 0;
 #pragma unroll
-  for (int c = 0; c < 4; c++) {
-    if (!(fl & (kWideValid << c))) continue;
-    const float b[6] = {N.lo[0][c], N.lo[1][c], N.lo[2][c], N.hi[0][c], N.hi[1][c], N.hi[2][c]};
-    float tn, tf;
-    slab_span<SKIP, REL>(b, r, tn, tf);
-    const int ch = N.child[c];
-    const bool guard = (fl & (kWideGuard << c)) != 0;
-#if RT_MASK_SLOTS
-    // the slot's decisions as wave masks straight from the compares (decide_sure's rules)
-    const float band = __builtin_fmaf(__builtin_fabsf(tn) + __builtin_fabsf(tf), 0x1p-20f, 0x1p-120f);
-    const float d = tn - tf;
-    const uint64_t out_m = lanes_lt(tf, 0.0f) | lanes_gt(d, band);
-    uint64_t hm;
-    if (guard) {
-      const uint64_t in_m = lanes_lt(d, -band) & lanes_ge(tf, 0.0f);
-      hm = m & in_m;
-      const uint64_t um = m & ~(in_m | out_m);
-      if (um) {
-        const bool ok = ((um >> lane_id()) & 1) && guard_exact(P, ch, r);
-        hm |= ballot(ok);
-        DIAG(if ((um >> lane_id()) & 1) atomicAdd(&g_exact_fallbacks, 1ull));
-      }
-    } else {
-      hm = m & ~out_m;
+  for (int c = 0; c < kWideSlots; c++) {
+    float n3[3], f3[3];
+#pragma unroll
+    for (int x = 0; x < 3; x++) {
+      const int w = RT_NODE_WORD(8 + 3 * c + x);
+      const float tl = __builtin_fmaf(half_lo(w), S[x], Alo[x]);
+      const float th = __builtin_fmaf(half_hi(w), S[x], Ahi[x]);
+      n3[x] = __builtin_fminf(tl, th);
+      f3[x] = __builtin_fmaxf(tl, th);
     }
-    hm &= alive;
-#else
-    bool sin, sout;
-    decide_sure(tn, tf, sin, sout);
-    bool h;
-    if (guard) {
-      h = in & sin;
-      const bool u = in & !(sin | sout);
-      if (ballot(u)) {
-        if (u) h = guard_exact(P, ch, r);
-        DIAG(if (u) atomicAdd(&g_exact_fallbacks, 1ull));
+    if (SKIP) {
+      const bool sk[3] = {r.skip0, r.skip1, r.skip2};
+#pragma unroll
+      for (int x = 0; x < 3; x++) {
+        n3[x] = sk[x] ? -RT_INF : n3[x];
+        f3[x] = sk[x] ? RT_INF : f3[x];
       }
-    } else {
-      h = in & !sout;
     }
-    const uint64_t hm = ballot(h) & alive;
-#endif
+    const float tn = __builtin_fmaxf(__builtin_fmaxf(n3[0], n3[1]), n3[2]);
+    const float tf = __builtin_fminf(__builtin_fminf(f3[0], f3[1]), f3[2]);
+    // out: !(tf >= tn) or !(tf >= 0) — unordered, so a NaN (invalid slot) is out
+    const uint64_t hm = m & alive & ~(lanes_nge(tf, tn) | lanes_nge(tf, 0.0f));
     if (!hm) continue;
-    if (guard && ch < 0) {  // a leaf, or a leaf pair
-      const bool pair = (fl & (kWidePair << c)) != 0;
+    if (kinds & (kSlotLeafy << c)) {
+      const int leaf = leaf_base + (int)((offs >> (4 * c)) & 15u);
+      const bool pair = (kinds & (kSlotPair << c)) != 0;
       if (pending > kBatchCap - 128) {
-        batch_flush<SHADOW, SPHERES>(L, pending, prims, r, thr);
+        batch_flush<SHADOW, SPHERES, true>(P, L, pending, r, thr, dg);
         pending = 0;
       }
-      batch_push(L, pending, ~ch, hm);
-      if (pair) batch_push(L, pending, ~ch + 1, hm);
+      if (pair)
+        batch_push_pair(L, pending, leaf, hm);
+      else
+        batch_push(L, pending, leaf, hm);
       DIAG(dg.leaves += 1 + pair; dg.leaf_lanes += (1 + pair) * __builtin_popcountll(hm));
       continue;
     }
+    const int ch = (inner_base + 2 * __builtin_popcount(inner & ((1u << c) - 1u))) | kWideTag;
     if (SHADOW) {
-      const float key = __int_as_float(
-          __builtin_amdgcn_readlane(__float_as_int(tn), (int)__builtin_ctzll(hm)));
+      const unsigned key = (unsigned)__builtin_amdgcn_readlane(
+          __float_as_int(__builtin_fmaxf(tn, 0.0f)), (int)__builtin_ctzll(hm));
       if (nxt < 0 || key < nkey) {
         if (nxt >= 0) st.push(nxt, nm);
         nxt = ch;
@@ -617,32 +646,31 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
   }
   return st.pop_live(node, m, alive);
 }
+#undef RT_NODE_WORD
 
 // ------------------------------------------------------------------ closest hit
-// The reference's (t, leaf) for every active ray: leaf < 0 = miss.  FAST: the culling tree
-// over reference treelets (WO: every node the fast walk meets is a 4-wide node); otherwise the
-// reference tree itself.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, bool WO, bool REL = false>
+// The reference's (t, leaf) for every active ray: leaf < 0 = miss.  FAST: the 8-wide culling
+// tree over reference treelets (the launch takes it only when the scene has one); otherwise
+// the reference tree itself.
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES>
 __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode* __restrict__ nodes,
-                                            const DevPrim* __restrict__ prims, int* spill,
-                                            WaveLeafLds& L, const LaneRay& r, bool active,
-                                            float& best_t, int& best_leaf, Diag& dg) {
+                                            int* spill, WaveLeafLds& L, const LaneRay& r,
+                                            bool active, float& best_t, int& best_leaf, Diag& dg) {
   best_t = RT_INF;
   best_leaf = -1;
   if (P.root_kind != kRootNode) {  // the root IS the primitive (BVH.h:13-14): its own rule
     float t;
-    if (active && leaf_test<SPHERES>(prims, P.root_ref, r, t)) {
+    if (active && leaf_test<SPHERES>(P.prims, P.root_ref, r, t)) {
       best_t = t;
       best_leaf = P.root_ref;
     }
     return;
   }
-  const bool accel = FAST && P.accel_root >= 0;  // culling tree over treelets (§4.2)
   uint64_t m;
   {
     float tn, tf;
     bool acc, und;
-    if (accel) {
+    if (FAST) {  // the culling tree's root box (conservative, tested with the band)
       slab_span<SKIP>(P.accel_box, r, tn, tf);
       m = ballot(active && decide_cull(tn, tf));
     } else {
@@ -656,32 +684,29 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
   st.lds = spill;
   int pending = 0;
   L.key[lane] = kNoHitKey;
-  int node = accel ? P.accel_root : P.root_ref;
+  int node = FAST ? P.accel_root : P.root_ref;
   for (;;) {
     if (pending >= kBatchFlush) {  // between visits: only the ray and the stack are live
-      batch_flush<false, SPHERES>(L, pending, prims, r, 0.0f);
+      batch_flush<false, SPHERES, FAST>(P, L, pending, r, 0.0f, dg);
       pending = 0;
     }
     if constexpr (FAST) {
-      if (WO || (node & kWideTag)) {
-        if (!visit_wide<SKIP, false, DEEP, SPHERES, REL>(P, nodes, prims, L, pending, r, 0.0f,
-                                                         node, m, ~0ull, st, dg))
-          break;
-        continue;
-      }
+      if (!visit_wide<SKIP, false, DEEP, SPHERES>(P, nodes, L, pending, r, 0.0f, node, m, ~0ull, st, dg))
+        break;
+    } else {
+      const DevNode N = nodes[node];
+      bool h0, h1;
+      float t0, t1;
+      visit_node<SKIP>(N, r, (m >> lane) & 1, h0, h1, t0, t1);
+      DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m));
+      queue_binary_leaves(L, pending, N, h0, h1, ~0ull, dg);
+      // leaves are queued; only inner children are entered
+      const uint64_t m0 = N.child[0] >= 0 ? ballot(h0) : 0ull;
+      const uint64_t m1 = N.child[1] >= 0 ? ballot(h1) : 0ull;
+      if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, ~0ull)) break;
     }
-    const DevNode N = nodes[node];
-    bool h0, h1;
-    float t0, t1;
-    visit_node<SKIP>(P, N, r, (m >> lane) & 1, h0, h1, t0, t1);
-    DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m));
-    queue_binary_leaves(L, pending, N, h0, h1, ~0ull, dg);
-    // leaves are queued; only inner children are entered
-    const uint64_t m0 = N.child[0] >= 0 ? ballot(h0) : 0ull;
-    const uint64_t m1 = N.child[1] >= 0 ? ballot(h1) : 0ull;
-    if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, ~0ull)) break;
   }
-  if (pending) batch_flush<false, SPHERES>(L, pending, prims, r, 0.0f);
+  if (pending) batch_flush<false, SPHERES, FAST>(P, L, pending, r, 0.0f, dg);
   const unsigned long long key = L.key[lane];
   best_t = __uint_as_float((unsigned)(key >> 32));
   best_leaf = (int)(unsigned)key;
@@ -690,22 +715,20 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
 // ------------------------------------------------------------------ shadow (any hit)
 // Occluded iff some leaf the ray may reach has 0 < t < thr — identical to the reference's
 // closest-hit shadow test `0 < t_closest < dist - eps` (HW2/Scene.cpp:123-127), appendix A.7.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, bool WO>
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES>
 __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* __restrict__ nodes,
-                                         const DevPrim* __restrict__ prims, int* spill,
-                                         WaveLeafLds& L, const LaneRay& r, bool active, float thr,
-                                         Diag& dg) {
+                                         int* spill, WaveLeafLds& L, const LaneRay& r, bool active,
+                                         float thr, Diag& dg) {
   if (P.root_kind != kRootNode) {
     float t;
-    return active && leaf_test<SPHERES>(prims, P.root_ref, r, t) && t < thr && t > 0.0f;
+    return active && leaf_test<SPHERES>(P.prims, P.root_ref, r, t) && t < thr && t > 0.0f;
   }
-  const bool accel = FAST && P.accel_root >= 0;
   uint64_t m;
   {
     float tn, tf;
     bool acc, und;
     // thr <= 0 (or NaN): nothing can satisfy 0 < t < thr
-    if (accel) {
+    if (FAST) {
       slab_span<SKIP>(P.accel_box, r, tn, tf);
       m = ballot(active && thr > 0.0f && decide_cull(tn, tf));
     } else {
@@ -720,34 +743,31 @@ __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* _
   st.lds = spill;
   int pending = 0;
   L.key[lane] = 0ull;
-  int node = accel ? P.accel_root : P.root_ref;
+  int node = FAST ? P.accel_root : P.root_ref;
   for (;;) {
     if (pending >= kShadowFlush) {  // between visits; a lane found occluded stops entering nodes
-      batch_flush<true, SPHERES>(L, pending, prims, r, thr);
+      batch_flush<true, SPHERES, FAST>(P, L, pending, r, thr, dg);
       pending = 0;
       alive &= ~ballot(L.key[lane] != 0ull);
       m &= alive;
       if (!m && !st.pop_live(node, m, alive)) break;
     }
     if constexpr (FAST) {
-      if (WO || (node & kWideTag)) {
-        if (!visit_wide<SKIP, true, DEEP, SPHERES>(P, nodes, prims, L, pending, r, thr, node, m,
-                                                   alive, st, dg))
-          break;
-        continue;
-      }
+      if (!visit_wide<SKIP, true, DEEP, SPHERES>(P, nodes, L, pending, r, thr, node, m, alive, st, dg))
+        break;
+    } else {
+      const DevNode N = nodes[node];
+      bool h0, h1;
+      float t0, t1;
+      visit_node<SKIP>(N, r, (m >> lane) & 1, h0, h1, t0, t1);
+      DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m));
+      queue_binary_leaves(L, pending, N, h0, h1, alive, dg);  // the still-unoccluded lanes
+      const uint64_t m0 = N.child[0] >= 0 ? ballot(h0) & alive : 0ull;
+      const uint64_t m1 = N.child[1] >= 0 ? ballot(h1) & alive : 0ull;
+      if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, alive)) break;
     }
-    const DevNode N = nodes[node];
-    bool h0, h1;
-    float t0, t1;
-    visit_node<SKIP>(P, N, r, (m >> lane) & 1, h0, h1, t0, t1);
-    DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m));
-    queue_binary_leaves(L, pending, N, h0, h1, alive, dg);  // the still-unoccluded lanes
-    const uint64_t m0 = N.child[0] >= 0 ? ballot(h0) & alive : 0ull;
-    const uint64_t m1 = N.child[1] >= 0 ? ballot(h1) & alive : 0ull;
-    if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, alive)) break;
   }
-  if (pending) batch_flush<true, SPHERES>(L, pending, prims, r, thr);
+  if (pending) batch_flush<true, SPHERES, FAST>(P, L, pending, r, thr, dg);
   return L.key[lane] != 0ull;
 }
 
@@ -850,10 +870,9 @@ __device__ __forceinline__ int hit_leaf(int2_t rec) { return rec.x; }
 
 // One wave = the 8x8 packet of selected tile `sel` (< num_sel_tiles): closest hit per pixel
 // into its 8-B record.
-template <bool FAST, bool DEEP, bool SPHERES, bool WO, bool REL = false>
+template <bool FAST, bool DEEP, bool SPHERES>
 __device__ __forceinline__ void primary_packet(const RenderParams& P,
-                                               const DevNode* __restrict__ nodes,
-                                               const DevPrim* __restrict__ prims, int sel,
+                                               const DevNode* __restrict__ nodes, int sel,
                                                int* spill, WaveLeafLds& L) {
   const PacketPixel q = packet_pixel(P, sel);
   LaneRay ray = make_ray(ld3(P.cam_e), primary_dir(P, q.px, q.py), P.quot_ok);
@@ -866,9 +885,9 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
   float t;
   int leaf;
   if (ballot(any_skip))
-    closest_hit<true, FAST, DEEP, SPHERES, WO, REL>(P, nodes, prims, spill, L, ray, q.valid, t, leaf, dg);
+    closest_hit<true, FAST, DEEP, SPHERES>(P, nodes, spill, L, ray, q.valid, t, leaf, dg);
   else
-    closest_hit<false, FAST, DEEP, SPHERES, WO, REL>(P, nodes, prims, spill, L, ray, q.valid, t, leaf, dg);
+    closest_hit<false, FAST, DEEP, SPHERES>(P, nodes, spill, L, ray, q.valid, t, leaf, dg);
   const RenderParams& Pw = fresh_params(P);  // post-traversal fields: not live across it
   int2_t rec;  // key layout: leaf low, t bits high (rt_internal.h)
   rec.x = q.valid ? leaf : -2;  // -1 miss, -2 outside the image
@@ -886,7 +905,7 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
     atomicAdd(&c[kCntPrimLeaves], dg.leaves);
     atomicAdd(&c[kCntPrimLeafLanes], dg.leaf_lanes);
     atomicAdd(&c[kCntPrimWide], dg.wide);
-    atomicAdd(&c[kCntPrimTopWide], dg.top);
+    atomicAdd(&c[kCntGuardTests], dg.guard);
 #endif
   }
 }
@@ -899,10 +918,9 @@ __device__ __forceinline__ V3 hit_point(const RenderParams& P, const PacketPixel
 
 // Shadow rays of HW2/Scene.cpp:113-127: one bit per point light, set when the light is
 // occluded for this pixel's primary hit.
-template <bool FAST, bool DEEP, bool SPHERES, bool WO>
+template <bool FAST, bool DEEP, bool SPHERES>
 __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
                                               const DevNode* __restrict__ nodes,
-                                              const DevPrim* __restrict__ prims,
                                               const DevLight* __restrict__ lights, int sel,
                                               int* spill, WaveLeafLds& L) {
   Diag dg;
@@ -926,8 +944,8 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       const float thr = dist - P.eps;
       const bool any_skip = hit && (sr.skip0 || sr.skip1 || sr.skip2);
       const bool occ = ballot(any_skip)
-                           ? occluded<true, FAST, DEEP, SPHERES, WO>(P, nodes, prims, spill, L, sr, hit, thr, dg)
-                           : occluded<false, FAST, DEEP, SPHERES, WO>(P, nodes, prims, spill, L, sr, hit, thr, dg);
+                           ? occluded<true, FAST, DEEP, SPHERES>(P, nodes, spill, L, sr, hit, thr, dg)
+                           : occluded<false, FAST, DEEP, SPHERES>(P, nodes, spill, L, sr, hit, thr, dg);
       bits |= (occ ? 1u : 0u) << (li - 32 * w);
     }
     const RenderParams& Pw = fresh_params(P0);
@@ -946,6 +964,7 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       atomicAdd(&c[kCntShadLeaves], dg.leaves);
       atomicAdd(&c[kCntShadLeafLanes], dg.leaf_lanes);
       atomicAdd(&c[kCntShadWide], dg.wide);
+      atomicAdd(&c[kCntGuardTests], dg.guard);
 #endif
     }
   }
@@ -1067,8 +1086,8 @@ __device__ __forceinline__ V3 local_color(const RenderParams& P, const DevNode* 
     const LaneRay sr = make_ray(p + wi * P.eps, wi, P.quot_ok);
     const float thr = dist - P.eps;
     const bool sskip = ballot(shade && (sr.skip0 || sr.skip1 || sr.skip2)) != 0;
-    const bool occ = sskip ? occluded<true, FAST, DEEP, SPHERES, false>(P, nodes, prims, spill, L, sr, shade, thr, dg)
-                           : occluded<false, FAST, DEEP, SPHERES, false>(P, nodes, prims, spill, L, sr, shade, thr, dg);
+    const bool occ = sskip ? occluded<true, FAST, DEEP, SPHERES>(P, nodes, spill, L, sr, shade, thr, dg)
+                           : occluded<false, FAST, DEEP, SPHERES>(P, nodes, spill, L, sr, shade, thr, dg);
     shadow_rays += __builtin_popcountll(ballot(shade));
     if (shade && !occ) {
       const V3 I = ld3(lt.intensity);
@@ -1113,9 +1132,9 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
     float t;
     int leaf;
     if (skip)
-      closest_hit<true, FAST, DEEP, SPHERES, false>(P, nodes, prims, spill, L, ray, active, t, leaf, dg);
+      closest_hit<true, FAST, DEEP, SPHERES>(P, nodes, spill, L, ray, active, t, leaf, dg);
     else
-      closest_hit<false, FAST, DEEP, SPHERES, false>(P, nodes, prims, spill, L, ray, active, t, leaf, dg);
+      closest_hit<false, FAST, DEEP, SPHERES>(P, nodes, spill, L, ray, active, t, leaf, dg);
     const bool hit = active && leaf >= 0;
     if (first) n_hits = __builtin_popcountll(ballot(hit));
     first = false;
@@ -1278,7 +1297,7 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
 // (<= 64 VGPRs, <= 80 SGPRs); the primary kernel runs at 7, where the wide node's 32 SGPRs fit
 // without spills.  (Macros: A/B builds, `make exp EXTRA=-D...`.)
 #ifndef RT_TRACE_MIN_WAVES
-#define RT_TRACE_MIN_WAVES 8
+#define RT_TRACE_MIN_WAVES 7
 #endif
 #ifndef RT_PRIMARY_MIN_WAVES
 #define RT_PRIMARY_MIN_WAVES 7
@@ -1354,106 +1373,6 @@ __device__ __forceinline__ int dispatch_sel(const RenderParams& Q) {
   return sel < Q.num_sel_tiles ? sel : -1;
 }
 
-// Cost estimate of each selected tile before its primary traversal: kProbeRays rays per tile
-// (a 2x2 grid of its pixels), each walking the TOP probe_depth levels of the culling tree on
-// its own lane, with its own stack in LDS, and counting the nodes and leaves it enters there
-// (a node one level deeper counts as entered, not visited); the tile's cost is the sum over
-// its rays.  Rays that graze the geometry — the expensive packets — enter many boxes at every
-// level, so the top levels rank the tiles; and the top levels are the hot part of the tree
-// (L2 hits), which keeps this latency-bound kernel short: a wave runs as long as its longest
-// ray, one round trip per visit (the whole 128-B record in eight 16-B loads issued together).
-// Conservative box decisions only (a culling node's !sure_out; a guard's too): it is an
-// estimate, so no exact fallback.
-constexpr int kProbeStack = 40;
-constexpr int kProbeRays = 4;
-
-__global__ __launch_bounds__(256) void probe_kernel(RenderParams P, const DevNode* __restrict__ nodes) {
-  __shared__ int stack[4][kProbeStack][64];  // 256 threads
-  __shared__ unsigned char sdepth[4][kProbeStack][64];
-  const int gid = (int)blockIdx.x * 256 + (int)threadIdx.x;
-  const int sel = gid / kProbeRays, k = gid % kProbeRays;
-  const int wv = (int)threadIdx.x >> 6, lane = lane_id();
-  unsigned cost = 0;
-  if (sel < P.num_sel_tiles) {
-    const int tile = P.tile_begin + sel * P.tile_step;
-    const int px = min((tile % P.tiles_x) * kTile + 2 + 4 * (k & 1), P.width - 1);
-    const int lr = min((tile / P.tiles_x) * kTile + 2 + 4 * (k >> 1), P.rows - 1);
-    const LaneRay r = make_ray(ld3(P.cam_e), primary_dir(P, px, P.row0 + lr * P.row_stride), 0);
-    float tn, tf;
-    slab_span<true>(P.accel_box, r, tn, tf);
-    int node = decide_cull(tn, tf) ? P.accel_root : -1;
-    int depth = 0, sp = 0, visits = 0;
-    cost = 1;
-    while (node >= 0) {
-      cost += 4;
-      if (depth >= P.probe_depth || visits >= P.probe_visits) {  // entered, not visited
-        node = sp > 0 ? stack[wv][--sp][lane] : -1;
-        depth = sp >= 0 && node >= 0 ? sdepth[wv][sp][lane] : 0;
-        continue;
-      }
-      visits++;
-      typedef float v4f __attribute__((ext_vector_type(4)));
-      const v4f* q = reinterpret_cast<const v4f*>(nodes + (node & ~kWideTag));
-      v4f w[8];
-#pragma unroll
-      for (int i = 0; i < 8; i++) w[i] = q[i];  // (a binary node reads its neighbour too: unused)
-      int next = -1;
-      if (node & kWideTag) {  // DevNode4: lo[3][4] = w0..2, hi[3][4] = w3..5, child = w6, flags
-        const int fl = __float_as_int(w[7].x);
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          if (!(fl & (kWideValid << c))) continue;
-          const float b[6] = {w[0][c], w[1][c], w[2][c], w[3][c], w[4][c], w[5][c]};
-          slab_span<true>(b, r, tn, tf);
-          if (!decide_cull(tn, tf)) continue;
-          const int ch = __float_as_int(w[6][c]);
-          if ((fl & (kWideGuard << c)) && ch < 0) {
-            cost += (fl & (kWidePair << c)) ? 2 : 1;
-          } else if (next < 0) {
-            next = ch;
-          } else if (sp < kProbeStack) {
-            stack[wv][sp][lane] = ch;
-            sdepth[wv][sp++][lane] = (unsigned char)(depth + 1);
-          }
-        }
-      } else {  // DevNode: lo[3][2], hi[3][2] = w0..2, child[2] = w3.xy, pad = w3.w
-        const float f[12] = {w[0].x, w[0].y, w[0].z, w[0].w, w[1].x, w[1].y,
-                             w[1].z, w[1].w, w[2].x, w[2].y, w[2].z, w[2].w};
-        const int pad = __float_as_int(w[3].w);
-#pragma unroll
-        for (int c = 0; c < 2; c++) {
-          const float b[6] = {f[c], f[2 + c], f[4 + c], f[6 + c], f[8 + c], f[10 + c]};
-          slab_span<true>(b, r, tn, tf);
-          if (!decide_cull(tn, tf)) continue;
-          const int ch = __float_as_int(c ? w[3].y : w[3].x);
-          if (ch < 0) {
-            cost += (pad & (c ? kAccelPair1 : kAccelPair0)) ? 2 : 1;
-          } else if (next < 0) {
-            next = ch;
-          } else if (sp < kProbeStack) {
-            stack[wv][sp][lane] = ch;
-            sdepth[wv][sp++][lane] = (unsigned char)(depth + 1);
-          }
-        }
-      }
-      if (next >= 0) {
-        node = next;
-        depth++;
-      } else if (sp > 0) {
-        sp--;
-        node = stack[wv][sp][lane];
-        depth = sdepth[wv][sp][lane];
-      } else {
-        node = -1;
-      }
-    }
-  }
-  // a tile's rays are kProbeRays consecutive lanes: sum them
-#pragma unroll
-  for (int o = 1; o < kProbeRays; o <<= 1) cost += (unsigned)__shfl_xor((int)cost, o, 64);
-  if (k == 0 && sel < P.num_sel_tiles) P.tile_cost[sel] = cost;
-}
-
 // Units of region x: chunks c = x, x + regions, ... of order_chunk consecutive units.
 __device__ __forceinline__ int region_units(const RenderParams& P, int x) {
   const int full = P.order_units / P.order_chunk, rem = P.order_units % P.order_chunk;
@@ -1519,10 +1438,8 @@ constexpr int kTimelineWaves = 1 << 18;
 __device__ unsigned long long g_timeline[2][kTimelineWaves][3];
 #define TL_BEGIN                                                   \
   int tl_sel = -1;                                                  \
-  unsigned tl_est = 0;                                              \
   const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime()
 #define TL_SEL(x) tl_sel = (x)
-#define TL_EST(x) tl_est = (x)
 #define TL_END(k)                                                                         \
   do {                                                                                    \
     const unsigned long long tl1 = __builtin_amdgcn_s_memrealtime();                      \
@@ -1530,21 +1447,19 @@ __device__ unsigned long long g_timeline[2][kTimelineWaves][3];
     if (lane_id() == 0 && wid < kTimelineWaves) {                                         \
       g_timeline[k][wid][0] = tl0;                                                        \
       g_timeline[k][wid][1] = tl1;                                                        \
-      g_timeline[k][wid][2] = ((unsigned long long)tl_est << 32) | (unsigned)tl_sel;      \
+      g_timeline[k][wid][2] = (unsigned)tl_sel;                                           \
     }                                                                                     \
   } while (0)
 #else
 #define TL_BEGIN
 #define TL_SEL(x)
-#define TL_EST(x)
 #define TL_END(k)
 #endif
 
 // Traversal kernels: one packet per wave, XCD-remapped blocks of 2-D tile blocks.
-// REL (FAST, WO): `nodes` is RenderParams::rel_nodes, the wide nodes relative to the camera.
-template <bool FAST, bool DEEP, bool SPHERES, bool WO, bool REL = false>
+template <bool FAST, bool DEEP, bool SPHERES>
 __global__ __launch_bounds__(kTraceWaves * 64) RT_PRIMARY_OCCUPANCY void trace_primary_kernel(
-    RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims) {
+    RenderParams P, const DevNode* __restrict__ nodes) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
   __shared__ WaveLeafLds leaf_lds[kTraceWaves];  // 2.5 KiB per wave
   int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * kDeepWords * kDeepStack : nullptr;
@@ -1553,10 +1468,9 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_PRIMARY_OCCUPANCY void trace_p
   const RenderParams& Q = fresh_params(P);
   const int sel = dispatch_sel(Q);
   TL_SEL(sel);
-  TL_EST(sel >= 0 && Q.use_order ? Q.tile_cost[sel] : 0u);  // the probe's estimate
   if (sel >= 0) {
     const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
-    primary_packet<FAST, DEEP, SPHERES, WO, REL>(Q, nodes, prims, sel, spill, L);
+    primary_packet<FAST, DEEP, SPHERES>(Q, nodes, sel, spill, L);
     const RenderParams& Pw = fresh_params(P);
     if (Pw.tile_cost && lane_id() == 0)  // the shadow kernel's dispatch order
       Pw.tile_cost[sel] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - c0, 0xffffffffull);
@@ -1564,10 +1478,9 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_PRIMARY_OCCUPANCY void trace_p
   TL_END(0);
 }
 
-template <bool FAST, bool DEEP, bool SPHERES, bool WO>
+template <bool FAST, bool DEEP, bool SPHERES>
 __global__ __launch_bounds__(kTraceWaves * 64) RT_TRAVERSAL_OCCUPANCY void trace_shadow_kernel(
-    RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims,
-    const DevLight* __restrict__ lights) {
+    RenderParams P, const DevNode* __restrict__ nodes, const DevLight* __restrict__ lights) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
   __shared__ WaveLeafLds leaf_lds[kTraceWaves];
   int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * kDeepWords * kDeepStack : nullptr;
@@ -1576,7 +1489,7 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_TRAVERSAL_OCCUPANCY void trace
   const RenderParams& Q = fresh_params(P);
   const int sel = dispatch_sel(Q);
   TL_SEL(sel);
-  if (sel >= 0) shadow_packet<FAST, DEEP, SPHERES, WO>(Q, nodes, prims, lights, sel, spill, L);
+  if (sel >= 0) shadow_packet<FAST, DEEP, SPHERES>(Q, nodes, lights, sel, spill, L);
   TL_END(1);
 }
 
@@ -1609,7 +1522,7 @@ static inline void mark(const hipEvent_t* marks, int k, hipStream_t stream) {
   if (marks) (void)hipEventRecord(marks[k], stream);
 }
 
-template <bool FAST, bool DEEP, bool SPHERES, bool WO>
+template <bool FAST, bool DEEP, bool SPHERES>
 static void launch_variant(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                            const float* normals, const DevMaterial* mats,
                            const DevLight* lights, int blocks, const hipEvent_t* marks,
@@ -1647,29 +1560,11 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
               sched_words_for((unsigned long long)T.num_sel_tiles);
   }
   const int oblocks = ordered ? T.order_regions * T.order_stride : tblocks;
-  // probe -> order -> primary: the primary kernel LPT-scheduled by the probe's estimates
-  const bool probe = ordered && FAST && T.accel_root >= 0 && T.root_kind == kRootNode &&
-                     T.order_probe;
   RenderParams S = T;
   mark(marks, 0, stream);
-  if (probe) {
-    hipLaunchKernelGGL(probe_kernel, dim3((T.num_sel_tiles * kProbeRays + 255) / 256), dim3(256),
-                       0, stream, T, nodes);
-    hipLaunchKernelGGL(order_kernel, dim3(T.order_regions), dim3(1024), 0, stream, T);
-    T.use_order = 1;
-  }
   if (!ordered) T.tile_cost = nullptr;
-  bool rel = false;
-  if constexpr (FAST && WO) rel = T.rel_nodes != nullptr && T.accel_root >= 0 && T.root_kind == kRootNode;
-  if constexpr (FAST && WO) {
-    if (rel)
-      hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, WO, true>),
-                         dim3(T.use_order ? oblocks : tblocks), dim3(kTraceWaves * 64), tlds, stream,
-                         T, T.rel_nodes, prims);
-  }
-  if (!rel)
-    hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES, WO>), dim3(T.use_order ? oblocks : tblocks),
-                       dim3(kTraceWaves * 64), tlds, stream, T, nodes, prims);
+  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES>), dim3(tblocks),
+                     dim3(kTraceWaves * 64), tlds, stream, T, nodes);
   mark(marks, 1, stream);
   S.tile_cost = T.tile_cost;
   if (P.num_lights > 0) {
@@ -1678,8 +1573,8 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
       S.use_order = 1;
     }
     S.tile_cost = nullptr;  // (the shadow kernel reads the order only)
-    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES, WO>), dim3(S.use_order ? oblocks : tblocks),
-                       dim3(kTraceWaves * 64), tlds, stream, S, nodes, prims, lights);
+    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES>), dim3(S.use_order ? oblocks : tblocks),
+                       dim3(kTraceWaves * 64), tlds, stream, S, nodes, lights);
   }
   mark(marks, 2, stream);
   hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
@@ -1814,29 +1709,27 @@ hipError_t launch_quot_check(unsigned long long seed, long long count, unsigned 
 
 hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                          const float* normals, const DevMaterial* mats, const DevLight* lights,
-                         bool fast, bool deep, bool spheres, bool wide_only,
-                         const hipEvent_t* marks, hipStream_t stream) {
+                         bool fast, bool deep, bool spheres, const hipEvent_t* marks,
+                         hipStream_t stream) {
   if (P.num_sel_tiles <= 0) return hipSuccess;
   const int blocks = (P.num_sel_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-  // wide_only (the culling tree is 4-wide and reaches no binary node): kernels without the
-  // binary visit path, which costs the wide walk registers when compiled in
-  const bool wo = wide_only && fast && !deep;
-  const int v = (wo ? 8 : 0) | (fast ? 4 : 0) | (deep ? 2 : 0) | (spheres ? 1 : 0);
+  // FAST walks the culling tree: only when the scene has one (a root primitive or a tree of
+  // one treelet has none, accel_build.cpp)
+  fast = fast && P.accel_root >= 0 && P.root_kind == kRootNode && P.leaves != nullptr;
+  const int v = (fast ? 4 : 0) | (deep ? 2 : 0) | (spheres ? 1 : 0);
   switch (v) {
-#define RT_CASE(F, D, S, W)                                                                    \
-  case (W ? 8 : 0) | (F ? 4 : 0) | (D ? 2 : 0) | (S ? 1 : 0):                                  \
-    launch_variant<F, D, S, W>(P, nodes, prims, normals, mats, lights, blocks, marks, stream); \
+#define RT_CASE(F, D, S)                                                                 \
+  case (F ? 4 : 0) | (D ? 2 : 0) | (S ? 1 : 0):                                          \
+    launch_variant<F, D, S>(P, nodes, prims, normals, mats, lights, blocks, marks, stream); \
     break;
-    RT_CASE(true, false, false, true)
-    RT_CASE(true, false, true, true)
-    RT_CASE(true, false, false, false)
-    RT_CASE(true, false, true, false)
-    RT_CASE(true, true, false, false)
-    RT_CASE(true, true, true, false)
-    RT_CASE(false, false, false, false)
-    RT_CASE(false, false, true, false)
-    RT_CASE(false, true, false, false)
-    RT_CASE(false, true, true, false)
+    RT_CASE(true, false, false)
+    RT_CASE(true, false, true)
+    RT_CASE(true, true, false)
+    RT_CASE(true, true, true)
+    RT_CASE(false, false, false)
+    RT_CASE(false, false, true)
+    RT_CASE(false, true, false)
+    RT_CASE(false, true, true)
 #undef RT_CASE
   }
   return hipGetLastError();

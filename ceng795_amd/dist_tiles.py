@@ -192,6 +192,13 @@ class TileGatherRenderer:
             self.comm = torch.cuda.Stream(device=dev)
         self.local = [torch.zeros((L.buffer_tiles, TILE_FLOATS), dtype=torch.float32, device=dev)
                       for _ in range(F)]
+        if not host_staging:
+            # the zero fill above ran on the allocating (current) stream: every stream that
+            # writes or reads these buffers first waits for it
+            cur = torch.cuda.current_stream(dev)
+            for st in self.rstreams + [self.comm]:
+                if st != cur:
+                    st.wait_stream(cur)
         self.done = [torch.cuda.Event() if not host_staging else None for _ in range(F)]
         self.handoff = [torch.cuda.Event() if not host_staging else None for _ in range(F)]
         self.used = [False] * F
@@ -315,6 +322,11 @@ class FrameGatherRenderer:
         if owners.rank == 0:
             self.recv = [[torch.empty((h, w, 3), dtype=torch.float32, device=dev)
                           for _ in range(owners.rounds * W)] for _ in range(self.inflight)]
+        if not host_staging:  # the zero fill ran on the current stream (see TileGatherRenderer)
+            cur = torch.cuda.current_stream(dev)
+            for st in self.streams + [self.comm]:
+                if st != cur:
+                    st.wait_stream(cur)
         self.done = [torch.cuda.Event() if not host_staging else None for _ in range(self.inflight)]
         self.used = [False] * self.inflight
         self.k = 0
@@ -366,6 +378,39 @@ class FrameGatherRenderer:
         for st in self.streams[1:]:
             self.stream.wait_stream(st)
         self.stream.wait_stream(self.comm)
+
+
+class ShareRenderer:
+    """One GPU rendering ONE rank's share of the tile deal of `world` ranks (TileLayout), with
+    no exchange: the per-rank render work of the N > 1 path, measured on one GPU to predict
+    strong scaling before an N-GPU node is available (bench.py share probe).  Steps go to
+    `inflight` streams / buffer sets in turn, as in TileGatherRenderer."""
+
+    def __init__(self, scene, world: int, rank: int, stream, inflight: int = 1):
+        import torch
+        self.layout = L = TilePlan(scene, world, rank)
+        self.scene, self.stream = scene, stream
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.inflight = max(1, int(inflight))
+        self.streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(self.inflight - 1)]
+        self.local = [torch.empty((max(1, L.buffer_tiles), TILE_FLOATS), dtype=torch.float32,
+                                  device=dev) for _ in range(self.inflight)]
+        self.k = 0
+
+    def step(self, events=None):
+        s = self.k % self.inflight
+        self.k += 1
+        st = self.streams[s]
+        for sh in self.layout.shares:
+            if sh.count > 0:
+                slot = self.local[s][sh.offset:sh.offset + sh.slot]
+                self.scene.render_device(sh.camera, slot.data_ptr(), tile_begin=sh.tile_begin,
+                                         tile_step=sh.tile_step, tile_major=True,
+                                         stream=st.cuda_stream)
+
+    def finish(self):
+        for st in self.streams[1:]:
+            self.stream.wait_stream(st)
 
 
 def TilePlan(scene, world: int, rank: int) -> TileLayout:

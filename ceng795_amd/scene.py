@@ -164,7 +164,7 @@ class Scene:
     DIAG_NAMES = ["primary_rays", "shadow_rays", "secondary_rays", "primary_hits",
                   "prim_node_visits", "prim_node_lanes", "prim_leaf_visits", "prim_leaf_lanes",
                   "shad_node_visits", "shad_node_lanes", "shad_leaf_visits", "shad_leaf_lanes",
-                  "exact_box_fallbacks", "prim_top_wide_visits", "prim_wide_visits",
+                  "exact_box_fallbacks", "guard_tests", "prim_wide_visits",
                   "shad_wide_visits"]
 
     def debug_counters(self) -> dict:

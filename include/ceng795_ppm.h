@@ -135,7 +135,11 @@ int ppm_set_update_shard(ppm_scene* scene, int shard, int shards);
 int ppm_hit_point_shards(ppm_scene* scene, int* out);
 /* Overwrites the hit-point state with 5 floats per hit point (the ppm_read_hit_state layout:
  * flux xyz, radius_squared, n) — e.g. the merge of the shards' states before
- * ppm_density_estimation.  After ppm_build_hash_grid. */
+ * ppm_density_estimation.  After ppm_build_hash_grid.  n travels as float32, so it must be a
+ * whole number <= 2^24 (RT_E_INVALID otherwise); n sets rr(n) of later updates.
+ * A scene with shards > 1 that has traced photons holds only its own hit points' results:
+ * ppm_density_estimation refuses it until this call has written the merged state, and
+ * ppm_render refuses such a scene outright. */
 int ppm_write_hit_state(ppm_scene* scene, const float* in5);
 
 /* main.cpp:142-156 (no tone-mapping operator): c -> int(pow(1 - exp(-c), 1/2.2f)*255 + 0.5f),

@@ -228,8 +228,9 @@ int rt_collect_stats(rt_scene* scene, rt_stats* stats);
  * [2] secondary rays [3] primary hits; RT_DIAG builds (libceng795_rt_diag.so) add packet-level
  * work: [4..7] primary node visits / active lanes summed over visits / leaf visits / leaf
  * lane tests, [8..11] the same for shadow rays, [12] lanes that fell back to the exact slab
- * test, [13] unused, [14] / [15] the primary / shadow node visits that were 4-wide nodes
- * (included in [4] / [8]).
+ * test (node boxes and leaf guards), [13] leaf-batch guard tests (primary + shadow),
+ * [14] / [15] the primary / shadow node visits that were 8-wide culling nodes (included in
+ * [4] / [8]).
  * Returns 1 for a diagnostic build, 0 otherwise (columns 4..15 then read 0). */
 int rt_debug_counters(rt_scene* scene, long long* out16);
 

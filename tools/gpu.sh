@@ -1,0 +1,54 @@
+#!/bin/bash
+# One parameterised launcher for GPU-box steps (run under gpurun; each step has its own time
+# limit and the caller chains steps with &&, so the first failure ends the call).
+#
+#   tools/gpu.sh <out> tests [pytest args]         pytest -m gpu (verbose, per-test timeout)
+#   tools/gpu.sh <out> smoke                       __graft_entry__.smoke()
+#   tools/gpu.sh <out> bench <name> [bench args]   one bench.py line -> <out>/<name>.json
+#   tools/gpu.sh <out> stats <name> [bench args]   rocprofv3 --kernel-trace --stats of bench.py
+#   tools/gpu.sh <out> ab <variants> [rounds]      same-box A/B of library builds (tools/ab.py)
+#   tools/gpu.sh <out> kt <name> [kt args]         per-kernel HIP-event times (tools/kt.py)
+#   tools/gpu.sh <out> pmc <workload> [round]      PMC traffic passes -> <out>/traffic_<w>.json
+#
+# <out> is a directory under gpurun_out/.
+set -o pipefail
+O=gpurun_out/${1:?out}; shift
+CMD=${1:?command}; shift
+mkdir -p "$O"
+export TMPDIR=/tmp
+case "$CMD" in
+  tests)
+    timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" \
+      > "$O/tests.log" 2>&1 || { tail -40 "$O/tests.log"; exit 1; }
+    tail -3 "$O/tests.log" ;;
+  smoke)
+    timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
+      || { tail -20 "$O/smoke.log"; exit 1; }
+    tail -2 "$O/smoke.log" ;;
+  bench)
+    N=${1:?name}; shift
+    timeout -k 10 600 python3 -u bench.py "$@" > "$O/$N.json" 2> "$O/$N.err" || { tail -20 "$O/$N.err"; exit 1; }
+    tail -c 1500 "$O/$N.json" ;;
+  stats)
+    N=${1:?name}; shift
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/$N" -o run --output-format csv -- \
+      python3 bench.py "$@" > "$O/$N.out" 2>&1 || { tail -20 "$O/$N.out"; exit 1; }
+    f=$(find "$O/$N" -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cp "$f" "$O/${N}_kernel_stats.csv"
+    head -12 "$O/${N}_kernel_stats.csv" | cut -c1-200 ;;
+  ab)
+    V=${1:?variants}; R=${2:-3}
+    timeout -k 10 900 python3 tools/ab.py "$V" --rounds "$R" > "$O/ab.json" 2> "$O/ab.err" || { tail -20 "$O/ab.err"; exit 1; }
+    cat "$O/ab.json" ;;
+  kt)
+    N=${1:?name}; shift
+    timeout -k 10 300 python3 tools/kt.py "$@" > "$O/$N.json" 2> "$O/$N.err" || { tail -20 "$O/$N.err"; exit 1; }
+    cat "$O/$N.json" ;;
+  pmc)
+    W=${1:-c3}; R=${2:-r04}
+    BENCH_ARGS="--workload $W" bash tools/pmc_passes.sh "$O/pmc_$W" traffic || exit 1
+    LIB=ceng795_amd/lib/libceng795_rt.so; [ "$W" = c5 ] && LIB=ceng795_amd/lib/libceng795_ppm.so
+    python3 tools/pmc_traffic.py --fetch "$O/pmc_$W/fetch" --write "$O/pmc_$W/write" --workload "$W" \
+      --round "$R" --lib "$LIB" --out "$O/traffic_$W.json" || exit 1 ;;
+  *)
+    echo "unknown command $CMD" >&2; exit 2 ;;
+esac

@@ -4,10 +4,12 @@
 and lane tests per kernel.  bench.py runs this as a child process (CENG795_LIB=diag selects the
 diagnostic library; the timed library is never instrumented) to price its roofline:
 
-    algorithmic bytes of a traversal launch = 64 B x binary node visits + 128 B x 4-wide node
-                                              visits (one node's scalar loads per packet visit)
-                                            + 48 B x leaf visits   (one DevPrim per
-                                                                    (packet, leaf) pair)
+    algorithmic bytes of a traversal launch = 128 B x 8-wide node visits (one node's scalar
+                                              loads per packet visit; 64 B x reference-node
+                                              visits without a culling tree)
+                                            + 64 B x leaf visits   (one DevLeaf per
+                                                                    (packet, leaf) pair: the
+                                                                    primitive and its guard box)
                                             + per-pixel records    (primary: 8 B hit record
                                                                     written; shadow: 8 B hit
                                                                     record read + 4 B
@@ -47,10 +49,11 @@ def main():
         pixels = c.width * c.height
         words = max(1, (s.num_lights + 31) // 32)
         node_bytes = lambda n, wide: 64 * (n - wide) + 128 * wide  # noqa: E731
+        leaf_b = 64 if d["prim_wide_visits"] else 48  # DevLeaf (culling tree) or DevPrim
         prim = (node_bytes(d["prim_node_visits"], d["prim_wide_visits"])
-                + 48 * d["prim_leaf_visits"] + 8 * pixels)
+                + leaf_b * d["prim_leaf_visits"] + 8 * pixels)
         shad = (node_bytes(d["shad_node_visits"], d["shad_wide_visits"])
-                + 48 * d["shad_leaf_visits"] + (8 + 4 * words) * pixels) if s.num_lights else 0
+                + leaf_b * d["shad_leaf_visits"] + (8 + 4 * words) * pixels) if s.num_lights else 0
         out = {"pixels": pixels, "packets": ((c.width + 7) // 8) * ((c.height + 7) // 8),
                "counters": d,
                "primary_bytes": prim, "shadow_bytes": shad}
