@@ -104,9 +104,13 @@ struct Replica {
   DevMaterial* d_mats = nullptr;
   DevLight* d_lights = nullptr;
   unsigned long long* d_counters = nullptr;
-  std::mutex mu;  // ctx pool and stream table
+  std::mutex mu;  // ctx pool and stream tables
   std::vector<RenderCtx*> ctx_free, ctx_all;
   std::vector<std::unique_ptr<StreamScratch>> streams;
+  // multi-device scenes: the context each caller stream renders its shares on (one per caller
+  // stream and device, kept across calls), so frames on different caller streams have their
+  // own device streams and buffers and overlap (frames in flight, as scratch_for on one device)
+  std::vector<std::pair<void*, RenderCtx*>> stream_ctx;
 };
 
 struct rt_scene {
@@ -222,6 +226,7 @@ void free_replica(Replica& r) {
   for (RenderCtx* c : r.ctx_all) free_ctx(c);
   r.ctx_all.clear();
   r.ctx_free.clear();
+  r.stream_ctx.clear();
   for (auto& x : r.streams) free_scratch(*x);
   r.streams.clear();
   (void)hipFree(r.d_nodes);
@@ -594,14 +599,34 @@ void release_ctx(Replica& r, RenderCtx* c) {
   r.ctx_free.push_back(c);
 }
 
-// Contexts of one call on several replicas, handed back on scope exit.
+// The context of caller stream `stream` on replica r (created on first use, then kept).
+RenderCtx* stream_ctx_for(Replica& r, void* stream) {
+  {
+    std::lock_guard<std::mutex> lk(r.mu);
+    for (auto& e : r.stream_ctx)
+      if (e.first == stream) return e.second;
+  }
+  RenderCtx* c = acquire_ctx(r);
+  std::lock_guard<std::mutex> lk(r.mu);
+  r.stream_ctx.emplace_back(stream, c);
+  return c;
+}
+
+// Contexts of one call on several replicas: pooled ones handed back on scope exit (rt_render),
+// or the caller stream's own (rt_render_device: consecutive frames on different caller streams
+// then run on different device streams, and frames on one caller stream stay ordered).
 struct CtxSet {
   rt_scene* s;
   std::vector<RenderCtx*> x;
+  bool pooled = true;
   CtxSet(rt_scene* sc, size_t n) : s(sc) {
     for (size_t d = 0; d < n; d++) x.push_back(acquire_ctx(*s->rep[d]));
   }
+  CtxSet(rt_scene* sc, size_t n, void* stream) : s(sc), pooled(false) {
+    for (size_t d = 0; d < n; d++) x.push_back(stream_ctx_for(*s->rep[d], stream));
+  }
   ~CtxSet() {
+    if (!pooled) return;
     for (size_t d = 0; d < x.size(); d++) release_ctx(*s->rep[d], x[d]);
   }
 };
@@ -1028,7 +1053,7 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
       if (tile_begin != 0 || tile_step != 1 || tile_major || tile_count >= 0)
         throw std::domain_error("multi-device scenes render whole row-major frames only");
       std::lock_guard<std::mutex> lk(s->multi_mu);
-      CtxSet cx(s, s->rep.size());
+      CtxSet cx(s, s->rep.size(), stream);
       if (c.num_samples > 1)
         render_multi_msaa(s, cx, cam, d_out, (hipStream_t)stream, false);
       else
@@ -1069,6 +1094,7 @@ int rt_release_stream_scratch(rt_scene* s, void* stream) {
     for (auto& rp : s->rep) {
       Replica& r = *rp;
       std::unique_ptr<StreamScratch> x;
+      RenderCtx* sc = nullptr;
       {
         std::lock_guard<std::mutex> lk(r.mu);
         for (size_t k = 0; k < r.streams.size(); k++)
@@ -1077,6 +1103,17 @@ int rt_release_stream_scratch(rt_scene* s, void* stream) {
             r.streams.erase(r.streams.begin() + (long)k);
             break;
           }
+        for (size_t k = 0; k < r.stream_ctx.size(); k++)
+          if (r.stream_ctx[k].first == stream) {
+            sc = r.stream_ctx[k].second;
+            r.stream_ctx.erase(r.stream_ctx.begin() + (long)k);
+            break;
+          }
+      }
+      if (sc) {  // a multi-device scene's context of that caller stream: back to the pool
+        DeviceGuard g(r.device);
+        hip_check(hipStreamSynchronize(sc->stream), "synchronize context stream");
+        release_ctx(r, sc);
       }
       if (!x) continue;
       DeviceGuard g(r.device);

@@ -19,7 +19,14 @@ class Reader {
   explicit Reader(std::string doc) : s_(std::move(doc)) {}
 
   std::unique_ptr<Node> document_root() {
-    skip_prolog();
+    // The reference takes XMLDocument::FirstChild() as the scene root (HW2/Scene.cpp:206,
+    // PPM/src/Scene.cpp:381): a declaration, comment or DOCTYPE in front of the root element
+    // becomes the "root", and the loader then dereferences its missing <Cameras> child.  That
+    // file does not load there, so it does not load here either (an error, not a crash).
+    while (i_ < s_.size() && std::isspace((unsigned char)s_[i_])) ++i_;
+    if (at("<?") || at("<!"))
+      error("the first node is not the scene element (a declaration, comment or DOCTYPE; the "
+            "reference takes FirstChild() as the root and cannot load this file)");
     if (i_ >= s_.size() || s_[i_] != '<') error("no root element");
     return parse_element();
   }
@@ -36,15 +43,6 @@ class Reader {
     const size_t k = s_.find(end, i_);
     if (k == std::string::npos) error(std::string("missing ") + end);
     i_ = k + std::strlen(end);
-  }
-  void skip_prolog() {
-    for (;;) {
-      while (i_ < s_.size() && std::isspace((unsigned char)s_[i_])) ++i_;
-      if (at("<?")) skip_to("?>");
-      else if (at("<!--")) skip_to("-->");
-      else if (at("<!")) skip_to(">");
-      else return;
-    }
   }
   static std::string unescape(const std::string& raw) {
     std::string out;

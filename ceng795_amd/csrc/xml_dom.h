@@ -2,9 +2,9 @@
 // ppm_scene.cpp).  Covers what the scene files use: elements, attributes, text, CDATA,
 // comments, processing instructions, the five predefined entities and numeric character
 // references.  tinyxml2 semantics the loaders rely on: GetText() is the element's first child
-// when that child is text; Attribute() is NULL when absent.  Deviation: the reference takes
-// file.FirstChild() as the root, so a leading <?xml?> declaration or comment crashes it
-// (SURVEY appendix B); we skip those and use the first element — a strict superset.
+// when that child is text; Attribute() is NULL when absent; the document's FIRST node is the
+// scene root, so a leading <?xml?> declaration or comment makes the file unloadable, as in the
+// reference — here an error instead of the reference's crash.
 #ifndef CENG795_XML_DOM_H_
 #define CENG795_XML_DOM_H_
 

@@ -196,7 +196,9 @@ int rt_render(rt_scene* scene, int camera_index, int starting_row, int row_strid
  * in flight at the same time (their outputs must not overlap); host threads may enqueue
  * concurrently.  A stream's scratch lives until rt_release_stream_scratch or the scene's
  * destruction.  Multi-device scenes: whole frames only (tile_begin 0, tile_step 1,
- * tile_major 0; row subsets allowed), d_out and hip_stream on devices[0]. */
+ * tile_major 0; row subsets allowed), d_out and hip_stream on devices[0]; every caller stream
+ * gets a context (device stream + buffers) of its own on each device, kept until
+ * rt_release_stream_scratch, so frames on different caller streams overlap on every device. */
 int rt_render_device(rt_scene* scene, int camera_index, int starting_row, int row_stride,
                      int tile_begin, int tile_step, int tile_major, float* d_out,
                      void* hip_stream);

@@ -137,6 +137,33 @@ def test_multi_device_render_device_on_caller_stream(scene_dir, devices):
                             stream=st.cuda_stream)
 
 
+@pytest.mark.parametrize("devices", [[0], [0] * 8])
+def test_multi_device_frames_in_flight_on_streams(scene_dir, devices):
+    """Frames in flight through a multi-device scene: each caller stream renders on contexts of
+    its own (device streams and buffers per caller stream, include/ceng795_rt.h), so three
+    frames per stream on three streams overlap on every device — each bit-identical to the
+    oracle; releasing a stream hands its contexts back and it renders correctly again."""
+    import torch
+    import ceng795_amd
+    xml = scenes.write("soup_depth3", scene_dir)
+    ref, _ = oracle_frame(xml, 0)
+    with ceng795_amd.Scene(xml, devices=devices) as s:
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        for rnd in range(2):
+            bufs = []
+            for k in range(3):
+                for st in streams:
+                    b = torch.full(ref.shape, -1.0, dtype=torch.float32, device="cuda")
+                    st.wait_stream(torch.cuda.current_stream())
+                    s.render_device(0, b.data_ptr(), stream=st.cuda_stream)
+                    bufs.append(b)
+            torch.cuda.synchronize()
+            for b in bufs:
+                assert same(b.cpu().numpy(), ref), (devices, rnd)
+            for st in streams:
+                s.release_stream(st.cuda_stream)
+
+
 def test_multi_device_c3_frame_matches_reference_hash(scene_dir):
     """C3 through the multi-device path (RCCL self send / receive on one GPU) hashes to the
     frame the unmodified reference rendered (tests/golden/golden.json)."""

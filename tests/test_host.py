@@ -132,15 +132,20 @@ def _dump_rc(xml, tmp_path):
     return _lib.lib().rt_host_dump_bvh_xml(xml.encode(), str(tmp_path / "o.txt").encode())
 
 
-def test_xml_declaration_and_comments_are_accepted(scene_dir, tmp_path):
-    """The reference takes file.FirstChild() as root and would crash on a prolog (appendix B);
-    ours skips it — a superset — and builds the identical tree."""
+@pytest.mark.parametrize("prolog", ['<?xml version="1.0"?>\n', "<!-- scene -->\n",
+                                    "  \n<!DOCTYPE Scene>\n"])
+def test_xml_prolog_is_refused_like_the_reference(scene_dir, tmp_path, prolog):
+    """The reference takes file.FirstChild() as root (HW2/Scene.cpp:206): a prolog node becomes
+    the root and the load fails (a crash there, RT_E_PARSE here); comments
+    INSIDE the scene element are fine, and leading whitespace is no node."""
+    v = _variant(scene_dir, tmp_path, lambda t: prolog + t)
+    assert _dump_rc(v, tmp_path) == _lib.RT_E_PARSE
+    assert "FirstChild" in _lib.lib().rt_last_error().decode()
     plain = scenes.write("soup1", scene_dir)
     host_dump_bvh(plain, str(tmp_path / "a.txt"))
-    v = _variant(scene_dir, tmp_path,
-                 lambda t: '<?xml version="1.0"?>\n<!-- scene -->\n' +
-                 t.replace("<Objects>", "<Objects><!-- objects -->"))
-    host_dump_bvh(v, str(tmp_path / "b.txt"))
+    inner = _variant(scene_dir, tmp_path,
+                     lambda t: "\n  " + t.replace("<Objects>", "<Objects><!-- objects -->"))
+    host_dump_bvh(inner, str(tmp_path / "b.txt"))
     assert (tmp_path / "a.txt").read_text() == (tmp_path / "b.txt").read_text()
 
 
