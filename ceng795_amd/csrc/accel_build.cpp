@@ -250,7 +250,13 @@ void decode_slot(const DevNode8& W, int c, double* lo, double* hi) {
 // and eight slot tests per packet, whatever its fill), a treelet's leaf tests kLeafCost per
 // leaf (they run in full-wave batches), each weighted by the surface area of the box that
 // leads there (the chance a ray reaches it).
-constexpr double kNodeCost = 1.0, kLeafCost = 0.3;
+#ifndef RT_WIDE_NODE_COST  // (A/B builds: make exp EXTRA=-DRT_WIDE_LEAF_COST=...)
+#define RT_WIDE_NODE_COST 1.0
+#endif
+#ifndef RT_WIDE_LEAF_COST
+#define RT_WIDE_LEAF_COST 0.3
+#endif
+constexpr double kNodeCost = RT_WIDE_NODE_COST, kLeafCost = RT_WIDE_LEAF_COST;
 
 // Optimal 8-wide collapse of the binary SAH tree (dynamic programme over (binary node, slots)):
 // F[n][k] = least cost of covering n's subtree with k slots (a slot is a treelet, or an inner

@@ -19,6 +19,9 @@
 //   time   <xml> <cam> <threads> <reps> <row_step> [warm]  median wall time of render_image
 //          over rows, after `warm` untimed renders
 //                                                   j = 0 (mod row_step); prints one JSON line
+//   png    <xml> <cam> <out.png> [threads]          the reference's own output file: Pixel::
+//                                                   get_color() + alpha 255 -> lodepng::encode
+//                                                   (HW2/main.cpp:43-57, HW2/lodepng 20180114)
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -29,6 +32,7 @@
 #include <vector>
 
 #include "Bounding_volume_hierarchy.h"
+#include "lodepng/lodepng.h"
 #include "Mesh.h"
 #include "Pixel.h"
 #include "Scene.h"
@@ -124,6 +128,29 @@ int main(int argc, char** argv) {
     std::ofstream f(argv[4], std::ios::binary);
     f.write(reinterpret_cast<const char*>(out.data()), out.size() * sizeof(float));
     delete[] px;
+  } else if (cmd == "png") {
+    const int cam = std::atoi(argv[3]);
+    const int threads = argc > 5 ? std::atoi(argv[5]) : (int)std::thread::hardware_concurrency();
+    const Image_plane& ip = scene.cameras[cam].get_image_plane();
+    const int w = ip.width, h = ip.height;
+    Pixel* px = new Pixel[(size_t)w * h];
+    render_rows(scene, cam, px, 0, 1, threads);
+    std::vector<unsigned char> image((size_t)w * h * 4);
+    size_t idx = 0;
+    for (int j = 0; j < h; j++)
+      for (int i = 0; i < w; i++) {
+        const Vector3i p = px[(size_t)j * w + i].get_color();
+        image[idx++] = (unsigned char)p.x;
+        image[idx++] = (unsigned char)p.y;
+        image[idx++] = (unsigned char)p.z;
+        image[idx++] = 255;
+      }
+    delete[] px;
+    const unsigned err = lodepng::encode(argv[4], image.data(), (unsigned)w, (unsigned)h);
+    if (err) {
+      std::cerr << "lodepng error " << err << std::endl;
+      return 1;
+    }
   } else if (cmd == "bvh") {
     std::ofstream f(argv[3]);
     dump_shape(scene.bvh, f);

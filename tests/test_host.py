@@ -87,25 +87,66 @@ def test_camera_precompute_matches_reference(scene_dir, name):
         assert np.array_equal(d.view(np.uint32), ref.view(np.uint32)), (name, k)
 
 
-def decode_png_rgb(path):
+def png_parts(path):
+    """(IHDR fields, PLTE bytes, inflated IDAT bytes, other chunk types), CRCs checked."""
     data = open(path, "rb").read()
     assert data[:8] == b"\x89PNG\r\n\x1a\n"
-    pos, idat, w = 8, b"", None
+    pos, idat, plte, hdr, other = 8, b"", b"", None, []
     while pos < len(data):
         n = struct.unpack(">I", data[pos:pos + 4])[0]
         typ = data[pos + 4:pos + 8]
         body = data[pos + 8:pos + 8 + n]
         assert struct.unpack(">I", data[pos + 8 + n:pos + 12 + n])[0] == zlib.crc32(typ + body)
         if typ == b"IHDR":
-            w, h, depth, ctype = struct.unpack(">IIBB", body[:10])
-            assert depth == 8 and ctype == 2
+            hdr = struct.unpack(">IIBBBBB", body)
+        elif typ == b"PLTE":
+            plte += body
         elif typ == b"IDAT":
             idat += body
+        elif typ != b"IEND":
+            other.append(typ)
         pos += 12 + n
-    raw = zlib.decompress(idat)
-    rows = [raw[r * (1 + 3 * w) + 1:(r + 1) * (1 + 3 * w)] for r in range(h)]
-    assert all(raw[r * (1 + 3 * w)] == 0 for r in range(h))
-    return np.frombuffer(b"".join(rows), np.uint8).reshape(h, w, 3)
+    return hdr, plte, zlib.decompress(idat), other
+
+
+def decode_png_rgb(path):
+    """A minimal PNG decoder (colour types 0, 2, 3; bit depths 1-8; filters 0-4) -> RGB8."""
+    (w, h, depth, ctype, _, _, interlace), plte, raw, _ = png_parts(path)
+    assert interlace == 0 and ctype in (0, 2, 3)
+    bpp = depth * (3 if ctype == 2 else 1)
+    line, bw = (w * bpp + 7) // 8, max(1, bpp // 8)
+    prev = bytearray(line)
+    out = []
+    for r in range(h):
+        f = raw[r * (line + 1)]
+        cur = bytearray(raw[r * (line + 1) + 1:(r + 1) * (line + 1)])
+        for i in range(line):
+            a = cur[i - bw] if i >= bw else 0
+            b, c = prev[i], (prev[i - bw] if i >= bw else 0)
+            if f == 1:
+                cur[i] = (cur[i] + a) & 255
+            elif f == 2:
+                cur[i] = (cur[i] + b) & 255
+            elif f == 3:
+                cur[i] = (cur[i] + ((a + b) >> 1)) & 255
+            elif f == 4:
+                pa, pb, pc = abs(b - c), abs(a - c), abs(a + b - 2 * c)
+                cur[i] = (cur[i] + (a if pa <= pb and pa <= pc else (b if pb <= pc else c))) & 255
+        out.append(bytes(cur))
+        prev = cur
+    px = np.zeros((h, w, 3), np.uint8)
+    for r, row in enumerate(out):
+        if ctype == 2:
+            px[r] = np.frombuffer(row, np.uint8)[:3 * w].reshape(w, 3)
+            continue
+        bits = np.unpackbits(np.frombuffer(row, np.uint8))[:w * depth].reshape(w, depth)
+        v = bits.dot(1 << np.arange(depth - 1, -1, -1))
+        if ctype == 0:
+            px[r] = (v * (255 // ((1 << depth) - 1)))[:, None]
+        else:
+            pal = np.frombuffer(plte, np.uint8).reshape(-1, 3)
+            px[r] = pal[v]
+    return px
 
 
 def test_png_quantisation_like_pixel_get_color(tmp_path):
@@ -118,6 +159,30 @@ def test_png_quantisation_like_pixel_get_color(tmp_path):
     got = decode_png_rgb(str(path))
     exp = np.array([0, 0, 1, 254, 255, 255, 0, 0, 0, 0, 0, 127], np.uint8)
     assert np.array_equal(got.reshape(2, -1)[0], exp)
+
+
+@pytest.mark.parametrize("name", ["c1", "soup1", "hf_small", "hf_side", "single_sphere"])
+def test_png_matches_the_reference_file(scene_dir, tmp_path, name):
+    """rt_write_png against the PNG the reference itself wrote (HW2/main.cpp:43-57 through its
+    lodepng 20180114, tests/golden/png, make_golden_png.py) for the same frame: the colour type
+    and bit depth lodepng chose (RGB, grey and palette cases), the palette in its order, and the
+    filtered image data are byte-identical; the files differ only in the deflate stream
+    carrying that data (zlib here), so both decode to the same pixels."""
+    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "png", "golden_png.json")))[name]
+    xml = scenes.write(name, scene_dir)
+    assert hashlib.sha256(open(xml, "rb").read()).hexdigest() == meta["xml_sha256"]
+    ref_png = os.path.join(ROOT, "tests", "golden", "png", f"{name}_cam0.png")
+    assert hashlib.sha256(open(ref_png, "rb").read()).hexdigest() == meta["png_sha256"]
+    from oracle.cpu_ref import OracleScene
+    img, _ = OracleScene(xml).render(0, threads=4)  # = the reference's Pixel::color, bit for bit
+    ours = tmp_path / "ours.png"
+    write_png(str(ours), img)
+    a, b = png_parts(ref_png), png_parts(str(ours))
+    assert a[0] == b[0], (a[0], b[0])  # width, height, bit depth, colour type, ...
+    assert a[1] == b[1]                # palette
+    assert a[2] == b[2]                # filter bytes + filtered scanlines
+    assert a[3] == b[3] == []
+    assert np.array_equal(decode_png_rgb(ref_png), decode_png_rgb(str(ours)))
 
 
 # ---------------------------------------------------------------- loader error behaviour
