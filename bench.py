@@ -364,6 +364,7 @@ def share_probe(scene, stream, steps: int, inflight: int, t1_ms: float, ns=(2, 4
             scene.collect_stats()
         slow = max(per)
         out[str(n)] = {"share_ms_max": round(slow, 4), "share_ms_min": round(min(per), 4),
+                       "share_ms_per_rank": [round(x, 4) for x in per],
                        "predicted_efficiency": round(t1_ms / (n * slow), 4),
                        "predicted_Mrays_s_factor": round(t1_ms / slow, 3)}
     return {"t1_ms": round(t1_ms, 4), "frames_in_flight": inflight, "per_n": out,
@@ -557,10 +558,10 @@ def main() -> int:
         renderer = dist_tiles.FrameRenderer(scene, stream, inflight=args.inflight)
     elif tiled:
         layout = dist_tiles.TilePlan(scene, world, rank)
-        renderer = dist_tiles.TileGatherRenderer(layout, stream,
-                                                 dist_tiles.scene_tile_renderer(scene),
-                                                 inflight=args.inflight,
-                                                 host_staging=host_staging, device=dev)
+        renderer = dist_tiles.TileGatherRenderer(
+            layout, stream, dist_tiles.scene_tile_renderer(scene), inflight=args.inflight,
+            host_staging=host_staging, device=dev,
+            untile=None if host_staging else dist_tiles.scene_tile_untiler(scene, layout))
     else:
         owners = dist_tiles.FrameOwners(n_cams, world, rank)
         sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]

@@ -814,6 +814,7 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
   U.tiles_total = tp.tiles_total;
   U.devices = D;
   U.slot = slot;
+  U.tile_offset = 0;
   hip_check(launch_untile(U, x0->stream), "untile launch");
   if (s0 != x0->stream) {
     hip_check(hipEventRecord(x0->ev_out, x0->stream), "event record");
@@ -1084,6 +1085,34 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
       ensure(sc->samples, sc->samples_capacity, sample_floats(c), "alloc MSAA samples");
     }
     enqueue_frame(s, r, P, c.num_samples, sc->samples, (hipStream_t)stream, true);
+    return RT_OK;
+  });
+}
+
+int rt_untile_device(rt_scene* s, int cam, int row0, int row_stride, int devices, int slot,
+                     int tile_offset, const float* d_gathered, float* d_out, void* stream) {
+  return guarded([&] {
+    check_render_args(s, cam, row0, row_stride);
+    if (devices < 1 || slot < 0 || tile_offset < 0 || !d_gathered || !d_out)
+      throw std::invalid_argument("rt_untile_device: bad argument");
+    const rt_camera& c = s->host.cameras[cam];
+    const TilePlan tp = plan(c, row0, row_stride);
+    if ((long long)devices * slot < tp.tiles_total)
+      throw std::invalid_argument("rt_untile_device: devices * slot is smaller than the tile count");
+    DeviceGuard g(s->rep[0]->device);
+    UntileParams U;
+    U.recv = d_gathered;
+    U.out = d_out;
+    U.width = c.width;
+    U.row0 = row0;
+    U.row_stride = row_stride;
+    U.rows = tp.rows;
+    U.tiles_x = tp.tiles_x;
+    U.tiles_total = tp.tiles_total;
+    U.devices = devices;
+    U.slot = slot;
+    U.tile_offset = tile_offset % devices;
+    hip_check(launch_untile(U, (hipStream_t)stream), "untile launch");
     return RT_OK;
   });
 }

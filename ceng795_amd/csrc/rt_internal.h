@@ -166,6 +166,7 @@ struct UntileParams {
   const float* recv;
   float* out;
   int width, row0, row_stride, rows, tiles_x, tiles_total, devices, slot;
+  int tile_offset;  // tile t went to rank (t + tile_offset) mod devices (rt_untile_device)
 };
 
 // Words of the per-stream schedule buffer for a launch of `tiles` selected tiles: tile costs

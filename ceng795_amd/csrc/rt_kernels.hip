@@ -1406,29 +1406,46 @@ __device__ __forceinline__ unsigned unit_cost(const RenderParams& P, int u) {
 
 // One workgroup per region: a bucket sort of the region's units by cost, heaviest first (order
 // inside a bucket is free), into unit_order[x * stride ..]; -1 pads the list to `stride`.
-__global__ __launch_bounds__(1024) void order_kernel(RenderParams P) {
+// 256 threads: with frames in flight the GPU is full of traversal waves, and a bigger workgroup
+// waits for a CU with that many free wave slots (rocprof: 1024-thread order launches averaged
+// 79 us, up to 373, beside other frames' traversal; the sort itself takes 8 us).
+constexpr int kOrderThreads = 256;
+__global__ __launch_bounds__(kOrderThreads) void order_kernel(RenderParams P) {
   __shared__ int hist[kOrderBuckets];
   const int tid = (int)threadIdx.x, x = (int)blockIdx.x;
   const int n = region_units(P, x);
   int* out = P.unit_order + (size_t)x * P.order_stride;
-  for (int i = tid; i < kOrderBuckets; i += 1024) hist[i] = 0;
+  for (int i = tid; i < kOrderBuckets; i += kOrderThreads) hist[i] = 0;
   __syncthreads();
-  for (int i = tid; i < n; i += 1024) atomicAdd(&hist[cost_bucket(unit_cost(P, region_unit(P, x, i)))], 1);
+  for (int i = tid; i < n; i += kOrderThreads)
+    atomicAdd(&hist[cost_bucket(unit_cost(P, region_unit(P, x, i)))], 1);
   __syncthreads();
-  if (tid == 0) {  // exclusive offsets, heaviest bucket first
-    int run = 0;
-    for (int b = kOrderBuckets - 1; b >= 0; b--) {
-      const int c = hist[b];
-      hist[b] = run;
-      run += c;
+  if (tid < 64) {  // exclusive offsets, heaviest bucket first: one wave scans the 256 buckets
+    const int lane = tid;
+    int v[kOrderBuckets / 64], run = 0;
+#pragma unroll
+    for (int k = 0; k < kOrderBuckets / 64; k++) {
+      v[k] = hist[kOrderBuckets - 1 - (lane * (kOrderBuckets / 64) + k)];
+      run += v[k];
+    }
+    int x2 = run;  // inclusive scan of the lane totals
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x2, o, 64);
+      if (lane >= o) x2 += y;
+    }
+    int base = x2 - run;
+#pragma unroll
+    for (int k = 0; k < kOrderBuckets / 64; k++) {
+      hist[kOrderBuckets - 1 - (lane * (kOrderBuckets / 64) + k)] = base;
+      base += v[k];
     }
   }
   __syncthreads();
-  for (int i = tid; i < n; i += 1024) {
+  for (int i = tid; i < n; i += kOrderThreads) {
     const int u = region_unit(P, x, i);
     out[atomicAdd(&hist[cost_bucket(unit_cost(P, u))], 1)] = u;
   }
-  for (int i = n + tid; i < P.order_stride; i += 1024) out[i] = -1;
+  for (int i = n + tid; i < P.order_stride; i += kOrderThreads) out[i] = -1;
 }
 
 // RT_TIMELINE (experiment builds only): every traversal wave records its start and end on the
@@ -1569,7 +1586,7 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
   S.tile_cost = T.tile_cost;
   if (P.num_lights > 0) {
     if (ordered) {  // the shadow kernel LPT-scheduled by the primary kernel's measured times
-      hipLaunchKernelGGL(order_kernel, dim3(S.order_regions), dim3(1024), 0, stream, S);
+      hipLaunchKernelGGL(order_kernel, dim3(S.order_regions), dim3(kOrderThreads), 0, stream, S);
       S.use_order = 1;
     }
     S.tile_cost = nullptr;  // (the shadow kernel reads the order only)
@@ -1646,8 +1663,9 @@ __global__ __launch_bounds__(256) void untile_kernel(UntileParams U) {
   const int tx = t % U.tiles_x, ty = t / U.tiles_x;
   const int px = tx * kTile + (lane & 7), lr = ty * kTile + (lane >> 3);
   if (px >= U.width || lr >= U.rows) return;
-  const float* src =
-      U.recv + ((size_t)((t % U.devices) * U.slot + t / U.devices) * (kTile * kTile) + lane) * 3;
+  const int r = (t + U.tile_offset) % U.devices;
+  const int b = ((r - U.tile_offset) % U.devices + U.devices) % U.devices;  // rank r's first tile
+  const float* src = U.recv + ((size_t)(r * U.slot + (t - b) / U.devices) * (kTile * kTile) + lane) * 3;
   float* dst = U.out + ((size_t)(U.row0 + lr * U.row_stride) * U.width + px) * 3;
   dst[0] = src[0];
   dst[1] = src[1];

@@ -109,6 +109,17 @@ def untile_camera(gathered_c, layout: TileLayout, c: int, index=None, out=None):
     return out[:h, :w]
 
 
+def scene_tile_untiler(scene, layout: TileLayout) -> Callable:
+    """The GPU untile: rt_untile_device of camera c's gathered shares straight into its
+    row-major frame (one wave per tile), on the communication stream."""
+    def untile(c, gathered_c, frame, stream):
+        sh = layout.shares[c]
+        scene.untile_device(c, layout.world, sh.slot, gathered_c.data_ptr(), frame.data_ptr(),
+                            tile_offset=int(layout.offsets[c] % layout.world),
+                            stream=stream.cuda_stream)
+    return untile
+
+
 def scene_tile_renderer(scene) -> Callable:
     """The GPU tile renderer: rt_render_device of camera c's share, tile-major into `slot`."""
     def render(sh: CameraShare, slot, stream):
@@ -171,13 +182,16 @@ class TileGatherRenderer:
     host, one buffer set.  frames: rank 0's frames of the last step (complete after finish())."""
 
     def __init__(self, layout: TileLayout, stream, render: Callable, inflight: int = 2,
-                 host_staging: bool = False, device=None):
+                 host_staging: bool = False, device=None, untile: Optional[Callable] = None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
         self.layout = L = layout
         self.stream = stream
         self.render = render
+        # untile(c, gathered_c [world, slot, 192], frame [h, w, 3], stream): rank 0's untile
+        # (scene_tile_untiler: the library's kernel); None: one index_select into padded frames
+        self.untile = untile
         self.host_staging = host_staging
         self.inflight = 1 if host_staging else max(1, int(inflight))
         F = self.inflight
@@ -214,8 +228,8 @@ class TileGatherRenderer:
                 row = []
                 for (w, h) in L.sizes:
                     tx, ty = tiles_of((w, h))
-                    row.append(torch.empty((ty * TILE, tx * TILE, 3), dtype=torch.float32,
-                                           device=dev))
+                    shape = (h, w, 3) if untile is not None else (ty * TILE, tx * TILE, 3)
+                    row.append(torch.empty(shape, dtype=torch.float32, device=dev))
                 self.padded.append(row)
 
     def _slot(self, s: int, sh: CameraShare):
@@ -233,7 +247,9 @@ class TileGatherRenderer:
             else:
                 outs = list(self.gathered[s][c]) if root else None
                 dist.gather(self._slot(s, sh), outs, dst=0, async_op=True).wait()
-            if root:
+            if root and self.untile is not None:
+                self.untile(c, self.gathered[s][c], self.padded[s][c], self.comm)
+            elif root:
                 untile_camera(self.gathered[s][c].view(-1, TILE_FLOATS), L, c, self.index[c],
                               self.padded[s][c])
 

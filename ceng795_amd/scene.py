@@ -146,6 +146,14 @@ class Scene:
                                            tile_begin, tile_step, tile_count, int(tile_major),
                                            C.c_void_p(out_ptr), C.c_void_p(stream)))
 
+    def untile_device(self, camera_index: int, devices: int, slot: int, gathered_ptr: int,
+                      out_ptr: int, *, tile_offset: int = 0, stream: int = 0) -> None:
+        """rt_untile_device: the gathered [devices][slot][64][3] tile shares of a round-robin
+        deal (tile t to rank (t + tile_offset) mod devices) into the row-major frame."""
+        check(lib().rt_untile_device(self._h, camera_index, 0, 1, devices, slot, tile_offset,
+                                     C.c_void_p(gathered_ptr), C.c_void_p(out_ptr),
+                                     C.c_void_p(stream)))
+
     def release_stream(self, stream: int) -> None:
         """Frees the scratch the library keeps for HIP stream ``stream`` (after waiting for it)."""
         check(lib().rt_release_stream_scratch(self._h, C.c_void_p(stream)))

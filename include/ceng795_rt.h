@@ -210,6 +210,17 @@ int rt_render_device(rt_scene* scene, int camera_index, int starting_row, int ro
 int rt_render_device_range(rt_scene* scene, int camera_index, int starting_row, int row_stride,
                            int tile_begin, int tile_step, int tile_count, int tile_major,
                            float* d_out, void* hip_stream);
+/* The other half of the process-per-GPU tile deal: rank 0 holds every rank's share as
+ * d_gathered[devices][slot][8*8*3] (rank r rendered the frame's tiles t with
+ * (t + tile_offset) mod devices == r, tile-major, in order, into its slot of `slot` tiles — what
+ * one equal-size gather of rt_render_device(tile_begin, tile_step = devices, tile_major = 1)
+ * outputs leaves); this writes them into the row-major frame d_out (rows starting_row +
+ * k*row_stride of camera_index), one wave per tile, on hip_stream (device devices[0] of the
+ * scene).  Replaces nothing in the reference (its threads share one Pixel array,
+ * HW2/main.cpp:33-36): it is the gather's inverse. */
+int rt_untile_device(rt_scene* scene, int camera_index, int starting_row, int row_stride,
+                     int devices, int slot, int tile_offset, const float* d_gathered, float* d_out,
+                     void* hip_stream);
 /* Waits for `hip_stream` and frees the scratch rt_render_device keeps for it (no-op for a
  * stream the scene never rendered on).  Streams that come and go should release theirs. */
 int rt_release_stream_scratch(rt_scene* scene, void* hip_stream);

@@ -13,6 +13,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from ceng795_amd import dist_tiles
 from ceng795_amd.dist_tiles import TILE, TILE_FLOATS, TileLayout, untile_camera
 
 SIZES = [(37, 21), (64, 40), (5, 9), (96, 64)]  # (w, h): ragged edges, tiny frames
@@ -93,6 +94,27 @@ def test_untile_single_process(world):
         g = torch.stack([loc[sh.offset:sh.offset + sh.slot] for loc in locals_])
         got = untile_camera(g.view(-1, TILE_FLOATS), layouts[0], c)
         assert _same(got.contiguous().numpy(), frames[c])
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_library_untile_index_math(world):
+    """rt_untile_device (untile_kernel in rt_kernels.hip) finds frame tile t of camera c at
+    rank r = (t + off) mod world, slot position (t - b) / world with b = (r - off) mod world
+    (off = the camera's first global tile): the same tile TileLayout.row_index maps, for every
+    camera of a multi-camera layout (restated here in numpy; the GPU runs are the bench's
+    gather_verified and test_c4_eight_way_tile_split_matches_oracle)."""
+    sizes = [(64, 40), (24, 24), (1920, 1080)]
+    L = dist_tiles.TileLayout(sizes, world, 0)
+    for c, (w, h) in enumerate(sizes):
+        tx, ty = dist_tiles.tiles_of((w, h))
+        t = np.arange(tx * ty)
+        off = int(L.offsets[c] % world)
+        r = (t + off) % world
+        b = ((r - off) % world + world) % world
+        src = r * L.slots[c] + (t - b) // world
+        idx = L.row_index(c)  # [ty*8, tx] tile rows
+        want = idx[::dist_tiles.TILE, :].reshape(-1) // dist_tiles.TILE
+        assert np.array_equal(src, want), (world, c)
 
 
 @pytest.mark.parametrize("world", [1, 2, 5, 8])
