@@ -142,20 +142,13 @@ struct DeviceGuard {
 // (9.1 GB) run as one batch (one sort, one update launch).  The budget actually used is also
 // capped at a quarter of the device memory free when the pass starts (plus what the scene's
 // slots already hold), so a smaller or shared GPU falls back to more batches instead of failing
-// in hipMalloc.  ppm_set_slot_bytes sets it per scene; CENG795_PPM_SLOT_MB sets the default.
+// in hipMalloc.  ppm_set_batching sets it per scene.
 constexpr int kRRTable = 1 << 20;  // rr(n) tabulated for n < 2^20 (larger n computed inline)
 struct WidenInt {
   __host__ __device__ long long operator()(int x) const { return (long long)x; }
 };
 
-size_t default_slot_bytes() {
-  static const size_t v = [] {
-    const char* e = std::getenv("CENG795_PPM_SLOT_MB");
-    const long long mb = e ? std::atoll(e) : 0;
-    return mb > 0 ? size_t(mb) << 20 : size_t(16) << 30;
-  }();
-  return v;
-}
+size_t default_slot_bytes() { return size_t(16) << 30; }
 
 }  // namespace
 
@@ -287,29 +280,20 @@ struct ppm_scene {
 
 namespace {
 
-// Longest-first update order (tile_work_kernel); CENG795_PPM_LPT=0 keeps the group order for
-// A/B timing.  The order cannot change results: tiles own disjoint hit points.
-bool lpt_order() {
-  static const bool on = [] {
-    const char* e = std::getenv("CENG795_PPM_LPT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// Longest-first update order (tile_work_kernel); PPM_LPT_ORDER=0 (an exp build) keeps the group
+// order for A/B timing.  The order cannot change results: tiles own disjoint hit points.
+#ifndef PPM_LPT_ORDER
+#define PPM_LPT_ORDER 1
+#endif
+bool lpt_order() { return PPM_LPT_ORDER != 0; }
 
 // Tile-list compaction in the update pass (group_update_kernel phase (0)): tiles whose group
 // list holds at least this many deposits copy the reachable ones first.  Results do not depend
 // on it (the copy is a superset of every window's candidates, in order).
-// CENG795_PPM_COMPACT sets the default (0: off); ppm_set_update_compaction sets it per scene.
+// ppm_set_update_compaction sets it per scene (0: off).
 constexpr int kCompactShift = 2;  // scratch per compacted tile: a quarter of its list
 constexpr int kDefaultCompactSeg = 32768;  // deposits per compaction segment
-long long default_compact_min() {
-  static const long long v = [] {
-    const char* e = std::getenv("CENG795_PPM_COMPACT");
-    return e ? std::max(0LL, std::atoll(e)) : 65536LL;
-  }();
-  return v;
-}
+long long default_compact_min() { return 65536LL; }
 
 template <typename T>
 const T* own(ppm_scene* s, const std::vector<T>& v, const char* what) {
@@ -335,7 +319,9 @@ void create_device(ppm_scene* s, int device) {
   S.top_root = h.top_root;
   S.max_depth = h.max_depth;
   S.eps = h.eps;
-  if (const char* d = std::getenv("CENG795_PPM_DIAG")) S.diag = std::atoi(d);  // experiments
+#ifdef PPM_DIAG_LEVEL  // experiment builds (make ppm-exp EXTRA=-DPPM_DIAG_LEVEL=2): diag counters
+  S.diag = PPM_DIAG_LEVEL;
+#endif
   S.compact_seg = kDefaultCompactSeg;
   std::memcpy(S.light_pos, h.lights.data(), 12);  // lights[0] (Scene.cpp:97)
   std::memcpy(S.light_intensity, h.lights.data() + 3, 12);

@@ -9,6 +9,13 @@
 #   tools/gpu.sh <out> ab <variants> [rounds]      same-box A/B of library builds (tools/ab.py)
 #   tools/gpu.sh <out> kt <name> [kt args]         per-kernel HIP-event times (tools/kt.py)
 #   tools/gpu.sh <out> pmc <workload> [round]      PMC traffic passes -> <out>/traffic_<w>.json
+#   tools/gpu.sh <out> work <name> [workload] [lib] traversal work counters (RT_DIAG build,
+#                                                  tools/kernel_work.py; lib default "diag")
+#   tools/gpu.sh <out> ppmab "<variants>" [rounds] C5 frames of lib/libceng795_ppm_<v>.so builds
+#                                                  ("base" = the shipping one), interleaved
+#   tools/gpu.sh <out> ppmdiag <variant>           C5 per-phase update-pass counters of an exp
+#                                                  build made with -DPPM_DIAG_LEVEL=2
+#                                                  (-DPPM_PHASE_TIMERS=1 for the phase timers)
 #
 # <out> is a directory under gpurun_out/.
 set -o pipefail
@@ -49,6 +56,25 @@ case "$CMD" in
     LIB=ceng795_amd/lib/libceng795_rt.so; [ "$W" = c5 ] && LIB=ceng795_amd/lib/libceng795_ppm.so
     python3 tools/pmc_traffic.py --fetch "$O/pmc_$W/fetch" --write "$O/pmc_$W/write" --workload "$W" \
       --round "$R" --lib "$LIB" --out "$O/traffic_$W.json" || exit 1 ;;
+  work)
+    N=${1:?name}; W=${2:-c3}; L=${3:-diag}
+    X=$(python3 -c "import bench; print(bench.scene_path('$W', 1))") || exit 1
+    timeout -k 10 300 env CENG795_LIB=$L python3 tools/kernel_work.py "$X" > "$O/$N.json" 2> "$O/$N.err" \
+      || { tail -20 "$O/$N.err"; exit 1; }
+    cat "$O/$N.json" ;;
+  ppmab)
+    V=${1:?variants}; R=${2:-2}
+    for r in $(seq "$R"); do for v in $V; do
+      L=$v; [ "$v" = base ] && L=
+      CENG795_PPM_LIB=$L timeout -k 10 200 python3 -u bench.py --workload c5 --steps 3 --warmup 1 \
+        --no-cpu-baseline > "$O/c5_$v$r.json" 2> "$O/c5_$v$r.err" || { tail -5 "$O/c5_$v$r.err"; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/c5_$v$r.json')); print('$v', d['ms_per_step'], d['value'], d['roofline']['kernel_ms_avg'])"
+    done; done ;;
+  ppmdiag)
+    V=${1:?variant}
+    CENG795_PPM_LIB=$V timeout -k 10 200 python3 -u bench.py --workload c5 --steps 1 --warmup 1 \
+      --no-cpu-baseline > "$O/c5d_$V.json" 2> "$O/c5d_$V.err" || { tail -5 "$O/c5d_$V.err"; exit 1; }
+    grep "ppm diag" "$O/c5d_$V.err" | tail -1 ;;
   *)
     echo "unknown command $CMD" >&2; exit 2 ;;
 esac
