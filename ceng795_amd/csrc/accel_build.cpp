@@ -542,6 +542,8 @@ std::string check_accel(const HostScene& s, int K, long long stats[4]) {
     order.push_back(idx);
     stats[2] = std::max<long long>(stats[2], f.depth);
     int valid = 0, r = 0;
+    const unsigned vbits = (unsigned)W.kinds & 0xffu;
+    if (vbits & (vbits + 1)) return "valid slots not first";  // the kernel stops at the first invalid
     for (int c = 0; c < kWideSlots; c++) {
       if (!(W.kinds & (kSlotValid << c))) {
         if (W.box[c][0] != (0x7e00u | 0x7e000000u)) return "invalid slot without NaN planes";

@@ -558,17 +558,36 @@ __device__ __forceinline__ float half_hi(int w) {
 // guard decision is taken there); of the entered inner slots one becomes `node` (SHADOW: the
 // nearest by the entry distance of the first entering lane, so occluders turn up early) and the
 // others are pushed.  `alive`: lanes still searching.  Returns false when the walk is over.
-template <bool SKIP, bool SHADOW, bool DEEP, bool SPHERES>
+// COH (a sign-coherent packet: every active ray's direction has the same sign per axis, none
+// below the axis-skip threshold; `neg` bit a = that sign is negative): the entry plane of each
+// axis is the same for every lane, so the slot words of the negative axes have their fp16
+// halves swapped once per visit (SALU) and a slot's near / far distances are three fma each,
+// with no per-lane min / max.
+template <bool SKIP, bool SHADOW, bool DEEP, bool SPHERES, bool COH = false>
 __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode* __restrict__ nodes,
                                            WaveLeafLds& L, int& pending, const LaneRay& r, float thr,
                                            int& node, uint64_t& m, uint64_t alive,
-                                           WaveStack<DEEP>& st, Diag& dg) {
+                                           WaveStack<DEEP>& st, Diag& dg, int neg = 0) {
   v16i a, b;
   load_node8(nodes, node & ~kWideTag, a, b);
+  if (COH) {
+#pragma unroll
+    for (int x = 0; x < 3; x++) {
+      if (!(neg & (1 << x))) continue;
+#pragma unroll
+      for (int c = 0; c < kWideSlots; c++) {
+        const int k = 8 + 3 * c + x;
+        const unsigned w = (unsigned)(k < 16 ? a[k] : b[k - 16]);
+        const int sw = (int)((w >> 16) | (w << 16));
+        if (k < 16) a[k] = sw; else b[k - 16] = sw;
+      }
+    }
+  }
   const unsigned scale = (unsigned)a[3];
   const int inner_base = a[4], leaf_base = a[5], kinds = a[6];
   const unsigned offs = (unsigned)a[7];
   const unsigned inner = (unsigned)kinds & ~((unsigned)kinds >> 8) & 0xffu;
+  const int nslots = __builtin_popcount((unsigned)kinds & 0xffu);  // valid slots come first
   DIAG(dg.nodes++; dg.wide++; dg.node_lanes += __builtin_popcountll(m));
   const float o[3] = {r.o.x, r.o.y, r.o.z}, rc[3] = {r.r.x, r.r.y, r.r.z}, mg[3] = {r.m.x, r.m.y, r.m.z};
   float S[3], Alo[3], Ahi[3];
@@ -576,22 +595,24 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
   for (int x = 0; x < 3; x++) {
     S[x] = __builtin_amdgcn_ldexpf(rc[x], (int)((scale >> (8 * x)) & 255u) - 128);
     const float A = (__int_as_float(a[x]) - o[x]) * rc[x];
-    Alo[x] = A - mg[x];
-    Ahi[x] = A + mg[x];
+    // lo plane down, hi plane up (mg has the sign of 1/d); COH: near plane in, far plane out
+    Alo[x] = COH ? A - __builtin_fabsf(mg[x]) : A - mg[x];
+    Ahi[x] = COH ? A + __builtin_fabsf(mg[x]) : A + mg[x];
   }
   int nxt = -1;
   uint64_t nm = 0;
   unsigned nkey = 0;
 #pragma unroll
   for (int c = 0; c < kWideSlots; c++) {
+    if (c >= nslots) break;  // (the NaN planes of an invalid slot would fail the test anyway)
     float n3[3], f3[3];
 #pragma unroll
     for (int x = 0; x < 3; x++) {
       const int w = RT_NODE_WORD(8 + 3 * c + x);
       const float tl = __builtin_fmaf(half_lo(w), S[x], Alo[x]);
       const float th = __builtin_fmaf(half_hi(w), S[x], Ahi[x]);
-      n3[x] = __builtin_fminf(tl, th);
-      f3[x] = __builtin_fmaxf(tl, th);
+      n3[x] = COH ? tl : __builtin_fminf(tl, th);
+      f3[x] = COH ? th : __builtin_fmaxf(tl, th);
     }
     if (SKIP) {
       const bool sk[3] = {r.skip0, r.skip1, r.skip2};
@@ -652,10 +673,11 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
 // The reference's (t, leaf) for every active ray: leaf < 0 = miss.  FAST: the 8-wide culling
 // tree over reference treelets (the launch takes it only when the scene has one); otherwise
 // the reference tree itself.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES>
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, bool COH = false>
 __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode* __restrict__ nodes,
                                             int* spill, WaveLeafLds& L, const LaneRay& r,
-                                            bool active, float& best_t, int& best_leaf, Diag& dg) {
+                                            bool active, float& best_t, int& best_leaf, Diag& dg,
+                                            int neg = 0) {
   best_t = RT_INF;
   best_leaf = -1;
   if (P.root_kind != kRootNode) {  // the root IS the primitive (BVH.h:13-14): its own rule
@@ -691,7 +713,8 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
       pending = 0;
     }
     if constexpr (FAST) {
-      if (!visit_wide<SKIP, false, DEEP, SPHERES>(P, nodes, L, pending, r, 0.0f, node, m, ~0ull, st, dg))
+      if (!visit_wide<SKIP, false, DEEP, SPHERES, COH>(P, nodes, L, pending, r, 0.0f, node, m, ~0ull,
+                                                       st, dg, neg))
         break;
     } else {
       const DevNode N = nodes[node];
@@ -715,10 +738,10 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
 // ------------------------------------------------------------------ shadow (any hit)
 // Occluded iff some leaf the ray may reach has 0 < t < thr — identical to the reference's
 // closest-hit shadow test `0 < t_closest < dist - eps` (HW2/Scene.cpp:123-127), appendix A.7.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES>
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, bool COH = false>
 __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* __restrict__ nodes,
                                          int* spill, WaveLeafLds& L, const LaneRay& r, bool active,
-                                         float thr, Diag& dg) {
+                                         float thr, Diag& dg, int neg = 0) {
   if (P.root_kind != kRootNode) {
     float t;
     return active && leaf_test<SPHERES>(P.prims, P.root_ref, r, t) && t < thr && t > 0.0f;
@@ -753,7 +776,8 @@ __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* _
       if (!m && !st.pop_live(node, m, alive)) break;
     }
     if constexpr (FAST) {
-      if (!visit_wide<SKIP, true, DEEP, SPHERES>(P, nodes, L, pending, r, thr, node, m, alive, st, dg))
+      if (!visit_wide<SKIP, true, DEEP, SPHERES, COH>(P, nodes, L, pending, r, thr, node, m, alive,
+                                                      st, dg, neg))
         break;
     } else {
       const DevNode N = nodes[node];
@@ -868,6 +892,23 @@ __device__ __forceinline__ unsigned long long* counter_row(const RenderParams& P
 __device__ __forceinline__ float hit_t(int2_t rec) { return __int_as_float(rec.y); }
 __device__ __forceinline__ int hit_leaf(int2_t rec) { return rec.x; }
 
+// Sign-coherence of a packet's rays (see visit_wide's COH): -1 when some active lane has a
+// skipped axis or the active lanes' direction signs differ on some axis, else the negative-axis
+// bits.  Off (always -1) unless built with RT_COHERENT.
+#ifndef RT_COHERENT
+#define RT_COHERENT 0
+#endif
+__device__ __forceinline__ int packet_signs(const LaneRay& r, bool active) {
+  if (!RT_COHERENT) return -1;
+  const uint64_t act = ballot(active);
+  if (ballot(active && (r.skip0 || r.skip1 || r.skip2))) return -1;
+  const uint64_t nx = ballot(active && __float_as_int(r.r.x) < 0);
+  const uint64_t ny = ballot(active && __float_as_int(r.r.y) < 0);
+  const uint64_t nz = ballot(active && __float_as_int(r.r.z) < 0);
+  if ((nx && nx != act) || (ny && ny != act) || (nz && nz != act)) return -1;
+  return (nx ? 1 : 0) | (ny ? 2 : 0) | (nz ? 4 : 0);
+}
+
 // One wave = the 8x8 packet of selected tile `sel` (< num_sel_tiles): closest hit per pixel
 // into its 8-B record.
 template <bool FAST, bool DEEP, bool SPHERES>
@@ -884,8 +925,11 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
   Diag dg;
   float t;
   int leaf;
+  const int neg = FAST ? packet_signs(ray, q.valid) : -1;
   if (ballot(any_skip))
     closest_hit<true, FAST, DEEP, SPHERES>(P, nodes, spill, L, ray, q.valid, t, leaf, dg);
+  else if (FAST && RT_COHERENT && neg >= 0)
+    closest_hit<false, FAST, DEEP, SPHERES, true>(P, nodes, spill, L, ray, q.valid, t, leaf, dg, neg);
   else
     closest_hit<false, FAST, DEEP, SPHERES>(P, nodes, spill, L, ray, q.valid, t, leaf, dg);
   const RenderParams& Pw = fresh_params(P);  // post-traversal fields: not live across it
@@ -943,9 +987,12 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       const LaneRay sr = make_ray(pk + wi * P.eps, wi, P.quot_ok);  // p + eps * w_i
       const float thr = dist - P.eps;
       const bool any_skip = hit && (sr.skip0 || sr.skip1 || sr.skip2);
-      const bool occ = ballot(any_skip)
-                           ? occluded<true, FAST, DEEP, SPHERES>(P, nodes, spill, L, sr, hit, thr, dg)
-                           : occluded<false, FAST, DEEP, SPHERES>(P, nodes, spill, L, sr, hit, thr, dg);
+      const int neg = FAST ? packet_signs(sr, hit && thr > 0.0f) : -1;
+      const bool occ =
+          ballot(any_skip) ? occluded<true, FAST, DEEP, SPHERES>(P, nodes, spill, L, sr, hit, thr, dg)
+          : (FAST && RT_COHERENT && neg >= 0)
+              ? occluded<false, FAST, DEEP, SPHERES, true>(P, nodes, spill, L, sr, hit, thr, dg, neg)
+              : occluded<false, FAST, DEEP, SPHERES>(P, nodes, spill, L, sr, hit, thr, dg);
       bits |= (occ ? 1u : 0u) << (li - 32 * w);
     }
     const RenderParams& Pw = fresh_params(P0);
