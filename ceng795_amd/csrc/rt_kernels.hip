@@ -87,6 +87,10 @@ __device__ __forceinline__ LaneRay make_ray(V3 o, V3 d, int scene_quot_ok) {
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+// This lane's bit of a wave-uniform mask, as the exec mask itself (s_and_saveexec) — written as
+// (m >> lane) & 1 the compiler keeps a 64-bit 1 << lane per lane (two VGPRs, spilled in the
+// traversal kernels) and tests it with v_and + v_cmp_u64 at every queue push.
+__device__ __forceinline__ bool lane_in(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 // Lane masks of one fp32 compare, straight from the v_cmp (ballot of a combined boolean makes
 // the compiler round-trip it through a VGPR: v_cndmask + v_cmp per mask).  LLVM FCmp
 // predicates; ordered, so NaN gives false as the C++ operators do.
@@ -427,7 +431,7 @@ constexpr unsigned long long kNoHitKey = (0x7f800000ull << 32) | 0xffffffffull; 
 // Queue leaf `leaf` for the lanes of `m` (wave-uniform); n = pending entries (wave-uniform).
 __device__ __forceinline__ void batch_push(WaveLeafLds& L, int& n, int leaf, uint64_t m) {
   const int lane = lane_id();
-  if ((m >> lane) & 1) {
+  if (lane_in(m)) {
     const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                      __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
     L.q[n + below] = ((unsigned long long)lane << 32) | (unsigned)leaf;
@@ -439,7 +443,7 @@ __device__ __forceinline__ void batch_push(WaveLeafLds& L, int& n, int leaf, uin
 // adjacent (one 16-B LDS write), the queue order does not matter.
 __device__ __forceinline__ void batch_push_pair(WaveLeafLds& L, int& n, int leaf, uint64_t m) {
   const int lane = lane_id();
-  if ((m >> lane) & 1) {
+  if (lane_in(m)) {
     const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                      __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
     const unsigned long long hi = (unsigned long long)lane << 32;
@@ -720,7 +724,7 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
       const DevNode N = nodes[node];
       bool h0, h1;
       float t0, t1;
-      visit_node<SKIP>(N, r, (m >> lane) & 1, h0, h1, t0, t1);
+      visit_node<SKIP>(N, r, lane_in(m), h0, h1, t0, t1);
       DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m));
       queue_binary_leaves(L, pending, N, h0, h1, ~0ull, dg);
       // leaves are queued; only inner children are entered
@@ -783,7 +787,7 @@ __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* _
       const DevNode N = nodes[node];
       bool h0, h1;
       float t0, t1;
-      visit_node<SKIP>(N, r, (m >> lane) & 1, h0, h1, t0, t1);
+      visit_node<SKIP>(N, r, lane_in(m), h0, h1, t0, t1);
       DIAG(dg.nodes++; dg.node_lanes += __builtin_popcountll(m));
       queue_binary_leaves(L, pending, N, h0, h1, alive, dg);  // the still-unoccluded lanes
       const uint64_t m0 = N.child[0] >= 0 ? ballot(h0) & alive : 0ull;

@@ -13,6 +13,7 @@
 #                                                  tools/kernel_work.py; lib default "diag")
 #   tools/gpu.sh <out> ppmab "<variants>" [rounds] C5 frames of lib/libceng795_ppm_<v>.so builds
 #                                                  ("base" = the shipping one), interleaved
+#   tools/gpu.sh <out> py <name> <script> [args]   any tools/ script -> <out>/<name>.json
 #   tools/gpu.sh <out> ppmdiag <variant>           C5 per-phase update-pass counters of an exp
 #                                                  build made with -DPPM_DIAG_LEVEL=2
 #                                                  (-DPPM_PHASE_TIMERS=1 for the phase timers)
@@ -62,6 +63,10 @@ case "$CMD" in
     timeout -k 10 300 env CENG795_LIB=$L python3 tools/kernel_work.py "$X" > "$O/$N.json" 2> "$O/$N.err" \
       || { tail -20 "$O/$N.err"; exit 1; }
     cat "$O/$N.json" ;;
+  py)
+    N=${1:?name}; S=${2:?script}; shift 2
+    timeout -k 10 600 python3 -u "$S" "$@" > "$O/$N.json" 2> "$O/$N.err" || { tail -20 "$O/$N.err"; exit 1; }
+    tail -c 2000 "$O/$N.json" ;;
   ppmab)
     V=${1:?variants}; R=${2:-2}
     for r in $(seq "$R"); do for v in $V; do
