@@ -256,7 +256,11 @@ void decode_slot(const DevNode8& W, int c, double* lo, double* hi) {
 #ifndef RT_WIDE_LEAF_COST
 #define RT_WIDE_LEAF_COST 0.3
 #endif
-constexpr double kNodeCost = RT_WIDE_NODE_COST, kLeafCost = RT_WIDE_LEAF_COST;
+#ifndef RT_WIDE_SLOT_COST  // per valid slot of a visit (the kernel tests only the valid slots)
+#define RT_WIDE_SLOT_COST 0.0
+#endif
+constexpr double kNodeCost = RT_WIDE_NODE_COST, kLeafCost = RT_WIDE_LEAF_COST,
+                 kSlotCost = RT_WIDE_SLOT_COST;
 
 // Optimal 8-wide collapse of the binary SAH tree (dynamic programme over (binary node, slots)):
 // F[n][k] = least cost of covering n's subtree with k slots (a slot is a treelet, or an inner
@@ -300,9 +304,12 @@ struct WideCollapse {
         }
       }
     T[n] = INFINITY;
+    Box bn = B.nodes[n].box[0];
+    bn.grow(B.nodes[n].box[1]);
+    const double slot = kSlotCost * bn.area();
     for (int k = 2; k <= kWideSlots; k++)
-      if (F[n][k] < T[n]) {
-        T[n] = F[n][k];
+      if (F[n][k] + slot * k < T[n]) {
+        T[n] = F[n][k] + slot * k;
         tk[n] = (signed char)k;
       }
   }

@@ -64,6 +64,7 @@ struct LaneRay {
   V3 m;       // 2^-18 |o| / d per axis: the ray's share of the culling margin (visit_wide)
   bool skip0, skip1, skip2;  // |d_i| < 1e-6: axis ignored (HW2/bounding_box.cpp:21)
   bool quot;  // origin and scene in the shared-reciprocal range (tri_quotients)
+  int sh0, sh1, sh2;  // 16 where 1/d_i < 0 (the slot's hi plane is the entry plane), else 0
 };
 
 __device__ __forceinline__ bool quot_coord(float x) {  // quot_coord_ok of rt_internal.h
@@ -82,6 +83,9 @@ __device__ __forceinline__ LaneRay make_ray(V3 o, V3 d, int scene_quot_ok) {
   r.skip1 = __builtin_fabsf(d.y) < kEps;
   r.skip2 = __builtin_fabsf(d.z) < kEps;
   r.quot = scene_quot_ok && quot_coord(o.x) && quot_coord(o.y) && quot_coord(o.z);
+  r.sh0 = (int)((__float_as_uint(r.r.x) >> 27) & 16u);
+  r.sh1 = (int)((__float_as_uint(r.r.y) >> 27) & 16u);
+  r.sh2 = (int)((__float_as_uint(r.r.z) >> 27) & 16u);
   return r;
 }
 
@@ -555,38 +559,26 @@ __device__ __forceinline__ float half_hi(int w) {
 #define RT_NODE_WORD(k) ((k) < 16 ? a[(k)] : b[(k) - 16])
 
 // One packet visit of an 8-wide culling node.  Every slot takes a plain slab test on its
-// conservative box (plane t = fma(h, 2^k / d, (origin - o) / d), the lo planes moved down and
-// the hi planes up by the ray's own margin 2^-18 |o| — DESIGN.md §4.2: with the host's margin
-// the test never culls a treelet the reference would enter, so no decision band is needed);
-// an invalid slot's NaN planes fail it.  A leafy slot's leaves go to the leaf queue (the exact
+// conservative box (plane t = fma(h, 2^k / d, (origin - o) / d), the entry plane moved earlier
+// and the exit plane later by the ray's own margin 2^-18 |o| / |d| — DESIGN.md §4.2: with the
+// host's margin the test never culls a treelet the reference would enter, so no decision band
+// is needed); the valid slots come first and the visit stops at the first invalid one (whose
+// NaN planes would fail the test anyway).  A leafy slot's leaves go to the leaf queue (the exact
 // guard decision is taken there); of the entered inner slots one becomes `node` (SHADOW: the
 // nearest by the entry distance of the first entering lane, so occluders turn up early) and the
 // others are pushed.  `alive`: lanes still searching.  Returns false when the walk is over.
-// COH (a sign-coherent packet: every active ray's direction has the same sign per axis, none
-// below the axis-skip threshold; `neg` bit a = that sign is negative): the entry plane of each
-// axis is the same for every lane, so the slot words of the negative axes have their fp16
-// halves swapped once per visit (SALU) and a slot's near / far distances are three fma each,
-// with no per-lane min / max.
-template <bool SKIP, bool SHADOW, bool DEEP, bool SPHERES, bool COH = false>
+// Plane order per lane: a slot word holds the lo plane in its low half and the hi plane in its
+// high half; one v_alignbit by the ray's sh (16 where 1/d < 0) puts the lane's ENTRY plane low,
+// so a slot costs 3 alignbit + 6 fma_mix + max3 + min3 + 2 compares instead of a min and a max
+// per axis on top (same values: the entry plane moved down, the exit plane up by |m|).  A
+// skipped axis (SKIP) gets S = 0 and planes -inf / +inf, once per visit.
+template <bool SKIP, bool SHADOW, bool DEEP, bool SPHERES>
 __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode* __restrict__ nodes,
                                            WaveLeafLds& L, int& pending, const LaneRay& r, float thr,
                                            int& node, uint64_t& m, uint64_t alive,
-                                           WaveStack<DEEP>& st, Diag& dg, int neg = 0) {
+                                           WaveStack<DEEP>& st, Diag& dg) {
   v16i a, b;
   load_node8(nodes, node & ~kWideTag, a, b);
-  if (COH) {
-#pragma unroll
-    for (int x = 0; x < 3; x++) {
-      if (!(neg & (1 << x))) continue;
-#pragma unroll
-      for (int c = 0; c < kWideSlots; c++) {
-        const int k = 8 + 3 * c + x;
-        const unsigned w = (unsigned)(k < 16 ? a[k] : b[k - 16]);
-        const int sw = (int)((w >> 16) | (w << 16));
-        if (k < 16) a[k] = sw; else b[k - 16] = sw;
-      }
-    }
-  }
   const unsigned scale = (unsigned)a[3];
   const int inner_base = a[4], leaf_base = a[5], kinds = a[6];
   const unsigned offs = (unsigned)a[7];
@@ -594,14 +586,20 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
   const int nslots = __builtin_popcount((unsigned)kinds & 0xffu);  // valid slots come first
   DIAG(dg.nodes++; dg.wide++; dg.node_lanes += __builtin_popcountll(m));
   const float o[3] = {r.o.x, r.o.y, r.o.z}, rc[3] = {r.r.x, r.r.y, r.r.z}, mg[3] = {r.m.x, r.m.y, r.m.z};
+  const int sh[3] = {r.sh0, r.sh1, r.sh2};
   float S[3], Alo[3], Ahi[3];
 #pragma unroll
   for (int x = 0; x < 3; x++) {
     S[x] = __builtin_amdgcn_ldexpf(rc[x], (int)((scale >> (8 * x)) & 255u) - 128);
     const float A = (__int_as_float(a[x]) - o[x]) * rc[x];
-    // lo plane down, hi plane up (mg has the sign of 1/d); COH: near plane in, far plane out
-    Alo[x] = COH ? A - __builtin_fabsf(mg[x]) : A - mg[x];
-    Ahi[x] = COH ? A + __builtin_fabsf(mg[x]) : A + mg[x];
+    Alo[x] = A - __builtin_fabsf(mg[x]);  // entry plane earlier
+    Ahi[x] = A + __builtin_fabsf(mg[x]);  // exit plane later
+    if (SKIP) {  // a skipped axis: every plane at -inf / +inf (fma(h, 0, -+inf), h finite)
+      const bool sk = x == 0 ? r.skip0 : (x == 1 ? r.skip1 : r.skip2);
+      S[x] = sk ? 0.0f : S[x];
+      Alo[x] = sk ? -RT_INF : Alo[x];
+      Ahi[x] = sk ? RT_INF : Ahi[x];
+    }
   }
   int nxt = -1;
   uint64_t nm = 0;
@@ -612,19 +610,12 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
     float n3[3], f3[3];
 #pragma unroll
     for (int x = 0; x < 3; x++) {
-      const int w = RT_NODE_WORD(8 + 3 * c + x);
-      const float tl = __builtin_fmaf(half_lo(w), S[x], Alo[x]);
-      const float th = __builtin_fmaf(half_hi(w), S[x], Ahi[x]);
-      n3[x] = COH ? tl : __builtin_fminf(tl, th);
-      f3[x] = COH ? th : __builtin_fmaxf(tl, th);
-    }
-    if (SKIP) {
-      const bool sk[3] = {r.skip0, r.skip1, r.skip2};
-#pragma unroll
-      for (int x = 0; x < 3; x++) {
-        n3[x] = sk[x] ? -RT_INF : n3[x];
-        f3[x] = sk[x] ? RT_INF : f3[x];
-      }
+      // this lane's entry plane into the low half
+      const int w = (int)__builtin_amdgcn_alignbit((unsigned)RT_NODE_WORD(8 + 3 * c + x),
+                                                   (unsigned)RT_NODE_WORD(8 + 3 * c + x),
+                                                   (unsigned)sh[x]);
+      n3[x] = __builtin_fmaf(half_lo(w), S[x], Alo[x]);
+      f3[x] = __builtin_fmaf(half_hi(w), S[x], Ahi[x]);
     }
     const float tn = __builtin_fmaxf(__builtin_fmaxf(n3[0], n3[1]), n3[2]);
     const float tf = __builtin_fminf(__builtin_fminf(f3[0], f3[1]), f3[2]);
@@ -677,11 +668,10 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
 // The reference's (t, leaf) for every active ray: leaf < 0 = miss.  FAST: the 8-wide culling
 // tree over reference treelets (the launch takes it only when the scene has one); otherwise
 // the reference tree itself.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, bool COH = false>
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES>
 __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode* __restrict__ nodes,
                                             int* spill, WaveLeafLds& L, const LaneRay& r,
-                                            bool active, float& best_t, int& best_leaf, Diag& dg,
-                                            int neg = 0) {
+                                            bool active, float& best_t, int& best_leaf, Diag& dg) {
   best_t = RT_INF;
   best_leaf = -1;
   if (P.root_kind != kRootNode) {  // the root IS the primitive (BVH.h:13-14): its own rule
@@ -717,8 +707,7 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
       pending = 0;
     }
     if constexpr (FAST) {
-      if (!visit_wide<SKIP, false, DEEP, SPHERES, COH>(P, nodes, L, pending, r, 0.0f, node, m, ~0ull,
-                                                       st, dg, neg))
+      if (!visit_wide<SKIP, false, DEEP, SPHERES>(P, nodes, L, pending, r, 0.0f, node, m, ~0ull, st, dg))
         break;
     } else {
       const DevNode N = nodes[node];
@@ -742,10 +731,10 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
 // ------------------------------------------------------------------ shadow (any hit)
 // Occluded iff some leaf the ray may reach has 0 < t < thr — identical to the reference's
 // closest-hit shadow test `0 < t_closest < dist - eps` (HW2/Scene.cpp:123-127), appendix A.7.
-template <bool SKIP, bool FAST, bool DEEP, bool SPHERES, bool COH = false>
+template <bool SKIP, bool FAST, bool DEEP, bool SPHERES>
 __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* __restrict__ nodes,
                                          int* spill, WaveLeafLds& L, const LaneRay& r, bool active,
-                                         float thr, Diag& dg, int neg = 0) {
+                                         float thr, Diag& dg) {
   if (P.root_kind != kRootNode) {
     float t;
     return active && leaf_test<SPHERES>(P.prims, P.root_ref, r, t) && t < thr && t > 0.0f;
@@ -780,8 +769,7 @@ __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* _
       if (!m && !st.pop_live(node, m, alive)) break;
     }
     if constexpr (FAST) {
-      if (!visit_wide<SKIP, true, DEEP, SPHERES, COH>(P, nodes, L, pending, r, thr, node, m, alive,
-                                                      st, dg, neg))
+      if (!visit_wide<SKIP, true, DEEP, SPHERES>(P, nodes, L, pending, r, thr, node, m, alive, st, dg))
         break;
     } else {
       const DevNode N = nodes[node];
@@ -896,23 +884,6 @@ __device__ __forceinline__ unsigned long long* counter_row(const RenderParams& P
 __device__ __forceinline__ float hit_t(int2_t rec) { return __int_as_float(rec.y); }
 __device__ __forceinline__ int hit_leaf(int2_t rec) { return rec.x; }
 
-// Sign-coherence of a packet's rays (see visit_wide's COH): -1 when some active lane has a
-// skipped axis or the active lanes' direction signs differ on some axis, else the negative-axis
-// bits.  Off (always -1) unless built with RT_COHERENT.
-#ifndef RT_COHERENT
-#define RT_COHERENT 0
-#endif
-__device__ __forceinline__ int packet_signs(const LaneRay& r, bool active) {
-  if (!RT_COHERENT) return -1;
-  const uint64_t act = ballot(active);
-  if (ballot(active && (r.skip0 || r.skip1 || r.skip2))) return -1;
-  const uint64_t nx = ballot(active && __float_as_int(r.r.x) < 0);
-  const uint64_t ny = ballot(active && __float_as_int(r.r.y) < 0);
-  const uint64_t nz = ballot(active && __float_as_int(r.r.z) < 0);
-  if ((nx && nx != act) || (ny && ny != act) || (nz && nz != act)) return -1;
-  return (nx ? 1 : 0) | (ny ? 2 : 0) | (nz ? 4 : 0);
-}
-
 // One wave = the 8x8 packet of selected tile `sel` (< num_sel_tiles): closest hit per pixel
 // into its 8-B record.
 template <bool FAST, bool DEEP, bool SPHERES>
@@ -929,11 +900,8 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
   Diag dg;
   float t;
   int leaf;
-  const int neg = FAST ? packet_signs(ray, q.valid) : -1;
   if (ballot(any_skip))
     closest_hit<true, FAST, DEEP, SPHERES>(P, nodes, spill, L, ray, q.valid, t, leaf, dg);
-  else if (FAST && RT_COHERENT && neg >= 0)
-    closest_hit<false, FAST, DEEP, SPHERES, true>(P, nodes, spill, L, ray, q.valid, t, leaf, dg, neg);
   else
     closest_hit<false, FAST, DEEP, SPHERES>(P, nodes, spill, L, ray, q.valid, t, leaf, dg);
   const RenderParams& Pw = fresh_params(P);  // post-traversal fields: not live across it
@@ -991,12 +959,9 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       const LaneRay sr = make_ray(pk + wi * P.eps, wi, P.quot_ok);  // p + eps * w_i
       const float thr = dist - P.eps;
       const bool any_skip = hit && (sr.skip0 || sr.skip1 || sr.skip2);
-      const int neg = FAST ? packet_signs(sr, hit && thr > 0.0f) : -1;
-      const bool occ =
-          ballot(any_skip) ? occluded<true, FAST, DEEP, SPHERES>(P, nodes, spill, L, sr, hit, thr, dg)
-          : (FAST && RT_COHERENT && neg >= 0)
-              ? occluded<false, FAST, DEEP, SPHERES, true>(P, nodes, spill, L, sr, hit, thr, dg, neg)
-              : occluded<false, FAST, DEEP, SPHERES>(P, nodes, spill, L, sr, hit, thr, dg);
+      const bool occ = ballot(any_skip)
+                           ? occluded<true, FAST, DEEP, SPHERES>(P, nodes, spill, L, sr, hit, thr, dg)
+                           : occluded<false, FAST, DEEP, SPHERES>(P, nodes, spill, L, sr, hit, thr, dg);
       bits |= (occ ? 1u : 0u) << (li - 32 * w);
     }
     const RenderParams& Pw = fresh_params(P0);

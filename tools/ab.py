@@ -45,6 +45,8 @@ def main():
                 sys.exit(1)
             for k, t in json.loads(out.stdout).items():
                 res[v][k].append(t["median_ms"])
+            # progress line per run (a GPU box kills a command silent for minutes)
+            print(v, json.dumps({k: x[-1] for k, x in res[v].items()}), file=sys.stderr, flush=True)
     summary = {v: {k: round(sorted(x)[len(x) // 2], 4) for k, x in d.items()} for v, d in res.items()}
     print(json.dumps(summary, indent=1))
 
