@@ -406,9 +406,13 @@ def cpu_rehearsal(args) -> int:
                              .reshape(tx * ty, dist_tiles.TILE_FLOATS).copy())
     rendered = []
 
+    share = torch.from_numpy(L.share_tiles(0, rank))  # frame tile of each slot tile (-1: none)
+
     def render(sh, slot, stream):
-        rendered.append(sh.count)
-        slot[:sh.count].copy_(tiles[sh.tile_begin::sh.tile_step][:sh.count])
+        rendered.append(len(share))
+        part = tiles[share.clamp(min=0)]
+        part[share < 0] = 0.0
+        slot[:len(share)].copy_(part)
 
     R = dist_tiles.TileGatherRenderer(L, None, render, host_staging=True, device="cpu")
     for _ in range(args.warmup):

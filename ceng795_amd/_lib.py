@@ -81,7 +81,7 @@ SIGNATURES = {
     "rt_scene_device_count": (C.c_int, [C.c_void_p]),
     "rt_release_stream_scratch": (C.c_int, [C.c_void_p, C.c_void_p]),
     "rt_untile_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
-                                   C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
+                                   C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     "rt_scene_num_cameras": (C.c_int, [C.c_void_p]),
     "rt_scene_camera": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(rt_camera)]),
     "rt_scene_image_name": (C.c_char_p, [C.c_void_p, C.c_int]),

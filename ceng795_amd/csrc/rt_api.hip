@@ -421,9 +421,11 @@ RenderParams make_params(const rt_scene* s, const Replica& r, int cam, int row0,
   P.tiles_total = tp.tiles_total;
   P.tile_begin = tile_begin;
   P.tile_step = tile_step;
-  P.num_sel_tiles =
-      tile_begin < tp.tiles_total ? (tp.tiles_total - tile_begin + tile_step - 1) / tile_step : 0;
-  P.tile_major = tile_major;
+  P.block_deal = (tile_major & RT_TILE_BLOCKS) ? 1 : 0;
+  const int units = P.block_deal ? deal_blocks(tp.tiles_x, tp.tiles_total / tp.tiles_x) : tp.tiles_total;
+  const int sel_units = tile_begin < units ? (units - tile_begin + tile_step - 1) / tile_step : 0;
+  P.num_sel_tiles = P.block_deal ? 4 * sel_units : sel_units;
+  P.tile_major = tile_major & RT_TILE_MAJOR;
   P.out = out;
   P.occ_words = occ_words(h);
   P.counters = counters;
@@ -747,10 +749,10 @@ void render_multi_msaa(rt_scene* s, CtxSet& cx, int cam, float* d_frame, hipStre
 
 // One frame (rows row0 + k*row_stride) of a pixel-centre camera over every device of a
 // multi-device scene, into the row-major frame d_frame on the first device, ordered on its
-// stream s0.  The frame's 8x8 tiles are dealt round-robin over the D devices (the reference's
-// row interleave over threads, HW2/main.cpp:33-36, at tile granularity; tile t -> device
-// t mod D); each device renders its tiles tile-major into a slot of ceil(T / D) tiles on its
-// context's stream; one RCCL group of send / receive pairs (single process, one communicator
+// stream s0.  The frame's 2x2-tile blocks are dealt round-robin over the D devices in deal
+// order (the reference's row interleave over threads, HW2/main.cpp:33-36, at block
+// granularity; block d -> device d mod D, deal_block_tile); each device renders its blocks
+// tile-major into a slot of 4 ceil(B / D) tiles on its context's stream; one RCCL group of send / receive pairs (single process, one communicator
 // per device) gathers the slots onto the first device, whose untile kernel writes the rows.
 // Counters: `per_call` adds each device's rays to its context's counters (rt_render's stats),
 // else to the replica's (rt_collect_stats).  Caller holds s->multi_mu.
@@ -760,7 +762,8 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
   const rt_camera& c = s->host.cameras[cam];
   const TilePlan tp = plan(c, row0, row_stride);
   if (tp.tiles_total == 0) return;
-  const int slot = (tp.tiles_total + D - 1) / D;
+  const int blocks = deal_blocks(tp.tiles_x, tp.tiles_total / tp.tiles_x);
+  const int slot = 4 * ((blocks + D - 1) / D);  // tiles: whole 2x2 blocks (block deal)
   RenderCtx* x0 = cx.x[0];
   {
     DeviceGuard g(s->rep[0]->device);
@@ -771,8 +774,8 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
     RenderCtx* x = cx.x[d];
     DeviceGuard g(r.device);
     ensure(x->d_out, x->out_floats, (size_t)slot * kTileFloats, "alloc tile slot");
-    RenderParams P = make_params(s, r, cam, row0, row_stride, d, D, 1, x->d_out,
-                                 per_call ? x->d_cnt : r.d_counters);
+    RenderParams P = make_params(s, r, cam, row0, row_stride, d, D, RT_TILE_MAJOR | RT_TILE_BLOCKS,
+                                 x->d_out, per_call ? x->d_cnt : r.d_counters);
     bind_ctx(s, x, P, c);
     enqueue_frame(s, r, P, 1, nullptr, x->stream, d == 0);
   }
@@ -815,6 +818,7 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
   U.devices = D;
   U.slot = slot;
   U.tile_offset = 0;
+  U.blocks = 1;
   hip_check(launch_untile(U, x0->stream), "untile launch");
   if (s0 != x0->stream) {
     hip_check(hipEventRecord(x0->ev_out, x0->stream), "event record");
@@ -1046,7 +1050,7 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
                            void* stream) {
   return guarded([&] {
     check_render_args(s, cam, row0, row_stride);
-    if (tile_begin < 0 || tile_step < 1 || !d_out)
+    if (tile_begin < 0 || tile_step < 1 || !d_out || (tile_major & ~(RT_TILE_MAJOR | RT_TILE_BLOCKS)))
       throw std::invalid_argument("rt_render_device: bad tile selection / output");
     const rt_camera& c = s->host.cameras[cam];
     if (s->multi) {
@@ -1070,9 +1074,10 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
     P.hits = sc->hits;
     P.occ = sc->occ;
     set_schedule(P, sc->sched);
-    if (tile_count >= 0 && tile_count < P.num_sel_tiles) {
+    const int unit_tiles = P.block_deal ? 4 : 1;  // tile_count counts deal units
+    if (tile_count >= 0 && (long long)tile_count * unit_tiles < P.num_sel_tiles) {
       if (c.num_samples > 1) throw std::domain_error("NumSamples > 1 renders whole row-major frames only");
-      P.num_sel_tiles = tile_count;
+      P.num_sel_tiles = tile_count * unit_tiles;
     }
     if (s->needs_recursion) {
       ensure(sc->frames, sc->frames_capacity, frame_floats(s->host, P.num_sel_tiles),
@@ -1090,15 +1095,18 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
 }
 
 int rt_untile_device(rt_scene* s, int cam, int row0, int row_stride, int devices, int slot,
-                     int tile_offset, const float* d_gathered, float* d_out, void* stream) {
+                     int tile_offset, int blocks, const float* d_gathered, float* d_out,
+                     void* stream) {
   return guarded([&] {
     check_render_args(s, cam, row0, row_stride);
-    if (devices < 1 || slot < 0 || tile_offset < 0 || !d_gathered || !d_out)
+    if (devices < 1 || slot < 0 || tile_offset < 0 || !d_gathered || !d_out ||
+        (blocks != 0 && blocks != 1) || (blocks && slot % 4))
       throw std::invalid_argument("rt_untile_device: bad argument");
     const rt_camera& c = s->host.cameras[cam];
     const TilePlan tp = plan(c, row0, row_stride);
-    if ((long long)devices * slot < tp.tiles_total)
-      throw std::invalid_argument("rt_untile_device: devices * slot is smaller than the tile count");
+    const long long units = blocks ? deal_blocks(tp.tiles_x, tp.tiles_total / tp.tiles_x) : tp.tiles_total;
+    if ((long long)devices * (blocks ? slot / 4 : slot) < units)
+      throw std::invalid_argument("rt_untile_device: devices * slot is smaller than the frame's share");
     DeviceGuard g(s->rep[0]->device);
     UntileParams U;
     U.recv = d_gathered;
@@ -1112,6 +1120,7 @@ int rt_untile_device(rt_scene* s, int cam, int row0, int row_stride, int devices
     U.devices = devices;
     U.slot = slot;
     U.tile_offset = tile_offset % devices;
+    U.blocks = blocks;
     hip_check(launch_untile(U, (hipStream_t)stream), "untile launch");
     return RT_OK;
   });

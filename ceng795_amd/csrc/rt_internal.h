@@ -162,11 +162,43 @@ struct MsaaResolveParams {
 // round-robin over `devices` (tile t -> device t mod devices, slot position t / devices) and
 // gathered as recv[devices][slot][64 pixels][3]; writes the selected rows of the row-major
 // frame out[h][w][3] (logical row k = image row row0 + k*row_stride).
+#if defined(__HIPCC__)
+#define RT_HD __host__ __device__
+#else
+#define RT_HD
+#endif
+
+// Block deal (rt_render_device with RT_TILE_BLOCKS, multi-device frames): the unit dealt over
+// devices is a 2x2 block of tiles (the traversal workgroup's unit, so a share keeps the
+// in-place frame's coherence), numbered with each block row rotated by its row index —
+// d = by * nbx + (bx - by) mod nbx — so that a deal d = r (mod N) takes diagonal stripes of
+// blocks rather than the same columns in every row (nbx is often a multiple of N).  Selected
+// block k holds tiles 4k .. 4k + 3 of the selection (w = 2 * (ty & 1) + (tx & 1)).
+RT_HD inline int deal_blocks_x(int tiles_x) { return (tiles_x + 1) >> 1; }
+RT_HD inline int deal_blocks(int tiles_x, int tiles_y) {
+  return deal_blocks_x(tiles_x) * ((tiles_y + 1) >> 1);
+}
+RT_HD inline void deal_block_tile(int tiles_x, int d, int w, int& tx, int& ty) {
+  const int nbx = deal_blocks_x(tiles_x), by = d / nbx;
+  int bx = d - by * nbx + by % nbx;
+  if (bx >= nbx) bx -= nbx;
+  tx = 2 * bx + (w & 1);
+  ty = 2 * by + (w >> 1);
+}
+RT_HD inline int deal_block_index(int tiles_x, int tx, int ty, int& w) {
+  const int nbx = deal_blocks_x(tiles_x), bx = tx >> 1, by = ty >> 1;
+  w = ((ty & 1) << 1) | (tx & 1);
+  int c = bx - by % nbx;
+  if (c < 0) c += nbx;
+  return by * nbx + c;
+}
+
 struct UntileParams {
   const float* recv;
   float* out;
   int width, row0, row_stride, rows, tiles_x, tiles_total, devices, slot;
-  int tile_offset;  // tile t went to rank (t + tile_offset) mod devices (rt_untile_device)
+  int tile_offset;  // deal unit u went to rank (u + tile_offset) mod devices (rt_untile_device)
+  int blocks;       // 1: the units are 2x2 blocks in deal order (deal_block_index), else tiles
 };
 
 // Words of the per-stream schedule buffer for a launch of `tiles` selected tiles: tile costs
@@ -204,6 +236,7 @@ struct RenderParams {
   // tiles over (rows x width), row-major; this launch does tile_begin + i*tile_step
   int tiles_x, tiles_total, tile_begin, tile_step, num_sel_tiles;
   int tile_major;
+  int block_deal;  // the selection counts 2x2 blocks in deal order (deal_block_tile)
   int tile_block;  // traversal kernels: workgroups take 2-D blocks of tiles (rt_kernels.hip)
   // jittered MSAA (HW2/Scene.cpp:32-69): 0 = pixel centres; else this launch traces sample
   // msaa_s = x*n + y of every pixel, whose minstd_rand0 draws 2s+1, 2s+2 are

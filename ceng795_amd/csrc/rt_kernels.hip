@@ -813,8 +813,14 @@ struct PacketPixel {
 __device__ __forceinline__ PacketPixel packet_pixel(const RenderParams& P, int sel) {
   PacketPixel q;
   q.lane = lane_id();
-  const int tile = P.tile_begin + sel * P.tile_step;
-  const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+  int tx, ty;
+  if (P.block_deal) {  // selected block sel / 4, its tile sel % 4
+    deal_block_tile(P.tiles_x, P.tile_begin + (sel >> 2) * P.tile_step, sel & 3, tx, ty);
+  } else {
+    const int tile = P.tile_begin + sel * P.tile_step;
+    tx = tile % P.tiles_x;
+    ty = tile / P.tiles_x;
+  }
   q.px = tx * kTile + (q.lane & 7);
   const int lr = ty * kTile + (q.lane >> 3);  // logical row
   q.valid = q.px < P.width && lr < P.rows;
@@ -1572,7 +1578,7 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
     return;
   }
   RenderParams T = P;
-  T.tile_block = P.tile_begin == 0 && P.tile_step == 1;
+  T.tile_block = P.tile_begin == 0 && P.tile_step == 1 && !P.block_deal;
   const int tblocks = (trace_packets(T) + kTraceWaves - 1) / kTraceWaves;
   const size_t tlds = DEEP ? sizeof(int) * kDeepWords * kDeepStack * kTraceWaves : 0;
   // dispatch order: units of one traversal workgroup, `regions` regions of
@@ -1679,9 +1685,12 @@ __global__ __launch_bounds__(256) void untile_kernel(UntileParams U) {
   const int tx = t % U.tiles_x, ty = t / U.tiles_x;
   const int px = tx * kTile + (lane & 7), lr = ty * kTile + (lane >> 3);
   if (px >= U.width || lr >= U.rows) return;
-  const int r = (t + U.tile_offset) % U.devices;
-  const int b = ((r - U.tile_offset) % U.devices + U.devices) % U.devices;  // rank r's first tile
-  const float* src = U.recv + ((size_t)(r * U.slot + (t - b) / U.devices) * (kTile * kTile) + lane) * 3;
+  int w = 0;
+  const int u = U.blocks ? deal_block_index(U.tiles_x, tx, ty, w) : t;  // deal unit
+  const int r = (u + U.tile_offset) % U.devices;
+  const int b = ((r - U.tile_offset) % U.devices + U.devices) % U.devices;  // rank r's first unit
+  const int k = U.blocks ? 4 * ((u - b) / U.devices) + w : (u - b) / U.devices;  // slot tile
+  const float* src = U.recv + ((size_t)(r * U.slot + k) * (kTile * kTile) + lane) * 3;
   float* dst = U.out + ((size_t)(U.row0 + lr * U.row_stride) * U.width + px) * 3;
   dst[0] = src[0];
   dst[1] = src[1];

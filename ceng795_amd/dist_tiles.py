@@ -1,14 +1,16 @@
 """Image-tile sharding over GPUs + framebuffer gather, one process per GPU.
 
 The reference splits a frame over host threads by interleaved rows (HW2/main.cpp:33-36,
-HW2/Scene.cpp:25).  Here the 8x8-pixel tiles (one wavefront each) of every camera's frame are
-numbered globally, camera after camera, and dealt round-robin over ranks — rank r renders
-global tiles g = r (mod world) — which balances cost the way the row interleave does.  There
-is no other exchange: the scene is replicated, rays are independent.
+HW2/Scene.cpp:25).  Here the deal units of every camera's frame — 2x2 blocks of 8x8-pixel tiles
+(one wavefront per tile, one traversal workgroup per block), block rows rotated by their row
+index (RT_TILE_BLOCKS, include/ceng795_rt.h) — are numbered globally, camera after camera, and
+dealt round-robin over ranks: rank r renders global units g = r (mod world), diagonal stripes
+of blocks, which balances cost the way the row interleave does while each workgroup's rays
+stay neighbours.  There is no other exchange: the scene is replicated, rays are independent.
 
 Buffer layout.  Each rank's HBM buffer holds one fixed-size SLOT per camera
-(ceil(tiles / world) tiles, the largest share any rank gets), and the rank's tiles of that
-camera are written back to back (tile-major) at the slot's start.  Every rank's slot c has the
+(4 ceil(blocks / world) tiles, the largest share any rank gets), and the rank's tiles of that
+camera are written back to back (tile-major, 4 per block) at the slot's start.  Every rank's slot c has the
 same size, so camera c's shares are gathered to rank 0 by one equal-size collective
 (torch.distributed "nccl" = RCCL over xGMI).  Rank 0 then untiles camera c with ONE
 index_select of 8-pixel tile rows (96 B, contiguous in both layouts) straight into the
@@ -39,45 +41,83 @@ def tiles_of(size: Tuple[int, int]) -> Tuple[int, int]:
     return (w + TILE - 1) // TILE, (h + TILE - 1) // TILE
 
 
+def deal_block_tile(tiles_x: int, d, w):
+    """Tile (tx, ty) of tile w of deal block d (rt_internal.h deal_block_tile: block rows
+    rotated by their row index; numpy arrays welcome)."""
+    nbx = (tiles_x + 1) // 2
+    by = d // nbx
+    bx = (d - by * nbx + by % nbx) % nbx
+    return 2 * bx + (w & 1), 2 * by + (w >> 1)
+
+
+def deal_block_index(tiles_x: int, tx, ty):
+    """(deal block d, tile w within it) of tile (tx, ty): the inverse of deal_block_tile."""
+    nbx = (tiles_x + 1) // 2
+    bx, by = tx // 2, ty // 2
+    return by * nbx + (bx - by) % nbx, 2 * (ty & 1) + (tx & 1)
+
+
 @dataclass
 class CameraShare:
     camera: int
-    tile_begin: int   # first camera-local tile of this rank
+    tile_begin: int   # first camera-local deal unit of this rank
     tile_step: int    # = world
-    count: int        # tiles of this camera rendered by this rank
+    count: int        # deal units of this camera rendered by this rank
     offset: int       # start (in tiles) of this camera's slot in the rank buffer
     slot: int         # slot size in tiles (same on every rank)
+    blocks: bool      # deal units are 2x2 tile blocks (RT_TILE_BLOCKS), else tiles
 
 
 class TileLayout:
-    """Global round-robin assignment of tiles to ranks for a list of camera frame sizes."""
+    """Global round-robin assignment of deal units to ranks for a list of camera frame sizes.
+    A deal unit is a 2x2 block of tiles in deal order (blocks=True, the default: what
+    rt_render_device's RT_TILE_BLOCKS renders, 4 tiles per unit in the slot) or one tile."""
 
-    def __init__(self, sizes: Sequence[Tuple[int, int]], world: int, rank: int):
+    def __init__(self, sizes: Sequence[Tuple[int, int]], world: int, rank: int,
+                 blocks: bool = True):
         self.sizes = [tuple(s) for s in sizes]
-        self.tiles_per_camera = [tx * ty for tx, ty in map(tiles_of, self.sizes)]
+        self.blocks = bool(blocks)
+        self.unit_tiles = 4 if self.blocks else 1
+        txy = [tiles_of(s) for s in self.sizes]
+        self.tiles_per_camera = [tx * ty for tx, ty in txy]
+        self.units_per_camera = [((tx + 1) // 2) * ((ty + 1) // 2) if self.blocks else tx * ty
+                                 for tx, ty in txy]
         self.world = world
         self.rank = rank
-        self.offsets = np.concatenate([[0], np.cumsum(self.tiles_per_camera)]).astype(np.int64)
+        self.offsets = np.concatenate([[0], np.cumsum(self.units_per_camera)]).astype(np.int64)
         self.total = int(self.offsets[-1])
-        self.slots = [(T + world - 1) // world for T in self.tiles_per_camera]
+        self.slots = [self.unit_tiles * ((U + world - 1) // world) for U in self.units_per_camera]
         self.slot_offsets = np.concatenate([[0], np.cumsum(self.slots)]).astype(np.int64)
         self.buffer_tiles = int(self.slot_offsets[-1])
         self.per_rank = [self._shares(r) for r in range(world)]
         self.shares = self.per_rank[rank]
-        self.local_tiles = sum(s.count for s in self.shares)
+        self.local_tiles = sum(s.count for s in self.shares) * self.unit_tiles
 
     def begin(self, r: int, c: int) -> int:
-        """First tile of camera c dealt to rank r (global tile g goes to rank g mod world)."""
+        """First unit of camera c dealt to rank r (global unit g goes to rank g mod world)."""
         return int((r - self.offsets[c]) % self.world)
 
     def _shares(self, r: int) -> List[CameraShare]:
         out = []
-        for c, T in enumerate(self.tiles_per_camera):
+        for c, U in enumerate(self.units_per_camera):
             b = self.begin(r, c)
-            count = 0 if b >= T else (T - b + self.world - 1) // self.world
+            count = 0 if b >= U else (U - b + self.world - 1) // self.world
             out.append(CameraShare(c, b, self.world, count, int(self.slot_offsets[c]),
-                                   self.slots[c]))
+                                   self.slots[c], self.blocks))
         return out
+
+    def share_tiles(self, c: int, r: int) -> np.ndarray:
+        """Row-major frame tile index of each tile rank r renders for camera c, in slot order
+        (-1: a block tile outside the tile grid, rendered as zeros)."""
+        sh = self.per_rank[r][c]
+        tx, ty = tiles_of(self.sizes[c])
+        u = sh.tile_begin + np.arange(sh.count, dtype=np.int64) * sh.tile_step
+        if not self.blocks:
+            return u
+        d = np.repeat(u, 4)
+        w = np.tile(np.arange(4, dtype=np.int64), sh.count)
+        x, y = deal_block_tile(tx, d, w)
+        return np.where((x < tx) & (y < ty), y * tx + x, -1)
 
     def row_index(self, c: int) -> np.ndarray:
         """Untile index of camera c.  The gathered slots [world, slot, 8 rows, 24 floats] are
@@ -85,9 +125,13 @@ class TileLayout:
         row that becomes pixel row y, pixels 8x..8x+7, of the (tile-padded) frame."""
         tx, ty = tiles_of(self.sizes[c])
         t = np.arange(tx * ty, dtype=np.int64)
-        r = (t + self.offsets[c]) % self.world
+        if self.blocks:
+            u, w = deal_block_index(tx, t % tx, t // tx)
+        else:
+            u, w = t, 0
+        r = (u + self.offsets[c]) % self.world
         b = (r - self.offsets[c]) % self.world
-        pos = (t - b) // self.world
+        pos = self.unit_tiles * ((u - b) // self.world) + w
         tile_src = (r * self.slots[c] + pos).reshape(ty, tx)  # gathered tile of each frame tile
         y = np.arange(ty * TILE, dtype=np.int64)
         return (tile_src[y // TILE] * TILE + (y % TILE)[:, None]).astype(np.int64)
@@ -116,7 +160,7 @@ def scene_tile_untiler(scene, layout: TileLayout) -> Callable:
         sh = layout.shares[c]
         scene.untile_device(c, layout.world, sh.slot, gathered_c.data_ptr(), frame.data_ptr(),
                             tile_offset=int(layout.offsets[c] % layout.world),
-                            stream=stream.cuda_stream)
+                            blocks=layout.blocks, stream=stream.cuda_stream)
     return untile
 
 
@@ -124,7 +168,8 @@ def scene_tile_renderer(scene) -> Callable:
     """The GPU tile renderer: rt_render_device of camera c's share, tile-major into `slot`."""
     def render(sh: CameraShare, slot, stream):
         scene.render_device(sh.camera, slot.data_ptr(), tile_begin=sh.tile_begin,
-                            tile_step=sh.tile_step, tile_major=True, stream=stream.cuda_stream)
+                            tile_step=sh.tile_step, tile_major=True, blocks=sh.blocks,
+                            stream=stream.cuda_stream)
     return render
 
 
@@ -422,17 +467,17 @@ class ShareRenderer:
                 slot = self.local[s][sh.offset:sh.offset + sh.slot]
                 self.scene.render_device(sh.camera, slot.data_ptr(), tile_begin=sh.tile_begin,
                                          tile_step=sh.tile_step, tile_major=True,
-                                         stream=st.cuda_stream)
+                                         blocks=sh.blocks, stream=st.cuda_stream)
 
     def finish(self):
         for st in self.streams[1:]:
             self.stream.wait_stream(st)
 
 
-def TilePlan(scene, world: int, rank: int) -> TileLayout:
+def TilePlan(scene, world: int, rank: int, blocks: bool = True) -> TileLayout:
     """Tile layout for every camera of `scene`, checked against the library's tile count."""
     sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
-    L = TileLayout(sizes, world, rank)
+    L = TileLayout(sizes, world, rank, blocks=blocks)
     for c in range(scene.num_cameras):
         assert L.tiles_per_camera[c] == scene.num_tiles(c), "tile count disagrees with the library"
     return L

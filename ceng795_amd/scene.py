@@ -10,6 +10,8 @@ import numpy as np
 from . import _lib
 from ._lib import check, lib
 
+RT_TILE_MAJOR, RT_TILE_BLOCKS = 1, 2  # rt_render_device tile_major flags (include/ceng795_rt.h)
+
 
 @dataclass
 class CameraInfo:
@@ -138,20 +140,25 @@ class Scene:
 
     def render_device(self, camera_index: int, out_ptr: int, *, starting_row: int = 0,
                       row_stride: int = 1, tile_begin: int = 0, tile_step: int = 1,
-                      tile_major: bool = False, stream: int = 0,
+                      tile_major: bool = False, blocks: bool = False, stream: int = 0,
                       tile_count: int = -1) -> None:
         """Asynchronous render into device memory at ``out_ptr`` on HIP stream ``stream``
-        (tiles tile_begin + k*tile_step, k < tile_count; tile_count < 0: all of them)."""
+        (deal units tile_begin + k*tile_step, k < tile_count; tile_count < 0: all of them; a
+        unit is a tile, or with ``blocks`` a 2x2 block of tiles in deal order —
+        RT_TILE_BLOCKS of include/ceng795_rt.h)."""
+        flags = (RT_TILE_MAJOR if tile_major else 0) | (RT_TILE_BLOCKS if blocks else 0)
         check(lib().rt_render_device_range(self._h, camera_index, starting_row, row_stride,
-                                           tile_begin, tile_step, tile_count, int(tile_major),
+                                           tile_begin, tile_step, tile_count, flags,
                                            C.c_void_p(out_ptr), C.c_void_p(stream)))
 
     def untile_device(self, camera_index: int, devices: int, slot: int, gathered_ptr: int,
-                      out_ptr: int, *, tile_offset: int = 0, stream: int = 0) -> None:
+                      out_ptr: int, *, tile_offset: int = 0, blocks: bool = False,
+                      stream: int = 0) -> None:
         """rt_untile_device: the gathered [devices][slot][64][3] tile shares of a round-robin
-        deal (tile t to rank (t + tile_offset) mod devices) into the row-major frame."""
+        deal (unit u to rank (u + tile_offset) mod devices; units are tiles, or 2x2 blocks in
+        deal order with ``blocks``) into the row-major frame."""
         check(lib().rt_untile_device(self._h, camera_index, 0, 1, devices, slot, tile_offset,
-                                     C.c_void_p(gathered_ptr), C.c_void_p(out_ptr),
+                                     int(blocks), C.c_void_p(gathered_ptr), C.c_void_p(out_ptr),
                                      C.c_void_p(stream)))
 
     def release_stream(self, stream: int) -> None:

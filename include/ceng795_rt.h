@@ -181,13 +181,23 @@ int rt_set_traversal(rt_scene* scene, int mode);
 int rt_render(rt_scene* scene, int camera_index, int starting_row, int row_stride,
               float* out_rgb, rt_stats* stats);
 
+/* tile_major flags of rt_render_device / rt_render_device_range */
+enum { RT_TILE_MAJOR = 1, RT_TILE_BLOCKS = 2 };
+
 /* Device-resident variant (the building block of the one-process-per-GPU image tiling, and
  * of frames kept in HBM).  The image (rows starting_row +
- * k*row_stride) is cut into 8x8 tiles numbered row-major; this call renders tiles
- * tile_begin, tile_begin + tile_step, ... into d_out (device memory):
- *   tile_major == 0: d_out is a full w*h*3 frame, written in place;
- *   tile_major == 1: d_out holds the selected tiles back to back, 8*8*3 floats each
- *                    (pixels outside the image are written as 0).
+ * k*row_stride) is cut into 8x8 tiles; this call renders the deal units
+ * tile_begin, tile_begin + tile_step, ... into d_out (device memory).  A deal unit is
+ *   one tile, tiles numbered row-major (tile_major without RT_TILE_BLOCKS), or
+ *   with RT_TILE_BLOCKS one 2x2 block of tiles, blocks numbered row-major with block row by
+ *   rotated left by by (unit d = by*nbx + (bx - by) mod nbx, nbx = ceil(tiles_x / 2)); a
+ *   block's tiles are taken in the order (0,0) (1,0) (0,1) (1,1).  This is the deal the
+ *   multi-GPU paths use: a share keeps whole blocks (the traversal workgroup's unit, so the
+ *   rays of a workgroup stay neighbours) and a deal d = r (mod N) takes diagonal stripes.
+ * Output (tile_major & RT_TILE_MAJOR):
+ *   0: d_out is a full w*h*3 frame, written in place;
+ *   1: d_out holds the selected units' tiles back to back, 8*8*3 floats each (pixels or
+ *      block tiles outside the image are written as 0).
  * MSAA cameras: only the whole frame, row-major (tile_begin 0, tile_step 1, tile_major 0).
  * Asynchronous on `hip_stream` (a hipStream_t, NULL = default stream).  Ray counts
  * accumulate on the device until rt_collect_stats.  Calls on one stream run in order and share
@@ -202,25 +212,26 @@ int rt_render(rt_scene* scene, int camera_index, int starting_row, int row_strid
 int rt_render_device(rt_scene* scene, int camera_index, int starting_row, int row_stride,
                      int tile_begin, int tile_step, int tile_major, float* d_out,
                      void* hip_stream);
-/* rt_render_device restricted to the first `tile_count` selected tiles (tile_count < 0: all):
- * tiles tile_begin + k*tile_step for k < tile_count.  With tile_major the k-th of them lands
- * at d_out + k*192 floats.  Lets a rank render its share of a frame in chunks and hand each
+/* rt_render_device restricted to the first `tile_count` selected deal units (tile_count < 0:
+ * all): units tile_begin + k*tile_step for k < tile_count.  With RT_TILE_MAJOR the k-th tile
+ * rendered lands at d_out + k*192 floats (4 tiles per unit with RT_TILE_BLOCKS).  Lets a rank render its share of a frame in chunks and hand each
  * chunk to the framebuffer gather while the next one renders (multi-GPU).
  * MSAA cameras: whole frames only. */
 int rt_render_device_range(rt_scene* scene, int camera_index, int starting_row, int row_stride,
                            int tile_begin, int tile_step, int tile_count, int tile_major,
                            float* d_out, void* hip_stream);
 /* The other half of the process-per-GPU tile deal: rank 0 holds every rank's share as
- * d_gathered[devices][slot][8*8*3] (rank r rendered the frame's tiles t with
- * (t + tile_offset) mod devices == r, tile-major, in order, into its slot of `slot` tiles — what
- * one equal-size gather of rt_render_device(tile_begin, tile_step = devices, tile_major = 1)
- * outputs leaves); this writes them into the row-major frame d_out (rows starting_row +
- * k*row_stride of camera_index), one wave per tile, on hip_stream (device devices[0] of the
- * scene).  Replaces nothing in the reference (its threads share one Pixel array,
- * HW2/main.cpp:33-36): it is the gather's inverse. */
+ * d_gathered[devices][slot][8*8*3] (rank r rendered the frame's deal units u with
+ * (u + tile_offset) mod devices == r, tile-major, in order, into its slot of `slot` tiles — what
+ * one equal-size gather of rt_render_device(tile_begin, tile_step = devices, RT_TILE_MAJOR
+ * [| RT_TILE_BLOCKS when blocks = 1]) outputs leaves; with blocks, slot is a multiple of 4);
+ * this writes them into the row-major frame d_out (rows starting_row + k*row_stride of
+ * camera_index), one wave per tile, on hip_stream (device devices[0] of the scene).  Replaces
+ * nothing in the reference (its threads share one Pixel array, HW2/main.cpp:33-36): it is the
+ * gather's inverse. */
 int rt_untile_device(rt_scene* scene, int camera_index, int starting_row, int row_stride,
-                     int devices, int slot, int tile_offset, const float* d_gathered, float* d_out,
-                     void* hip_stream);
+                     int devices, int slot, int tile_offset, int blocks, const float* d_gathered,
+                     float* d_out, void* hip_stream);
 /* Waits for `hip_stream` and frees the scratch rt_render_device keeps for it (no-op for a
  * stream the scene never rendered on).  Streams that come and go should release theirs. */
 int rt_release_stream_scratch(rt_scene* scene, void* hip_stream);

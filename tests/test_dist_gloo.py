@@ -43,12 +43,13 @@ def _tile(frame, t):
 
 
 def _render_local(L, frames):
-    """What rt_render_device(tile_major=True) writes: each share at its slot's start."""
+    """What rt_render_device(tile_major=True[, blocks]) writes: each share at its slot's start,
+    zeros for a block's tiles outside the tile grid."""
     local = torch.full((L.buffer_tiles, TILE_FLOATS), float("nan"))
     for sh in L.shares:
-        for k in range(sh.count):
-            local[sh.offset + k] = torch.from_numpy(
-                _tile(frames[sh.camera], sh.tile_begin + k * sh.tile_step))
+        for k, t in enumerate(L.share_tiles(sh.camera, L.rank)):
+            local[sh.offset + k] = (torch.from_numpy(_tile(frames[sh.camera], int(t))) if t >= 0
+                                    else torch.zeros(TILE_FLOATS))
     return local
 
 
@@ -56,12 +57,12 @@ def _same(a, b):
     return np.array_equal(np.asarray(a).view(np.uint32), np.asarray(b).view(np.uint32))
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, blocks=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     frames = _frames()
-    L = TileLayout(SIZES, world, rank)
+    L = TileLayout(SIZES, world, rank, blocks=blocks)
     local = _render_local(L, frames)
     ok = True
     for c, sh in enumerate(L.shares):  # one equal-size gather per camera slot
@@ -77,17 +78,18 @@ def _worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gather_reassembles_frames(tmp_path, world):
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+@pytest.mark.parametrize("world,blocks", [(2, True), (3, True), (2, False)])
+def test_gather_reassembles_frames(tmp_path, world, blocks):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), blocks), nprocs=world, join=True)
     assert (tmp_path / "result").read_text() == "ok"
 
 
+@pytest.mark.parametrize("blocks", [True, False])
 @pytest.mark.parametrize("world", [1, 2, 5, 8, 13])
-def test_untile_single_process(world):
+def test_untile_single_process(world, blocks):
     """All ranks simulated in one process: gathered slots -> frames, bit for bit."""
     frames = _frames(3)
-    layouts = [TileLayout(SIZES, world, r) for r in range(world)]
+    layouts = [TileLayout(SIZES, world, r, blocks=blocks) for r in range(world)]
     locals_ = [_render_local(L, frames) for L in layouts]
     for c in range(len(SIZES)):
         sh = layouts[0].shares[c]
@@ -96,42 +98,76 @@ def test_untile_single_process(world):
         assert _same(got.contiguous().numpy(), frames[c])
 
 
+@pytest.mark.parametrize("blocks", [True, False])
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_library_untile_index_math(world):
-    """rt_untile_device (untile_kernel in rt_kernels.hip) finds frame tile t of camera c at
-    rank r = (t + off) mod world, slot position (t - b) / world with b = (r - off) mod world
-    (off = the camera's first global tile): the same tile TileLayout.row_index maps, for every
-    camera of a multi-camera layout (restated here in numpy; the GPU runs are the bench's
-    gather_verified and test_c4_eight_way_tile_split_matches_oracle)."""
-    sizes = [(64, 40), (24, 24), (1920, 1080)]
-    L = dist_tiles.TileLayout(sizes, world, 0)
+def test_library_untile_index_math(world, blocks):
+    """rt_untile_device (untile_kernel in rt_kernels.hip, deal_block_index in rt_internal.h)
+    finds frame tile (tx, ty) of camera c in deal unit u — the tile itself, or block
+    d = by*nbx + (bx - by) mod nbx with w = 2*(ty&1) + (tx&1) — at rank
+    r = (u + off) mod world, slot tile k = (u - b) / world (times 4, plus w, for blocks),
+    b = (r - off) mod world, off = the camera's first global unit: the same tile
+    TileLayout.row_index maps, for every camera of a multi-camera layout (restated here in
+    numpy; the GPU runs are the bench's gather_verified and the multi-device / 8-way split
+    tests)."""
+    sizes = [(64, 40), (24, 24), (1920, 1080), (40, 8)]
+    L = dist_tiles.TileLayout(sizes, world, 0, blocks=blocks)
     for c, (w, h) in enumerate(sizes):
         tx, ty = dist_tiles.tiles_of((w, h))
         t = np.arange(tx * ty)
+        x, y = t % tx, t // tx
+        nbx = (tx + 1) >> 1
+        if blocks:
+            cc = (x >> 1) - (y >> 1) % nbx
+            u = (y >> 1) * nbx + np.where(cc < 0, cc + nbx, cc)
+            wi = ((y & 1) << 1) | (x & 1)
+        else:
+            u, wi = t, 0
         off = int(L.offsets[c] % world)
-        r = (t + off) % world
+        r = (u + off) % world
         b = ((r - off) % world + world) % world
-        src = r * L.slots[c] + (t - b) // world
+        k = 4 * ((u - b) // world) + wi if blocks else (u - b) // world
+        src = r * L.slots[c] + k
         idx = L.row_index(c)  # [ty*8, tx] tile rows
         want = idx[::dist_tiles.TILE, :].reshape(-1) // dist_tiles.TILE
         assert np.array_equal(src, want), (world, c)
 
 
+def test_block_deal_order():
+    """deal_block_tile / deal_block_index (the kernel's packet_pixel and untile) are inverse
+    bijections, and a deal d = r (mod N) takes every block column in turn (diagonal stripes)
+    even when the block row length is a multiple of N (C3: 120 blocks, N = 8)."""
+    for tx, ty in [(240, 135), (5, 3), (1, 1), (7, 8)]:
+        nbx, nby = (tx + 1) // 2, (ty + 1) // 2
+        d = np.arange(nbx * nby)
+        for w in range(4):
+            x, y = dist_tiles.deal_block_tile(tx, d, w)
+            d2, w2 = dist_tiles.deal_block_index(tx, x, y)
+            assert np.array_equal(d2, d) and np.all(w2 == w)
+        x, y = dist_tiles.deal_block_tile(tx, d, 0)
+        assert len(set(zip(x.tolist(), y.tolist()))) == len(d)
+    x, y = dist_tiles.deal_block_tile(240, np.arange(120 * 68), 0)
+    for r in range(8):
+        cols = (x[r::8] // 2) % 8
+        assert len(set(cols.tolist())) == 8  # not one column class per rank
+
+
+@pytest.mark.parametrize("blocks", [True, False])
 @pytest.mark.parametrize("world", [1, 2, 5, 8])
-def test_every_tile_rendered_exactly_once(world):
-    L0 = TileLayout(SIZES, world, 0)
-    seen = np.zeros(L0.total, np.int64)
+def test_every_tile_rendered_exactly_once(world, blocks):
+    L0 = TileLayout(SIZES, world, 0, blocks=blocks)
+    seen = [np.zeros(T, np.int64) for T in L0.tiles_per_camera]
     loads = []
     for r in range(world):
-        L = TileLayout(SIZES, world, r)
-        loads.append(L.local_tiles)
+        L = TileLayout(SIZES, world, r, blocks=blocks)
+        loads.append(sum(sh.count for sh in L.shares))
         assert L.buffer_tiles == L0.buffer_tiles
         for sh in L.shares:
-            assert sh.count <= sh.slot and sh.slot == L0.shares[sh.camera].slot
-            for k in range(sh.count):
-                seen[L.offsets[sh.camera] + sh.tile_begin + k * sh.tile_step] += 1
-    assert np.all(seen == 1)
-    assert max(loads) - min(loads) <= 1  # round-robin: balanced to one tile
+            assert sh.count * L.unit_tiles <= sh.slot and sh.slot == L0.shares[sh.camera].slot
+            t = L.share_tiles(sh.camera, r)
+            assert len(t) == sh.count * L.unit_tiles
+            np.add.at(seen[sh.camera], t[t >= 0], 1)
+    assert all(np.all(x == 1) for x in seen)
+    assert max(loads) - min(loads) <= 1  # round-robin: balanced to one unit
     for c in range(len(SIZES)):  # the untile reads every tile row of camera c exactly once
         idx = L0.row_index(c).reshape(-1)
         assert len(np.unique(idx)) == len(idx)
@@ -155,10 +191,10 @@ def _pipeline_worker(rank, world, port, outdir, sizes, steps):
 
     state = {"step": 0}
 
-    def render(sh, slot, stream):  # what rt_render_device(tile_major=True) writes
+    def render(sh, slot, stream):  # what rt_render_device(tile_major=True, blocks) writes
         frame = truth(state["step"])[sh.camera]
-        for k in range(sh.count):
-            slot[k] = torch.from_numpy(_tile(frame, sh.tile_begin + k * sh.tile_step))
+        for k, t in enumerate(L.share_tiles(sh.camera, rank)):
+            slot[k] = torch.from_numpy(_tile(frame, int(t))) if t >= 0 else 0.0
         done.append((sh.camera, sh.count))
 
     R = TileGatherRenderer(L, None, render, host_staging=True, device="cpu")

@@ -87,6 +87,37 @@ def test_tile_major_device_render(rt, scene_dir):
                 assert np.array_equal(tiles[k].view(np.uint32), exp.view(np.uint32)), (begin, step, t)
 
 
+def test_block_deal_device_render(rt, scene_dir):
+    """The multi-GPU deal (RT_TILE_BLOCKS): units are 2x2 tile blocks in deal order, 4 tiles per
+    unit tile-major (zeros outside the tile grid), tile_count limits units; every tile
+    bit-identical to the oracle frame."""
+    import torch
+    from ceng795_amd import dist_tiles
+    xml = scenes.write("hf_side", scene_dir)
+    ref, _ = oracle_frame(xml, 0)
+    h, w, _ = ref.shape
+    tx, ty = (w + 7) // 8, (h + 7) // 8
+    nb = ((tx + 1) // 2) * ((ty + 1) // 2)
+    with rt.Scene(xml) as s:
+        for begin, step, count in [(0, 1, -1), (1, 3, -1), (2, 8, -1), (0, 2, 3)]:
+            units = list(range(begin, nb, step))
+            if count >= 0:
+                units = units[:count]
+            out = torch.full((len(units) * 4 * 64 * 3,), -1.0, dtype=torch.float32, device="cuda")
+            s.render_device(0, out.data_ptr(), tile_begin=begin, tile_step=step, tile_major=True,
+                            blocks=True, tile_count=count,
+                            stream=torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            tiles = out.cpu().numpy().reshape(len(units) * 4, 8, 8, 3)
+            for k in range(len(units) * 4):
+                x, y = dist_tiles.deal_block_tile(tx, units[k // 4], k % 4)
+                exp = np.zeros((8, 8, 3), np.float32)
+                if x < tx and y < ty:
+                    blk = ref[y * 8:y * 8 + 8, x * 8:x * 8 + 8]
+                    exp[:blk.shape[0], :blk.shape[1]] = blk
+                assert np.array_equal(tiles[k].view(np.uint32), exp.view(np.uint32)), (begin, step, k)
+
+
 @pytest.mark.parametrize("mode", ["fast", "reference"])
 @pytest.mark.parametrize("name", list(scenes.RECURSIVE))
 def test_recursive_scenes_match_oracle(rt, scene_dir, name, mode):

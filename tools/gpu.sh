@@ -9,6 +9,8 @@
 #   tools/gpu.sh <out> ab <variants> [rounds]      same-box A/B of library builds (tools/ab.py)
 #   tools/gpu.sh <out> kt <name> [kt args]         per-kernel HIP-event times (tools/kt.py)
 #   tools/gpu.sh <out> pmc <workload> [round]      PMC traffic passes -> <out>/traffic_<w>.json
+#   tools/gpu.sh <out> pmcg <name> <groups...>      other counter groups (tools/pmc_passes.sh:
+#                                                  sq, insts, cycles, sqc, sqcbusy) of the C3 bench
 #   tools/gpu.sh <out> work <name> [workload] [lib] traversal work counters (RT_DIAG build,
 #                                                  tools/kernel_work.py; lib default "diag")
 #   tools/gpu.sh <out> ppmab "<variants>" [rounds] C5 frames of lib/libceng795_ppm_<v>.so builds
@@ -57,6 +59,10 @@ case "$CMD" in
     LIB=ceng795_amd/lib/libceng795_rt.so; [ "$W" = c5 ] && LIB=ceng795_amd/lib/libceng795_ppm.so
     python3 tools/pmc_traffic.py --fetch "$O/pmc_$W/fetch" --write "$O/pmc_$W/write" --workload "$W" \
       --round "$R" --lib "$LIB" --out "$O/traffic_$W.json" || exit 1 ;;
+  pmcg)
+    N=${1:?name}; shift
+    bash tools/pmc_passes.sh "$O/$N" "$@" || exit 1
+    ls "$O/$N" ;;
   work)
     N=${1:?name}; W=${2:-c3}; L=${3:-diag}
     X=$(python3 -c "import bench; print(bench.scene_path('$W', 1))") || exit 1
