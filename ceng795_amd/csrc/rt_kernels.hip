@@ -464,8 +464,12 @@ __device__ __forceinline__ float lane_f(int src, float v) {
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 // Runs the n queued tests; SHADOW: 0 < t < thr of the owner sets its flag, else the owner's
-// key takes min(key, (t, leaf)) for 0 < t < inf.  All lanes of the wave take part.
-template <bool SHADOW, bool SPHERES, bool CULL>
+// key takes min(key, (t, leaf)) for 0 < t < inf.  All lanes of the wave take part.  SKIP:
+// some lane of the wave skips an axis (else the guard test needs no skip flags).
+#ifndef RT_FLUSH_RCP_PERMUTE  // (A/B builds)
+#define RT_FLUSH_RCP_PERMUTE 0
+#endif
+template <bool SHADOW, bool SPHERES, bool CULL, bool SKIP = true>
 __device__ __forceinline__ void batch_flush(const RenderParams& P, WaveLeafLds& L, int n,
                                             const LaneRay& r, float thr, Diag& dg) {
   const int lane = lane_id();
@@ -488,14 +492,18 @@ __device__ __forceinline__ void batch_flush(const RenderParams& P, WaveLeafLds& 
       const int tag = __float_as_int(q0.w);
       leaf = tag & ~kLeafSphere;
       // the guard: the holder box {q1.w, q2.w, q3.x, q3.y, q3.z, q3.w}
+#if RT_FLUSH_RCP_PERMUTE  // the owner's reciprocals (the same v_rcp_f32 of the same d)
+      rr.r = v3(lane_f(src, r.r.x), lane_f(src, r.r.y), lane_f(src, r.r.z));
+#else
       rr.r = v3(__builtin_amdgcn_rcpf(rr.d.x), __builtin_amdgcn_rcpf(rr.d.y),
                 __builtin_amdgcn_rcpf(rr.d.z));
-      rr.skip0 = __builtin_fabsf(rr.d.x) < kEps;
-      rr.skip1 = __builtin_fabsf(rr.d.y) < kEps;
-      rr.skip2 = __builtin_fabsf(rr.d.z) < kEps;
+#endif
+      rr.skip0 = SKIP && __builtin_fabsf(rr.d.x) < kEps;
+      rr.skip1 = SKIP && __builtin_fabsf(rr.d.y) < kEps;
+      rr.skip2 = SKIP && __builtin_fabsf(rr.d.z) < kEps;
       const float g[6] = {q1.w, q2.w, q3.x, q3.y, q3.z, q3.w};
       float tn, tf;
-      slab_span<true>(g, rr, tn, tf);
+      slab_span<SKIP>(g, rr, tn, tf);
       bool in, out;
       decide_sure(tn, tf, in, out);
       bool ok = valid & in;
@@ -626,7 +634,7 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
       const int leaf = leaf_base + (int)((offs >> (4 * c)) & 15u);
       const bool pair = (kinds & (kSlotPair << c)) != 0;
       if (pending > kBatchCap - 128) {
-        batch_flush<SHADOW, SPHERES, true>(P, L, pending, r, thr, dg);
+        batch_flush<SHADOW, SPHERES, true, SKIP>(P, L, pending, r, thr, dg);
         pending = 0;
       }
       if (pair)
@@ -703,7 +711,7 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
   int node = FAST ? P.accel_root : P.root_ref;
   for (;;) {
     if (pending >= kBatchFlush) {  // between visits: only the ray and the stack are live
-      batch_flush<false, SPHERES, FAST>(P, L, pending, r, 0.0f, dg);
+      batch_flush<false, SPHERES, FAST, SKIP>(P, L, pending, r, 0.0f, dg);
       pending = 0;
     }
     if constexpr (FAST) {
@@ -722,7 +730,7 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
       if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, ~0ull)) break;
     }
   }
-  if (pending) batch_flush<false, SPHERES, FAST>(P, L, pending, r, 0.0f, dg);
+  if (pending) batch_flush<false, SPHERES, FAST, SKIP>(P, L, pending, r, 0.0f, dg);
   const unsigned long long key = L.key[lane];
   best_t = __uint_as_float((unsigned)(key >> 32));
   best_leaf = (int)(unsigned)key;
@@ -762,7 +770,7 @@ __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* _
   int node = FAST ? P.accel_root : P.root_ref;
   for (;;) {
     if (pending >= kShadowFlush) {  // between visits; a lane found occluded stops entering nodes
-      batch_flush<true, SPHERES, FAST>(P, L, pending, r, thr, dg);
+      batch_flush<true, SPHERES, FAST, SKIP>(P, L, pending, r, thr, dg);
       pending = 0;
       alive &= ~ballot(L.key[lane] != 0ull);
       m &= alive;
@@ -783,7 +791,7 @@ __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* _
       if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, alive)) break;
     }
   }
-  if (pending) batch_flush<true, SPHERES, FAST>(P, L, pending, r, thr, dg);
+  if (pending) batch_flush<true, SPHERES, FAST, SKIP>(P, L, pending, r, thr, dg);
   return L.key[lane] != 0ull;
 }
 
