@@ -471,6 +471,9 @@ def main() -> int:
     ap.add_argument("--no-weak", action="store_true",
                     help="N>1: skip the extra weak-scaling measurement (one frame per rank)")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="no HIP events around the kernels inside the timed region (A/B of "
+                         "their cost; the roofline then uses the one-frame-at-a-time times)")
     ap.add_argument("--no-share-probe", action="store_true",
                     help="N=1: skip the one-GPU prediction of strong scaling (share probe)")
     ap.add_argument("--cpu-rehearsal", action="store_true",
@@ -588,7 +591,8 @@ def main() -> int:
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
     scene.read_kernel_times()  # discard
-    scene.set_kernel_timing(True)  # HIP events around each traversal kernel, on its stream
+    # HIP events around each traversal kernel, on its stream
+    scene.set_kernel_timing(not args.no_kernel_timing)
     elapsed = timed_steps(renderer, args.steps, world, coll_dev, ev)
     scene.set_kernel_timing(False)
     kt, launches = scene.read_kernel_times()

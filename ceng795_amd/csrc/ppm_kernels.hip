@@ -892,6 +892,9 @@ __device__ __forceinline__ float radius_reduction(unsigned n) {
 #ifndef PPM_CPER
 #define PPM_CPER 4
 #endif
+#ifndef PPM_WAVE_COMPACT  // 1: each wave compacts its own part of a segment, no barriers (below)
+#define PPM_WAVE_COMPACT 0
+#endif
 __global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tiles, int ntiles,
                                                                 const int* list_start,
                                                                 const int* list_end,
@@ -905,7 +908,8 @@ __global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tile
   }
   const int g = tiles[t].x;
   const long long L = list_end[g] - list_start[g];
-  need[t] = L >= min_len ? ((L < seg ? L : (long long)seg) >> shift) : 0;
+  // (PPM_WAVE_COMPACT: twice that, per-wave scratch regions + the contiguous copy)
+  need[t] = L >= min_len ? ((L < seg ? L : (long long)seg) >> shift) * (PPM_WAVE_COMPACT ? 2 : 1) : 0;
 }
 
 #ifndef PPM_GATE_RUNS  // gate_round (A1): candidates per accept/reject run pair below which (A2) takes over
@@ -1272,6 +1276,93 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   int ls = seg, le = seg_e;
   const float4* src = pos;
   visits += (unsigned long long)(seg_e - seg);
+#if PPM_WAVE_COMPACT
+  if (compact) {
+    // (0) compaction, wave-parallel: wave w streams its own contiguous part of the segment
+    // (no barrier until the end), keeping the deposits within any tile hit point's radius at
+    // the segment start, in order, in its own scratch region of cap / 2 / waves records; then
+    // the waves' runs are copied back to back (in wave order = photon order) into the second
+    // half of the tile's range, which the windows read.  A wave whose run would not fit makes
+    // the segment fall back to uncompacted windows, as the workgroup-wide version does.
+    constexpr int kCW = kUpdThreads / 64;
+    constexpr int kCPer = PPM_CPER;
+    __shared__ int s_wn[kCW + 1];
+    const long long c0 = cofs[blockIdx.x];
+    const int half = (int)((cofs[blockIdx.x + 1] - c0) >> 1);
+    const int wcap = half / kCW;
+    float4* scratch = cbuf + c0;
+    float4* dst = cbuf + c0 + half;
+    const int wave = tid >> 6;
+    float r2c[kTileHP];
+#pragma unroll
+    for (int j = 0; j < kTileHP; j++) r2c[j] = j < nh ? s_r2[j] : -1.0f;
+#if PPM_PHASE_TIMERS
+    const unsigned long long t_c0 = S.diag == 2 && tid == 0 ? wall_clock64() : 0;
+#endif
+    const int per = ((le - ls + kCW - 1) / kCW + 63) & ~63;
+    const int wb = min(le, ls + wave * per), we = min(le, wb + per);
+    float4* wdst = scratch + (size_t)wave * wcap;
+    int n = 0;  // this wave's kept records so far (wave-uniform)
+    float4 cd[kCPer];
+    auto cfetch = [&](int base) {
+#pragma unroll
+      for (int q = 0; q < kCPer; q++) {
+        const int k = base + lane + q * 64;
+        if (k < we) cd[q] = pos[k];
+      }
+    };
+    cfetch(wb);
+    for (int base = wb; base < we; base += kCPer * 64) {
+      float4 cw[kCPer];
+#pragma unroll
+      for (int q = 0; q < kCPer; q++) cw[q] = cd[q];
+      cfetch(base + kCPer * 64);  // next round in flight
+#pragma unroll
+      for (int q = 0; q < kCPer; q++) {
+        const V x = mk(cw[q].x, cw[q].y, cw[q].z);
+        bool kp = false;
+#pragma unroll
+        for (int j = 0; j < kTileHP; j++) {
+          const V v = tp[j] - x;
+          kp = kp || (dot(v, v) <= r2c[j]);
+        }
+        kp = kp && base + lane + q * 64 < we;
+        const unsigned long long bal = __ballot(kp);
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+        if (kp && n + rank < wcap) wdst[n + rank] = cw[q];
+        n += __builtin_popcountll(bal);
+      }
+    }
+    if (lane == 0) s_wn[wave] = n;
+    __syncthreads();
+    int kept = 0, off = 0;
+    bool fits = true;
+#pragma unroll
+    for (int w = 0; w < kCW; w++) {
+      const int nw = s_wn[w];
+      fits = fits && nw <= wcap;
+      if (w < wave) off += nw;
+      kept += nw;
+    }
+    if (fits) {  // this wave's run to its place in the contiguous copy
+      for (int i = lane; i < n; i += 64) dst[off + i] = wdst[i];
+    }
+    __syncthreads();  // the copy is read by other threads of the workgroup below
+#if PPM_PHASE_TIMERS
+    if (S.diag == 2 && tid == 0) ctick += wall_clock64() - t_c0;
+#endif
+    if (fits) {
+      src = dst, ls = 0, le = kept;
+      visits += (unsigned long long)kept;
+    }
+    if (stats && tid == 0) {
+      atomicAdd(&stats[fits ? 20 : 21], 1ull);
+      atomicAdd(&stats[22], (unsigned long long)kept);
+    }
+    PPM_PHASE(0)
+  }
+#else
   if (compact) {
     // (0) compaction: rounds of 64 records per thread-row; one count per (record row, wave),
     // scanned by wave 0, keeps the copy in photon order
@@ -1355,6 +1446,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     }
     PPM_PHASE(0)
   }
+#endif
   windows += (unsigned long long)((le - ls + kWinMax - 1) / kWinMax);
   float4 dep[kPer];  // position, photon-order index << kRepBits | multiplicity
   auto fetch = [&](int base) {
