@@ -471,6 +471,9 @@ def main() -> int:
     ap.add_argument("--no-weak", action="store_true",
                     help="N>1: skip the extra weak-scaling measurement (one frame per rank)")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--gather-stream", choices=("render", "comm"), default="render",
+                    help="N>1 tile split: enqueue a step's gather + untile on its own render "
+                         "stream (default) or on one communication stream")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no HIP events around the kernels inside the timed region (A/B of "
                          "their cost; the roofline then uses the one-frame-at-a-time times)")
@@ -568,7 +571,8 @@ def main() -> int:
         renderer = dist_tiles.TileGatherRenderer(
             layout, stream, dist_tiles.scene_tile_renderer(scene), inflight=args.inflight,
             host_staging=host_staging, device=dev,
-            untile=None if host_staging else dist_tiles.scene_tile_untiler(scene, layout))
+            untile=None if host_staging else dist_tiles.scene_tile_untiler(scene, layout),
+            gather_stream=args.gather_stream)
     else:
         owners = dist_tiles.FrameOwners(n_cams, world, rank)
         sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]

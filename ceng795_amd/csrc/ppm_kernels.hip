@@ -893,7 +893,7 @@ __device__ __forceinline__ float radius_reduction(unsigned n) {
 #define PPM_CPER 4
 #endif
 #ifndef PPM_WAVE_COMPACT  // 1: each wave compacts its own part of a segment, no barriers (below)
-#define PPM_WAVE_COMPACT 0
+#define PPM_WAVE_COMPACT 1
 #endif
 __global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tiles, int ntiles,
                                                                 const int* list_start,

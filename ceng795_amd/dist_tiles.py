@@ -227,7 +227,8 @@ class TileGatherRenderer:
     host, one buffer set.  frames: rank 0's frames of the last step (complete after finish())."""
 
     def __init__(self, layout: TileLayout, stream, render: Callable, inflight: int = 2,
-                 host_staging: bool = False, device=None, untile: Optional[Callable] = None):
+                 host_staging: bool = False, device=None, untile: Optional[Callable] = None,
+                 gather_stream: str = "render"):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -238,6 +239,11 @@ class TileGatherRenderer:
         # (scene_tile_untiler: the library's kernel); None: one index_select into padded frames
         self.untile = untile
         self.host_staging = host_staging
+        # "render": a step's gather and untile are enqueued on its own render stream after the
+        # render (the other steps' streams keep rendering meanwhile; set s is reused on the same
+        # stream, so no events); "comm": on one communication stream, handed over by events
+        assert gather_stream in ("render", "comm")
+        self.gather_on_render = gather_stream == "render"
         self.inflight = 1 if host_staging else max(1, int(inflight))
         F = self.inflight
         dev = device if device is not None else (
@@ -280,7 +286,7 @@ class TileGatherRenderer:
     def _slot(self, s: int, sh: CameraShare):
         return self.local[s][sh.offset:sh.offset + sh.slot]
 
-    def _gather(self, s: int):
+    def _gather(self, s: int, stream=None):
         torch, dist, L = self.torch, self.dist, self.layout
         root = self.rank == 0
         for c, sh in enumerate(L.shares):
@@ -293,7 +299,7 @@ class TileGatherRenderer:
                 outs = list(self.gathered[s][c]) if root else None
                 dist.gather(self._slot(s, sh), outs, dst=0, async_op=True).wait()
             if root and self.untile is not None:
-                self.untile(c, self.gathered[s][c], self.padded[s][c], self.comm)
+                self.untile(c, self.gathered[s][c], self.padded[s][c], stream)
             elif root:
                 untile_camera(self.gathered[s][c].view(-1, TILE_FLOATS), L, c, self.index[c],
                               self.padded[s][c])
@@ -302,8 +308,8 @@ class TileGatherRenderer:
         s = self.k % self.inflight
         self.k += 1
         st = self.rstreams[s]
-        if not self.host_staging and self.used[s]:  # its gather `inflight` steps ago
-            st.wait_event(self.done[s])
+        if not self.host_staging and self.used[s] and not self.gather_on_render:
+            st.wait_event(self.done[s])  # its gather `inflight` steps ago
         if events is not None:
             events[0].record(st)
         for sh in self.layout.shares:
@@ -313,11 +319,14 @@ class TileGatherRenderer:
             events[1].record(st)
         if self.host_staging:
             self._gather(s)
+        elif self.gather_on_render:
+            with self.torch.cuda.stream(st):
+                self._gather(s, st)
         else:
             self.handoff[s].record(st)
             with self.torch.cuda.stream(self.comm):
                 self.comm.wait_event(self.handoff[s])
-                self._gather(s)
+                self._gather(s, self.comm)
                 self.done[s].record(self.comm)
             self.used[s] = True
         if self.rank == 0:

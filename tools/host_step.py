@@ -58,15 +58,21 @@ def main():
     out["inplace"] = measure(dist_tiles.FrameRenderer(scene, stream, inflight=a.inflight),
                              a.steps, torch)
     layout = dist_tiles.TilePlan(scene, 1, 0)
-    for label, untile in (("tile_gather_lib_untile", dist_tiles.scene_tile_untiler(scene, layout)),
-                          ("tile_gather_index_untile", None)):
+    for label, untile, gs in (
+            ("tile_gather_render_stream", dist_tiles.scene_tile_untiler(scene, layout), "render"),
+            ("tile_gather_comm_stream", dist_tiles.scene_tile_untiler(scene, layout), "comm"),
+            ("tile_gather_index_untile", None, "render")):
         R = dist_tiles.TileGatherRenderer(layout, stream, dist_tiles.scene_tile_renderer(scene),
-                                          inflight=a.inflight, device=dev, untile=untile)
+                                          inflight=a.inflight, device=dev, untile=untile,
+                                          gather_stream=gs)
         out[label] = measure(R, a.steps, torch)
+    out["inplace_again"] = measure(dist_tiles.FrameRenderer(scene, stream, inflight=a.inflight),
+                                   a.steps, torch)
     # the pieces of one tile-gather step, host time only
     R = dist_tiles.TileGatherRenderer(layout, stream, dist_tiles.scene_tile_renderer(scene),
                                       inflight=a.inflight, device=dev,
-                                      untile=dist_tiles.scene_tile_untiler(scene, layout))
+                                      untile=dist_tiles.scene_tile_untiler(scene, layout),
+                                      gather_stream="comm")
     for _ in range(5):
         R.step()
     R.finish()
