@@ -84,7 +84,7 @@ def main():
     t1 = time.perf_counter()
     with torch.cuda.stream(R.comm):
         for k in range(a.steps):
-            R._gather(k % R.inflight)
+            R._gather(k % R.inflight, R.comm)
     t2 = time.perf_counter()
     torch.cuda.synchronize()
     out["pieces_host_ms"] = {"render_call": round((t1 - t0) / a.steps * 1e3, 4),

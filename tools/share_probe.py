@@ -34,6 +34,20 @@ def timed(scene, world, rank, stream, inflight, steps, torch, dist_tiles):
     return round(ms, 4)
 
 
+def timed_inplace(scene, stream, inflight, steps, torch, dist_tiles):
+    R = dist_tiles.FrameRenderer(scene, stream, inflight=inflight)
+    for _ in range(3):
+        R.step()
+    R.finish()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        R.step()
+    R.finish()
+    torch.cuda.synchronize()
+    return round((time.perf_counter() - t0) / steps * 1e3, 4)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
@@ -47,10 +61,11 @@ def main():
     stream = torch.cuda.current_stream()
     out = {"world": a.world}
     N = a.world
+    out["inplace_inflight4"] = timed_inplace(scene, stream, 4, a.steps, torch, dist_tiles)
     out["forward"] = [timed(scene, N, r, stream, 4, a.steps, torch, dist_tiles) for r in range(N)]
     out["reverse"] = [timed(scene, N, r, stream, 4, a.steps, torch, dist_tiles)
                       for r in reversed(range(N))][::-1]
-    for r in (0, 2):
+    for r in sorted({0, min(2, N - 1)}):
         out[f"rank{r}_inflight"] = {k: timed(scene, N, r, stream, k, a.steps, torch, dist_tiles)
                                     for k in (1, 2, 3, 4, 6, 8)}
         print(json.dumps(out), file=sys.stderr, flush=True)
