@@ -474,6 +474,8 @@ def main() -> int:
     ap.add_argument("--gather-stream", choices=("render", "comm"), default="render",
                     help="N>1 tile split: enqueue a step's gather + untile on its own render "
                          "stream (default) or on one communication stream")
+    ap.add_argument("--no-step-events", action="store_true",
+                    help="no per-step timing events in the timed region (render_ms_avg = 0)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no HIP events around the kernels inside the timed region (A/B of "
                          "their cost; the roofline then uses the one-frame-at-a-time times)")
@@ -592,15 +594,16 @@ def main() -> int:
         dist.all_reduce(rays_step)
     rays_step = float(rays_step.item())
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    ev = None if args.no_step_events else [
+        (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        for _ in range(args.steps)]
     scene.read_kernel_times()  # discard
     # HIP events around each traversal kernel, on its stream
     scene.set_kernel_timing(not args.no_kernel_timing)
     elapsed = timed_steps(renderer, args.steps, world, coll_dev, ev)
     scene.set_kernel_timing(False)
     kt, launches = scene.read_kernel_times()
-    render_ms = [a.elapsed_time(b) for a, b in ev]
+    render_ms = [a.elapsed_time(b) for a, b in ev] if ev else [0.0]
     scene.collect_stats()  # reset counters
 
     verified = None

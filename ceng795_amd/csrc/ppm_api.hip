@@ -291,7 +291,10 @@ bool lpt_order() { return PPM_LPT_ORDER != 0; }
 // list holds at least this many deposits copy the reachable ones first.  Results do not depend
 // on it (the copy is a superset of every window's candidates, in order).
 // ppm_set_update_compaction sets it per scene (0: off).
-constexpr int kCompactShift = 2;  // scratch per compacted tile: a quarter of its list
+#ifndef PPM_COMPACT_SHIFT  // (A/B builds)
+#define PPM_COMPACT_SHIFT 2
+#endif
+constexpr int kCompactShift = PPM_COMPACT_SHIFT;  // scratch per compacted tile: a quarter of its list
 constexpr int kDefaultCompactSeg = 32768;  // deposits per compaction segment
 long long default_compact_min() { return 65536LL; }
 
