@@ -913,7 +913,7 @@ __global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tile
 }
 
 #ifndef PPM_GATE_RUNS  // gate_round (A1): candidates per accept/reject run pair below which (A2) takes over
-#define PPM_GATE_RUNS 32
+#define PPM_GATE_RUNS 16
 #endif
 #ifndef PPM_GATE_PRIO  // wave priority of the gate waves while they run gate_round
 #define PPM_GATE_PRIO 3

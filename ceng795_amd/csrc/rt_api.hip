@@ -79,6 +79,10 @@ struct StreamScratch {
   size_t frames_capacity = 0;
   float* samples = nullptr;
   size_t samples_capacity = 0;
+  // warm order: the selection whose heavy-first unit order the last frame on this stream left
+  // in `sched` (valid: that frame ran the order kernel)
+  std::array<long long, 7> order_key{};
+  bool order_valid = false;
 };
 
 // Per-kernel HIP-event timing of render launches (rt_set_kernel_timing): one quad of events per
@@ -294,6 +298,15 @@ constexpr size_t kCounterAlloc = (size_t)kCounterWidth * kCounterRows;
 #define RT_ORDER_CHUNKS 1
 #endif
 // sched: sched_words_for(num_sel_tiles) words — tile costs, then the unit order lists
+// The untile kernel copies 16-B chunks when every frame row and both buffers are 16-B aligned.
+int untile_vec(const UntileParams& U) {
+  return (U.width % 4 == 0) && ((uintptr_t)U.out % 16 == 0) && ((uintptr_t)U.recv % 16 == 0);
+}
+
+#ifndef RT_WARM_ORDER  // (A/B builds: 0 = the primary kernel in block order)
+#define RT_WARM_ORDER 1
+#endif
+
 void set_schedule(RenderParams& P, unsigned* sched) {
   const int regions = RT_ORDER_REGIONS;
   P.tile_cost = regions ? sched : nullptr;
@@ -819,6 +832,7 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
   U.slot = slot;
   U.tile_offset = 0;
   U.blocks = 1;
+  U.vec = untile_vec(U);
   hip_check(launch_untile(U, x0->stream), "untile launch");
   if (s0 != x0->stream) {
     hip_check(hipEventRecord(x0->ev_out, x0->stream), "event record");
@@ -1089,7 +1103,15 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
         throw std::domain_error("NumSamples > 1 renders whole row-major frames only");
       ensure(sc->samples, sc->samples_capacity, sample_floats(c), "alloc MSAA samples");
     }
+    // warm order: a frame of the same selection as the stream's previous one
+    // dispatches its primary kernel heaviest-first by that frame's measured tile costs
+    const std::array<long long, 7> key{cam, row0, row_stride, tile_begin, tile_step,
+                                       P.num_sel_tiles, P.block_deal};
+    const bool orderable = RT_WARM_ORDER && c.num_samples <= 1 && !P.frames && P.num_lights > 0;
+    P.primary_order = orderable && sc->order_valid && sc->order_key == key ? 1 : 0;
     enqueue_frame(s, r, P, c.num_samples, sc->samples, (hipStream_t)stream, true);
+    sc->order_key = key;
+    sc->order_valid = orderable;
     return RT_OK;
   });
 }
@@ -1121,6 +1143,7 @@ int rt_untile_device(rt_scene* s, int cam, int row0, int row_stride, int devices
     U.slot = slot;
     U.tile_offset = tile_offset % devices;
     U.blocks = blocks;
+    U.vec = untile_vec(U);
     hip_check(launch_untile(U, (hipStream_t)stream), "untile launch");
     return RT_OK;
   });

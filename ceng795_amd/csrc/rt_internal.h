@@ -199,6 +199,7 @@ struct UntileParams {
   int width, row0, row_stride, rows, tiles_x, tiles_total, devices, slot;
   int tile_offset;  // deal unit u went to rank (u + tile_offset) mod devices (rt_untile_device)
   int blocks;       // 1: the units are 2x2 blocks in deal order (deal_block_index), else tiles
+  int vec;          // 1: rows and buffers 16-B aligned (untile by 16-B chunks)
 };
 
 // Words of the per-stream schedule buffer for a launch of `tiles` selected tiles: tile costs
@@ -261,6 +262,8 @@ struct RenderParams {
   int* unit_order;
   int order_regions, order_chunk, order_stride, order_units;
   int use_order;
+  int primary_order;  // the primary kernel too dispatches by unit_order: the order the previous
+                      // frame of the same selection left on this stream (rt_api.hip warm order)
   float* frames;  // recursive scenes only: (max_depth+1) * 28 * lanes ray-tree frames, else null
   // kCounterRows rows of kCounterWidth u64 (columns: kCnt*)
   unsigned long long* counters;

@@ -1610,7 +1610,9 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
   RenderParams S = T;
   mark(marks, 0, stream);
   if (!ordered) T.tile_cost = nullptr;
-  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES>), dim3(tblocks),
+  // warm order: the previous frame's heavy-first unit order (same selection, same stream)
+  T.use_order = ordered && P.primary_order ? 1 : 0;
+  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES>), dim3(T.use_order ? oblocks : tblocks),
                      dim3(kTraceWaves * 64), tlds, stream, T, nodes);
   mark(marks, 1, stream);
   S.tile_cost = T.tile_cost;
@@ -1684,30 +1686,48 @@ hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream) {
   return hipGetLastError();
 }
 
-// The gathered tiles of a multi-device frame back into rows (UntileParams): one wave per tile,
-// one lane per pixel; each 8-pixel row of a tile is 96 contiguous bytes in both layouts.
-__global__ __launch_bounds__(256) void untile_kernel(UntileParams U) {
-  const int t = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
-  if (t >= U.tiles_total) return;
-  const int lane = lane_id();
-  const int tx = t % U.tiles_x, ty = t / U.tiles_x;
-  const int px = tx * kTile + (lane & 7), lr = ty * kTile + (lane >> 3);
-  if (px >= U.width || lr >= U.rows) return;
+// The gathered tiles of a multi-device frame back into rows (UntileParams).  Each 8-pixel row
+// of a tile is 96 contiguous bytes in both layouts: six 16-B chunks, one per thread (a wave
+// covers 10 tile rows); a tile row on the frame's right edge, or a frame whose rows are not
+// 16-B aligned (width % 4 != 0), is copied by pixel instead.
+__device__ __forceinline__ const float* untile_src(const UntileParams& U, int t, int tx, int ty) {
   int w = 0;
   const int u = U.blocks ? deal_block_index(U.tiles_x, tx, ty, w) : t;  // deal unit
   const int r = (u + U.tile_offset) % U.devices;
   const int b = ((r - U.tile_offset) % U.devices + U.devices) % U.devices;  // rank r's first unit
   const int k = U.blocks ? 4 * ((u - b) / U.devices) + w : (u - b) / U.devices;  // slot tile
-  const float* src = U.recv + ((size_t)(r * U.slot + k) * (kTile * kTile) + lane) * 3;
-  float* dst = U.out + ((size_t)(U.row0 + lr * U.row_stride) * U.width + px) * 3;
-  dst[0] = src[0];
-  dst[1] = src[1];
-  dst[2] = src[2];
+  return U.recv + (size_t)(r * U.slot + k) * (kTile * kTile * 3);
+}
+
+constexpr int kUntileChunks = 6;  // 16-B chunks per 8-pixel tile row
+__global__ __launch_bounds__(256) void untile_kernel(UntileParams U) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long trow = i / kUntileChunks;  // tile row: tile * 8 + row in tile
+  const int c = (int)(i - trow * kUntileChunks);
+  if (trow >= (long long)U.tiles_total * kTile) return;
+  const int t = (int)(trow >> 3), y = (int)(trow & 7);
+  const int tx = t % U.tiles_x, ty = t / U.tiles_x;
+  const int lr = ty * kTile + y, px0 = tx * kTile;
+  if (lr >= U.rows) return;
+  const float* src = untile_src(U, t, tx, ty) + y * (kTile * 3);
+  float* dst = U.out + ((size_t)(U.row0 + lr * U.row_stride) * U.width + px0) * 3;
+  if (px0 + kTile <= U.width && U.vec) {
+    reinterpret_cast<float4*>(dst)[c] = reinterpret_cast<const float4*>(src)[c];
+    return;
+  }
+  // edge tile row / unaligned frame: this thread's four floats, those inside the frame
+  const int lim = (U.width - px0) * 3;
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const int f = 4 * c + e;
+    if (f < lim) dst[f] = src[f];
+  }
 }
 
 hipError_t launch_untile(const UntileParams& U, hipStream_t stream) {
   if (U.tiles_total <= 0) return hipSuccess;
-  hipLaunchKernelGGL(untile_kernel, dim3((U.tiles_total + 3) / 4), dim3(256), 0, stream, U);
+  const long long threads = (long long)U.tiles_total * kTile * kUntileChunks;
+  hipLaunchKernelGGL(untile_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, U);
   return hipGetLastError();
 }
 

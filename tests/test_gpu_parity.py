@@ -168,6 +168,36 @@ def test_c3_frame_matches_reference_golden_hash(rt, scene_dir):
             assert st.rays() == gc["rays"]
 
 
+def test_c3_warm_order_frames_match_reference_golden_hash(rt, scene_dir):
+    """Repeated frames on one stream: from the second frame on, the primary kernel dispatches
+    its units heaviest-first by the tile costs the previous frame measured (warm order,
+    rt_api.hip); the order must not change a bit.  Frames on two streams alternate, and a
+    different tile selection in between invalidates the order."""
+    import hashlib
+    import json
+    import torch
+    golden = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+    gc = golden["c3"]["cameras"][0]
+    xml = scenes.write_c3(scene_dir)
+    with rt.Scene(xml) as s:
+        c = s.camera(0)
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        bufs = [torch.empty((c.height, c.width, 3), dtype=torch.float32, device="cuda")
+                for _ in range(6)]
+        tiles = torch.empty((s.num_tiles(0) * 64 * 3,), dtype=torch.float32, device="cuda")
+        for k, b in enumerate(bufs):
+            st = streams[k % 2]
+            if k == 3:  # another selection on stream 1: its next frame runs cold again
+                s.render_device(0, tiles.data_ptr(), tile_begin=1, tile_step=3, tile_major=True,
+                                stream=st.cuda_stream)
+            s.render_device(0, b.data_ptr(), stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        for k, b in enumerate(bufs):
+            assert hashlib.sha256(b.cpu().numpy().tobytes()).hexdigest() == gc["frame_sha256"], k
+        for st in streams:
+            s.release_stream(st.cuda_stream)
+
+
 @pytest.mark.slow
 def test_c3_full_resolution_matches_oracle(rt, scene_dir):
     xml = scenes.write_c3(scene_dir)
