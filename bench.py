@@ -709,6 +709,9 @@ def main() -> int:
                        "parallelism": (f"tiles{world}+{comm}_gather" if tiled else
                                        f"frames{world}+{comm}_gather" if use_pg else "frames1"),
                        "frames_in_flight": renderer.inflight,
+                       "dispatch": "heavy-first per XCD region; the primary kernel by the tile "
+                                   "costs of the previous frame on its stream (warm order, "
+                                   "DESIGN.md 4.8), every frame's rays all traced",
                        "gather_verified": verified,
                        "render_ms_avg": round(sum(render_ms) / len(render_ms), 4)},
             "roofline": roof, "cpu_baseline": cpu, "pcie_inclusive": host_rate,
