@@ -425,19 +425,28 @@ constexpr int kBatchFlush = RT_BATCH_FLUSH;   // run the queue once this many te
 constexpr int kBatchCap = kBatchFlush + 256;  // a wide visit flushes before a slot could overflow
 constexpr int kShadowFlush = kBatchFlush;
 
+// Queue pushes write every lane: lanes outside the push mask write a junk entry past the
+// queue (q[kBatchCap + ...], never read) instead of taking an exec-mask branch (RT_PUSH_ALL).
+#ifndef RT_PUSH_ALL
+#define RT_PUSH_ALL 1
+#endif
+constexpr int kPushJunk = RT_PUSH_ALL ? 128 : 0;
 struct WaveLeafLds {
-  unsigned long long q[kBatchCap];  // lo 32: leaf (DevLeaf or DFS index), hi 32: lane
+  unsigned long long q[kBatchCap + kPushJunk];  // lo 32: leaf (DevLeaf or DFS index), hi 32: lane
   unsigned long long key[64];       // per lane: closest-hit key, or shadow flag
 };
 
 constexpr unsigned long long kNoHitKey = (0x7f800000ull << 32) | 0xffffffffull;  // (+inf, -1)
 
 // Queue leaf `leaf` for the lanes of `m` (wave-uniform); n = pending entries (wave-uniform).
+template <bool ALL = false>
 __device__ __forceinline__ void batch_push(WaveLeafLds& L, int& n, int leaf, uint64_t m) {
   const int lane = lane_id();
-  if (lane_in(m)) {
-    const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+  const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+  if (ALL) {
+    L.q[lane_in(m) ? n + below : kBatchCap + lane] = ((unsigned long long)lane << 32) | (unsigned)leaf;
+  } else if (lane_in(m)) {
     L.q[n + below] = ((unsigned long long)lane << 32) | (unsigned)leaf;
   }
   n += __builtin_popcountll(m);
@@ -445,12 +454,17 @@ __device__ __forceinline__ void batch_push(WaveLeafLds& L, int& n, int leaf, uin
 
 // Queue leaves `leaf` and `leaf + 1` (a pair) for the lanes of `m`: each lane's two entries are
 // adjacent (one 16-B LDS write), the queue order does not matter.
+template <bool ALL = false>
 __device__ __forceinline__ void batch_push_pair(WaveLeafLds& L, int& n, int leaf, uint64_t m) {
   const int lane = lane_id();
-  if (lane_in(m)) {
-    const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-    const unsigned long long hi = (unsigned long long)lane << 32;
+  const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+  const unsigned long long hi = (unsigned long long)lane << 32;
+  if (ALL) {
+    const int at = lane_in(m) ? n + 2 * below : kBatchCap + 2 * lane;
+    L.q[at] = hi | (unsigned)leaf;
+    L.q[at + 1] = hi | (unsigned)(leaf + 1);
+  } else if (lane_in(m)) {
     L.q[n + 2 * below] = hi | (unsigned)leaf;
     L.q[n + 2 * below + 1] = hi | (unsigned)(leaf + 1);
   }
@@ -627,8 +641,9 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
     }
     const float tn = __builtin_fmaxf(__builtin_fmaxf(n3[0], n3[1]), n3[2]);
     const float tf = __builtin_fminf(__builtin_fminf(f3[0], f3[1]), f3[2]);
-    // out: !(tf >= tn) or !(tf >= 0) — unordered, so a NaN (invalid slot) is out
-    const uint64_t hm = m & alive & ~(lanes_nge(tf, tn) | lanes_nge(tf, 0.0f));
+    // out: !(tf >= max(tn, 0)) — one compare (tn and tf are never NaN on a valid slot: finite
+    // fp16 planes, finite scales, skipped axes at -inf / +inf)
+    const uint64_t hm = m & alive & ~lanes_nge(tf, __builtin_fmaxf(tn, 0.0f));
     if (!hm) continue;
     if (kinds & (kSlotLeafy << c)) {
       const int leaf = leaf_base + (int)((offs >> (4 * c)) & 15u);
@@ -637,10 +652,11 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
         batch_flush<SHADOW, SPHERES, true, SKIP>(P, L, pending, r, thr, dg);
         pending = 0;
       }
+      // (the shadow kernel keeps the exec-mask pushes: junk writes cost it VGPR spills)
       if (pair)
-        batch_push_pair(L, pending, leaf, hm);
+        batch_push_pair<RT_PUSH_ALL && !SHADOW>(L, pending, leaf, hm);
       else
-        batch_push(L, pending, leaf, hm);
+        batch_push<RT_PUSH_ALL && !SHADOW>(L, pending, leaf, hm);
       DIAG(dg.leaves += 1 + pair; dg.leaf_lanes += (1 + pair) * __builtin_popcountll(hm));
       continue;
     }
