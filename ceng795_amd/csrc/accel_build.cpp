@@ -221,8 +221,9 @@ void encode_node(DevNode8& W, const Slot* sl, int n, const double* margin) {
     int k = (int)std::ceil(std::log2(std::max(ext, 1e-300) / 32768.0));
     k = std::min(std::max(k, -120), 120);
     while (std::ldexp(ext, -k) > 32768.0) k++;  // (log2 rounding)
+    if (k > 127) throw std::runtime_error("culling node extent beyond the fp16 scale range");
     ka[a] = k;
-    W.scale |= (uint32_t)(k + 128) << (8 * a);
+    W.scale |= (uint32_t)(uint8_t)(int8_t)k << (8 * a);  // signed byte: one s_bfe_i32 in the kernel
   }
   for (int c = 0; c < kWideSlots; c++)
     for (int a = 0; a < 3; a++) {
@@ -240,7 +241,7 @@ void encode_node(DevNode8& W, const Slot* sl, int n, const double* margin) {
 // The decoded box of slot c (for the invariant check).
 void decode_slot(const DevNode8& W, int c, double* lo, double* hi) {
   for (int a = 0; a < 3; a++) {
-    const int k = (int)((W.scale >> (8 * a)) & 255) - 128;
+    const int k = (int)(int8_t)(uint8_t)((W.scale >> (8 * a)) & 255);
     lo[a] = (double)W.origin[a] + std::ldexp(half_value((uint16_t)(W.box[c][a] & 0xffff)), k);
     hi[a] = (double)W.origin[a] + std::ldexp(half_value((uint16_t)(W.box[c][a] >> 16)), k);
   }

@@ -52,7 +52,7 @@ static_assert(sizeof(DevNode) == 64, "node must be one 64-byte scalar load");
 // 16 + c a leaf pair; its leaves are DevLeaf records leaf_base + (offs >> 4c & 15) and the next
 // one) or INNER (a child node: inner_base + 2 * (number of inner slots before c)).  Every slot
 // carries a CONSERVATIVE box in fp16, relative to `origin` and scaled by 2^k per axis:
-//   plane = origin[a] + h * 2^(scale byte a - 128)
+//   plane = origin[a] + h * 2^(scale byte a, signed)
 // rounded outward and inflated by the scene's culling margin (HostScene::cull_margin), so a
 // plain slab test (no decision band) never culls a treelet the reference would enter; the
 // exact decision (the treelet's guard box) is taken per ray in the leaf batch.  An invalid
@@ -62,7 +62,7 @@ constexpr int kWideSlots = 8;
 enum : int32_t { kSlotValid = 1, kSlotLeafy = 1 << 8, kSlotPair = 1 << 16 };
 struct alignas(16) DevNode8 {
   float origin[3];
-  uint32_t scale;      // byte a: k_a + 128
+  uint32_t scale;      // byte a: k_a as a signed byte
   int32_t inner_base;  // DevNode index of the first inner child (children contiguous, 2 slots each)
   int32_t leaf_base;   // DevLeaf index of the first leafy slot's first leaf
   int32_t kinds;       // kSlotValid << c | kSlotLeafy << c | kSlotPair << c

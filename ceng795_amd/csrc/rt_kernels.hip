@@ -605,14 +605,13 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
   const int inner_base = a[4], leaf_base = a[5], kinds = a[6];
   const unsigned offs = (unsigned)a[7];
   const unsigned inner = (unsigned)kinds & ~((unsigned)kinds >> 8) & 0xffu;
-  const int nslots = __builtin_popcount((unsigned)kinds & 0xffu);  // valid slots come first
   DIAG(dg.nodes++; dg.wide++; dg.node_lanes += __builtin_popcountll(m));
   const float o[3] = {r.o.x, r.o.y, r.o.z}, rc[3] = {r.r.x, r.r.y, r.r.z}, mg[3] = {r.m.x, r.m.y, r.m.z};
   const int sh[3] = {r.sh0, r.sh1, r.sh2};
   float S[3], Alo[3], Ahi[3];
 #pragma unroll
   for (int x = 0; x < 3; x++) {
-    S[x] = __builtin_amdgcn_ldexpf(rc[x], (int)((scale >> (8 * x)) & 255u) - 128);
+    S[x] = __builtin_amdgcn_ldexpf(rc[x], (int)(signed char)(scale >> (8 * x)));
     const float A = (__int_as_float(a[x]) - o[x]) * rc[x];
     Alo[x] = A - __builtin_fabsf(mg[x]);  // entry plane earlier
     Ahi[x] = A + __builtin_fabsf(mg[x]);  // exit plane later
@@ -628,7 +627,9 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
   unsigned nkey = 0;
 #pragma unroll
   for (int c = 0; c < kWideSlots; c++) {
-    if (c >= nslots) break;  // (the NaN planes of an invalid slot would fail the test anyway)
+    // the valid slots come first (check_accel): stop at the first invalid one (its NaN planes
+    // would fail the test anyway)
+    if (!(kinds & (kSlotValid << c))) break;
     float n3[3], f3[3];
 #pragma unroll
     for (int x = 0; x < 3; x++) {
