@@ -499,6 +499,13 @@ void build_accel(HostScene& s, int K) {
   }
   s.accel_items = (int)items.size();
   s.accel_root = collapse_wide(s, B, broot, holder, ref_box);
+  if (s.nodes.size() >= kMaxNodeSlots) {  // the kernels address wide nodes by 32-bit byte offset
+    s.nodes.resize(s.accel_root & ~kWideTag);
+    s.accel_root = -1;  // (the reference traversal has no such limit)
+    s.accel_depth = 0;
+    s.accel_items = 0;
+    s.leaves.clear();
+  }
 }
 
 // Structural invariants of the culling tree the kernels' exactness argument relies on

@@ -58,6 +58,9 @@ static_assert(sizeof(DevNode) == 64, "node must be one 64-byte scalar load");
 // exact decision (the treelet's guard box) is taken per ray in the leaf batch.  An invalid
 // slot holds NaN planes, which every slab test rejects.
 constexpr int32_t kWideTag = 1 << 30;
+// node slots a scene may have with a culling tree: the traversal loads a wide node at the 32-bit
+// byte offset (ref << 6) (rt_kernels.hip load_node8); larger scenes walk the reference tree
+constexpr size_t kMaxNodeSlots = size_t(1) << 26;
 constexpr int kWideSlots = 8;
 enum : int32_t { kSlotValid = 1, kSlotLeafy = 1 << 8, kSlotPair = 1 << 16 };
 struct alignas(16) DevNode8 {

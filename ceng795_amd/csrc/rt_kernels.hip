@@ -563,11 +563,14 @@ __device__ __forceinline__ void queue_binary_leaves(WaveLeafLds& L, int& pending
 // ------------------------------------------------------------------ 8-wide culling nodes
 // The whole 128-B node (DevNode8) in one round trip: two s_load_dwordx16 and one wait.
 typedef int v16i __attribute__((ext_vector_type(16)));
-__device__ __forceinline__ void load_node8(const DevNode* __restrict__ nodes, int idx, v16i& a,
+// `ref` is the tagged node reference: (ref << 6) as 32 bits is the byte offset of its first slot
+// (the tag bit falls off the top; the host keeps the node array below 2^26 slots), used as the
+// loads' SGPR offset — one shift and one add per visit instead of a 64-bit address.
+__device__ __forceinline__ void load_node8(const DevNode* __restrict__ nodes, int ref, v16i& a,
                                            v16i& b) {
-  const void* p = nodes + idx;
-  asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
-               : "=s"(a), "=s"(b) : "s"(p) : "memory");
+  const unsigned off = (unsigned)ref << 6, off2 = off + 64u;
+  asm volatile("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx16 %1, %2, %4\n\ts_waitcnt lgkmcnt(0)"
+               : "=&s"(a), "=&s"(b) : "s"(nodes), "s"(off), "s"(off2) : "memory");
 }
 
 // fp16 halves of a slot word: the compiler feeds them to v_fma_mix_f32 straight from the SGPR
@@ -600,7 +603,7 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
                                            int& node, uint64_t& m, uint64_t alive,
                                            WaveStack<DEEP>& st, Diag& dg) {
   v16i a, b;
-  load_node8(nodes, node & ~kWideTag, a, b);
+  load_node8(nodes, node, a, b);
   const unsigned scale = (unsigned)a[3];
   const int inner_base = a[4], leaf_base = a[5], kinds = a[6];
   const unsigned offs = (unsigned)a[7];
