@@ -474,6 +474,9 @@ def main() -> int:
     ap.add_argument("--gather-stream", choices=("render", "comm"), default="render",
                     help="N>1 tile split: enqueue a step's gather + untile on its own render "
                          "stream (default) or on one communication stream")
+    ap.add_argument("--root-gather", action="store_true",
+                    help="N>1 tile split: rank 0 renders its share tile-major and gathers it "
+                         "with the others (default: in place, point-to-point receives only)")
     ap.add_argument("--no-step-events", action="store_true",
                     help="no per-step timing events in the timed region (render_ms_avg = 0)")
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -574,7 +577,9 @@ def main() -> int:
             layout, stream, dist_tiles.scene_tile_renderer(scene), inflight=args.inflight,
             host_staging=host_staging, device=dev,
             untile=None if host_staging else dist_tiles.scene_tile_untiler(scene, layout),
-            gather_stream=args.gather_stream)
+            gather_stream=args.gather_stream,
+            render_inplace=None if (host_staging or args.root_gather)
+            else dist_tiles.scene_inplace_renderer(scene))
     else:
         owners = dist_tiles.FrameOwners(n_cams, world, rank)
         sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]

@@ -832,6 +832,7 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
   U.slot = slot;
   U.tile_offset = 0;
   U.blocks = 1;
+  U.skip_root = 0;
   U.vec = untile_vec(U);
   hip_check(launch_untile(U, x0->stream), "untile launch");
   if (s0 != x0->stream) {
@@ -1117,15 +1118,17 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
 }
 
 int rt_untile_device(rt_scene* s, int cam, int row0, int row_stride, int devices, int slot,
-                     int tile_offset, int blocks, const float* d_gathered, float* d_out,
+                     int tile_offset, int flags, const float* d_gathered, float* d_out,
                      void* stream) {
   return guarded([&] {
     check_render_args(s, cam, row0, row_stride);
     if (devices < 1 || slot < 0 || tile_offset < 0 || !d_gathered || !d_out ||
-        (blocks != 0 && blocks != 1) || (blocks && slot % 4))
+        (flags & ~(RT_UNTILE_BLOCKS | RT_UNTILE_SKIP_ROOT)) ||
+        ((flags & RT_UNTILE_BLOCKS) && slot % 4))
       throw std::invalid_argument("rt_untile_device: bad argument");
     const rt_camera& c = s->host.cameras[cam];
     const TilePlan tp = plan(c, row0, row_stride);
+    const int blocks = (flags & RT_UNTILE_BLOCKS) ? 1 : 0;
     const long long units = blocks ? deal_blocks(tp.tiles_x, tp.tiles_total / tp.tiles_x) : tp.tiles_total;
     if ((long long)devices * (blocks ? slot / 4 : slot) < units)
       throw std::invalid_argument("rt_untile_device: devices * slot is smaller than the frame's share");
@@ -1143,6 +1146,7 @@ int rt_untile_device(rt_scene* s, int cam, int row0, int row_stride, int devices
     U.slot = slot;
     U.tile_offset = tile_offset % devices;
     U.blocks = blocks;
+    U.skip_root = (flags & RT_UNTILE_SKIP_ROOT) ? 1 : 0;
     U.vec = untile_vec(U);
     hip_check(launch_untile(U, (hipStream_t)stream), "untile launch");
     return RT_OK;

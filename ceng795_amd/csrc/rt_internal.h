@@ -203,6 +203,7 @@ struct UntileParams {
   int tile_offset;  // deal unit u went to rank (u + tile_offset) mod devices (rt_untile_device)
   int blocks;       // 1: the units are 2x2 blocks in deal order (deal_block_index), else tiles
   int vec;          // 1: rows and buffers 16-B aligned (untile by 16-B chunks)
+  int skip_root;    // 1: rank 0's units are left alone (it rendered them in place)
 };
 
 // Words of the per-stream schedule buffer for a launch of `tiles` selected tiles: tile costs

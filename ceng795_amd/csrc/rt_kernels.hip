@@ -1710,10 +1710,12 @@ hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream) {
 // of a tile is 96 contiguous bytes in both layouts: six 16-B chunks, one per thread (a wave
 // covers 10 tile rows); a tile row on the frame's right edge, or a frame whose rows are not
 // 16-B aligned (width % 4 != 0), is copied by pixel instead.
+// (nullptr: a unit of rank 0 under skip_root)
 __device__ __forceinline__ const float* untile_src(const UntileParams& U, int t, int tx, int ty) {
   int w = 0;
   const int u = U.blocks ? deal_block_index(U.tiles_x, tx, ty, w) : t;  // deal unit
   const int r = (u + U.tile_offset) % U.devices;
+  if (U.skip_root && r == 0) return nullptr;
   const int b = ((r - U.tile_offset) % U.devices + U.devices) % U.devices;  // rank r's first unit
   const int k = U.blocks ? 4 * ((u - b) / U.devices) + w : (u - b) / U.devices;  // slot tile
   return U.recv + (size_t)(r * U.slot + k) * (kTile * kTile * 3);
@@ -1729,7 +1731,9 @@ __global__ __launch_bounds__(256) void untile_kernel(UntileParams U) {
   const int tx = t % U.tiles_x, ty = t / U.tiles_x;
   const int lr = ty * kTile + y, px0 = tx * kTile;
   if (lr >= U.rows) return;
-  const float* src = untile_src(U, t, tx, ty) + y * (kTile * 3);
+  const float* src0 = untile_src(U, t, tx, ty);
+  if (!src0) return;
+  const float* src = src0 + y * (kTile * 3);
   float* dst = U.out + ((size_t)(U.row0 + lr * U.row_stride) * U.width + px0) * 3;
   if (px0 + kTile <= U.width && U.vec) {
     reinterpret_cast<float4*>(dst)[c] = reinterpret_cast<const float4*>(src)[c];

@@ -155,13 +155,22 @@ def untile_camera(gathered_c, layout: TileLayout, c: int, index=None, out=None):
 
 def scene_tile_untiler(scene, layout: TileLayout) -> Callable:
     """The GPU untile: rt_untile_device of camera c's gathered shares straight into its
-    row-major frame (one wave per tile), on the communication stream."""
-    def untile(c, gathered_c, frame, stream):
+    row-major frame, on `stream`; skip_root: rank 0's own units are already in the frame."""
+    def untile(c, gathered_c, frame, stream, skip_root=False):
         sh = layout.shares[c]
         scene.untile_device(c, layout.world, sh.slot, gathered_c.data_ptr(), frame.data_ptr(),
                             tile_offset=int(layout.offsets[c] % layout.world),
-                            blocks=layout.blocks, stream=stream.cuda_stream)
+                            blocks=layout.blocks, skip_root=skip_root, stream=stream.cuda_stream)
     return untile
+
+
+def scene_inplace_renderer(scene) -> Callable:
+    """Rank 0's own share rendered in place into camera c's row-major frame (its units only)."""
+    def render(sh: CameraShare, frame, stream):
+        scene.render_device(sh.camera, frame.data_ptr(), tile_begin=sh.tile_begin,
+                            tile_step=sh.tile_step, tile_major=False, blocks=sh.blocks,
+                            stream=stream.cuda_stream)
+    return render
 
 
 def scene_tile_renderer(scene) -> Callable:
@@ -228,7 +237,7 @@ class TileGatherRenderer:
 
     def __init__(self, layout: TileLayout, stream, render: Callable, inflight: int = 2,
                  host_staging: bool = False, device=None, untile: Optional[Callable] = None,
-                 gather_stream: str = "render"):
+                 gather_stream: str = "render", render_inplace: Optional[Callable] = None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -244,6 +253,12 @@ class TileGatherRenderer:
         # stream, so no events); "comm": on one communication stream, handed over by events
         assert gather_stream in ("render", "comm")
         self.gather_on_render = gather_stream == "render"
+        # root_inplace (GPU, library untile): rank 0 renders its own share in place into the
+        # frame, receives only the other ranks' slots (point-to-point, no self-copy) and the
+        # untile skips its units — at N = 1 the step is the in-place render alone
+        self.render_inplace = render_inplace
+        self.root_inplace = (render_inplace is not None and untile is not None
+                             and not host_staging)
         self.inflight = 1 if host_staging else max(1, int(inflight))
         F = self.inflight
         dev = device if device is not None else (
@@ -295,10 +310,20 @@ class TileGatherRenderer:
                 dist.gather(self._slot(s, sh).cpu(), glist, dst=0)
                 if root:
                     self.gathered[s][c].copy_(torch.stack(glist))
+            elif self.root_inplace:
+                if L.world > 1:
+                    ops = ([dist.P2POp(dist.irecv, self.gathered[s][c][r], r)
+                            for r in range(1, L.world)] if root else
+                           [dist.P2POp(dist.isend, self._slot(s, sh), 0)])
+                    for req in dist.batch_isend_irecv(ops):
+                        req.wait()
             else:
                 outs = list(self.gathered[s][c]) if root else None
                 dist.gather(self._slot(s, sh), outs, dst=0, async_op=True).wait()
-            if root and self.untile is not None:
+            if root and self.root_inplace:
+                if L.world > 1:
+                    self.untile(c, self.gathered[s][c], self.padded[s][c], stream, skip_root=True)
+            elif root and self.untile is not None:
                 self.untile(c, self.gathered[s][c], self.padded[s][c], stream)
             elif root:
                 untile_camera(self.gathered[s][c].view(-1, TILE_FLOATS), L, c, self.index[c],
@@ -312,9 +337,12 @@ class TileGatherRenderer:
             st.wait_event(self.done[s])  # its gather `inflight` steps ago
         if events is not None:
             events[0].record(st)
-        for sh in self.layout.shares:
+        for c, sh in enumerate(self.layout.shares):
             if sh.count > 0:
-                self.render(sh, self._slot(s, sh), st)
+                if self.root_inplace and self.rank == 0:
+                    self.render_inplace(sh, self.padded[s][c], st)
+                else:
+                    self.render(sh, self._slot(s, sh), st)
         if events is not None:
             events[1].record(st)
         if self.host_staging:

@@ -11,6 +11,7 @@ from . import _lib
 from ._lib import check, lib
 
 RT_TILE_MAJOR, RT_TILE_BLOCKS = 1, 2  # rt_render_device tile_major flags (include/ceng795_rt.h)
+RT_UNTILE_BLOCKS, RT_UNTILE_SKIP_ROOT = 1, 2  # rt_untile_device flags
 
 
 @dataclass
@@ -153,12 +154,14 @@ class Scene:
 
     def untile_device(self, camera_index: int, devices: int, slot: int, gathered_ptr: int,
                       out_ptr: int, *, tile_offset: int = 0, blocks: bool = False,
-                      stream: int = 0) -> None:
+                      skip_root: bool = False, stream: int = 0) -> None:
         """rt_untile_device: the gathered [devices][slot][64][3] tile shares of a round-robin
         deal (unit u to rank (u + tile_offset) mod devices; units are tiles, or 2x2 blocks in
-        deal order with ``blocks``) into the row-major frame."""
+        deal order with ``blocks``) into the row-major frame; ``skip_root``: rank 0's units
+        are left as they are (rendered in place)."""
+        flags = (RT_UNTILE_BLOCKS if blocks else 0) | (RT_UNTILE_SKIP_ROOT if skip_root else 0)
         check(lib().rt_untile_device(self._h, camera_index, 0, 1, devices, slot, tile_offset,
-                                     int(blocks), C.c_void_p(gathered_ptr), C.c_void_p(out_ptr),
+                                     flags, C.c_void_p(gathered_ptr), C.c_void_p(out_ptr),
                                      C.c_void_p(stream)))
 
     def release_stream(self, stream: int) -> None:

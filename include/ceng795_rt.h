@@ -224,14 +224,20 @@ int rt_render_device_range(rt_scene* scene, int camera_index, int starting_row, 
  * d_gathered[devices][slot][8*8*3] (rank r rendered the frame's deal units u with
  * (u + tile_offset) mod devices == r, tile-major, in order, into its slot of `slot` tiles — what
  * one equal-size gather of rt_render_device(tile_begin, tile_step = devices, RT_TILE_MAJOR
- * [| RT_TILE_BLOCKS when blocks = 1]) outputs leaves; with blocks, slot is a multiple of 4);
+ * [| RT_TILE_BLOCKS with RT_UNTILE_BLOCKS]) outputs leaves; with blocks, slot is a multiple of
+ * 4);
  * this writes them into the row-major frame d_out (rows starting_row + k*row_stride of
  * camera_index), one wave per tile, on hip_stream (device devices[0] of the scene).  Replaces
  * nothing in the reference (its threads share one Pixel array, HW2/main.cpp:33-36): it is the
  * gather's inverse. */
 int rt_untile_device(rt_scene* scene, int camera_index, int starting_row, int row_stride,
-                     int devices, int slot, int tile_offset, int blocks, const float* d_gathered,
+                     int devices, int slot, int tile_offset, int flags, const float* d_gathered,
                      float* d_out, void* hip_stream);
+/* rt_untile_device flags */
+enum { RT_UNTILE_BLOCKS = 1,    /* the units are 2x2 blocks (shares rendered with RT_TILE_BLOCKS) */
+       RT_UNTILE_SKIP_ROOT = 2  /* rank 0's units are not touched: the gathering rank rendered its
+                                   own share in place into d_out (tile_major without
+                                   RT_TILE_MAJOR), so its slot need not be gathered */ };
 /* Waits for `hip_stream` and frees the scratch rt_render_device keeps for it (no-op for a
  * stream the scene never rendered on).  Streams that come and go should release theirs. */
 int rt_release_stream_scratch(rt_scene* scene, void* hip_stream);

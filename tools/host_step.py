@@ -61,10 +61,12 @@ def main():
     for label, untile, gs in (
             ("tile_gather_render_stream", dist_tiles.scene_tile_untiler(scene, layout), "render"),
             ("tile_gather_comm_stream", dist_tiles.scene_tile_untiler(scene, layout), "comm"),
-            ("tile_gather_index_untile", None, "render")):
-        R = dist_tiles.TileGatherRenderer(layout, stream, dist_tiles.scene_tile_renderer(scene),
-                                          inflight=a.inflight, device=dev, untile=untile,
-                                          gather_stream=gs)
+            ("tile_gather_index_untile", None, "render"),
+            ("tile_root_inplace", dist_tiles.scene_tile_untiler(scene, layout), "inplace")):
+        R = dist_tiles.TileGatherRenderer(
+            layout, stream, dist_tiles.scene_tile_renderer(scene), inflight=a.inflight,
+            device=dev, untile=untile, gather_stream="render" if gs == "inplace" else gs,
+            render_inplace=dist_tiles.scene_inplace_renderer(scene) if gs == "inplace" else None)
         out[label] = measure(R, a.steps, torch)
     out["inplace_again"] = measure(dist_tiles.FrameRenderer(scene, stream, inflight=a.inflight),
                                    a.steps, torch)
