@@ -781,22 +781,28 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
   {
     DeviceGuard g(s->rep[0]->device);
     hip_check(hipEventRecord(x0->ev_in, s0), "event record");  // d_frame's earlier work
+    // the first device renders its own blocks in place into d_frame (after d_frame's earlier
+    // work); the others render tile-major into their slots for the gather
+    hip_check(hipStreamWaitEvent(x0->stream, x0->ev_in, 0), "wait event");
   }
   for (int d = 0; d < D; d++) {
     Replica& r = *s->rep[d];
     RenderCtx* x = cx.x[d];
     DeviceGuard g(r.device);
-    ensure(x->d_out, x->out_floats, (size_t)slot * kTileFloats, "alloc tile slot");
-    RenderParams P = make_params(s, r, cam, row0, row_stride, d, D, RT_TILE_MAJOR | RT_TILE_BLOCKS,
-                                 x->d_out, per_call ? x->d_cnt : r.d_counters);
+    if (d > 0) ensure(x->d_out, x->out_floats, (size_t)slot * kTileFloats, "alloc tile slot");
+    RenderParams P = make_params(s, r, cam, row0, row_stride, d, D,
+                                 d == 0 ? RT_TILE_BLOCKS : RT_TILE_MAJOR | RT_TILE_BLOCKS,
+                                 d == 0 ? d_frame : x->d_out, per_call ? x->d_cnt : r.d_counters);
     bind_ctx(s, x, P, c);
     enqueue_frame(s, r, P, 1, nullptr, x->stream, d == 0);
   }
   DeviceGuard g(s->rep[0]->device);
   ensure(x0->d_recv, x0->recv_floats, (size_t)D * slot * kTileFloats, "alloc gathered slots");
   const size_t count = (size_t)slot * kTileFloats;
-  if (s->copy_gather) {
-    for (int d = 0; d < D; d++) {
+  if (D == 1) {
+    // nothing to gather: the one device rendered the frame in place
+  } else if (s->copy_gather) {
+    for (int d = 1; d < D; d++) {
       {
         DeviceGuard gd(s->rep[d]->device);
         hip_check(hipEventRecord(cx.x[d]->ev_out, cx.x[d]->stream), "event record");
@@ -809,16 +815,15 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
     }
   } else {
     nccl_check(ncclGroupStart(), "ncclGroupStart");
-    for (int d = 0; d < D; d++)
+    for (int d = 1; d < D; d++)
       nccl_check(ncclSend(cx.x[d]->d_out, count, ncclFloat, 0, s->comms[d], cx.x[d]->stream),
                  "ncclSend");
-    for (int d = 0; d < D; d++)
+    for (int d = 1; d < D; d++)
       nccl_check(ncclRecv(x0->d_recv + (size_t)d * count, count, ncclFloat, d, s->comms[0],
                           x0->stream),
                  "ncclRecv");
     nccl_check(ncclGroupEnd(), "ncclGroupEnd");
   }
-  hip_check(hipStreamWaitEvent(x0->stream, x0->ev_in, 0), "wait event");
   UntileParams U;
   U.recv = x0->d_recv;
   U.out = d_frame;
@@ -832,9 +837,9 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
   U.slot = slot;
   U.tile_offset = 0;
   U.blocks = 1;
-  U.skip_root = 0;
+  U.skip_root = 1;  // the first device's blocks are already in d_frame
   U.vec = untile_vec(U);
-  hip_check(launch_untile(U, x0->stream), "untile launch");
+  if (D > 1) hip_check(launch_untile(U, x0->stream), "untile launch");
   if (s0 != x0->stream) {
     hip_check(hipEventRecord(x0->ev_out, x0->stream), "event record");
     hip_check(hipStreamWaitEvent(s0, x0->ev_out, 0), "wait event");
