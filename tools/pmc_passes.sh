@@ -7,7 +7,7 @@ OUT=${1:?outdir}
 shift
 export TMPDIR=/tmp
 mkdir -p "$OUT"
-CMD="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-roofline --no-c5 --inflight 1 ${BENCH_ARGS:-}"
+CMD="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-roofline --no-c5 --no-share-probe --inflight 1 ${BENCH_ARGS:-}"
 run() {
   local name=$1
   shift
