@@ -1612,7 +1612,11 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
   // dispatch order: units of one traversal workgroup, `regions` regions of
   // `chunk`-unit chunks (tile_block: half a row of 2x2 blocks), LPT within each region
   T.use_order = 0;
-  bool ordered = T.tile_cost != nullptr && T.unit_order != nullptr && T.order_regions > 0;
+#ifndef RT_ORDER_MIN_TILES  // launches selecting fewer tiles run in block order (no order kernel)
+#define RT_ORDER_MIN_TILES 0
+#endif
+  bool ordered = T.tile_cost != nullptr && T.unit_order != nullptr && T.order_regions > 0 &&
+                 T.num_sel_tiles >= RT_ORDER_MIN_TILES;
   if (ordered) {
     T.order_units = tblocks;
     const int nbx = (T.tiles_x + kBlockW - 1) / kBlockW;
