@@ -257,8 +257,7 @@ class TileGatherRenderer:
         # frame, receives only the other ranks' slots (point-to-point, no self-copy) and the
         # untile skips its units — at N = 1 the step is the in-place render alone
         self.render_inplace = render_inplace
-        self.root_inplace = (render_inplace is not None and untile is not None
-                             and not host_staging)
+        self.root_inplace = render_inplace is not None and untile is not None
         self.inflight = 1 if host_staging else max(1, int(inflight))
         F = self.inflight
         dev = device if device is not None else (
@@ -305,18 +304,18 @@ class TileGatherRenderer:
         torch, dist, L = self.torch, self.dist, self.layout
         root = self.rank == 0
         for c, sh in enumerate(L.shares):
-            if self.host_staging:
-                glist = list(torch.empty((L.world, sh.slot, TILE_FLOATS))) if root else None
-                dist.gather(self._slot(s, sh).cpu(), glist, dst=0)
-                if root:
-                    self.gathered[s][c].copy_(torch.stack(glist))
-            elif self.root_inplace:
+            if self.root_inplace:
                 if L.world > 1:
                     ops = ([dist.P2POp(dist.irecv, self.gathered[s][c][r], r)
                             for r in range(1, L.world)] if root else
                            [dist.P2POp(dist.isend, self._slot(s, sh), 0)])
                     for req in dist.batch_isend_irecv(ops):
                         req.wait()
+            elif self.host_staging:
+                glist = list(torch.empty((L.world, sh.slot, TILE_FLOATS))) if root else None
+                dist.gather(self._slot(s, sh).cpu(), glist, dst=0)
+                if root:
+                    self.gathered[s][c].copy_(torch.stack(glist))
             else:
                 outs = list(self.gathered[s][c]) if root else None
                 dist.gather(self._slot(s, sh), outs, dst=0, async_op=True).wait()

@@ -222,6 +222,73 @@ def test_tile_gather_renderer_pipeline(tmp_path, world, sizes, steps):
     assert (tmp_path / "result").read_text() == "ok"
 
 
+def _root_inplace_worker(rank, world, port, outdir, sizes, steps):
+    """The N>1 GPU exchange (TileGatherRenderer with render_inplace): rank 0 renders its own
+    units in place into its frames, the other ranks send their slots point-to-point
+    (batch_isend_irecv), and rank 0's untile fills everything but its own units."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ceng795_amd.dist_tiles import TileGatherRenderer
+    L = TileLayout(sizes, world, rank)
+    state = {"step": 0}
+
+    def truth(step):
+        return [np.random.default_rng(300 + step).standard_normal((h, w, 3)).astype(np.float32)
+                for (w, h) in sizes]
+
+    def render(sh, slot, stream):  # tile-major share (ranks > 0)
+        frame = truth(state["step"])[sh.camera]
+        for k, t in enumerate(L.share_tiles(sh.camera, rank)):
+            slot[k] = torch.from_numpy(_tile(frame, int(t))) if t >= 0 else 0.0
+
+    def render_inplace(sh, out, stream):  # rank 0: its own tiles straight into the frame
+        frame = truth(state["step"])[sh.camera]
+        h, w, _ = frame.shape
+        tx = (w + TILE - 1) // TILE
+        for t in L.share_tiles(sh.camera, 0):
+            if t < 0:
+                continue
+            y0, x0 = (t // tx) * TILE, (t % tx) * TILE
+            out[y0:y0 + TILE, x0:x0 + TILE] = torch.from_numpy(frame[y0:y0 + TILE, x0:x0 + TILE])
+
+    def untile(c, gathered_c, out, stream, skip_root=False):  # rt_untile_device's contract
+        full = untile_camera(gathered_c.view(-1, TILE_FLOATS), L, c)
+        h, w, _ = out.shape
+        tx = (w + TILE - 1) // TILE
+        mine = set(int(t) for t in L.share_tiles(c, 0) if t >= 0) if skip_root else set()
+        for t in range(tx * ((h + TILE - 1) // TILE)):
+            if t in mine:
+                continue
+            y0, x0 = (t // tx) * TILE, (t % tx) * TILE
+            out[y0:y0 + TILE, x0:x0 + TILE] = full[y0:y0 + TILE, x0:x0 + TILE]
+
+    R = TileGatherRenderer(L, None, render, host_staging=True, device="cpu", untile=untile,
+                           render_inplace=render_inplace)
+    assert R.root_inplace
+    ok = True
+    for step in range(steps):
+        state["step"] = step
+        frames = R.step()
+        if rank == 0:
+            ok &= all(_same(frames[c].contiguous().numpy(), truth(step)[c])
+                      for c in range(len(sizes)))
+    R.finish()
+    if rank == 0:
+        with open(os.path.join(outdir, "result"), "w") as fh:
+            fh.write("ok" if ok else "mismatch")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,sizes", [(2, [(64, 40), (37, 21)]), (3, [(96, 64)]),
+                                         (1, [(40, 24)])])
+def test_root_inplace_exchange(tmp_path, world, sizes):
+    mp.spawn(_root_inplace_worker, args=(world, _free_port(), str(tmp_path), sizes, 2),
+             nprocs=world, join=True)
+    assert (tmp_path / "result").read_text() == "ok"
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_bench_self_launches_ranks(tmp_path, world):
     """`python bench.py --gpus N` with no launcher: bench.py starts N ranks itself (before
