@@ -351,12 +351,14 @@ def share_probe(scene, stream, steps: int, inflight: int, t1_ms: float, ns=(2, 4
     as in the N > 1 path) is rendered alone on this GPU and timed; the N-GPU step can be no
     shorter than the slowest share, so t1 / (N * max_r t_share) bounds the efficiency from
     above.  Excludes the gather to rank 0 and its untile (rehearsed by --gather-rehearsal)."""
+    import torch
     from ceng795_amd import dist_tiles
     out = {}
+    extra = [torch.cuda.Stream() for _ in range(max(0, inflight - 1))]  # one set for every rank
     for n in ns:
         per = []
         for r in range(n):
-            R = dist_tiles.ShareRenderer(scene, n, r, stream, inflight=inflight)
+            R = dist_tiles.ShareRenderer(scene, n, r, stream, inflight=inflight, streams=extra)
             for _ in range(3):
                 R.step()
             R.finish()
@@ -368,9 +370,10 @@ def share_probe(scene, stream, steps: int, inflight: int, t1_ms: float, ns=(2, 4
                        "predicted_efficiency": round(t1_ms / (n * slow), 4),
                        "predicted_Mrays_s_factor": round(t1_ms / slow, 3)}
     return {"t1_ms": round(t1_ms, 4), "frames_in_flight": inflight, "per_n": out,
-            "note": "PREDICTION from one GPU: each rank's tile share of one frame rendered alone "
-                    "(same frames in flight), t1 / (N * slowest share); the gather to rank 0 "
-                    "and its untile are not included"}
+            "note": "PREDICTION from one GPU: each rank's block share of one frame rendered alone "
+                    "(same frames in flight, the same render streams for every rank, as each "
+                    "rank's fresh process would have), t1 / (N * slowest share); the exchange "
+                    "to rank 0 and its untile are not included"}
 
 
 def synthetic_frame(w: int, h: int, seed: int = 795):

@@ -483,13 +483,18 @@ class ShareRenderer:
     strong scaling before an N-GPU node is available (bench.py share probe).  Steps go to
     `inflight` streams / buffer sets in turn, as in TileGatherRenderer."""
 
-    def __init__(self, scene, world: int, rank: int, stream, inflight: int = 1):
+    def __init__(self, scene, world: int, rank: int, stream, inflight: int = 1, streams=None):
         import torch
         self.layout = L = TilePlan(scene, world, rank)
         self.scene, self.stream = scene, stream
         dev = torch.device("cuda", torch.cuda.current_device())
         self.inflight = max(1, int(inflight))
-        self.streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(self.inflight - 1)]
+        # streams: the extra render streams to reuse (one set for every rank probed: each rank of
+        # an N-GPU run creates its streams in a fresh process, so they always land on the same
+        # hardware queues; new streams per probed rank cycle over the queues, which made the
+        # probe's per-rank times bimodal — DESIGN.md §6)
+        self.streams = [stream] + (list(streams)[:self.inflight - 1] if streams is not None else
+                                   [torch.cuda.Stream(device=dev) for _ in range(self.inflight - 1)])
         self.local = [torch.empty((max(1, L.buffer_tiles), TILE_FLOATS), dtype=torch.float32,
                                   device=dev) for _ in range(self.inflight)]
         self.k = 0

@@ -17,8 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def timed(scene, world, rank, stream, inflight, steps, torch, dist_tiles):
-    R = dist_tiles.ShareRenderer(scene, world, rank, stream, inflight=inflight)
+def timed(scene, world, rank, stream, inflight, steps, torch, dist_tiles, streams=None):
+    R = dist_tiles.ShareRenderer(scene, world, rank, stream, inflight=inflight, streams=streams)
     for _ in range(3):
         R.step()
     R.finish()
@@ -29,8 +29,9 @@ def timed(scene, world, rank, stream, inflight, steps, torch, dist_tiles):
     R.finish()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
-    for st in R.streams[1:]:
-        scene.release_stream(st.cuda_stream)
+    if streams is None:
+        for st in R.streams[1:]:
+            scene.release_stream(st.cuda_stream)
     return round(ms, 4)
 
 
@@ -62,6 +63,9 @@ def main():
     out = {"world": a.world}
     N = a.world
     out["inplace_inflight4"] = timed_inplace(scene, stream, 4, a.steps, torch, dist_tiles)
+    shared = [torch.cuda.Stream() for _ in range(3)]  # one stream set for every rank
+    out["forward_shared_streams"] = [timed(scene, N, r, stream, 4, a.steps, torch, dist_tiles,
+                                           shared) for r in range(N)]
     out["forward"] = [timed(scene, N, r, stream, 4, a.steps, torch, dist_tiles) for r in range(N)]
     out["reverse"] = [timed(scene, N, r, stream, 4, a.steps, torch, dist_tiles)
                       for r in reversed(range(N))][::-1]
