@@ -419,7 +419,7 @@ __device__ __forceinline__ bool advance(WaveStack<DEEP>& st, int c0, int c1, uin
 // ancestry — so exactly the leaves the reference reaches are tested.  Without CULL (reference
 // walk) an entry is a DFS leaf whose boxes the walk has already decided.
 #ifndef RT_BATCH_FLUSH
-#define RT_BATCH_FLUSH 64
+#define RT_BATCH_FLUSH 160
 #endif
 constexpr int kBatchFlush = RT_BATCH_FLUSH;   // run the queue once this many tests are pending
 constexpr int kBatchCap = kBatchFlush + 256;  // a wide visit flushes before a slot could overflow
