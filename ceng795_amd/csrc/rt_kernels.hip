@@ -1023,6 +1023,12 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
 // Local shading of HW2/Scene.cpp:101-138 given the occlusion bits, in the reference's
 // accumulation order: ambient, then per light diffuse then specular.  No traversal here, so
 // the fp64 pow (HW2 calls ::pow(double, double)) costs no occupancy in the traversal kernels.
+// The leaf's normal and material come in one 16-B load (normals[4 * leaf + 3] holds the
+// material index); the DevPrim record is read only in scenes with spheres (its kind).
+#ifndef RT_SHADE_NORMAL_MAT
+#define RT_SHADE_NORMAL_MAT 1
+#endif
+template <bool SPHERES>
 __device__ __forceinline__ void shade_pixel(const RenderParams& P,
                                             const DevPrim* __restrict__ prims,
                                             const float* __restrict__ normals,
@@ -1038,9 +1044,16 @@ __device__ __forceinline__ void shade_pixel(const RenderParams& P,
     const int leaf = hit_leaf(rec);
     const V3 e = ld3(P.cam_e);
     const V3 p = hit_point(P, q, hit_t(rec));
+#if RT_SHADE_NORMAL_MAT
+    const float4 nm = *reinterpret_cast<const float4*>(normals + 4 * leaf);
+    const bool tri = !SPHERES || prims[leaf].kind == kPrimTriangle;
+    const V3 n = tri ? v3(nm.x, nm.y, nm.z) : normalize(p - ld3(prims[leaf].v0));
+    const DevMaterial& m = mats[__float_as_int(nm.w)];
+#else
     const DevPrim& pr = prims[leaf];
     const V3 n = pr.kind == kPrimTriangle ? ld3(normals + 4 * leaf) : normalize(p - ld3(pr.v0));
     const DevMaterial& m = mats[pr.material];
+#endif
     const V3 w0 = normalize(e - p);  // (ray.o - intersection_point).normalize()
     color = color + ld3(m.ambient) * ld3(P.ambient);
     for (int li = 0; li < P.num_lights; li++) {
@@ -1574,12 +1587,13 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void recursive_kernel(
                                         leaf_lds[threadIdx.x >> 6]);
 }
 
+template <bool SPHERES>
 __global__ __launch_bounds__(kWavesPerBlock * 64) void shade_kernel(
     RenderParams P, const DevPrim* __restrict__ prims, const float* __restrict__ normals,
     const DevMaterial* __restrict__ mats, const DevLight* __restrict__ lights) {
   const int sel = uniform((int)blockIdx.x * kWavesPerBlock + ((int)threadIdx.x >> 6));
   if (sel >= P.num_sel_tiles) return;
-  shade_pixel(P, prims, normals, mats, lights, sel);
+  shade_pixel<SPHERES>(P, prims, normals, mats, lights, sel);
 }
 
 // marks (nullable): 4 events recorded before the primary kernel, after it, after the shadow
@@ -1650,7 +1664,7 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
                        dim3(kTraceWaves * 64), tlds, stream, S, nodes, lights);
   }
   mark(marks, 2, stream);
-  hipLaunchKernelGGL(shade_kernel, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
+  hipLaunchKernelGGL(shade_kernel<SPHERES>, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
                      prims, normals, mats, lights);
   mark(marks, 3, stream);
 }
