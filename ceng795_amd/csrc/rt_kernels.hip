@@ -838,9 +838,10 @@ struct PacketPixel {
   bool valid;
 };
 
-__device__ __forceinline__ PacketPixel packet_pixel(const RenderParams& P, int sel) {
+__device__ __forceinline__ PacketPixel packet_pixel(const RenderParams& P, int sel,
+                                                   int lane = lane_id()) {
   PacketPixel q;
-  q.lane = lane_id();
+  q.lane = lane;
   int tx, ty;
   if (P.block_deal) {  // selected block sel / 4, its tile sel % 4
     deal_block_tile(P.tiles_x, P.tile_begin + (sel >> 2) * P.tile_step, sel & 3, tx, ty);
@@ -968,6 +969,9 @@ __device__ __forceinline__ V3 hit_point(const RenderParams& P, const PacketPixel
 
 // Shadow rays of HW2/Scene.cpp:113-127: one bit per point light, set when the light is
 // occluded for this pixel's primary hit.
+#ifndef RT_SHADOW_REMAT
+#define RT_SHADOW_REMAT 1
+#endif
 template <bool FAST, bool DEEP, bool SPHERES>
 __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
                                               const DevNode* __restrict__ nodes,
@@ -983,8 +987,17 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       // 8-B record is an L2 hit)
       const RenderParams& P = fresh_params(P0);
       const DevLight& lt = lights[li];
-      const PacketPixel q = packet_pixel(P, sel);
-      const int2_t rec = P.hits[(size_t)sel * (kTile * kTile) + q.lane];
+#if RT_SHADOW_REMAT
+      // the packet's pixel indices recomputed here, not hoisted out of the light loop (where
+      // they would be live across the traversal and spilled to scratch)
+      int sel_l = sel, lane_l;
+      asm volatile("" : "+s"(sel_l));
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_l));
+#else
+      const int sel_l = sel, lane_l = lane_id();
+#endif
+      const PacketPixel q = packet_pixel(P, sel_l, lane_l);
+      const int2_t rec = P.hits[(size_t)sel_l * (kTile * kTile) + q.lane];
       const bool hit = hit_leaf(rec) >= 0;
       const V3 pk = hit ? hit_point(P, q, hit_t(rec)) : v3(0, 0, 0);
       const V3 ld = ld3(lt.position) - pk;
@@ -999,7 +1012,14 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       bits |= (occ ? 1u : 0u) << (li - 32 * w);
     }
     const RenderParams& Pw = fresh_params(P0);
-    Pw.occ[((size_t)sel * (kTile * kTile) + lane_id()) * Pw.occ_words + w] = bits;
+#if RT_SHADOW_REMAT
+    int sel_w = sel, lane_w;
+    asm volatile("" : "+s"(sel_w));
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_w));
+#else
+    const int sel_w = sel, lane_w = lane_id();
+#endif
+    Pw.occ[((size_t)sel_w * (kTile * kTile) + lane_w) * Pw.occ_words + w] = bits;
   }
   const RenderParams& Pc = fresh_params(P0);
   if (Pc.counters) {
