@@ -786,7 +786,9 @@ __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* _
   WaveStack<DEEP> st;
   st.lds = spill;
   int pending = 0;
-  L.key[lane] = 0ull;
+  unsigned long long clear = 0ull;
+  asm volatile("" : "+v"(clear));  // a fresh zero here, not one kept (and spilled) across the walk
+  L.key[lane] = clear;
   int node = FAST ? P.accel_root : P.root_ref;
   for (;;) {
     if (pending >= kShadowFlush) {  // between visits; a lane found occluded stops entering nodes
