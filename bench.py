@@ -345,35 +345,67 @@ def one_frame_ms(scene, stream, frames: int):
     return round(ms, 4)
 
 
-def share_probe(scene, stream, steps: int, inflight: int, t1_ms: float, ns=(2, 4, 8)):
-    """Prediction of strong scaling on one GPU (no N-GPU node needed): for each N, every rank
-    r's share of the N-way tile deal (tile_begin r, tile_step N, tile-major, frames in flight
-    as in the N > 1 path) is rendered alone on this GPU and timed; the N-GPU step can be no
-    shorter than the slowest share, so t1 / (N * max_r t_share) bounds the efficiency from
-    above.  Excludes the gather to rank 0 and its untile (rehearsed by --gather-rehearsal)."""
+def cold_frame_ms(scene, frames: int = 3):
+    """Wall time of a COLD frame of camera 0: the first whole frame of that selection on a fresh
+    stream, so its primary kernel runs in block order (no previous frame's tile costs to order
+    it by).  The stream's scratch is allocated beforehand by a one-tile render
+    of another selection (that allocation is a one-time cost, not a frame's); median of
+    `frames` fresh streams."""
     import torch
+    cam = scene.camera(0)
+    buf = torch.empty((cam.height, cam.width, 3), dtype=torch.float32, device="cuda")
+    out = []
+    for _ in range(frames):
+        st = torch.cuda.Stream()
+        scene.render_device(0, buf.data_ptr(), tile_count=1, stream=st.cuda_stream)
+        st.synchronize()
+        t0 = time.perf_counter()
+        scene.render_device(0, buf.data_ptr(), stream=st.cuda_stream)
+        st.synchronize()
+        out.append((time.perf_counter() - t0) * 1e3)
+        scene.release_stream(st.cuda_stream)
+    scene.collect_stats()
+    return round(sorted(out)[len(out) // 2], 4)
+
+
+def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8)):
+    """Prediction of strong scaling on one GPU (no N-GPU node needed).  t1 = the whole frame
+    rendered in place with `inflight` frames in flight, and for each N every rank r's share of
+    the N-way block deal (tile_begin r, tile_step N, tile-major, the same frames in flight) alone
+    on this GPU — ALL timed over the same `steps` steps after the same warm-up, with one set of
+    render streams (each rank of an N-GPU run creates its streams in a fresh process).  The N-GPU
+    step can be no shorter than the slowest share: t1 / (N * max_r t_share) bounds the
+    efficiency from above (the gather to rank 0 and its untile are not included)."""
     from ceng795_amd import dist_tiles
+    import torch
+    extra = [torch.cuda.Stream() for _ in range(max(0, inflight - 1))]  # one set for every run
+
+    def timed(R):
+        for _ in range(3):
+            R.step()
+        R.finish()
+        ms = timed_steps(R, steps, 1, "cuda") / steps * 1e3
+        scene.collect_stats()
+        return ms
+
+    one = dist_tiles.FrameRenderer(scene, stream, inflight=inflight, streams=extra)
+    t1 = timed(one)
     out = {}
-    extra = [torch.cuda.Stream() for _ in range(max(0, inflight - 1))]  # one set for every rank
     for n in ns:
-        per = []
-        for r in range(n):
-            R = dist_tiles.ShareRenderer(scene, n, r, stream, inflight=inflight, streams=extra)
-            for _ in range(3):
-                R.step()
-            R.finish()
-            per.append(timed_steps(R, steps, 1, "cuda") / steps * 1e3)
-            scene.collect_stats()
+        per = [timed(dist_tiles.ShareRenderer(scene, n, r, stream, inflight=inflight, streams=extra))
+               for r in range(n)]
         slow = max(per)
         out[str(n)] = {"share_ms_max": round(slow, 4), "share_ms_min": round(min(per), 4),
                        "share_ms_per_rank": [round(x, 4) for x in per],
-                       "predicted_efficiency": round(t1_ms / (n * slow), 4),
-                       "predicted_Mrays_s_factor": round(t1_ms / slow, 3)}
-    return {"t1_ms": round(t1_ms, 4), "frames_in_flight": inflight, "per_n": out,
-            "note": "PREDICTION from one GPU: each rank's block share of one frame rendered alone "
-                    "(same frames in flight, the same render streams for every rank, as each "
-                    "rank's fresh process would have), t1 / (N * slowest share); the exchange "
-                    "to rank 0 and its untile are not included"}
+                       "predicted_efficiency": round(t1 / (n * slow), 4),
+                       "predicted_Mrays_s_factor": round(t1 / slow, 3)}
+    cam = scene.camera(0)
+    return {"frame": f"{cam.width}x{cam.height}", "t1_ms": round(t1, 4), "steps": steps,
+            "frames_in_flight": inflight, "per_n": out,
+            "note": "PREDICTION from one GPU: t1 and each rank's block share of one frame timed "
+                    "over the same number of steps with the same frames in flight and render "
+                    "streams; t1 / (N * slowest share); the exchange to rank 0 and its untile "
+                    "are not included"}
 
 
 def synthetic_frame(w: int, h: int, seed: int = 795):
@@ -680,14 +712,19 @@ def main() -> int:
                                            "make those fetches)")
             except Exception as e:  # the checker must never hide the measurement
                 log(f"roofline accounting failed: {e!r}")
-        single = None
-        probe = None
+        single = cold = None
+        probe = probe_c4 = None
         if world == 1 and not use_pg:
             try:
                 single = one_frame_ms(scene, stream, max(10, args.steps // 2))
+                cold = cold_frame_ms(scene)
                 if not args.no_share_probe:
-                    probe = share_probe(scene, stream, max(10, args.steps // 2), args.inflight,
-                                        elapsed / args.steps * 1e3)
+                    probe = share_probe(scene, stream, max(20, args.steps), args.inflight)
+                    if args.workload == "c3":
+                        # the north star's 8-GPU configuration: C4 (3840x2160), same mesh
+                        with ceng795_amd.Scene(scene_path("c4", 1), device=device,
+                                               traversal=args.traversal) as s4:
+                            probe_c4 = share_probe(s4, stream, max(20, args.steps), args.inflight)
             except Exception as e:
                 log(f"one-frame / share probe failed: {e!r}")
         host_rate = None
@@ -709,7 +746,9 @@ def main() -> int:
             "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32",
+            # N = 1 is the base of the default N > 1 run, the tile split of one frame (strong)
+            "scaling": "strong" if (strong or world == 1) else "weak",
+            "vs_baseline": None, "dtype": "f32",
             "data": "synthetic",
             "config": {"workload": desc, "frame": f"{w}x{h}", "frames_per_step": n_cams,
                        "triangles": 2 * (n - 1) ** 2, "rays_per_step": int(rays_step),
@@ -727,8 +766,16 @@ def main() -> int:
         if single is not None:
             line["one_frame_ms"] = single
             line["one_frame_Mrays_s"] = round(rays_step / n_cams / (single * 1e-3) / 1e6, 2)
+            line["one_frame_note"] = ("one frame at a time on one stream, warm (the previous "
+                                      "frame's tile costs order its primary work)")
+        if cold is not None:
+            line["cold_frame_ms"] = cold
+            line["cold_frame_note"] = ("the first frame of camera 0 on a fresh stream (block "
+                                       "order, nothing else in flight), median of 3 streams")
         if probe is not None:
             line["predicted_strong_scaling"] = probe
+        if probe_c4 is not None:
+            line["predicted_strong_scaling_c4"] = probe_c4
         if strong and t1_ms is not None:
             line["strong_scaling"] = {"t1_ms": round(t1_ms, 4), "tN_ms": round(ms_step, 4),
                                       "efficiency_t1_over_N_tN": round(t1_ms / (world * ms_step), 4)}

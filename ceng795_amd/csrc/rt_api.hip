@@ -64,6 +64,10 @@ struct RenderCtx {
   float* d_image = nullptr;  // multi-device rt_render, first device: the row-major frame
   size_t image_floats = 0;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;  // multi-device frames: caller-stream ordering
+  // copy-gather frames (a device listed twice): recorded on the first device's stream after it
+  // has copied the shares out of the other contexts' buffers; a context renders its next share
+  // only after it (the copy reads d_out / d_image on another stream: write-after-read)
+  hipEvent_t ev_gathered = nullptr;
 };
 
 // rt_render_device scratch of one stream (hit records, occlusion bits, tile schedule, ray-tree
@@ -83,7 +87,14 @@ struct StreamScratch {
   // in `sched` (valid: that frame ran the order kernel)
   std::array<long long, 7> order_key{};
   bool order_valid = false;
+  hipEvent_t done = nullptr;  // after the last frame enqueued on the stream (eviction waits on it)
+  unsigned long long used = 0;  // Replica::tick of the last lookup (least recently used first)
 };
+
+// Streams a replica keeps scratch / a multi-device context for: beyond this many, the least
+// recently used one is released (after its work has finished), so callers that make a new
+// stream per frame do not grow device memory without bound.
+constexpr size_t kMaxStreamTables = 64;
 
 // Per-kernel HIP-event timing of render launches (rt_set_kernel_timing): one quad of events per
 // launch of the first device.  Completed quads beyond kTimingPending are folded into `sum` so
@@ -115,6 +126,7 @@ struct Replica {
   // stream and device, kept across calls), so frames on different caller streams have their
   // own device streams and buffers and overlap (frames in flight, as scratch_for on one device)
   std::vector<std::pair<void*, RenderCtx*>> stream_ctx;
+  unsigned long long tick = 0;  // lookups of `streams` (LRU order)
 };
 
 struct rt_scene {
@@ -210,6 +222,7 @@ void free_ctx(RenderCtx* c) {
   (void)hipFree(c->d_image);
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
   if (c->ev_out) (void)hipEventDestroy(c->ev_out);
+  if (c->ev_gathered) (void)hipEventDestroy(c->ev_gathered);
   if (c->e0) (void)hipEventDestroy(c->e0);
   if (c->e1) (void)hipEventDestroy(c->e1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -222,6 +235,8 @@ void free_scratch(StreamScratch& x) {
   (void)hipFree(x.sched);
   (void)hipFree(x.frames);
   (void)hipFree(x.samples);
+  if (x.done) (void)hipEventDestroy(x.done);
+  x.done = nullptr;
 }
 
 void free_replica(Replica& r) {
@@ -599,6 +614,8 @@ RenderCtx* acquire_ctx(Replica& r) {
     hip_check(hipEventCreate(&c->e1), "event");
     hip_check(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming), "event");
     hip_check(hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming), "event");
+    hip_check(hipEventCreateWithFlags(&c->ev_gathered, hipEventDisableTiming), "event");
+    hip_check(hipEventRecord(c->ev_gathered, c->stream), "event record");  // (complete)
     hip_check(hipMalloc(&c->d_cnt, sizeof(unsigned long long) * kCounterAlloc), "alloc counters");
   } catch (...) {
     free_ctx(c.release());
@@ -614,12 +631,29 @@ void release_ctx(Replica& r, RenderCtx* c) {
   r.ctx_free.push_back(c);
 }
 
-// The context of caller stream `stream` on replica r (created on first use, then kept).
+// The context of caller stream `stream` on replica r (created on first use, then kept; the
+// table is capped at kMaxStreamTables: the oldest caller stream's context goes back to the pool
+// once its device stream has drained).  Caller holds s->multi_mu (no other multi-device frame
+// is being enqueued).
 RenderCtx* stream_ctx_for(Replica& r, void* stream) {
+  RenderCtx* old = nullptr;
   {
     std::lock_guard<std::mutex> lk(r.mu);
-    for (auto& e : r.stream_ctx)
-      if (e.first == stream) return e.second;
+    for (size_t k = 0; k < r.stream_ctx.size(); k++)
+      if (r.stream_ctx[k].first == stream) {
+        std::rotate(r.stream_ctx.begin() + (long)k, r.stream_ctx.begin() + (long)k + 1,
+                    r.stream_ctx.end());  // most recently used last
+        return r.stream_ctx.back().second;
+      }
+    if (r.stream_ctx.size() >= kMaxStreamTables) {
+      old = r.stream_ctx.front().second;
+      r.stream_ctx.erase(r.stream_ctx.begin());
+    }
+  }
+  if (old) {
+    DeviceGuard g(r.device);
+    hip_check(hipStreamSynchronize(old->stream), "synchronize evicted context");
+    release_ctx(r, old);
   }
   RenderCtx* c = acquire_ctx(r);
   std::lock_guard<std::mutex> lk(r.mu);
@@ -701,6 +735,9 @@ void render_multi_msaa(rt_scene* s, CtxSet& cx, int cam, float* d_frame, hipStre
     RenderCtx* x = cx.x[d];
     DeviceGuard g(r.device);
     float* dst = d_frame;
+    // copy gather: the previous frame's band copy out of d_image (on the first device's
+    // stream) has finished before this frame renders into it
+    if (d > 0 && s->copy_gather) hip_check(hipStreamWaitEvent(x->stream, x0->ev_gathered, 0), "wait event");
     if (d > 0) {
       ensure(x->d_image, x->image_floats, frame, "alloc band frame");
       dst = x->d_image;
@@ -740,6 +777,7 @@ void render_multi_msaa(rt_scene* s, CtxSet& cx, int cam, float* d_frame, hipStre
                                      s->rep[d]->device, src.second * sizeof(float), x0->stream),
                   "gather copy");
       }
+      hip_check(hipEventRecord(x0->ev_gathered, x0->stream), "event record");
     } else {
       nccl_check(ncclGroupStart(), "ncclGroupStart");
       for (int d = 1; d < D; d++) {
@@ -789,6 +827,9 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
     Replica& r = *s->rep[d];
     RenderCtx* x = cx.x[d];
     DeviceGuard g(r.device);
+    // copy gather: the previous frame's peer copy out of d_out (on the first device's stream)
+    // has finished before this frame renders into it
+    if (d > 0 && s->copy_gather) hip_check(hipStreamWaitEvent(x->stream, x0->ev_gathered, 0), "wait event");
     if (d > 0) ensure(x->d_out, x->out_floats, (size_t)slot * kTileFloats, "alloc tile slot");
     RenderParams P = make_params(s, r, cam, row0, row_stride, d, D,
                                  d == 0 ? RT_TILE_BLOCKS : RT_TILE_MAJOR | RT_TILE_BLOCKS,
@@ -813,6 +854,7 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
                                    x0->stream),
                 "gather copy");
     }
+    hip_check(hipEventRecord(x0->ev_gathered, x0->stream), "event record");
   } else {
     nccl_check(ncclGroupStart(), "ncclGroupStart");
     for (int d = 1; d < D; d++)
@@ -846,15 +888,41 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
   }
 }
 
-// The scratch of `stream` on replica r: allocated on first use at the largest camera's size.
-StreamScratch* scratch_for(rt_scene* s, Replica& r, void* stream) {
+// Frees the least recently used scratch no host thread is enqueueing on (its mutex is free:
+// holders of a scratch pointer keep it locked, and new ones need r.mu), after the GPU work of
+// its last frame.  Caller holds r.mu.
+void evict_scratch(Replica& r) {
+  size_t victim = r.streams.size();
+  for (size_t k = 0; k < r.streams.size(); k++) {
+    if (!r.streams[k]->mu.try_lock()) continue;
+    r.streams[k]->mu.unlock();
+    if (victim == r.streams.size() || r.streams[k]->used < r.streams[victim]->used) victim = k;
+  }
+  if (victim == r.streams.size()) return;  // every one in use: let the table grow
+  StreamScratch& x = *r.streams[victim];
+  if (x.done) hip_check(hipEventSynchronize(x.done), "synchronize evicted scratch");
+  free_scratch(x);
+  r.streams.erase(r.streams.begin() + (long)victim);
+}
+
+// The scratch of `stream` on replica r, returned with its mutex held in `held`: allocated on
+// first use at the largest camera's size; beyond kMaxStreamTables streams the least recently
+// used one is evicted.
+StreamScratch* scratch_for(rt_scene* s, Replica& r, void* stream, std::unique_lock<std::mutex>& held) {
   std::lock_guard<std::mutex> lk(r.mu);
   for (auto& x : r.streams)
-    if (x->stream == stream) return x.get();
+    if (x->stream == stream) {
+      held = std::unique_lock<std::mutex>(x->mu);
+      x->used = ++r.tick;
+      return x.get();
+    }
+  if (r.streams.size() >= kMaxStreamTables) evict_scratch(r);
   auto x = std::make_unique<StreamScratch>();
   x->stream = stream;
+  x->used = ++r.tick;
   const size_t most = s->most;
   try {
+    hip_check(hipEventCreateWithFlags(&x->done, hipEventDisableTiming), "event");
     hip_check(hipMalloc(&x->hits, most * sizeof(int2_t)), "alloc hit records");
     hip_check(hipMalloc(&x->occ, most * sizeof(unsigned) * occ_words(s->host)),
               "alloc occlusion bits");
@@ -865,6 +933,7 @@ StreamScratch* scratch_for(rt_scene* s, Replica& r, void* stream) {
     throw;
   }
   r.streams.push_back(std::move(x));
+  held = std::unique_lock<std::mutex>(r.streams.back()->mu);
   return r.streams.back().get();
 }
 
@@ -1087,8 +1156,8 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
     }
     Replica& r = *s->rep[0];
     DeviceGuard g(r.device);
-    StreamScratch* sc = scratch_for(s, r, stream);
-    std::lock_guard<std::mutex> lk(sc->mu);
+    std::unique_lock<std::mutex> lk;
+    StreamScratch* sc = scratch_for(s, r, stream, lk);
     RenderParams P = make_params(s, r, cam, row0, row_stride, tile_begin, tile_step, tile_major,
                                  d_out, r.d_counters);
     P.hits = sc->hits;
@@ -1116,6 +1185,7 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
     const bool orderable = RT_WARM_ORDER && c.num_samples <= 1 && !P.frames && P.num_lights > 0;
     P.primary_order = orderable && sc->order_valid && sc->order_key == key ? 1 : 0;
     enqueue_frame(s, r, P, c.num_samples, sc->samples, (hipStream_t)stream, true);
+    hip_check(hipEventRecord(sc->done, (hipStream_t)stream), "event record");
     sc->order_key = key;
     sc->order_valid = orderable;
     return RT_OK;

@@ -32,6 +32,10 @@ namespace rt {
 
 #define RT_INF __builtin_huge_valf()
 constexpr float kEps = 0.000001f;  // HW2/Vector3.h:7 kEpsilon
+
+#ifndef RT_FUSED  // 1: one kernel per frame (trace_frame_kernel)
+#define RT_FUSED 0
+#endif
 constexpr int kCounterSlots = kCounterRows;
 
 #ifdef RT_DIAG
@@ -431,6 +435,9 @@ constexpr int kShadowFlush = kBatchFlush;
 #define RT_PUSH_ALL 1
 #endif
 constexpr int kPushJunk = RT_PUSH_ALL ? 128 : 0;
+#ifndef RT_PUSH_FRESH_LANE
+#define RT_PUSH_FRESH_LANE RT_FUSED
+#endif
 struct WaveLeafLds {
   unsigned long long q[kBatchCap + kPushJunk];  // lo 32: leaf (DevLeaf or DFS index), hi 32: lane
   unsigned long long key[64];       // per lane: closest-hit key, or shadow flag
@@ -439,9 +446,17 @@ struct WaveLeafLds {
 constexpr unsigned long long kNoHitKey = (0x7f800000ull << 32) | 0xffffffffull;  // (+inf, -1)
 
 // Queue leaf `leaf` for the lanes of `m` (wave-uniform); n = pending entries (wave-uniform).
+// This lane's index computed afresh (asm-opaque): a lane id (or lane << 32) kept live across the
+// traversal is one more VGPR, and the fused kernel spilled it to scratch at every push.
+__device__ __forceinline__ int fresh_lane() {
+  int lane;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  return lane;
+}
+
 template <bool ALL = false>
 __device__ __forceinline__ void batch_push(WaveLeafLds& L, int& n, int leaf, uint64_t m) {
-  const int lane = lane_id();
+  const int lane = RT_PUSH_FRESH_LANE ? fresh_lane() : lane_id();
   const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
   if (ALL) {
@@ -456,7 +471,7 @@ __device__ __forceinline__ void batch_push(WaveLeafLds& L, int& n, int leaf, uin
 // adjacent (one 16-B LDS write), the queue order does not matter.
 template <bool ALL = false>
 __device__ __forceinline__ void batch_push_pair(WaveLeafLds& L, int& n, int leaf, uint64_t m) {
-  const int lane = lane_id();
+  const int lane = RT_PUSH_FRESH_LANE ? fresh_lane() : lane_id();
   const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
   const unsigned long long hi = (unsigned long long)lane << 32;
@@ -1050,6 +1065,19 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
 #ifndef RT_SHADE_NORMAL_MAT
 #define RT_SHADE_NORMAL_MAT 1
 #endif
+// (float)pow((double)c, (double)p) of HW2/Scene.cpp:133-137.  p == 1 returns c itself: the exact
+// result is the double c, and both glibc's pow (< 0.52 ulp) and ocml's (< 1 ulp) return an exact
+// result when one exists, so the reference gets c too.  Any other exponent takes the fp64 pow.
+// Out of line: inlined, ocml's fp64 pow needs ~60 VGPRs and set the register budget of every
+// kernel that shades (the fused frame kernel spilled to scratch around it).
+__device__ __attribute__((noinline)) float phong_pow_f64(float c, float p) {
+  return (float)pow((double)c, (double)p);
+}
+__device__ __forceinline__ float phong_pow(float c, float p) {
+  if (p == 1.0f) return c;
+  return phong_pow_f64(c, p);
+}
+
 template <bool SPHERES>
 __device__ __forceinline__ void shade_pixel(const RenderParams& P,
                                             const DevPrim* __restrict__ prims,
@@ -1089,7 +1117,7 @@ __device__ __forceinline__ void shade_pixel(const RenderParams& P,
       const float cos_d = dot(n, wi);
       color = color + ((ld3(m.diffuse) * I) * cos_d) / d2;
       const float cos_s = __builtin_fmaxf(dot(n, normalize(w0 + wi)), 0.0f);
-      const float pw = (float)pow((double)cos_s, (double)m.phong_exponent);
+      const float pw = phong_pow(cos_s, m.phong_exponent);
       color = color + ((ld3(m.specular) * I) * pw) / d2;
     }
   } else if (valid) {
@@ -1595,6 +1623,39 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_TRAVERSAL_OCCUPANCY void trace
   TL_END(1);
 }
 
+// One launch per frame (RT_FUSED): each wave runs its packet's primary traversal, its shadow
+// rays and its shading back to back, so a frame is one kernel with one tail instead of the chain
+// primary -> order -> shadow -> shade (each with its own tail).  The hit record and occlusion bits
+// still go through the stream's scratch (same lane writes, then reads: program order), which
+// keeps the register state of the three phases apart.  tile_cost: the whole packet's time.
+template <bool FAST, bool DEEP, bool SPHERES>
+__global__ __launch_bounds__(kTraceWaves * 64) RT_PRIMARY_OCCUPANCY void trace_frame_kernel(
+    RenderParams P, const DevNode* __restrict__ nodes, const DevLight* __restrict__ lights) {
+  extern __shared__ __attribute__((aligned(16))) int deep_stack[];
+  __shared__ WaveLeafLds leaf_lds[kTraceWaves];
+  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * kDeepWords * kDeepStack : nullptr;
+  WaveLeafLds& L = leaf_lds[threadIdx.x >> 6];
+  TL_BEGIN;
+  const RenderParams& Q = fresh_params(P);
+  const int sel = dispatch_sel(Q);
+  TL_SEL(sel);
+  if (sel >= 0) {
+    // the packet's start time waits in LDS (kept in SGPRs across the traversals it spilled)
+    __shared__ unsigned long long start[kTraceWaves];
+    start[threadIdx.x >> 6] = __builtin_amdgcn_s_memrealtime();
+    primary_packet<FAST, DEEP, SPHERES>(Q, nodes, sel, spill, L);
+    if (fresh_params(P).num_lights > 0)
+      shadow_packet<FAST, DEEP, SPHERES>(fresh_params(P), nodes, lights, sel, spill, L);
+    const RenderParams& Ps = fresh_params(P);
+    shade_pixel<SPHERES>(Ps, Ps.prims, Ps.normals, Ps.materials, lights, sel);
+    const RenderParams& Pw = fresh_params(P);
+    if (Pw.tile_cost && lane_id() == 0)  // the next frame's dispatch order
+      Pw.tile_cost[sel] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - start[threadIdx.x >> 6],
+                                        0xffffffffull);
+  }
+  TL_END(0);
+}
+
 template <bool FAST, bool DEEP, bool SPHERES>
 __global__ __launch_bounds__(kWavesPerBlock * 64) void recursive_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevPrim* __restrict__ prims,
@@ -1668,6 +1729,24 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
   }
   const int oblocks = ordered ? T.order_regions * T.order_stride : tblocks;
   RenderParams S = T;
+#if RT_FUSED
+  // one kernel per frame (trace_frame_kernel), dispatched by the previous frame's order when
+  // there is one; the order kernel then sorts this frame's packet costs for the next frame
+  mark(marks, 0, stream);
+  if (!ordered) T.tile_cost = nullptr;
+  T.use_order = ordered && P.primary_order ? 1 : 0;
+  hipLaunchKernelGGL((trace_frame_kernel<FAST, DEEP, SPHERES>), dim3(T.use_order ? oblocks : tblocks),
+                     dim3(kTraceWaves * 64), tlds, stream, T, nodes, lights);
+  mark(marks, 1, stream);
+  mark(marks, 2, stream);
+  if (ordered) hipLaunchKernelGGL(order_kernel, dim3(S.order_regions), dim3(kOrderThreads), 0, stream, S);
+  mark(marks, 3, stream);
+  (void)prims;
+  (void)normals;
+  (void)mats;
+  (void)blocks;
+  return;
+#endif
   mark(marks, 0, stream);
   if (!ordered) T.tile_cost = nullptr;
   // warm order: the previous frame's heavy-first unit order (same selection, same stream)

@@ -188,7 +188,7 @@ class FrameRenderer:
     frames and, in the library, its own scratch), so a frame's last, sparsely occupied waves
     overlap the next frame's work; finish() joins them back into `stream`."""
 
-    def __init__(self, scene, stream, inflight: int = 1):
+    def __init__(self, scene, stream, inflight: int = 1, streams=None):
         import torch
         self.scene = scene
         self.stream = stream
@@ -196,7 +196,9 @@ class FrameRenderer:
                       for c in range(scene.num_cameras)]
         dev = torch.device("cuda", torch.cuda.current_device())
         self.inflight = max(1, int(inflight))
-        self.streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(self.inflight - 1)]
+        # streams: extra render streams to reuse (as ShareRenderer)
+        self.streams = [stream] + (list(streams)[:self.inflight - 1] if streams is not None else
+                                   [torch.cuda.Stream(device=dev) for _ in range(self.inflight - 1)])
         self.frame_sets = [[torch.empty((h, w, 3), dtype=torch.float32, device=dev)
                             for (w, h) in self.sizes] for _ in range(self.inflight)]
         self.frames = self.frame_sets[0]
@@ -237,7 +239,8 @@ class TileGatherRenderer:
 
     def __init__(self, layout: TileLayout, stream, render: Callable, inflight: int = 2,
                  host_staging: bool = False, device=None, untile: Optional[Callable] = None,
-                 gather_stream: str = "render", render_inplace: Optional[Callable] = None):
+                 gather_stream: str = "render", render_inplace: Optional[Callable] = None,
+                 cpu_fakes: bool = False):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -258,6 +261,10 @@ class TileGatherRenderer:
         # untile skips its units — at N = 1 the step is the in-place render alone
         self.render_inplace = render_inplace
         self.root_inplace = render_inplace is not None and untile is not None
+        if self.root_inplace and host_staging and not cpu_fakes:
+            # the library's in-place renderer and untiler write device pointers; with host
+            # staging the frames are host tensors (cpu_fakes: host-memory test doubles)
+            raise ValueError("render_inplace + untile need device buffers (host_staging=False)")
         self.inflight = 1 if host_staging else max(1, int(inflight))
         F = self.inflight
         dev = device if device is not None else (

@@ -1,0 +1,82 @@
+"""The reference-side binding of INTEGRATION.md §2, compiled and run.
+
+oracle/_ref/hw2_gpu is the UNMODIFIED reference HW2 Scene / Pixel / tinyxml2 / lodepng sources
+linked with oracle/ref/Scene_gpu.cpp (render_image_gpu over libceng795_rt.so) and
+oracle/ref/hw2_gpu_main.cpp (HW2/main.cpp:17-57 with the two-line patch).  Its Pixel::color
+must hash to the reference's own frame hashes (tests/golden/golden.json, written by the
+reference's Scene::render_image), and its PNG files — the reference's Pixel::get_color and
+lodepng::encode — must be byte-identical to the PNGs the reference itself wrote
+(tests/golden/png).  So the drop-in holds at the reference's own seam, not only through ctypes."""
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import scenes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BINDING = os.path.join(ROOT, "oracle", "_ref", "hw2_gpu")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not os.path.exists(BINDING),
+                                 reason="oracle/_ref/hw2_gpu not built (make -C oracle binding)")]
+
+
+def run_binding(xml, workdir, *args):
+    """Runs hw2_gpu in `workdir` (the PNGs land there under their <ImageName>); returns the
+    dumped Pixel::color frames, one per camera."""
+    prefix = os.path.join(workdir, "px")
+    r = subprocess.run([BINDING, xml, "--dump", prefix, *args], cwd=workdir, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    frames = []
+    k = 0
+    while os.path.exists(f"{prefix}_cam{k}.f32"):
+        frames.append(np.fromfile(f"{prefix}_cam{k}.f32", dtype=np.float32))
+        k += 1
+    return frames
+
+
+def image_name(xml, cam=0):
+    import re
+    names = re.findall(r"<ImageName>\s*(\S+?)\s*</ImageName>", open(xml).read())
+    return names[cam]
+
+
+@pytest.mark.parametrize("name", ["c1", "hf_small", "hf_side", "soup1", "single_sphere"])
+def test_binding_frames_and_pngs_match_the_reference(scene_dir, tmp_path, name):
+    golden = json.load(open(os.path.join(GOLDEN, "golden.json")))[name]
+    pngs = json.load(open(os.path.join(GOLDEN, "png", "golden_png.json")))[name]
+    xml = scenes.write(name, scene_dir)
+    assert hashlib.sha256(open(xml, "rb").read()).hexdigest() == golden["xml_sha256"]
+    frames = run_binding(xml, str(tmp_path))
+    assert len(frames) == len(golden["cameras"])
+    for cam, gc in enumerate(golden["cameras"]):
+        assert hashlib.sha256(frames[cam].tobytes()).hexdigest() == gc["frame_sha256"], cam
+    png = open(os.path.join(str(tmp_path), image_name(xml)), "rb").read()
+    assert hashlib.sha256(png).hexdigest() == pngs["png_sha256"]
+    assert png == open(os.path.join(GOLDEN, "png", f"{name}_cam0.png"), "rb").read()
+
+
+def test_binding_with_the_reference_threads(scene_dir, tmp_path):
+    """HW2/main.cpp:33-36's T threads kept, each calling render_image_gpu on its own rows
+    (rt_render is reentrant): the same Pixel::color as the reference."""
+    golden = json.load(open(os.path.join(GOLDEN, "golden.json")))
+    for name in ("soup2", "c2"):
+        xml = scenes.write(name, scene_dir)
+        frames = run_binding(xml, str(tmp_path), "--threads", "7")
+        for cam, gc in enumerate(golden[name]["cameras"]):
+            assert hashlib.sha256(frames[cam].tobytes()).hexdigest() == gc["frame_sha256"], name
+
+
+def test_binding_c3_matches_reference_hash(scene_dir, tmp_path):
+    """C3 (999,698 triangles, 1920x1080) through the reference's own driver + the binding."""
+    gc = json.load(open(os.path.join(GOLDEN, "golden.json")))["c3"]["cameras"][0]
+    xml = scenes.write_c3(scene_dir)
+    frames = run_binding(xml, str(tmp_path), "--threads", "16")
+    assert frames[0].size == gc["width"] * gc["height"] * 3
+    assert hashlib.sha256(frames[0].tobytes()).hexdigest() == gc["frame_sha256"]

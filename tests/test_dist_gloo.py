@@ -264,7 +264,7 @@ def _root_inplace_worker(rank, world, port, outdir, sizes, steps):
             out[y0:y0 + TILE, x0:x0 + TILE] = full[y0:y0 + TILE, x0:x0 + TILE]
 
     R = TileGatherRenderer(L, None, render, host_staging=True, device="cpu", untile=untile,
-                           render_inplace=render_inplace)
+                           render_inplace=render_inplace, cpu_fakes=True)
     assert R.root_inplace
     ok = True
     for step in range(steps):

@@ -266,3 +266,56 @@ def test_release_stream_scratch(scene_dir):
             st.synchronize()
             assert same(b.cpu().numpy(), ref)
             s.release_stream(st.cuda_stream)
+
+
+@pytest.mark.parametrize("devices", [[0, 0, 0], [0] * 8])
+def test_multi_device_back_to_back_frames_on_one_stream(scene_dir, tmp_path, devices):
+    """Consecutive frames of two cameras on ONE caller stream, never synchronised in between:
+    with a device listed twice the shares are gathered by peer copies on the first device's
+    stream while the next frame already renders on the others' streams; each context waits for
+    the copy out of its buffers before rendering into them again, so every frame
+    stays the oracle's."""
+    import torch
+    import gen_scene as G
+    import ceng795_amd
+    xml = str(tmp_path / "hf2cam.xml")
+    with open(xml, "w") as f:
+        f.write(G.heightfield_scene(40, 120, 72, cameras=2).to_xml())
+    refs = [oracle_frame(xml, c)[0] for c in range(2)]
+    assert not np.array_equal(refs[0], refs[1])
+    with ceng795_amd.Scene(xml, devices=devices) as s:
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        bufs = []
+        for k in range(8):
+            b = torch.full(refs[0].shape, -1.0, dtype=torch.float32, device="cuda")
+            st.wait_stream(torch.cuda.current_stream())
+            s.render_device(k % 2, b.data_ptr(), stream=st.cuda_stream)
+            bufs.append(b)
+        torch.cuda.synchronize()
+        for k, b in enumerate(bufs):
+            assert same(b.cpu().numpy(), refs[k % 2]), (devices, k)
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_many_caller_streams_stay_bounded(scene_dir, devices):
+    """A caller that makes a new stream per frame: beyond the library's per-replica table
+    (64 streams) the least recently used stream's scratch / contexts are released after its
+    work has finished, and every frame is still right."""
+    import torch
+    import ceng795_amd
+    xml = scenes.write("hf_side", scene_dir)
+    ref, _ = oracle_frame(xml, 0)
+    kw = {"devices": devices} if devices else {"device": 0}
+    with ceng795_amd.Scene(xml, **kw) as s:
+        bufs, streams = [], []
+        for k in range(80):
+            st = torch.cuda.Stream()
+            b = torch.full(ref.shape, -1.0, dtype=torch.float32, device="cuda")
+            st.wait_stream(torch.cuda.current_stream())
+            s.render_device(0, b.data_ptr(), stream=st.cuda_stream)
+            bufs.append(b)
+            streams.append(st)
+        torch.cuda.synchronize()
+        for k, b in enumerate(bufs):
+            assert same(b.cpu().numpy(), ref), k
