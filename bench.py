@@ -614,7 +614,9 @@ def main() -> int:
             untile=None if host_staging else dist_tiles.scene_tile_untiler(scene, layout),
             gather_stream=args.gather_stream,
             render_inplace=None if (host_staging or args.root_gather)
-            else dist_tiles.scene_inplace_renderer(scene))
+            else dist_tiles.scene_inplace_renderer(scene),
+            # one-rank rehearsal: rank 0's share through a real RCCL self send / receive + untile
+            self_exchange=args.gather_rehearsal and world == 1)
     else:
         owners = dist_tiles.FrameOwners(n_cams, world, rank)
         sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
@@ -760,6 +762,13 @@ def main() -> int:
                                    "costs of the previous frame on its stream (warm order, "
                                    "DESIGN.md 4.8), every frame's rays all traced",
                        "gather_verified": verified,
+                       "exchange": None if not tiled else (
+                           "dist.gather (RCCL) of every rank's tile-major share, whole-frame untile"
+                           if args.root_gather or host_staging else
+                           "rank 0 in place + batch_isend_irecv (RCCL send / receive) of the other "
+                           "ranks' shares, untile around rank 0's units" if world > 1 else
+                           "one-rank rehearsal: rank 0's tile-major share through an RCCL self "
+                           "send / receive pair (batch_isend_irecv), whole-frame untile"),
                        "render_ms_avg": round(sum(render_ms) / len(render_ms), 4)},
             "roofline": roof, "cpu_baseline": cpu, "pcie_inclusive": host_rate,
         }

@@ -318,9 +318,6 @@ int untile_vec(const UntileParams& U) {
   return (U.width % 4 == 0) && ((uintptr_t)U.out % 16 == 0) && ((uintptr_t)U.recv % 16 == 0);
 }
 
-#ifndef RT_WARM_ORDER  // (A/B builds: 0 = the primary kernel in block order)
-#define RT_WARM_ORDER 1
-#endif
 
 void set_schedule(RenderParams& P, unsigned* sched) {
   const int regions = RT_ORDER_REGIONS;
@@ -1182,7 +1179,7 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
     // dispatches its primary kernel heaviest-first by that frame's measured tile costs
     const std::array<long long, 7> key{cam, row0, row_stride, tile_begin, tile_step,
                                        P.num_sel_tiles, P.block_deal};
-    const bool orderable = RT_WARM_ORDER && c.num_samples <= 1 && !P.frames && P.num_lights > 0;
+    const bool orderable = c.num_samples <= 1 && !P.frames && P.num_lights > 0;
     P.primary_order = orderable && sc->order_valid && sc->order_key == key ? 1 : 0;
     enqueue_frame(s, r, P, c.num_samples, sc->samples, (hipStream_t)stream, true);
     hip_check(hipEventRecord(sc->done, (hipStream_t)stream), "event record");

@@ -429,12 +429,10 @@ constexpr int kBatchFlush = RT_BATCH_FLUSH;   // run the queue once this many te
 constexpr int kBatchCap = kBatchFlush + 256;  // a wide visit flushes before a slot could overflow
 constexpr int kShadowFlush = kBatchFlush;
 
-// Queue pushes write every lane: lanes outside the push mask write a junk entry past the
-// queue (q[kBatchCap + ...], never read) instead of taking an exec-mask branch (RT_PUSH_ALL).
-#ifndef RT_PUSH_ALL
-#define RT_PUSH_ALL 1
-#endif
-constexpr int kPushJunk = RT_PUSH_ALL ? 128 : 0;
+// The primary traversal's queue pushes write every lane: lanes outside the push mask write a
+// junk entry past the queue (q[kBatchCap + ...], never read) instead of taking an exec-mask
+// branch (the shadow traversal keeps the branch: junk writes cost it VGPR spills).
+constexpr int kPushJunk = 128;
 #ifndef RT_PUSH_FRESH_LANE
 #define RT_PUSH_FRESH_LANE RT_FUSED
 #endif
@@ -495,9 +493,6 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 // Runs the n queued tests; SHADOW: 0 < t < thr of the owner sets its flag, else the owner's
 // key takes min(key, (t, leaf)) for 0 < t < inf.  All lanes of the wave take part.  SKIP:
 // some lane of the wave skips an axis (else the guard test needs no skip flags).
-#ifndef RT_FLUSH_RCP_PERMUTE  // (A/B builds)
-#define RT_FLUSH_RCP_PERMUTE 0
-#endif
 template <bool SHADOW, bool SPHERES, bool CULL, bool SKIP = true>
 __device__ __forceinline__ void batch_flush(const RenderParams& P, WaveLeafLds& L, int n,
                                             const LaneRay& r, float thr, Diag& dg) {
@@ -521,12 +516,8 @@ __device__ __forceinline__ void batch_flush(const RenderParams& P, WaveLeafLds& 
       const int tag = __float_as_int(q0.w);
       leaf = tag & ~kLeafSphere;
       // the guard: the holder box {q1.w, q2.w, q3.x, q3.y, q3.z, q3.w}
-#if RT_FLUSH_RCP_PERMUTE  // the owner's reciprocals (the same v_rcp_f32 of the same d)
-      rr.r = v3(lane_f(src, r.r.x), lane_f(src, r.r.y), lane_f(src, r.r.z));
-#else
       rr.r = v3(__builtin_amdgcn_rcpf(rr.d.x), __builtin_amdgcn_rcpf(rr.d.y),
                 __builtin_amdgcn_rcpf(rr.d.z));
-#endif
       rr.skip0 = SKIP && __builtin_fabsf(rr.d.x) < kEps;
       rr.skip1 = SKIP && __builtin_fabsf(rr.d.y) < kEps;
       rr.skip2 = SKIP && __builtin_fabsf(rr.d.z) < kEps;
@@ -673,9 +664,9 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
       }
       // (the shadow kernel keeps the exec-mask pushes: junk writes cost it VGPR spills)
       if (pair)
-        batch_push_pair<RT_PUSH_ALL && !SHADOW>(L, pending, leaf, hm);
+        batch_push_pair<!SHADOW>(L, pending, leaf, hm);
       else
-        batch_push<RT_PUSH_ALL && !SHADOW>(L, pending, leaf, hm);
+        batch_push<!SHADOW>(L, pending, leaf, hm);
       DIAG(dg.leaves += 1 + pair; dg.leaf_lanes += (1 + pair) * __builtin_popcountll(hm));
       continue;
     }
@@ -986,9 +977,6 @@ __device__ __forceinline__ V3 hit_point(const RenderParams& P, const PacketPixel
 
 // Shadow rays of HW2/Scene.cpp:113-127: one bit per point light, set when the light is
 // occluded for this pixel's primary hit.
-#ifndef RT_SHADOW_REMAT
-#define RT_SHADOW_REMAT 1
-#endif
 template <bool FAST, bool DEEP, bool SPHERES>
 __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
                                               const DevNode* __restrict__ nodes,
@@ -1004,15 +992,11 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       // 8-B record is an L2 hit)
       const RenderParams& P = fresh_params(P0);
       const DevLight& lt = lights[li];
-#if RT_SHADOW_REMAT
       // the packet's pixel indices recomputed here, not hoisted out of the light loop (where
       // they would be live across the traversal and spilled to scratch)
-      int sel_l = sel, lane_l;
+      int sel_l = sel;
       asm volatile("" : "+s"(sel_l));
-      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_l));
-#else
-      const int sel_l = sel, lane_l = lane_id();
-#endif
+      const int lane_l = fresh_lane();
       const PacketPixel q = packet_pixel(P, sel_l, lane_l);
       const int2_t rec = P.hits[(size_t)sel_l * (kTile * kTile) + q.lane];
       const bool hit = hit_leaf(rec) >= 0;
@@ -1029,13 +1013,9 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       bits |= (occ ? 1u : 0u) << (li - 32 * w);
     }
     const RenderParams& Pw = fresh_params(P0);
-#if RT_SHADOW_REMAT
-    int sel_w = sel, lane_w;
+    int sel_w = sel;
     asm volatile("" : "+s"(sel_w));
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_w));
-#else
-    const int sel_w = sel, lane_w = lane_id();
-#endif
+    const int lane_w = fresh_lane();
     Pw.occ[((size_t)sel_w * (kTile * kTile) + lane_w) * Pw.occ_words + w] = bits;
   }
   const RenderParams& Pc = fresh_params(P0);
@@ -1062,9 +1042,6 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
 // the fp64 pow (HW2 calls ::pow(double, double)) costs no occupancy in the traversal kernels.
 // The leaf's normal and material come in one 16-B load (normals[4 * leaf + 3] holds the
 // material index); the DevPrim record is read only in scenes with spheres (its kind).
-#ifndef RT_SHADE_NORMAL_MAT
-#define RT_SHADE_NORMAL_MAT 1
-#endif
 // (float)pow((double)c, (double)p) of HW2/Scene.cpp:133-137.  p == 1 returns c itself: the exact
 // result is the double c, and both glibc's pow (< 0.52 ulp) and ocml's (< 1 ulp) return an exact
 // result when one exists, so the reference gets c too.  Any other exponent takes the fp64 pow.
@@ -1094,16 +1071,10 @@ __device__ __forceinline__ void shade_pixel(const RenderParams& P,
     const int leaf = hit_leaf(rec);
     const V3 e = ld3(P.cam_e);
     const V3 p = hit_point(P, q, hit_t(rec));
-#if RT_SHADE_NORMAL_MAT
     const float4 nm = *reinterpret_cast<const float4*>(normals + 4 * leaf);
     const bool tri = !SPHERES || prims[leaf].kind == kPrimTriangle;
     const V3 n = tri ? v3(nm.x, nm.y, nm.z) : normalize(p - ld3(prims[leaf].v0));
     const DevMaterial& m = mats[__float_as_int(nm.w)];
-#else
-    const DevPrim& pr = prims[leaf];
-    const V3 n = pr.kind == kPrimTriangle ? ld3(normals + 4 * leaf) : normalize(p - ld3(pr.v0));
-    const DevMaterial& m = mats[pr.material];
-#endif
     const V3 w0 = normalize(e - p);  // (ray.o - intersection_point).normalize()
     color = color + ld3(m.ambient) * ld3(P.ambient);
     for (int li = 0; li < P.num_lights; li++) {

@@ -240,7 +240,7 @@ class TileGatherRenderer:
     def __init__(self, layout: TileLayout, stream, render: Callable, inflight: int = 2,
                  host_staging: bool = False, device=None, untile: Optional[Callable] = None,
                  gather_stream: str = "render", render_inplace: Optional[Callable] = None,
-                 cpu_fakes: bool = False):
+                 cpu_fakes: bool = False, self_exchange: bool = False):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -265,6 +265,11 @@ class TileGatherRenderer:
             # the library's in-place renderer and untiler write device pointers; with host
             # staging the frames are host tensors (cpu_fakes: host-memory test doubles)
             raise ValueError("render_inplace + untile need device buffers (host_staging=False)")
+        # self_exchange (the one-rank rehearsal of the root-in-place exchange): with nobody else
+        # to receive from, rank 0 renders its share tile-major anyway, posts it to itself as one
+        # isend / irecv pair (batch_isend_irecv: RCCL send / receive) and untiles all of it —
+        # the exchange an N-rank run makes, with rank 0 standing in for every peer
+        self.self_loop = bool(self_exchange) and self.root_inplace and L.world == 1
         self.inflight = 1 if host_staging else max(1, int(inflight))
         F = self.inflight
         dev = device if device is not None else (
@@ -318,6 +323,13 @@ class TileGatherRenderer:
                            [dist.P2POp(dist.isend, self._slot(s, sh), 0)])
                     for req in dist.batch_isend_irecv(ops):
                         req.wait()
+                elif self.self_loop and self.host_staging:  # (gloo has no pair to itself)
+                    self.gathered[s][c][0].copy_(self._slot(s, sh))
+                elif self.self_loop:
+                    ops = [dist.P2POp(dist.isend, self._slot(s, sh), 0),
+                           dist.P2POp(dist.irecv, self.gathered[s][c][0], 0)]
+                    for req in dist.batch_isend_irecv(ops):
+                        req.wait()
             elif self.host_staging:
                 glist = list(torch.empty((L.world, sh.slot, TILE_FLOATS))) if root else None
                 dist.gather(self._slot(s, sh).cpu(), glist, dst=0)
@@ -329,6 +341,8 @@ class TileGatherRenderer:
             if root and self.root_inplace:
                 if L.world > 1:
                     self.untile(c, self.gathered[s][c], self.padded[s][c], stream, skip_root=True)
+                elif self.self_loop:
+                    self.untile(c, self.gathered[s][c], self.padded[s][c], stream, skip_root=False)
             elif root and self.untile is not None:
                 self.untile(c, self.gathered[s][c], self.padded[s][c], stream)
             elif root:
@@ -345,7 +359,7 @@ class TileGatherRenderer:
             events[0].record(st)
         for c, sh in enumerate(self.layout.shares):
             if sh.count > 0:
-                if self.root_inplace and self.rank == 0:
+                if self.root_inplace and self.rank == 0 and not self.self_loop:
                     self.render_inplace(sh, self.padded[s][c], st)
                 else:
                     self.render(sh, self._slot(s, sh), st)

@@ -222,7 +222,7 @@ def test_tile_gather_renderer_pipeline(tmp_path, world, sizes, steps):
     assert (tmp_path / "result").read_text() == "ok"
 
 
-def _root_inplace_worker(rank, world, port, outdir, sizes, steps):
+def _root_inplace_worker(rank, world, port, outdir, sizes, steps, self_exchange=False):
     """The N>1 GPU exchange (TileGatherRenderer with render_inplace): rank 0 renders its own
     units in place into its frames, the other ranks send their slots point-to-point
     (batch_isend_irecv), and rank 0's untile fills everything but its own units."""
@@ -264,8 +264,9 @@ def _root_inplace_worker(rank, world, port, outdir, sizes, steps):
             out[y0:y0 + TILE, x0:x0 + TILE] = full[y0:y0 + TILE, x0:x0 + TILE]
 
     R = TileGatherRenderer(L, None, render, host_staging=True, device="cpu", untile=untile,
-                           render_inplace=render_inplace, cpu_fakes=True)
-    assert R.root_inplace
+                           render_inplace=render_inplace, cpu_fakes=True,
+                           self_exchange=self_exchange)
+    assert R.root_inplace and R.self_loop == (self_exchange and world == 1)
     ok = True
     for step in range(steps):
         state["step"] = step
@@ -281,11 +282,15 @@ def _root_inplace_worker(rank, world, port, outdir, sizes, steps):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,sizes", [(2, [(64, 40), (37, 21)]), (3, [(96, 64)]),
-                                         (1, [(40, 24)])])
-def test_root_inplace_exchange(tmp_path, world, sizes):
-    mp.spawn(_root_inplace_worker, args=(world, _free_port(), str(tmp_path), sizes, 2),
-             nprocs=world, join=True)
+@pytest.mark.parametrize("world,sizes,self_exchange", [(2, [(64, 40), (37, 21)], False),
+                                                       (3, [(96, 64)], False),
+                                                       (1, [(40, 24)], False),
+                                                       (1, [(40, 24), (17, 9)], True)])
+def test_root_inplace_exchange(tmp_path, world, sizes, self_exchange):
+    """world 1 with self_exchange: the one-rank rehearsal's self send / receive pair + the
+    whole-frame untile (what bench.py --gather-rehearsal runs over RCCL)."""
+    mp.spawn(_root_inplace_worker, args=(world, _free_port(), str(tmp_path), sizes, 2,
+                                         self_exchange), nprocs=world, join=True)
     assert (tmp_path / "result").read_text() == "ok"
 
 

@@ -27,6 +27,10 @@ def main():
     ap.add_argument("--slots", type=int, default=8192)
     ap.add_argument("--bins", type=int, default=20)
     ap.add_argument("--save", help="npz of per-tile wave durations (us), one map per kernel")
+    ap.add_argument("--world", type=int, default=1,
+                    help="> 1: render rank --rank's share of the block deal (tile-major), as one "
+                         "rank of an N-GPU run does")
+    ap.add_argument("--rank", type=int, default=0)
     a = ap.parse_args()
     import torch
     import bench
@@ -39,8 +43,13 @@ def main():
     with ceng795_amd.Scene(xml, device=0) as s:
         cam = s.camera(0)
         fb = torch.empty((cam.height, cam.width, 3), device="cuda")
-        for _ in range(3):
-            s.render_device(0, fb.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+        for _ in range(3):  # the last launch's waves are read back (warm order from the 2nd on)
+            if a.world > 1:
+                s.render_device(0, fb.data_ptr(), tile_begin=a.rank, tile_step=a.world,
+                                tile_major=True, blocks=True,
+                                stream=torch.cuda.current_stream().cuda_stream)
+            else:
+                s.render_device(0, fb.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         got = _lib.lib().rt_debug_timeline(buf, n)
         if got <= 0:
@@ -51,6 +60,8 @@ def main():
     for k, name in enumerate(["trace_primary_kernel", "trace_shadow_kernel"]):
         t = tl[k]
         t = t[t[:, 0] > 0]
+        if not len(t):  # (the fused build records its one kernel as the first)
+            continue
         m = np.zeros(((cam.height + 7) // 8, tiles_x), np.float32)
         sel = (t[:, 2] & 0xffffffff).astype(np.uint32).astype(np.int32)
         est = (t[:, 2] >> 32) & 0xffffffff
