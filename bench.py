@@ -228,60 +228,68 @@ def host_buffer_rate(scene, rays_frame: float, frames: int = 5):
 
 def roofline_line(xml, world, local_share, kt, launches, prof, kt_iso=None, n_iso=0):
     # local_share: fraction of one frame's pixels a timed launch renders
-    """Roofline of the dominant kernel (trace_primary_kernel): algorithmic bytes per launch
-    (the kernel's own node / leaf fetches and its per-pixel record, tools/kernel_work.py) over
-    its HIP-event duration.  With frames in flight the timed region's launches share the GPU
-    with another frame's kernels, which stretches their start-to-end times; the roofline then
-    uses the same launches run one frame at a time right after the timed region (kt_iso), and
-    reports the timed-region average beside it.  traffic = HBM bytes per launch of that kernel
-    from the PMC profile of this build (or null)."""
+    """Roofline of the dominant kernel, trace_frame_kernel (primary rays, shadow rays and
+    shading of every packet in one launch): algorithmic bytes per launch (the kernel's own node
+    / leaf fetches of both traversals and its per-pixel records, tools/kernel_work.py) over its
+    HIP-event duration.  With frames in flight the timed region's launches share the GPU with
+    other frames' kernels, which stretches their start-to-end times; the roofline then uses the
+    same launches run one frame at a time right after the timed region (kt_iso), and reports the
+    timed-region average beside it.  traffic = HBM bytes per launch of that kernel from the PMC
+    profile of this build (or null); issue = its instruction counts from the same profile."""
     work = kernel_work(xml)
-    per_launch = work["primary_bytes"] * local_share
-    prim_ms_timed = kt["primary"] / max(1, launches)
+    per_launch = work["frame_bytes"] * local_share
+    ms_timed = kt["frame"] / max(1, launches)
     if kt_iso is not None and n_iso:
-        kt, launches, per_launch = kt_iso, n_iso, work["primary_bytes"]
-    prim_ms = kt["primary"] / max(1, launches)
-    achieved = per_launch / (prim_ms * 1e-3) / 1e9
+        kt, launches, per_launch = kt_iso, n_iso, work["frame_bytes"]
+    ms = kt["frame"] / max(1, launches)
+    achieved = per_launch / (ms * 1e-3) / 1e9
     c = work["counters"]
     roof = {"bound": "latency", "peak_of": "hbm", "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-            "kernel": "trace_primary_kernel",
-            "kernel_ms_avg": round(prim_ms, 4),
-            "kernel_ms_avg_timed_region": round(prim_ms_timed, 4),
+            "kernel": "trace_frame_kernel",
+            "kernel_ms_avg": round(ms, 4),
+            "kernel_ms_avg_timed_region": round(ms_timed, 4),
             "kernel_timing": "one frame at a time after the timed region" if kt_iso is not None
                              and n_iso else "timed region",
             "algorithmic_bytes_per_launch": int(per_launch),
-            "bytes_model": "128 B x 8-wide node visits + 64 B x leaf visits (DevLeaf: primitive "
-                           "+ guard box) + 8 B hit record per pixel (tools/kernel_work.py, RT_DIAG "
-                           "build, same frame)",
-            "work_per_frame": {"node_visits": c["prim_node_visits"],
-                               "wide_node_visits": c.get("prim_wide_visits"),
-                               "leaf_visits": c["prim_leaf_visits"],
-                               "lanes_per_node_visit": round(c["prim_node_lanes"] /
-                                                             max(1, c["prim_node_visits"]), 2),
-                               "leaf_lane_tests": c["prim_leaf_lanes"]},
-            "other_kernels_ms_avg": {"trace_shadow_kernel": round(kt["shadow"] / max(1, launches), 4),
-                                     "shade_kernel": round(kt["shade"] / max(1, launches), 4)},
-            "shadow_kernel_frac": None}
-    sh_ms = kt["shadow"] / max(1, launches)
-    if sh_ms > 0 and work["shadow_bytes"]:
-        roof["shadow_kernel_frac"] = round(work["shadow_bytes"] * local_share /
-                                           (sh_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+            "algorithmic_bytes_split": {"primary": work["primary_bytes"],
+                                        "shadow": work["shadow_bytes"],
+                                        "shading": work["shade_bytes"]},
+            "bytes_model": "per traversal: 128 B x 8-wide node visits + 64 B x leaf visits "
+                           "(DevLeaf: primitive + guard box); per pixel: 8 B hit record written, "
+                           "8 B read + 4 B occlusion word written by the shadow phase, 8 B hit "
+                           "record + 16 B normal/material + 4 B occlusion read and 12 B RGB "
+                           "written by the shading (tools/kernel_work.py, RT_DIAG build, same "
+                           "frame)",
+            "work_per_frame": {"primary_wide_node_visits": c.get("prim_wide_visits"),
+                               "primary_leaf_visits": c["prim_leaf_visits"],
+                               "primary_lanes_per_node_visit": round(
+                                   c["prim_node_lanes"] / max(1, c["prim_node_visits"]), 2),
+                               "primary_leaf_lane_tests": c["prim_leaf_lanes"],
+                               "shadow_wide_node_visits": c.get("shad_wide_visits"),
+                               "shadow_leaf_visits": c["shad_leaf_visits"],
+                               "shadow_leaf_lane_tests": c["shad_leaf_lanes"]},
+            "other_kernels_ms_avg": {"order_kernel": round(kt["order"] / max(1, launches), 4)}}
     if prof is not None and world == 1:
-        k = prof["per_kernel"].get("trace_primary_kernel", {})
+        k = prof["per_kernel"].get("trace_frame_kernel", {})
         roof["traffic"] = k.get("hbm_bytes")
         roof["traffic_source"] = os.path.join("profiles", os.path.basename(prof["path"]))
         if "issue" in k:
             i = k["issue"]
+            visits = (c.get("prim_wide_visits") or 0) + (c.get("shad_wide_visits") or 0)
             roof["issue"] = {
+                "source": roof["traffic_source"],
+                "wave_insts": i.get("SQ_INSTS"),
                 "valu_wave_insts": i.get("SQ_INSTS_VALU"), "salu_wave_insts": i.get("SQ_INSTS_SALU"),
                 "smem_wave_insts": i.get("SQ_INSTS_SMEM"),
+                "insts_per_wide_visit": round(i["SQ_INSTS"] / visits, 1)
+                if i.get("SQ_INSTS") and visits else None,
                 # 2 cycles per wave64 VALU instruction on a SIMD-32, 1024 SIMDs; 1 SALU per
                 # cycle per CU, 256 CUs; at 2.4 GHz, over the live kernel time
-                "valu_issue_frac": round(i["valu_issue_us_at_2.4GHz"] / (prim_ms * 1e3), 3)
+                "valu_issue_frac": round(i["valu_issue_us_at_2.4GHz"] / (ms * 1e3), 3)
                 if "valu_issue_us_at_2.4GHz" in i else None,
-                "salu_issue_frac": round(i["salu_issue_us_at_2.4GHz"] / (prim_ms * 1e3), 3)
+                "salu_issue_frac": round(i["salu_issue_us_at_2.4GHz"] / (ms * 1e3), 3)
                 if "salu_issue_us_at_2.4GHz" in i else None}
         if "wave_states" in k:
             roof["wave_states"] = k["wave_states"]
@@ -377,8 +385,7 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8)):
     step can be no shorter than the slowest share: t1 / (N * max_r t_share) bounds the
     efficiency from above (the gather to rank 0 and its untile are not included)."""
     from ceng795_amd import dist_tiles
-    import torch
-    extra = [torch.cuda.Stream() for _ in range(max(0, inflight - 1))]  # one set for every run
+    streams = dist_tiles.render_streams(inflight)  # one set for every run (pool streams)
 
     def timed(R):
         for _ in range(3):
@@ -388,11 +395,12 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8)):
         scene.collect_stats()
         return ms
 
-    one = dist_tiles.FrameRenderer(scene, stream, inflight=inflight, streams=extra)
+    one = dist_tiles.FrameRenderer(scene, stream, inflight=inflight, streams=streams)
     t1 = timed(one)
     out = {}
     for n in ns:
-        per = [timed(dist_tiles.ShareRenderer(scene, n, r, stream, inflight=inflight, streams=extra))
+        per = [timed(dist_tiles.ShareRenderer(scene, n, r, stream, inflight=inflight,
+                                              streams=streams))
                for r in range(n)]
         slow = max(per)
         out[str(n)] = {"share_ms_max": round(slow, 4), "share_ms_min": round(min(per), 4),

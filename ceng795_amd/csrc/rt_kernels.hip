@@ -33,9 +33,6 @@ namespace rt {
 #define RT_INF __builtin_huge_valf()
 constexpr float kEps = 0.000001f;  // HW2/Vector3.h:7 kEpsilon
 
-#ifndef RT_FUSED  // 1: one kernel per frame (trace_frame_kernel)
-#define RT_FUSED 0
-#endif
 constexpr int kCounterSlots = kCounterRows;
 
 #ifdef RT_DIAG
@@ -433,9 +430,7 @@ constexpr int kShadowFlush = kBatchFlush;
 // junk entry past the queue (q[kBatchCap + ...], never read) instead of taking an exec-mask
 // branch (the shadow traversal keeps the branch: junk writes cost it VGPR spills).
 constexpr int kPushJunk = 128;
-#ifndef RT_PUSH_FRESH_LANE
-#define RT_PUSH_FRESH_LANE RT_FUSED
-#endif
+
 struct WaveLeafLds {
   unsigned long long q[kBatchCap + kPushJunk];  // lo 32: leaf (DevLeaf or DFS index), hi 32: lane
   unsigned long long key[64];       // per lane: closest-hit key, or shadow flag
@@ -445,7 +440,7 @@ constexpr unsigned long long kNoHitKey = (0x7f800000ull << 32) | 0xffffffffull; 
 
 // Queue leaf `leaf` for the lanes of `m` (wave-uniform); n = pending entries (wave-uniform).
 // This lane's index computed afresh (asm-opaque): a lane id (or lane << 32) kept live across the
-// traversal is one more VGPR, and the fused kernel spilled it to scratch at every push.
+// traversals is one more VGPR, which the frame kernel spilled to scratch at every push.
 __device__ __forceinline__ int fresh_lane() {
   int lane;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
@@ -454,7 +449,7 @@ __device__ __forceinline__ int fresh_lane() {
 
 template <bool ALL = false>
 __device__ __forceinline__ void batch_push(WaveLeafLds& L, int& n, int leaf, uint64_t m) {
-  const int lane = RT_PUSH_FRESH_LANE ? fresh_lane() : lane_id();
+  const int lane = fresh_lane();
   const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
   if (ALL) {
@@ -469,7 +464,7 @@ __device__ __forceinline__ void batch_push(WaveLeafLds& L, int& n, int leaf, uin
 // adjacent (one 16-B LDS write), the queue order does not matter.
 template <bool ALL = false>
 __device__ __forceinline__ void batch_push_pair(WaveLeafLds& L, int& n, int leaf, uint64_t m) {
-  const int lane = RT_PUSH_FRESH_LANE ? fresh_lane() : lane_id();
+  const int lane = fresh_lane();
   const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
   const unsigned long long hi = (unsigned long long)lane << 32;
@@ -1377,17 +1372,13 @@ __device__ __forceinline__ void recursive_packet(const RenderParams& P,
   }
 }
 
-// Traversal kernels hide their dependent node loads with occupancy: hold them to 8 waves/SIMD
-// (<= 64 VGPRs, <= 80 SGPRs); the primary kernel runs at 7, where the wide node's 32 SGPRs fit
-// without spills.  (Macros: A/B builds, `make exp EXTRA=-D...`.)
-#ifndef RT_TRACE_MIN_WAVES
-#define RT_TRACE_MIN_WAVES 7
+// The frame kernel hides its dependent node loads with occupancy: 7 waves/SIMD (<= 72 VGPRs),
+// where the wide node's 32 SGPRs and the fp32 traversal state fit without scratch (at 8 the
+// traversal spills).  (Macro: A/B builds, `make exp EXTRA=-D...`.)
+#ifndef RT_FRAME_MIN_WAVES
+#define RT_FRAME_MIN_WAVES 7
 #endif
-#ifndef RT_PRIMARY_MIN_WAVES
-#define RT_PRIMARY_MIN_WAVES 7
-#endif
-#define RT_PRIMARY_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_PRIMARY_MIN_WAVES, 8)))
-#define RT_TRAVERSAL_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_TRACE_MIN_WAVES, 8)))
+#define RT_FRAME_OCCUPANCY __attribute__((amdgpu_waves_per_eu(RT_FRAME_MIN_WAVES, 8)))
 
 // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so hand each
 // XCD a contiguous run of blocks — neighbouring packets share BVH nodes through its L2.
@@ -1557,50 +1548,14 @@ __device__ unsigned long long g_timeline[2][kTimelineWaves][3];
 #define TL_END(k)
 #endif
 
-// Traversal kernels: one packet per wave, XCD-remapped blocks of 2-D tile blocks.
+// One launch per frame: each wave runs its packet's primary traversal, its shadow rays and its
+// shading back to back, so a frame is one kernel with one tail (round 4 chained primary ->
+// order -> shadow -> shade kernels, each with its own tail: a 1/8 share of a C3 frame then took
+// 0.16 ms one at a time).  The hit record and occlusion bits still go through the
+// stream's scratch (the same lane writes, then reads them: program order), which keeps the
+// register state of the three phases apart.  tile_cost: the whole packet's time.
 template <bool FAST, bool DEEP, bool SPHERES>
-__global__ __launch_bounds__(kTraceWaves * 64) RT_PRIMARY_OCCUPANCY void trace_primary_kernel(
-    RenderParams P, const DevNode* __restrict__ nodes) {
-  extern __shared__ __attribute__((aligned(16))) int deep_stack[];
-  __shared__ WaveLeafLds leaf_lds[kTraceWaves];  // 2.5 KiB per wave
-  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * kDeepWords * kDeepStack : nullptr;
-  WaveLeafLds& L = leaf_lds[threadIdx.x >> 6];
-  TL_BEGIN;
-  const RenderParams& Q = fresh_params(P);
-  const int sel = dispatch_sel(Q);
-  TL_SEL(sel);
-  if (sel >= 0) {
-    const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
-    primary_packet<FAST, DEEP, SPHERES>(Q, nodes, sel, spill, L);
-    const RenderParams& Pw = fresh_params(P);
-    if (Pw.tile_cost && lane_id() == 0)  // the shadow kernel's dispatch order
-      Pw.tile_cost[sel] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - c0, 0xffffffffull);
-  }
-  TL_END(0);
-}
-
-template <bool FAST, bool DEEP, bool SPHERES>
-__global__ __launch_bounds__(kTraceWaves * 64) RT_TRAVERSAL_OCCUPANCY void trace_shadow_kernel(
-    RenderParams P, const DevNode* __restrict__ nodes, const DevLight* __restrict__ lights) {
-  extern __shared__ __attribute__((aligned(16))) int deep_stack[];
-  __shared__ WaveLeafLds leaf_lds[kTraceWaves];
-  int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * kDeepWords * kDeepStack : nullptr;
-  WaveLeafLds& L = leaf_lds[threadIdx.x >> 6];
-  TL_BEGIN;
-  const RenderParams& Q = fresh_params(P);
-  const int sel = dispatch_sel(Q);
-  TL_SEL(sel);
-  if (sel >= 0) shadow_packet<FAST, DEEP, SPHERES>(Q, nodes, lights, sel, spill, L);
-  TL_END(1);
-}
-
-// One launch per frame (RT_FUSED): each wave runs its packet's primary traversal, its shadow
-// rays and its shading back to back, so a frame is one kernel with one tail instead of the chain
-// primary -> order -> shadow -> shade (each with its own tail).  The hit record and occlusion bits
-// still go through the stream's scratch (same lane writes, then reads: program order), which
-// keeps the register state of the three phases apart.  tile_cost: the whole packet's time.
-template <bool FAST, bool DEEP, bool SPHERES>
-__global__ __launch_bounds__(kTraceWaves * 64) RT_PRIMARY_OCCUPANCY void trace_frame_kernel(
+__global__ __launch_bounds__(kTraceWaves * 64) RT_FRAME_OCCUPANCY void trace_frame_kernel(
     RenderParams P, const DevNode* __restrict__ nodes, const DevLight* __restrict__ lights) {
   extern __shared__ __attribute__((aligned(16))) int deep_stack[];
   __shared__ WaveLeafLds leaf_lds[kTraceWaves];
@@ -1641,18 +1596,8 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void recursive_kernel(
                                         leaf_lds[threadIdx.x >> 6]);
 }
 
-template <bool SPHERES>
-__global__ __launch_bounds__(kWavesPerBlock * 64) void shade_kernel(
-    RenderParams P, const DevPrim* __restrict__ prims, const float* __restrict__ normals,
-    const DevMaterial* __restrict__ mats, const DevLight* __restrict__ lights) {
-  const int sel = uniform((int)blockIdx.x * kWavesPerBlock + ((int)threadIdx.x >> 6));
-  if (sel >= P.num_sel_tiles) return;
-  shade_pixel<SPHERES>(P, prims, normals, mats, lights, sel);
-}
-
-// marks (nullable): 4 events recorded before the primary kernel, after it, after the shadow
-// kernel and after the shade kernel (rt_set_kernel_timing).  A recursive scene's single kernel
-// is timed between marks 2 and 3.
+// marks (nullable): 4 events recorded before the frame kernel (or the recursive kernel), after
+// it, after the order kernel and at the end (rt_set_kernel_timing).
 static inline void mark(const hipEvent_t* marks, int k, hipStream_t stream) {
   if (marks) (void)hipEventRecord(marks[k], stream);
 }
@@ -1665,11 +1610,11 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
   if (P.frames) {  // recursive scenes: one kernel walks each pixel's ray tree
     const size_t lds = DEEP ? sizeof(int) * kDeepWords * kDeepStack * kWavesPerBlock : 0;
     mark(marks, 0, stream);
-    mark(marks, 1, stream);
-    mark(marks, 2, stream);
     hipLaunchKernelGGL((recursive_kernel<FAST, DEEP, SPHERES>), dim3(blocks),
                        dim3(kWavesPerBlock * 64), lds, stream, P, nodes, prims, normals, mats,
                        lights);
+    mark(marks, 1, stream);
+    mark(marks, 2, stream);
     mark(marks, 3, stream);
     return;
   }
@@ -1699,45 +1644,18 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
               sched_words_for((unsigned long long)T.num_sel_tiles);
   }
   const int oblocks = ordered ? T.order_regions * T.order_stride : tblocks;
-  RenderParams S = T;
-#if RT_FUSED
-  // one kernel per frame (trace_frame_kernel), dispatched by the previous frame's order when
-  // there is one; the order kernel then sorts this frame's packet costs for the next frame
+  const RenderParams S = T;
+  // one kernel per frame, dispatched by the previous frame's heavy-first order when there is one
+  // (warm order: same selection, same stream); the order kernel then sorts this frame's packet
+  // costs for the next frame
   mark(marks, 0, stream);
   if (!ordered) T.tile_cost = nullptr;
   T.use_order = ordered && P.primary_order ? 1 : 0;
   hipLaunchKernelGGL((trace_frame_kernel<FAST, DEEP, SPHERES>), dim3(T.use_order ? oblocks : tblocks),
                      dim3(kTraceWaves * 64), tlds, stream, T, nodes, lights);
   mark(marks, 1, stream);
-  mark(marks, 2, stream);
   if (ordered) hipLaunchKernelGGL(order_kernel, dim3(S.order_regions), dim3(kOrderThreads), 0, stream, S);
-  mark(marks, 3, stream);
-  (void)prims;
-  (void)normals;
-  (void)mats;
-  (void)blocks;
-  return;
-#endif
-  mark(marks, 0, stream);
-  if (!ordered) T.tile_cost = nullptr;
-  // warm order: the previous frame's heavy-first unit order (same selection, same stream)
-  T.use_order = ordered && P.primary_order ? 1 : 0;
-  hipLaunchKernelGGL((trace_primary_kernel<FAST, DEEP, SPHERES>), dim3(T.use_order ? oblocks : tblocks),
-                     dim3(kTraceWaves * 64), tlds, stream, T, nodes);
-  mark(marks, 1, stream);
-  S.tile_cost = T.tile_cost;
-  if (P.num_lights > 0) {
-    if (ordered) {  // the shadow kernel LPT-scheduled by the primary kernel's measured times
-      hipLaunchKernelGGL(order_kernel, dim3(S.order_regions), dim3(kOrderThreads), 0, stream, S);
-      S.use_order = 1;
-    }
-    S.tile_cost = nullptr;  // (the shadow kernel reads the order only)
-    hipLaunchKernelGGL((trace_shadow_kernel<FAST, DEEP, SPHERES>), dim3(S.use_order ? oblocks : tblocks),
-                       dim3(kTraceWaves * 64), tlds, stream, S, nodes, lights);
-  }
   mark(marks, 2, stream);
-  hipLaunchKernelGGL(shade_kernel<SPHERES>, dim3(blocks), dim3(kWavesPerBlock * 64), 0, stream, P,
-                     prims, normals, mats, lights);
   mark(marks, 3, stream);
 }
 

@@ -36,6 +36,23 @@ TILE_FLOATS = TILE * TILE * 3
 ROW_FLOATS = TILE * 3  # one pixel row of a tile
 
 
+def render_streams(n: int, device=None, streams=None) -> list:
+    """`n` render streams for frames in flight: `streams` when given (reused, e.g. one set for
+    every renderer of a probe), else n consecutive streams of torch's per-device stream pool —
+    never the caller's default stream.  HIP hands the process's hardware queues
+    (GPU_MAX_HW_QUEUES, 4 on this pool) to streams in turn at creation, and two streams on one
+    queue serialise their kernels; the pool's streams were created together, so n <= 4
+    consecutive ones sit on n different queues, whereas the default stream shares its queue with
+    one pool stream in four.  (Rendering on the default stream plus three pool streams made the
+    one-GPU share probe bimodal: 0.056 or 0.093 ms for the same 1/8 share)"""
+    import torch
+    if streams is not None:
+        out = list(streams)[:n]
+        assert len(out) == n, "need one stream per frame in flight"
+        return out
+    return [torch.cuda.Stream(device=device) for _ in range(n)]
+
+
 def tiles_of(size: Tuple[int, int]) -> Tuple[int, int]:
     w, h = size
     return (w + TILE - 1) // TILE, (h + TILE - 1) // TILE
@@ -196,9 +213,10 @@ class FrameRenderer:
                       for c in range(scene.num_cameras)]
         dev = torch.device("cuda", torch.cuda.current_device())
         self.inflight = max(1, int(inflight))
-        # streams: extra render streams to reuse (as ShareRenderer)
-        self.streams = [stream] + (list(streams)[:self.inflight - 1] if streams is not None else
-                                   [torch.cuda.Stream(device=dev) for _ in range(self.inflight - 1)])
+        # render streams (render_streams: pool streams, or `streams`); `stream` only joins them
+        self.streams = render_streams(self.inflight, dev, streams)
+        for st in self.streams:
+            st.wait_stream(stream)
         self.frame_sets = [[torch.empty((h, w, 3), dtype=torch.float32, device=dev)
                             for (w, h) in self.sizes] for _ in range(self.inflight)]
         self.frames = self.frame_sets[0]
@@ -218,7 +236,7 @@ class FrameRenderer:
         return self.frames
 
     def finish(self):
-        for st in self.streams[1:]:
+        for st in self.streams:
             self.stream.wait_stream(st)
 
 
@@ -279,7 +297,7 @@ class TileGatherRenderer:
             self.rstreams = [stream]
             self.comm = None
         else:
-            self.rstreams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(F - 1)]
+            self.rstreams = render_streams(F, dev)  # (pool streams, one per frame in flight)
             self.comm = torch.cuda.Stream(device=dev)
         self.local = [torch.zeros((L.buffer_tiles, TILE_FLOATS), dtype=torch.float32, device=dev)
                       for _ in range(F)]
@@ -288,8 +306,9 @@ class TileGatherRenderer:
             # writes or reads these buffers first waits for it
             cur = torch.cuda.current_stream(dev)
             for st in self.rstreams + [self.comm]:
-                if st != cur:
-                    st.wait_stream(cur)
+                st.wait_stream(cur)
+                if stream is not None:
+                    st.wait_stream(stream)
         self.done = [torch.cuda.Event() if not host_staging else None for _ in range(F)]
         self.handoff = [torch.cuda.Event() if not host_staging else None for _ in range(F)]
         self.used = [False] * F
@@ -385,7 +404,7 @@ class TileGatherRenderer:
         """Make `stream` wait for every render stream and every outstanding gather / untile."""
         if self.host_staging:
             return
-        for st in self.rstreams[1:]:
+        for st in self.rstreams:
             self.stream.wait_stream(st)
         self.stream.wait_stream(self.comm)
 
@@ -430,8 +449,7 @@ class FrameGatherRenderer:
             c, out.data_ptr(), stream=st.cuda_stream))
         self.inflight = max(1, int(inflight)) if not host_staging else 1
         dev = device
-        self.streams = [stream] + ([torch.cuda.Stream(device=dev)
-                                    for _ in range(self.inflight - 1)] if not host_staging else [])
+        self.streams = render_streams(self.inflight, dev) if not host_staging else []
         self.comm = torch.cuda.Stream(device=dev) if not host_staging else None
         W = owners.world
         self.send = [[torch.zeros((h, w, 3), dtype=torch.float32, device=dev)
@@ -443,8 +461,9 @@ class FrameGatherRenderer:
         if not host_staging:  # the zero fill ran on the current stream (see TileGatherRenderer)
             cur = torch.cuda.current_stream(dev)
             for st in self.streams + [self.comm]:
-                if st != cur:
-                    st.wait_stream(cur)
+                st.wait_stream(cur)
+                if stream is not None:
+                    st.wait_stream(stream)
         self.done = [torch.cuda.Event() if not host_staging else None for _ in range(self.inflight)]
         self.used = [False] * self.inflight
         self.k = 0
@@ -454,7 +473,7 @@ class FrameGatherRenderer:
         torch, dist, O = self.torch, self.dist, self.owners
         slot = self.k % self.inflight
         self.k += 1
-        st = self.streams[slot] if not self.host_staging else self.stream
+        st = self.streams[slot] if not self.host_staging else None
         if events is not None and st is not None:
             events[0].record(st)
         if self.used[slot] and not self.host_staging:  # its gathers `inflight` steps ago
@@ -493,7 +512,7 @@ class FrameGatherRenderer:
         """Make `stream` wait for every render stream and every outstanding gather."""
         if self.host_staging:
             return
-        for st in self.streams[1:]:
+        for st in self.streams:
             self.stream.wait_stream(st)
         self.stream.wait_stream(self.comm)
 
@@ -510,12 +529,11 @@ class ShareRenderer:
         self.scene, self.stream = scene, stream
         dev = torch.device("cuda", torch.cuda.current_device())
         self.inflight = max(1, int(inflight))
-        # streams: the extra render streams to reuse (one set for every rank probed: each rank of
-        # an N-GPU run creates its streams in a fresh process, so they always land on the same
-        # hardware queues; new streams per probed rank cycle over the queues, which made the
-        # probe's per-rank times bimodal — DESIGN.md §6)
-        self.streams = [stream] + (list(streams)[:self.inflight - 1] if streams is not None else
-                                   [torch.cuda.Stream(device=dev) for _ in range(self.inflight - 1)])
+        # streams: the render streams to reuse (render_streams; one set for every rank probed, as
+        # each rank of an N-GPU run creates its own set in a fresh process)
+        self.streams = render_streams(self.inflight, dev, streams)
+        for st in self.streams:
+            st.wait_stream(stream)
         self.local = [torch.empty((max(1, L.buffer_tiles), TILE_FLOATS), dtype=torch.float32,
                                   device=dev) for _ in range(self.inflight)]
         self.k = 0
@@ -532,7 +550,7 @@ class ShareRenderer:
                                          blocks=sh.blocks, stream=st.cuda_stream)
 
     def finish(self):
-        for st in self.streams[1:]:
+        for st in self.streams:
             self.stream.wait_stream(st)
 
 

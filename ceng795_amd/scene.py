@@ -172,11 +172,11 @@ class Scene:
         check(lib().rt_set_kernel_timing(self._h, int(enable)))
 
     def read_kernel_times(self):
-        """(ms summed per kernel {primary, shadow, shade, total}, launches) since the last read."""
+        """(ms summed {frame kernel, order kernel, other, total}, launches) since the last read."""
         ms = (C.c_double * 4)()
         n = C.c_longlong()
         check(lib().rt_read_kernel_times(self._h, ms, C.byref(n)))
-        keys = ("primary", "shadow", "shade", "total")
+        keys = ("frame", "order", "other", "total")
         return dict(zip(keys, list(ms))), n.value
 
     DIAG_NAMES = ["primary_rays", "shadow_rays", "secondary_rays", "primary_hits",

@@ -242,9 +242,10 @@ enum { RT_UNTILE_BLOCKS = 1,    /* the units are 2x2 blocks (shares rendered wit
  * stream the scene never rendered on).  Streams that come and go should release theirs. */
 int rt_release_stream_scratch(rt_scene* scene, void* hip_stream);
 /* Per-kernel timing of render launches: while enabled, every launch records HIP events around
- * its traversal kernels on the launch's stream.  rt_read_kernel_times returns (and resets)
- * the summed milliseconds ms4 = {primary-ray kernel, shadow-ray kernel, shade kernel (or the
- * recursive kernel), all three} and the number of launches timed. */
+ * its kernels on the launch's stream.  rt_read_kernel_times returns (and resets) the summed
+ * milliseconds ms4 = {frame kernel (primary rays, shadow rays and shading of every packet; or
+ * the recursive kernel), order kernel (the next frame's dispatch order), other (0), all} and
+ * the number of launches timed. */
 int rt_set_kernel_timing(rt_scene* scene, int enable);
 int rt_read_kernel_times(rt_scene* scene, double* ms4, long long* launches);
 /* Seed of the per-pixel MSAA generators (see rt_render).  Replaces the reference's

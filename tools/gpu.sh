@@ -55,9 +55,10 @@ case "$CMD" in
     cat "$O/$N.json" ;;
   pmc)
     W=${1:-c3}; R=${2:-r04}
-    BENCH_ARGS="--workload $W" bash tools/pmc_passes.sh "$O/pmc_$W" traffic || exit 1
+    BENCH_ARGS="--workload $W" bash tools/pmc_passes.sh "$O/pmc_$W" traffic insts sq || exit 1
     LIB=ceng795_amd/lib/libceng795_rt.so; [ "$W" = c5 ] && LIB=ceng795_amd/lib/libceng795_ppm.so
     python3 tools/pmc_traffic.py --fetch "$O/pmc_$W/fetch" --write "$O/pmc_$W/write" --workload "$W" \
+      --insts "$O/pmc_$W/insts" --sq "$O/pmc_$W/sq" \
       --round "$R" --lib "$LIB" --out "$O/traffic_$W.json" || exit 1 ;;
   pmcg)
     N=${1:?name}; shift

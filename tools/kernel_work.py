@@ -13,7 +13,13 @@ diagnostic library; the timed library is never instrumented) to price its roofli
                                             + per-pixel records    (primary: 8 B hit record
                                                                     written; shadow: 8 B hit
                                                                     record read + 4 B
-                                                                    occlusion word written)
+                                                                    occlusion word written;
+                                                                    shading: 8 B hit record +
+                                                                    16 B normal / material + 4 B
+                                                                    occlusion read, 12 B RGB
+                                                                    written)
+
+The frame kernel runs all three phases per packet: frame_bytes = primary + shadow + shading.
 
 usage: CENG795_LIB=diag python tools/kernel_work.py <scene.xml> [--camera 0] [--traversal fast]
 prints one JSON object.
@@ -54,9 +60,11 @@ def main():
                 + leaf_b * d["prim_leaf_visits"] + 8 * pixels)
         shad = (node_bytes(d["shad_node_visits"], d["shad_wide_visits"])
                 + leaf_b * d["shad_leaf_visits"] + (8 + 4 * words) * pixels) if s.num_lights else 0
+        shade = (8 + 16 + 4 * words + 12) * pixels
         out = {"pixels": pixels, "packets": ((c.width + 7) // 8) * ((c.height + 7) // 8),
                "counters": d,
-               "primary_bytes": prim, "shadow_bytes": shad}
+               "primary_bytes": prim, "shadow_bytes": shad, "shade_bytes": shade,
+               "frame_bytes": prim + shad + shade}
     print(json.dumps(out))
 
 

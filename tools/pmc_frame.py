@@ -25,7 +25,7 @@ def main(argv):
             with open(path) as f:
                 for row in csv.DictReader(f):
                     name = row["Kernel_Name"].split("(")[0].replace("void ", "")
-                    if "trace_" not in name and "shade" not in name:
+                    if "trace_" not in name and "order_kernel" not in name:
                         continue
                     key = (path, row["Dispatch_Id"], row["Counter_Name"])
                     vals[name][int(row["Grid_Size"])][key] += float(row["Counter_Value"])

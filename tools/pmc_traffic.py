@@ -31,7 +31,7 @@ import subprocess
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("trace_primary_kernel", "trace_shadow_kernel", "shade_kernel", "recursive_kernel",
+KERNELS = ("trace_frame_kernel", "order_kernel", "recursive_kernel",
            "group_update_kernel", "photon_kernel", "materialize_kernel", "deposit_keys_kernel")
 
 
@@ -47,16 +47,25 @@ def per_kernel(directory):
     files = glob.glob(os.path.join(directory, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {directory}")
-    vals = defaultdict(lambda: defaultdict(float))
-    disp = defaultdict(set)
+    rows = []
     for path in files:
         with open(path) as f:
             for row in csv.DictReader(f):
                 k = short(row["Kernel_Name"])
-                if k is None:
-                    continue
-                vals[k][row["Counter_Name"]] += float(row["Counter_Value"])
-                disp[k].add((path, row.get("Dispatch_Id", row.get("Correlation_Id", ""))))
+                if k is not None:
+                    rows.append((k, path, row))
+    # only each kernel's largest launches (the whole frame): the bench also makes small ones
+    # (the cold-frame probe's one-tile render, shares)
+    top = defaultdict(int)
+    for k, _, row in rows:
+        top[k] = max(top[k], int(row.get("Grid_Size", 0) or 0))
+    vals = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
+    for k, path, row in rows:
+        if int(row.get("Grid_Size", 0) or 0) != top[k]:
+            continue
+        vals[k][row["Counter_Name"]] += float(row["Counter_Value"])
+        disp[k].add((path, row.get("Dispatch_Id", row.get("Correlation_Id", ""))))
     n = {k: len(v) for k, v in disp.items()}
     return {k: {c: x / max(1, n[k]) for c, x in v.items()} for k, v in vals.items()}, n
 

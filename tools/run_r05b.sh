@@ -15,4 +15,11 @@ tail -4 $O/scale_mt.err
 GPU_MAX_HW_QUEUES=8 timeout -k 10 600 python3 -u tools/scale_probe.py fused,fusedmt --rounds 1 --workloads c3 --inflight 8 \
   > $O/scale_hwq8.json 2> $O/scale_hwq8.err || { tail -20 $O/scale_hwq8.err; exit 1; }
 tail -2 $O/scale_hwq8.err
-echo done
+
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
+tail -2 $O/gpu_tests.log
+timeout -k 10 600 python3 -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err \
+  || { tail -20 $O/bench.err; exit 1; }
+tail -c 600 $O/bench.json
+echo all done
