@@ -238,7 +238,7 @@ def roofline_line(xml, world, local_share, kt, launches, prof, kt_iso=None, n_is
     profile of this build (or null); issue = its instruction counts from the same profile."""
     work = kernel_work(xml)
     per_launch = work["frame_bytes"] * local_share
-    ms_timed = kt["frame"] / max(1, launches)
+    ms_timed = kt["frame"] / launches if launches else None  # (--kernel-timing only)
     if kt_iso is not None and n_iso:
         kt, launches, per_launch = kt_iso, n_iso, work["frame_bytes"]
     ms = kt["frame"] / max(1, launches)
@@ -249,7 +249,7 @@ def roofline_line(xml, world, local_share, kt, launches, prof, kt_iso=None, n_is
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
             "kernel": "trace_frame_kernel",
             "kernel_ms_avg": round(ms, 4),
-            "kernel_ms_avg_timed_region": round(ms_timed, 4),
+            "kernel_ms_avg_timed_region": round(ms_timed, 4) if ms_timed else None,
             "kernel_timing": "one frame at a time after the timed region" if kt_iso is not None
                              and n_iso else "timed region",
             "algorithmic_bytes_per_launch": int(per_launch),
@@ -520,11 +520,12 @@ def main() -> int:
     ap.add_argument("--root-gather", action="store_true",
                     help="N>1 tile split: rank 0 renders its share tile-major and gathers it "
                          "with the others (default: in place, point-to-point receives only)")
-    ap.add_argument("--no-step-events", action="store_true",
-                    help="no per-step timing events in the timed region (render_ms_avg = 0)")
-    ap.add_argument("--no-kernel-timing", action="store_true",
-                    help="no HIP events around the kernels inside the timed region (A/B of "
-                         "their cost; the roofline then uses the one-frame-at-a-time times)")
+    ap.add_argument("--step-events", action="store_true",
+                    help="per-step timing events in the timed region (render_ms_avg; they cost "
+                         "a few %% of the step)")
+    ap.add_argument("--kernel-timing", action="store_true",
+                    help="HIP events around the kernels inside the timed region too (the "
+                         "roofline always uses one-frame-at-a-time times after it)")
     ap.add_argument("--no-share-probe", action="store_true",
                     help="N=1: skip the one-GPU prediction of strong scaling (share probe)")
     ap.add_argument("--cpu-rehearsal", action="store_true",
@@ -644,12 +645,12 @@ def main() -> int:
         dist.all_reduce(rays_step)
     rays_step = float(rays_step.item())
 
-    ev = None if args.no_step_events else [
+    ev = None if not args.step_events else [
         (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         for _ in range(args.steps)]
     scene.read_kernel_times()  # discard
     # HIP events around each traversal kernel, on its stream
-    scene.set_kernel_timing(not args.no_kernel_timing)
+    scene.set_kernel_timing(args.kernel_timing)
     elapsed = timed_steps(renderer, args.steps, world, coll_dev, ev)
     scene.set_kernel_timing(False)
     kt, launches = scene.read_kernel_times()
@@ -777,7 +778,9 @@ def main() -> int:
                            "ranks' shares, untile around rank 0's units" if world > 1 else
                            "one-rank rehearsal: rank 0's tile-major share through an RCCL self "
                            "send / receive pair (batch_isend_irecv), whole-frame untile"),
-                       "render_ms_avg": round(sum(render_ms) / len(render_ms), 4)},
+                       "render_ms_avg": round(sum(render_ms) / len(render_ms), 4) if ev else None,
+                       "timed_region": "the steps alone: no timing events inside it (kernel "
+                                       "and one-frame times are measured after it)"},
             "roofline": roof, "cpu_baseline": cpu, "pcie_inclusive": host_rate,
         }
         if single is not None:

@@ -434,6 +434,7 @@ constexpr int kPushJunk = 128;
 struct WaveLeafLds {
   unsigned long long q[kBatchCap + kPushJunk];  // lo 32: leaf (DevLeaf or DFS index), hi 32: lane
   unsigned long long key[64];       // per lane: closest-hit key, or shadow flag
+  int sub;  // the wave's quadrant of a split tile, -1: whole packet (trace_frame_kernel)
 };
 
 constexpr unsigned long long kNoHitKey = (0x7f800000ull << 32) | 0xffffffffull;  // (+inf, -1)
@@ -831,20 +832,35 @@ __device__ __forceinline__ const RenderParams& fresh_params(const RenderParams& 
 }
 
 // ------------------------------------------------------------------ render kernels
-// Three launches per frame (wavefront style): `trace_primary` finds each pixel's closest hit
-// and writes an 8-byte {t, leaf} record; `trace_shadow` rebuilds the hit point from it and
-// traces the point-light shadow rays into occlusion bits; `shade` runs the point-light loop.
-// Splitting keeps each kernel's live state small (occupancy is what hides the dependent node
-// loads), at 16 B of HBM traffic per pixel.
+// Three phases per packet (trace_frame_kernel): the primary phase finds each pixel's closest
+// hit and writes an 8-byte {t, leaf} record; the shadow phase rebuilds the hit point from it
+// and traces the point-light shadow rays into occlusion bits; the shading phase runs the
+// point-light loop.  Going through the records keeps each phase's live state small
+// (occupancy is what hides the dependent node loads).
+//
+// A packet is normally one wave's 64 lanes = the tile's 8x8 pixels.  A heavy tile can instead
+// be split over its workgroup's four waves (sub = 0..3: wave `sub` takes quadrant `sub` of the
+// tile, 4x4 pixels in lanes 0..15): fewer rays per wave walk a smaller union
+// of BVH paths, and the four quadrants run side by side.
 struct PacketPixel {
-  int lane, px, py;
-  bool valid;
+  int lane;  // pixel lane: the pixel's index within the tile's 8x8 (its record's slot)
+  int px, py;
+  bool own;    // this wave lane holds a pixel of the packet (all lanes unless split)
+  bool valid;  // ... inside the image
 };
 
-__device__ __forceinline__ PacketPixel packet_pixel(const RenderParams& P, int sel,
+// Pixel lane of wave lane `lane` (-1: none, the lanes 16..63 of a quadrant wave).
+__device__ __forceinline__ int pixel_lane(int lane, int sub) {
+  if (sub < 0) return lane;
+  return lane < 16 ? ((sub >> 1) * 4 + (lane >> 2)) * kTile + (sub & 1) * 4 + (lane & 3) : -1;
+}
+
+__device__ __forceinline__ PacketPixel packet_pixel(const RenderParams& P, int sel, int sub = -1,
                                                    int lane = lane_id()) {
   PacketPixel q;
-  q.lane = lane;
+  const int pl = pixel_lane(lane, sub);
+  q.own = pl >= 0;
+  q.lane = q.own ? pl : 0;
   int tx, ty;
   if (P.block_deal) {  // selected block sel / 4, its tile sel % 4
     deal_block_tile(P.tiles_x, P.tile_begin + (sel >> 2) * P.tile_step, sel & 3, tx, ty);
@@ -855,10 +871,14 @@ __device__ __forceinline__ PacketPixel packet_pixel(const RenderParams& P, int s
   }
   q.px = tx * kTile + (q.lane & 7);
   const int lr = ty * kTile + (q.lane >> 3);  // logical row
-  q.valid = q.px < P.width && lr < P.rows;
+  q.valid = q.own && q.px < P.width && lr < P.rows;
   q.py = P.row0 + lr * P.row_stride;
   return q;
 }
+
+// This wave's quadrant (-1: the whole packet), kept in the wave's LDS block instead of a
+// register across the traversals.
+__device__ __forceinline__ int wave_sub(const WaveLeafLds& L) { return uniform(L.sub); }
 
 // ------------------------------------------------------------------ MSAA sample positions
 // HW2/Scene.cpp:35-44: a std::default_random_engine (libstdc++ minstd_rand0, x <- 16807 x mod
@@ -928,7 +948,7 @@ template <bool FAST, bool DEEP, bool SPHERES>
 __device__ __forceinline__ void primary_packet(const RenderParams& P,
                                                const DevNode* __restrict__ nodes, int sel,
                                                int* spill, WaveLeafLds& L) {
-  const PacketPixel q = packet_pixel(P, sel);
+  const PacketPixel q = packet_pixel(P, sel, wave_sub(L));
   LaneRay ray = make_ray(ld3(P.cam_e), primary_dir(P, q.px, q.py), P.quot_ok);
   // The camera origin is wave-uniform; left to itself the compiler keeps it in 3 SGPRs and
   // copies it to VGPRs at every node visit (a VALU op takes one SGPR operand, the box
@@ -943,13 +963,14 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
   else
     closest_hit<false, FAST, DEEP, SPHERES>(P, nodes, spill, L, ray, q.valid, t, leaf, dg);
   const RenderParams& Pw = fresh_params(P);  // post-traversal fields: not live across it
+  const PacketPixel qw = packet_pixel(Pw, sel, wave_sub(L));  // (recomputed, not kept)
   int2_t rec;  // key layout: leaf low, t bits high (rt_internal.h)
-  rec.x = q.valid ? leaf : -2;  // -1 miss, -2 outside the image
+  rec.x = qw.valid ? leaf : -2;  // -1 miss, -2 outside the image
   rec.y = __float_as_int(t);
-  Pw.hits[(size_t)sel * (kTile * kTile) + q.lane] = rec;
-  const unsigned long long nvalid = __builtin_popcountll(ballot(q.valid));  // (all lanes)
-  const unsigned long long nhit = __builtin_popcountll(ballot(q.valid && leaf >= 0));
-  if (Pw.counters && q.lane == 0) {  // spread over kCounterSlots rows: no hot address
+  if (qw.own) Pw.hits[(size_t)sel * (kTile * kTile) + qw.lane] = rec;
+  const unsigned long long nvalid = __builtin_popcountll(ballot(qw.valid));  // (all lanes)
+  const unsigned long long nhit = __builtin_popcountll(ballot(qw.valid && leaf >= 0));
+  if (Pw.counters && lane_id() == 0) {  // spread over kCounterSlots rows: no hot address
     unsigned long long* c = counter_row(Pw, sel);
     atomicAdd(&c[kCntPrimary], nvalid);
     atomicAdd(&c[kCntHits], nhit);
@@ -992,9 +1013,9 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       int sel_l = sel;
       asm volatile("" : "+s"(sel_l));
       const int lane_l = fresh_lane();
-      const PacketPixel q = packet_pixel(P, sel_l, lane_l);
+      const PacketPixel q = packet_pixel(P, sel_l, wave_sub(L), lane_l);
       const int2_t rec = P.hits[(size_t)sel_l * (kTile * kTile) + q.lane];
-      const bool hit = hit_leaf(rec) >= 0;
+      const bool hit = q.own && hit_leaf(rec) >= 0;
       const V3 pk = hit ? hit_point(P, q, hit_t(rec)) : v3(0, 0, 0);
       const V3 ld = ld3(lt.position) - pk;
       const V3 wi = normalize(ld);
@@ -1010,12 +1031,13 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
     const RenderParams& Pw = fresh_params(P0);
     int sel_w = sel;
     asm volatile("" : "+s"(sel_w));
-    const int lane_w = fresh_lane();
-    Pw.occ[((size_t)sel_w * (kTile * kTile) + lane_w) * Pw.occ_words + w] = bits;
+    const int pl = pixel_lane(fresh_lane(), wave_sub(L));
+    if (pl >= 0) Pw.occ[((size_t)sel_w * (kTile * kTile) + pl) * Pw.occ_words + w] = bits;
   }
   const RenderParams& Pc = fresh_params(P0);
   if (Pc.counters) {
-    const bool hit = hit_leaf(Pc.hits[(size_t)sel * (kTile * kTile) + lane_id()]) >= 0;
+    const int pl = pixel_lane(lane_id(), wave_sub(L));
+    const bool hit = pl >= 0 && hit_leaf(Pc.hits[(size_t)sel * (kTile * kTile) + pl]) >= 0;
     const unsigned long long nhit = __builtin_popcountll(ballot(hit));
     if (lane_id() == 0) {
       unsigned long long* c = counter_row(Pc, sel);
@@ -1055,12 +1077,13 @@ __device__ __forceinline__ void shade_pixel(const RenderParams& P,
                                             const DevPrim* __restrict__ prims,
                                             const float* __restrict__ normals,
                                             const DevMaterial* __restrict__ mats,
-                                            const DevLight* __restrict__ lights, int sel) {
-  const PacketPixel q = packet_pixel(P, sel);
+                                            const DevLight* __restrict__ lights, int sel,
+                                            int sub) {
+  const PacketPixel q = packet_pixel(P, sel, sub);
   const size_t pix = (size_t)sel * (kTile * kTile) + q.lane;
   const int2_t rec = P.hits[pix];
-  const bool valid = hit_leaf(rec) != -2;
-  const bool hit = hit_leaf(rec) >= 0;
+  const bool valid = q.own && hit_leaf(rec) != -2;
+  const bool hit = q.own && hit_leaf(rec) >= 0;
   V3 color = v3(0.0f, 0.0f, 0.0f);
   if (hit) {
     const int leaf = hit_leaf(rec);
@@ -1098,7 +1121,7 @@ __device__ __forceinline__ void shade_pixel(const RenderParams& P,
     o[0] = 0.0f + color.x;  // Pixel::add_color(color, 1) onto a zeroed pixel
     o[1] = 0.0f + color.y;
     o[2] = 0.0f + color.z;
-  } else if (P.tile_major) {
+  } else if (P.tile_major && q.own) {
     float* o = P.out + 3 * pix;
     o[0] = o[1] = o[2] = 0.0f;
   }
@@ -1434,14 +1457,23 @@ __device__ __forceinline__ int unit_sel(const RenderParams& P, int unit, int w) 
   return sel < P.num_sel_tiles ? sel : -1;
 }
 
-// Selected tile of this wave in a traversal launch: ordered (block b of the grid takes the
-// b / regions-th heaviest unit of region b mod regions), else the XCD-remapped block order.
+// Selected tile of this wave in a traversal launch, and its quadrant (sub, -1: the whole
+// packet): ordered (block b of the grid takes entry b / regions of region b mod regions' list,
+// heaviest first: a unit, -1 = none, or -2 - (4 u + w) = tile w of unit u split over the
+// workgroup's four waves, wave k taking quadrant k), else the XCD-remapped block order.
+__device__ __forceinline__ int order_entry(const RenderParams& Q) {
+  const int b = (int)blockIdx.x;
+  return uniform(Q.unit_order[(b % Q.order_regions) * Q.order_stride + b / Q.order_regions]);
+}
+
 __device__ __forceinline__ int dispatch_sel(const RenderParams& Q) {
   const int w = (int)threadIdx.x >> 6;
   if (Q.use_order) {
-    const int b = (int)blockIdx.x;
-    const int u = uniform(Q.unit_order[(b % Q.order_regions) * Q.order_stride + b / Q.order_regions]);
-    return u < 0 ? -1 : uniform(unit_sel(Q, u, w));
+    const int e = order_entry(Q);
+    if (e >= 0) return uniform(unit_sel(Q, e, w));
+    if (e == -1) return -1;
+    const int k = -2 - e;
+    return uniform(unit_sel(Q, k >> 2, k & 3));
   }
   const int p = packet_index<kTraceWaves>();
   const int sel = p < trace_packets(Q) ? packet_sel(Q, p) : -1;
@@ -1484,9 +1516,31 @@ __device__ __forceinline__ unsigned unit_cost(const RenderParams& P, int u) {
 // 256 threads: with frames in flight the GPU is full of traversal waves, and a bigger workgroup
 // waits for a CU with that many free wave slots (rocprof: 1024-thread order launches averaged
 // 79 us, up to 373, beside other frames' traversal; the sort itself takes 8 us).
+//
+// Split: the heaviest units — at most order_split per region, each costing at
+// least kSplitBuckets buckets (2^(kSplitBuckets/8)) above the region's median — are listed as
+// one entry per tile (-2 - (4 u + w)), so each of their tiles gets a workgroup whose four waves
+// take one quadrant each.  Those tiles' costs are zeroed here: the next frame's quadrant waves
+// add their times into them (the tile's cost = the sum of its quadrants).
 constexpr int kOrderThreads = 256;
+// Split tuning (A/B builds): threshold in buckets above the median (8 per octave: 11 = 2.6 x),
+// units split per region at most (1 / RT_SPLIT_DIV of the region), and only in launches whose
+// regions hold at most RT_SPLIT_MAX_UNITS units (the shares of a frame split over GPUs: a whole
+// frame's tail is already hidden by the frames in flight, and splitting adds work)
+#ifndef RT_SPLIT_BUCKETS
+#define RT_SPLIT_BUCKETS 11
+#endif
+#ifndef RT_SPLIT_DIV
+#define RT_SPLIT_DIV 16
+#endif
+#ifndef RT_SPLIT_MAX_UNITS
+#define RT_SPLIT_MAX_UNITS 192
+#endif
+constexpr int kSplitBuckets = RT_SPLIT_BUCKETS;
+constexpr int kMaxSplit = 32;  // units split per region at most
 __global__ __launch_bounds__(kOrderThreads) void order_kernel(RenderParams P) {
   __shared__ int hist[kOrderBuckets];
+  __shared__ int split_info[2];  // [0] = split threshold bucket, [1] = units split
   const int tid = (int)threadIdx.x, x = (int)blockIdx.x;
   const int n = region_units(P, x);
   int* out = P.unit_order + (size_t)x * P.order_stride;
@@ -1509,18 +1563,49 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(RenderParams P) {
       if (lane >= o) x2 += y;
     }
     int base = x2 - run;
+    // the median unit's bucket (heaviest first: where the running count passes n / 2), and
+    // how many units lie kSplitBuckets or more above it
+    int med = -1;
 #pragma unroll
     for (int k = 0; k < kOrderBuckets / 64; k++) {
-      hist[kOrderBuckets - 1 - (lane * (kOrderBuckets / 64) + k)] = base;
+      const int bucket = kOrderBuckets - 1 - (lane * (kOrderBuckets / 64) + k);
+      if (base <= n / 2 && n / 2 < base + v[k]) med = bucket;
+      hist[bucket] = base;
       base += v[k];
+    }
+    const uint64_t has = ballot(med >= 0);
+    if (has) {
+      const int mb = __builtin_amdgcn_readlane(med, (int)__builtin_ctzll(has));
+      const int thr = mb + kSplitBuckets;
+      if (lane == 0) {
+        // hist[] now holds each bucket's first rank: units in buckets >= thr have ranks
+        // below hist[thr - 1]'s ... i.e. the first rank of the next lighter bucket
+        const int heavy = thr > kOrderBuckets - 1 ? 0 : hist[thr - 1];
+        split_info[0] = thr;
+        split_info[1] = min(P.order_split, heavy);
+      }
+    } else if (lane == 0) {
+      split_info[0] = kOrderBuckets;
+      split_info[1] = 0;
     }
   }
   __syncthreads();
+  const int nsplit = split_info[1];
   for (int i = tid; i < n; i += kOrderThreads) {
     const int u = region_unit(P, x, i);
-    out[atomicAdd(&hist[cost_bucket(unit_cost(P, u))], 1)] = u;
+    const int r = atomicAdd(&hist[cost_bucket(unit_cost(P, u))], 1);
+    if (r < nsplit) {  // one entry per tile, -1 for a padding tile of an edge block
+      for (int w = 0; w < kTraceWaves; w++) {
+        const int sel = unit_sel(P, u, w);
+        out[kTraceWaves * r + w] = sel >= 0 ? -2 - (kTraceWaves * u + w) : -1;
+        if (sel >= 0) P.tile_cost[sel] = 0u;
+      }
+    } else {
+      out[r + (kTraceWaves - 1) * nsplit] = u;
+    }
   }
-  for (int i = n + tid; i < P.order_stride; i += kOrderThreads) out[i] = -1;
+  for (int i = n + (kTraceWaves - 1) * nsplit + tid; i < P.order_stride; i += kOrderThreads)
+    out[i] = -1;
 }
 
 // RT_TIMELINE (experiment builds only): every traversal wave records its start and end on the
@@ -1566,6 +1651,7 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_FRAME_OCCUPANCY void trace_fra
   const int sel = dispatch_sel(Q);
   TL_SEL(sel);
   if (sel >= 0) {
+    L.sub = Q.use_order && order_entry(Q) <= -2 ? (int)threadIdx.x >> 6 : -1;
     // the packet's start time waits in LDS (kept in SGPRs across the traversals it spilled)
     __shared__ unsigned long long start[kTraceWaves];
     start[threadIdx.x >> 6] = __builtin_amdgcn_s_memrealtime();
@@ -1573,11 +1659,16 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_FRAME_OCCUPANCY void trace_fra
     if (fresh_params(P).num_lights > 0)
       shadow_packet<FAST, DEEP, SPHERES>(fresh_params(P), nodes, lights, sel, spill, L);
     const RenderParams& Ps = fresh_params(P);
-    shade_pixel<SPHERES>(Ps, Ps.prims, Ps.normals, Ps.materials, lights, sel);
+    shade_pixel<SPHERES>(Ps, Ps.prims, Ps.normals, Ps.materials, lights, sel, wave_sub(L));
     const RenderParams& Pw = fresh_params(P);
-    if (Pw.tile_cost && lane_id() == 0)  // the next frame's dispatch order
-      Pw.tile_cost[sel] = (unsigned)min(__builtin_amdgcn_s_memrealtime() - start[threadIdx.x >> 6],
-                                        0xffffffffull);
+    if (Pw.tile_cost && lane_id() == 0) {  // the next frame's dispatch order
+      const unsigned c = (unsigned)min(__builtin_amdgcn_s_memrealtime() - start[threadIdx.x >> 6],
+                                       0xffffffffull);
+      if (wave_sub(L) < 0)
+        Pw.tile_cost[sel] = c;
+      else  // a quadrant: the tile's cost is the sum of its quadrants' (zeroed by order_kernel)
+        atomicAdd(&Pw.tile_cost[sel], c);
+    }
   }
   TL_END(0);
 }
@@ -1628,6 +1719,9 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
 #ifndef RT_ORDER_MIN_TILES  // launches selecting fewer tiles run in block order (no order kernel)
 #define RT_ORDER_MIN_TILES 0
 #endif
+#ifndef RT_ORDER_SPLIT  // (A/B builds: 0 = no heavy-tile split)
+#define RT_ORDER_SPLIT 1
+#endif
   bool ordered = T.tile_cost != nullptr && T.unit_order != nullptr && T.order_regions > 0 &&
                  T.num_sel_tiles >= RT_ORDER_MIN_TILES;
   if (ordered) {
@@ -1638,7 +1732,11 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
     else
       T.order_chunk = T.tile_block ? max(1, (nbx + 1) / 2) : 64;
     const int chunks = (T.order_units + T.order_chunk - 1) / T.order_chunk;
-    T.order_stride = ((chunks + T.order_regions - 1) / T.order_regions) * T.order_chunk;
+    const int per_region = ((chunks + T.order_regions - 1) / T.order_regions) * T.order_chunk;
+    // room for order_split units per region listed tile by tile (kTraceWaves entries each)
+    T.order_split = RT_ORDER_SPLIT && per_region <= RT_SPLIT_MAX_UNITS
+                        ? min(kMaxSplit, max(1, per_region / RT_SPLIT_DIV)) : 0;
+    T.order_stride = per_region + (kTraceWaves - 1) * T.order_split;
     ordered = (unsigned long long)T.num_sel_tiles +
                   (unsigned long long)T.order_regions * T.order_stride <=
               sched_words_for((unsigned long long)T.num_sel_tiles);

@@ -292,3 +292,36 @@ def test_shared_reciprocal_quotients_are_ieee(rt):
         _lib.check(_lib.lib().rt_debug_quotient_check(0, seed, 1 << 26, out))
         assert out[1] == 1 << 26
         assert out[0] == 0, f"seed {seed}: {out[0]} quotients differ from IEEE division"
+
+
+@pytest.mark.parametrize("world,rank", [(1, 0), (8, 3)])
+def test_split_heavy_tiles_keep_every_bit(rt, scene_dir, world, rank):
+    """Warm frames dispatch by the previous frame's costs and split the heaviest tiles over
+    their workgroup's four waves, one quadrant each; the first frame of the
+    selection on a stream runs in block order, unsplit.  Every warm frame — the whole C3 frame
+    in place, or one rank's tile-major share of the 8-way block deal — must equal the cold one
+    bit for bit (and the whole frame the reference's own hash)."""
+    import hashlib
+    import json
+    import torch
+    xml = scenes.write_c3(scene_dir)
+    with rt.Scene(xml) as s:
+        c = s.camera(0)
+        st = torch.cuda.Stream()
+        n = c.height * c.width * 3 if world == 1 else s.num_tiles(0) * 64 * 3
+        bufs = [torch.full((n,), -7.0, dtype=torch.float32, device="cuda") for _ in range(5)]
+        for b in bufs:
+            if world == 1:
+                s.render_device(0, b.data_ptr(), stream=st.cuda_stream)
+            else:
+                s.render_device(0, b.data_ptr(), tile_begin=rank, tile_step=world,
+                                tile_major=True, blocks=True, stream=st.cuda_stream)
+        torch.cuda.synchronize()
+        cold = bufs[0].cpu().numpy()
+        for k, b in enumerate(bufs[1:], 1):
+            assert np.array_equal(b.cpu().numpy().view(np.uint32), cold.view(np.uint32)), k
+        if world == 1:
+            gc = json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                             "golden.json")))["c3"]["cameras"][0]
+            assert hashlib.sha256(cold.tobytes()).hexdigest() == gc["frame_sha256"]
+        s.release_stream(st.cuda_stream)
