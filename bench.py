@@ -531,6 +531,9 @@ def main() -> int:
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="no GPU: the N>1 tile deal / gather / untile with synthetic tiles over "
                          "gloo (tests of the launcher and the exchange)")
+    ap.add_argument("--precondition-ms", type=float, default=100.0,
+                    help="untimed steps for this long before the warm-up steps (the GPU's clock "
+                         "ramp; 0 = none)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="frames in flight per GPU: consecutive steps on that many streams / "
                          "buffer sets, so one frame's sparsely occupied last waves (and, N>1, "
@@ -633,6 +636,26 @@ def main() -> int:
                                                   host_staging=host_staging,
                                                   inflight=args.inflight, device=dev)
 
+    # device preconditioning: untimed steps for --precondition-ms of wall time before the
+    # warm-up.  Five warm-up steps are 2 ms of GPU work, too short for the GPU to leave its idle
+    # clock: the same 20 timed steps measured 0.431-0.441 ms per step after 5 warm-up steps and
+    # 0.395-0.401 after 50 or 200 (profiles/r05/warmup_sweep.txt).  Its rays are not counted.
+    pre_steps = 0
+    if args.precondition_ms > 0:
+        t_pre = time.perf_counter()
+        while True:  # rounds of steps; with several ranks every rank runs as many as rank 0
+            for _ in range(4 * renderer.inflight):
+                renderer.step()
+                pre_steps += 1
+            renderer.finish()
+            torch.cuda.synchronize()
+            go = torch.tensor([float((time.perf_counter() - t_pre) * 1e3 < args.precondition_ms)],
+                              dtype=torch.float64, device=coll_dev)
+            if world > 1:
+                dist.broadcast(go, 0)
+            if go.item() == 0.0:
+                break
+        scene.collect_stats()  # (discard the preconditioning's rays)
     # warmup (also yields the per-step ray count from the device counters)
     for _ in range(args.warmup):
         renderer.step()
@@ -780,7 +803,10 @@ def main() -> int:
                            "send / receive pair (batch_isend_irecv), whole-frame untile"),
                        "render_ms_avg": round(sum(render_ms) / len(render_ms), 4) if ev else None,
                        "timed_region": "the steps alone: no timing events inside it (kernel "
-                                       "and one-frame times are measured after it)"},
+                                       "and one-frame times are measured after it)",
+                       "preconditioning": {"ms": args.precondition_ms, "steps": pre_steps,
+                                           "note": "untimed steps before the warm-up: the "
+                                                   "GPU's clock ramp"}},
             "roofline": roof, "cpu_baseline": cpu, "pcie_inclusive": host_rate,
         }
         if single is not None:
