@@ -347,6 +347,8 @@ int create_from_host(rt_scene* s, const std::vector<int>& devices, bool multi) {
   build_accel(s->host, kDefaultTreeletLeaves);
   if (s->host.accel_depth > max_supported_depth()) build_accel(s->host, 0);
   const HostScene& h = s->host;
+  if (h.prims.size() >= (size_t(1) << 26))  // leaf indices share a 32-bit queue word with a lane
+    throw std::invalid_argument("scenes of 2^26 primitives or more are not supported");
   if (h.depth > max_supported_depth())
     throw std::invalid_argument("BVH deeper than " + std::to_string(max_supported_depth()) +
                                 " levels is not supported");

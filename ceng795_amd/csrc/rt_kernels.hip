@@ -431,51 +431,59 @@ constexpr int kShadowFlush = kBatchFlush;
 // branch (the shadow traversal keeps the branch: junk writes cost it VGPR spills).
 constexpr int kPushJunk = 128;
 
+// A queue entry is one 32-bit word: the owner lane above kQueueLeafBits, the leaf (DevLeaf or
+// DFS index, < 2^26: rt_api.hip refuses larger scenes) below.
+constexpr int kQueueLeafBits = 26;
+constexpr unsigned kQueueLeafMask = (1u << kQueueLeafBits) - 1u;
 struct WaveLeafLds {
-  unsigned long long q[kBatchCap + kPushJunk];  // lo 32: leaf (DevLeaf or DFS index), hi 32: lane
+  unsigned q[kBatchCap + kPushJunk];  // lane << kQueueLeafBits | leaf
   unsigned long long key[64];       // per lane: closest-hit key, or shadow flag
   int sub;  // the wave's quadrant of a split tile, -1: whole packet (trace_frame_kernel)
 };
 
 constexpr unsigned long long kNoHitKey = (0x7f800000ull << 32) | 0xffffffffull;  // (+inf, -1)
 
-// Queue leaf `leaf` for the lanes of `m` (wave-uniform); n = pending entries (wave-uniform).
-// This lane's index computed afresh (asm-opaque): a lane id (or lane << 32) kept live across the
-// traversals is one more VGPR, which the frame kernel spilled to scratch at every push.
+// This lane's index computed afresh (asm-opaque), so that it is not kept live (and spilled)
+// across a traversal: the shadow phase's light loop.
 __device__ __forceinline__ int fresh_lane() {
   int lane;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
   return lane;
 }
 
+// Queue leaf `leaf` for the lanes of `m` (wave-uniform); n = pending entries (wave-uniform).
+// (Round 5: 32-bit entries, and lane_id() left to the compiler instead of an asm-opaque
+// recomputation per push: C3 frame 0.3905 -> 0.3802 ms four in flight, profiles/r05/ab_queue32.json.)
+
 template <bool ALL = false>
 __device__ __forceinline__ void batch_push(WaveLeafLds& L, int& n, int leaf, uint64_t m) {
-  const int lane = fresh_lane();
+  const int lane = lane_id();
   const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+  const unsigned e = ((unsigned)lane << kQueueLeafBits) | (unsigned)leaf;
   if (ALL) {
-    L.q[lane_in(m) ? n + below : kBatchCap + lane] = ((unsigned long long)lane << 32) | (unsigned)leaf;
+    L.q[lane_in(m) ? n + below : kBatchCap + lane] = e;
   } else if (lane_in(m)) {
-    L.q[n + below] = ((unsigned long long)lane << 32) | (unsigned)leaf;
+    L.q[n + below] = e;
   }
   n += __builtin_popcountll(m);
 }
 
 // Queue leaves `leaf` and `leaf + 1` (a pair) for the lanes of `m`: each lane's two entries are
-// adjacent (one 16-B LDS write), the queue order does not matter.
+// adjacent (one ds_write2_b32), the queue order does not matter.
 template <bool ALL = false>
 __device__ __forceinline__ void batch_push_pair(WaveLeafLds& L, int& n, int leaf, uint64_t m) {
-  const int lane = fresh_lane();
+  const int lane = lane_id();
   const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-  const unsigned long long hi = (unsigned long long)lane << 32;
-  if (ALL) {
+  const unsigned e = ((unsigned)lane << kQueueLeafBits) | (unsigned)leaf;
+  if (ALL) {  // (n may be odd: two 4-B writes, ds_write2_b32)
     const int at = lane_in(m) ? n + 2 * below : kBatchCap + 2 * lane;
-    L.q[at] = hi | (unsigned)leaf;
-    L.q[at + 1] = hi | (unsigned)(leaf + 1);
+    L.q[at] = e;
+    L.q[at + 1] = e + 1u;
   } else if (lane_in(m)) {
-    L.q[n + 2 * below] = hi | (unsigned)leaf;
-    L.q[n + 2 * below + 1] = hi | (unsigned)(leaf + 1);
+    L.q[n + 2 * below] = e;
+    L.q[n + 2 * below + 1] = e + 1u;
   }
   n += 2 * __builtin_popcountll(m);
 }
@@ -496,8 +504,8 @@ __device__ __forceinline__ void batch_flush(const RenderParams& P, WaveLeafLds& 
   for (int base = 0; base < n; base += 64) {
     const int i = base + lane;
     const bool valid = i < n;
-    const unsigned long long e = valid ? L.q[i] : 0ull;
-    const int src = (int)(e >> 32), idx = (int)(unsigned)e;
+    const unsigned e = valid ? L.q[i] : 0u;
+    const int src = (int)(e >> kQueueLeafBits), idx = (int)(e & kQueueLeafMask);
     LaneRay rr;
     rr.o = v3(lane_f(src, r.o.x), lane_f(src, r.o.y), lane_f(src, r.o.z));
     rr.d = v3(lane_f(src, r.d.x), lane_f(src, r.d.y), lane_f(src, r.d.z));
