@@ -280,12 +280,6 @@ struct ppm_scene {
 
 namespace {
 
-// Longest-first update order (tile_work_kernel); PPM_LPT_ORDER=0 (an exp build) keeps the group
-// order for A/B timing.  The order cannot change results: tiles own disjoint hit points.
-#ifndef PPM_LPT_ORDER
-#define PPM_LPT_ORDER 1
-#endif
-bool lpt_order() { return PPM_LPT_ORDER != 0; }
 
 // Tile-list compaction in the update pass (group_update_kernel phase (0)): tiles whose group
 // list holds at least this many deposits copy the reachable ones first.  Results do not depend
@@ -594,8 +588,11 @@ void trace_photons(ppm_scene* s, long long first, long long count) {
           s->gpos.reserve(P, "alloc group deposit lists");
           hip_check(launch_materialize(s->pkey2.p, s->pval2.p, P, s->dpos.p, s->gpos.p, s->stream),
                     "materialise group lists");
+          // longest-first update order (tile_work_kernel): the hot groups' serial chains start
+          // in the first dispatch round.  The order cannot change results: tiles own disjoint
+          // hit points.
           const int2* tiles = s->tiles.p;
-          if (lpt_order()) {
+          {
             s->tkey.reserve(s->n_tiles, "alloc tile keys");
             s->tkey2.reserve(s->n_tiles, "alloc tile keys");
             s->tiles_lpt.reserve(s->n_tiles, "alloc tile order");

@@ -491,16 +491,13 @@ __global__ __launch_bounds__(1024) void grid_kernel(const PHitPoint* hps, int n,
 // one deposit per diffuse hit in slots[k * count + i], k < K = max(1, MaxRecursionDepth - 1)
 // (k-major, so deposit_keys reads the k-th deposits of consecutive photons coalesced).
 //
-// Lanes are refilled (PPM_REFILL, default): Russian roulette ends ~2/3 of the chains at every
+// Lanes are refilled: Russian roulette ends ~2/3 of the chains at every
 // diffuse hit (C5: 1.36 segments per photon), so a wave that traced one photon per lane ran
 // until its longest chain ended (~4-5 segments) with most lanes idle.  Here each workgroup owns
 // a contiguous range of photons; a lane whose chain ends takes the next photon of the range
 // (one LDS atomic per wave and round) and the wave runs one segment per round for all its live
 // lanes.  Every photon is computed exactly as before (own random stream, same arithmetic, its
 // deposits in its own slots), only the lane that computes it changes.
-#ifndef PPM_REFILL
-#define PPM_REFILL 1
-#endif
 #ifndef PPM_PHOTON_BLOCKS
 #define PPM_PHOTON_BLOCKS 4096
 #endif
@@ -598,7 +595,6 @@ __global__ __launch_bounds__(256) void photon_kernel(PScene S, unsigned long lon
                                                      unsigned long long* stats) {
   unsigned long long rays = 0, deps = 0;
   PhotonState P;
-#if PPM_REFILL
   __shared__ int s_next;
   const int per = (int)(((long long)count + gridDim.x - 1) / gridDim.x);
   const int beg = (int)min((long long)blockIdx.x * per, (long long)count);
@@ -628,15 +624,6 @@ __global__ __launch_bounds__(256) void photon_kernel(PScene S, unsigned long lon
       i = -1;
     }
   }
-#else
-  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  if (i < count) {
-    emit_photon(S, seed, first + i, P);
-    while (photon_segment(S, i, count, slots, P, rays, deps)) {
-    }
-    ndep[i] = P.k;
-  }
-#endif
   const unsigned long long tr = wave_sum(rays), td = wave_sum(deps);
   if (stats && (threadIdx.x & 63) == 0) {
     if (tr) atomicAdd(&stats[1], tr);
@@ -725,14 +712,8 @@ __global__ __launch_bounds__(256) void group_starts_kernel(const int* flags, con
 #ifndef PPM_GATE_B
 #define PPM_GATE_B 3
 #endif
-#ifndef PPM_RR_STAGE
-#define PPM_RR_STAGE 128
-#endif
 #ifndef PPM_CHUNK
 #define PPM_CHUNK 1024
-#endif
-#ifndef PPM_PRIO
-#define PPM_PRIO 1
 #endif
 #ifndef PPM_WPE
 #define PPM_WPE 4
@@ -892,9 +873,6 @@ __device__ __forceinline__ float radius_reduction(unsigned n) {
 #ifndef PPM_CPER
 #define PPM_CPER 4
 #endif
-#ifndef PPM_WAVE_COMPACT  // 1: each wave compacts its own part of a segment, no barriers (below)
-#define PPM_WAVE_COMPACT 1
-#endif
 __global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tiles, int ntiles,
                                                                 const int* list_start,
                                                                 const int* list_end,
@@ -908,8 +886,8 @@ __global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tile
   }
   const int g = tiles[t].x;
   const long long L = list_end[g] - list_start[g];
-  // (PPM_WAVE_COMPACT: twice that, per-wave scratch regions + the contiguous copy)
-  need[t] = L >= min_len ? ((L < seg ? L : (long long)seg) >> shift) * (PPM_WAVE_COMPACT ? 2 : 1) : 0;
+  // (twice that: per-wave scratch regions + the contiguous copy)
+  need[t] = L >= min_len ? ((L < seg ? L : (long long)seg) >> shift) * 2 : 0;
 }
 
 #ifndef PPM_GATE_RUNS  // gate_round (A1): candidates per accept/reject run pair below which (A2) takes over
@@ -918,14 +896,8 @@ __global__ __launch_bounds__(256) void tile_compact_need_kernel(const int2* tile
 #ifndef PPM_GATE_PRIO  // wave priority of the gate waves while they run gate_round
 #define PPM_GATE_PRIO 3
 #endif
-#ifndef PPM_LATE_FETCH  // 1: the next window's records are fetched after its rounds (registers)
-#define PPM_LATE_FETCH 0
-#endif
 #ifndef PPM_PHASE_TIMERS  // 1: per-phase wall-clock timers for CENG795_PPM_DIAG=2 (tools/ppm_diag.sh)
 #define PPM_PHASE_TIMERS 0
-#endif
-#ifndef PPM_WAVE_GATE  // 1: the recurrence of a tile's hit point run by its own wave (gate_round)
-#define PPM_WAVE_GATE 1
 #endif
 
 __device__ __forceinline__ float rr_at(const float* rrtab, int nrr, unsigned n) {
@@ -1186,18 +1158,12 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   // color * photon_flux, and in w the candidate's distance^2 for the gate: negated when its
   // multiplicity exceeds 1 (sign bit: the gate's scalar path), +inf when its normal fails
   __shared__ float4 s_ccf[kChunk + 4];  // (+4: gate_round reads two records ahead)
-  constexpr int kRRStage = PPM_RR_STAGE;  // rr(n) staged per hit point per window (more: computed inline)
-#if PPM_WAVE_GATE
   constexpr int kRRCache = 2 * kPerHp;
   static_assert(kPerHp <= 64 * kGateK, "gate_round: candidates per lane");
   __shared__ float s_grr[kTileHP][kRRCache + kGatePad];  // gate_round: rr(grrb + i), i < kRRCache
   __shared__ float s_gR[kTileHP][kPerHp + 1 + kGatePad];  // gate_round: R(a)
   __shared__ int s_gmulti[kTileHP];  // a candidate of this round has multiplicity > 1
   __shared__ float4 s_gacc[kTileHP][kPerHp + 4];  // gate_round: the accepted records
-  __shared__ __attribute__((aligned(16))) float s_rr[1][4];
-#else
-  __shared__ __attribute__((aligned(16))) float s_rr[kTileHP][kRRStage];
-#endif
   const int tid = (int)threadIdx.x, lane = tid & 63;
 #if PPM_PHASE_TIMERS
   const unsigned long long t_start = S.diag == 2 ? wall_clock64() : 0;
@@ -1224,11 +1190,9 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     s_cnt[tid] = cnt;
   }
   unsigned long long applied = 0, cands = 0;
-  unsigned long long d_max = 0, d_unstaged = 0;  // diag: per hit point, flushed once per tile
   const int list_s = list_start[g], list_e = list_end[g];
   unsigned long long visits = 0, windows = 0;  // 16-B records the filters read; windows run
   __syncthreads();
-#if PPM_WAVE_GATE
   // wave j runs hit point j's recurrence (wave_gate) and keeps its state for the whole tile
   const int gw = tid >> 6;
   float gfx = 0.0f, gfy = 0.0f, gfz = 0.0f, gr2 = 0.0f;
@@ -1248,7 +1212,6 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     for (int i = lane; i < kRRCache; i += 64) s_grr[gw][i] = rr_at(rrtab, nrr, grrb + (unsigned)i);
   }
   const unsigned cnt0 = cnt;  // this thread's hit point's count at the start (tid < nh)
-#endif
   V tp[kTileHP];
 #pragma unroll
   for (int j = 0; j < kTileHP; j++) {
@@ -1276,7 +1239,6 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   int ls = seg, le = seg_e;
   const float4* src = pos;
   visits += (unsigned long long)(seg_e - seg);
-#if PPM_WAVE_COMPACT
   if (compact) {
     // (0) compaction, wave-parallel: wave w streams its own contiguous part of the segment
     // (no barrier until the end), keeping the deposits within any tile hit point's radius at
@@ -1362,91 +1324,6 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     }
     PPM_PHASE(0)
   }
-#else
-  if (compact) {
-    // (0) compaction: rounds of 64 records per thread-row; one count per (record row, wave),
-    // scanned by wave 0, keeps the copy in photon order
-    constexpr int kCW = kUpdThreads / 64;
-    constexpr int kCPer = PPM_CPER;  // records per thread per round (registers: 8 spill)
-    static_assert(kCPer * kCW <= 64, "one count per lane of the scanning wave");
-    __shared__ int s_cc[64], s_cp[65];
-    const long long c0 = cofs[blockIdx.x];
-    const int cap = (int)(cofs[blockIdx.x + 1] - c0);
-    float4* dst = cbuf + c0;
-    const int wave = tid >> 6;
-    float r2c[kTileHP];
-#pragma unroll
-    for (int j = 0; j < kTileHP; j++) r2c[j] = j < nh ? s_r2[j] : -1.0f;
-#if PPM_PHASE_TIMERS
-    const unsigned long long t_c0 = S.diag == 2 && tid == 0 ? wall_clock64() : 0;
-#endif
-    int kept = 0;
-    float4 cd[kCPer];
-    auto cfetch = [&](int base) {
-#pragma unroll
-      for (int q = 0; q < kCPer; q++) {
-        const int k = base + tid + q * kUpdThreads;
-        if (k < le) cd[q] = pos[k];
-      }
-    };
-    cfetch(ls);
-    for (int base = ls; base < le; base += kCPer * kUpdThreads) {
-      float4 cw[kCPer];
-      unsigned rank[kCPer];
-      bool keep[kCPer];
-#pragma unroll
-      for (int q = 0; q < kCPer; q++) cw[q] = cd[q];
-      cfetch(base + kCPer * kUpdThreads);  // next round in flight
-#pragma unroll
-      for (int q = 0; q < kCPer; q++) {
-        const V x = mk(cw[q].x, cw[q].y, cw[q].z);
-        bool kp = false;
-#pragma unroll
-        for (int j = 0; j < kTileHP; j++) {
-          const V v = tp[j] - x;
-          kp = kp || (dot(v, v) <= r2c[j]);
-        }
-        keep[q] = kp && base + tid + q * kUpdThreads < le;
-        const unsigned long long bal = __ballot(keep[q]);
-        rank[q] = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
-                                            __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
-        if (lane == 0) s_cc[q * kCW + wave] = __builtin_popcountll(bal);
-      }
-      __syncthreads();
-      if (tid < 64) {
-        const int v = tid < kCPer * kCW ? s_cc[tid] : 0;
-        int x = v;
-        for (int o = 1; o < 64; o <<= 1) {
-          const int y = __shfl_up(x, o, 64);
-          if (lane >= o) x += y;
-        }
-        s_cp[tid] = x - v;
-        if (tid == 63) s_cp[64] = x;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int q = 0; q < kCPer; q++) {
-        if (!keep[q]) continue;
-        const int idx = kept + s_cp[q * kCW + wave] + (int)rank[q];
-        if (idx < cap) dst[idx] = cw[q];
-      }
-      kept += s_cp[64];
-    }
-    __syncthreads();  // the copy is read by other threads of the workgroup below
-#if PPM_PHASE_TIMERS
-    if (S.diag == 2 && tid == 0) ctick += wall_clock64() - t_c0;
-#endif
-    if (kept <= cap) {
-      src = dst, ls = 0, le = kept;
-      visits += (unsigned long long)kept;
-    }
-    if (stats && tid == 0) {
-      atomicAdd(&stats[kept <= cap ? 20 : 21], 1ull);
-      atomicAdd(&stats[22], (unsigned long long)kept);
-    }
-    PPM_PHASE(0)
-  }
-#endif
   windows += (unsigned long long)((le - ls + kWinMax - 1) / kWinMax);
   float4 dep[kPer];  // position, photon-order index << kRepBits | multiplicity
   auto fetch = [&](int base) {
@@ -1460,12 +1337,6 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
   for (int base = ls; base < le; base += kWinMax) {
     const int total = min(kWinMax, le - base);
     const int nwords = (total + 31) >> 5;
-    // stage rr(n) for the updates this window can make
-    for (int e = tid; !PPM_WAVE_GATE && e < nh * kRRStage; e += kUpdThreads) {
-      const int j = e / kRRStage, t = e % kRRStage;
-      const unsigned n = s_cnt[j] + (unsigned)t;
-      s_rr[j][t] = n < (unsigned)nrr ? rrtab[n] : radius_reduction(n);
-    }
     // (1) superset filter
     float r2w[kTileHP];
 #pragma unroll
@@ -1492,9 +1363,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         }
       }
     }
-#if !PPM_LATE_FETCH
     fetch(base + kWinMax);  // next window in flight
-#endif
     __syncthreads();
     PPM_PHASE(0)
     // (2) candidates per hit point, in photon order: exclusive scan of the per-word counts,
@@ -1532,14 +1401,6 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     PPM_PHASE(3)
     const int ncand = s_wc[nh * nwords];
     cands += (unsigned)ncand;
-#if !PPM_WAVE_GATE
-    const int my_beg = h >= 0 ? s_wc[tid * nwords] : 0;
-    const int my_end = h >= 0 ? (tid + 1 < nh ? s_wc[(tid + 1) * nwords] : ncand) : 0;
-#endif
-    const unsigned cnt_w = cnt;  // count at the window start: rr(n) is staged from there
-#if !PPM_WAVE_GATE
-    unsigned rbase = cnt_w;      // the gate lane's staged rr(n) start (restaged in the gate)
-#endif
     // Rounds of up to kPerHp candidates of EVERY hit point, so that the gate lanes run side by
     // side however the window's candidates are spread over the tile's hit points.
     int most = 0;
@@ -1572,9 +1433,7 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         const float d2 = dot(dv, dv);
         const bool multi = normal_ok && (s_ck[e] & kRepMask) > 1u;
         const float d2c = !normal_ok ? kInf : (multi ? -d2 : d2);
-#if PPM_WAVE_GATE
         if (multi) s_gmulti[j] = 1;
-#endif
         s_ccf[x] = make_float4(cf.x, cf.y, cf.z, d2c);
       }
       __syncthreads();
@@ -1590,7 +1449,6 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
       // batch (it changes nothing; the ones after it are redone with the right rr).  A batch
       // holding a multiplicity > 1, or reaching past the staged rr(n), takes the scalar path
       // for its first candidate.
-#if PPM_WAVE_GATE
       if (gw < nh && S.diag != 1) {
         const int gb = s_wc[gw * nwords];
         const int ge = gw + 1 < nh ? s_wc[(gw + 1) * nwords] : ncand;
@@ -1614,120 +1472,19 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
         __builtin_amdgcn_s_setprio(0);
         if (lane == 0) s_r2[gw] = gr2, s_cnt[gw] = gcnt, s_gmulti[gw] = 0;
       }
-#else
-#if PPM_PRIO
-      if (tid < 64) __builtin_amdgcn_s_setprio(3);  // the gate wave is the tile's critical path
-#endif
-      if (h >= 0 && S.diag != 1) {
-        constexpr int kB = PPM_GATE_B;
-        const int e1 = min(my_end, my_beg + c0 + kPerHp);
-        const int cbase = my_beg + c0 - tid * kPerHp;  // candidate e's record: s_ccf[e - cbase]
-        f32x2 fxy = {flux.x, flux.y}, fzr = {flux.z, r2};
-        int e = my_beg + c0;
-        while (e < e1) {
-          // a window with more updates than the staged rr(n) (long compacted windows): the
-          // lane restages its own row from the table, from a 16-B aligned count
-          if (cnt - rbase + kB > (unsigned)kRRStage && (cnt & ~3u) + kRRStage <= (unsigned)nrr) {
-            rbase = cnt & ~3u;
-            const float4* rt = reinterpret_cast<const float4*>(rrtab + rbase);
-            float4* row = reinterpret_cast<float4*>(&s_rr[tid][0]);
-#pragma unroll 8
-            for (int i = 0; i < kRRStage / 4; i++) row[i] = rt[i];
-          }
-          const int nb = min(kB, e1 - e);
-          const unsigned t = cnt - rbase;
-          bool fast = t + kB <= (unsigned)kRRStage;
-          float d2b[kB], rrb[kB];
-          float4 cb[kB];
-#pragma unroll
-          for (int k = 0; k < kB; k++) {  // one 16-B record per candidate (+ its staged rr)
-            const int ek = min(e + k, e1 - 1);
-            cb[k] = s_ccf[ek - cbase];
-            rrb[k] = s_rr[tid][min(t + (unsigned)k, (unsigned)kRRStage - 1)];
-          }
-#pragma unroll
-          for (int k = 0; k < kB; k++) {
-            fast = fast & ((__float_as_uint(cb[k].w) >> 31) == 0u);  // multiplicity 1
-            d2b[k] = k < nb ? cb[k].w : kInf;
-          }
-          if (fast) {
-            bool alive = true;
-            int used = 0;
-#pragma unroll
-            for (int k = 0; k < kB; k++) {
-              const bool acc = alive && d2b[k] <= fzr.y;
-              const f32x2 rr2 = {rrb[k], rrb[k]};
-              const f32x2 cxy = {cb[k].x, cb[k].y}, cz0 = {cb[k].z, 0.0f};
-              const f32x2 nxy = (fxy + cxy) * rr2, nzr = (fzr + cz0) * rr2;
-              fxy.x = acc ? nxy.x : fxy.x;
-              fxy.y = acc ? nxy.y : fxy.y;
-              fzr.x = acc ? nzr.x : fzr.x;
-              fzr.y = acc ? nzr.y : fzr.y;
-              used += alive ? 1 : 0;  // consumed: accepted, or the first reject
-              cnt += acc ? 1u : 0u;
-              alive = acc;
-            }
-            e += min(used, nb);
-          } else {
-            const float d2 = __builtin_fabsf(cb[0].w);
-            if (d2 <= fzr.y) {
-              const unsigned reps = s_ck[e] & kRepMask;
-              const f32x2 cxy = {cb[0].x, cb[0].y}, cz0 = {cb[0].z, 0.0f};
-              unsigned r = 0;
-              do {
-                const unsigned tt = cnt - rbase;
-                const float rr = tt < (unsigned)kRRStage ? s_rr[tid][tt] : radius_reduction(cnt);
-                cnt++;
-                const f32x2 rr2 = {rr, rr};
-                fxy = (fxy + cxy) * rr2;
-                fzr = (fzr + cz0) * rr2;
-              } while (++r < reps && d2 <= fzr.y);
-            }
-            e++;
-          }
-        }
-        flux = mk(fxy.x, fxy.y, fzr.x);
-        r2 = fzr.y;
-      }
-#if PPM_PRIO
-      if (tid < 64) __builtin_amdgcn_s_setprio(0);
-#endif
-#endif  // PPM_WAVE_GATE
       __syncthreads();
       PPM_PHASE(5)
     }
-    if (h >= 0 && !PPM_WAVE_GATE) {
-      if (S.diag == 2) {  // experiment counters: most updates in one window, unstaged rr(n)
-        const unsigned t_rr = cnt - cnt_w;  // updates made by this hit point in this window
-        d_max = max(d_max, (unsigned long long)t_rr);
-        if (t_rr > kRRStage) d_unstaged += t_rr - kRRStage;
-      }
-      applied += cnt - s_cnt[tid];
-      s_r2[tid] = r2, s_cnt[tid] = cnt;
-    }
-#if PPM_LATE_FETCH
-    fetch(base + kWinMax);  // next window in flight (issued here: nothing is live across the rounds)
-#endif
     __syncthreads();
     PPM_PHASE(5)
   }
   }  // segments
-#if PPM_WAVE_GATE
   if (gw < nh && lane == 0) {
     state[perm[first + gw]] = make_float4(gfx, gfy, gfz, gr2);
     nupd[perm[first + gw]] = gcnt;
   }
   __syncthreads();
   if (h >= 0) applied = s_cnt[tid] - cnt0;
-#endif
-  if (h >= 0 && !PPM_WAVE_GATE) {
-    state[h] = make_float4(flux.x, flux.y, flux.z, r2);
-    nupd[h] = cnt;
-    if (stats && S.diag == 2) {
-      atomicMax(&stats[14], d_max);
-      if (d_unstaged) atomicAdd(&stats[15], d_unstaged);
-    }
-  }
   const unsigned long long tot = wave_sum(applied);
   if (stats && (tid & 63) == 0 && tot) atomicAdd(&stats[3], tot);
   if (stats && tid == 0) {  // the pass's work: (tile, deposit) pairs filtered, candidates
@@ -1740,10 +1497,8 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
     const unsigned long long dur = wall_clock64() - t_start;
     atomicMax(&stats[7], dur);  // longest tile, in wall-clock ticks
     atomicAdd(&stats[23], dur);  // sum over tiles, and of each phase (23..29)
-#if PPM_WAVE_GATE
     atomicAdd(&stats[30], gtick[0]);  // hit point 0's gate_round: (R)+(K), all phases
     atomicAdd(&stats[31], gtick[1]);
-#endif
     for (int i = 0; i < 6; i++) atomicAdd(&stats[24 + i], ph[i]);
     atomicAdd(&stats[32], ctick);
     atomicMax(&stats[33], ctick);
@@ -1796,12 +1551,8 @@ hipError_t launch_grid(const PHitPoint* hps, int n, int w, int h, PGrid* grid, f
 hipError_t launch_photons(const PScene& S, unsigned long long seed, long long first, int count,
                           int K, PDeposit* slots, int* ndep, unsigned long long* stats,
                           hipStream_t st) {
-#if PPM_REFILL
   // workgroups of a contiguous photon range each (2048: 3.99 ms, 4096: 3.72 ms on C5)
   const int blocks = std::min(blocks_for(count), PPM_PHOTON_BLOCKS);
-#else
-  const int blocks = blocks_for(count);
-#endif
   if (blocks <= 0) return hipSuccess;
   hipLaunchKernelGGL(photon_kernel, dim3(blocks), dim3(kThreads), 0, st, S, seed,
                      first, count, K, slots, ndep, stats);
