@@ -376,14 +376,17 @@ def cold_frame_ms(scene, frames: int = 3):
     return round(sorted(out)[len(out) // 2], 4)
 
 
-def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8)):
+def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange: str = "rgb",
+                split: str = "bands"):
     """Prediction of strong scaling on one GPU (no N-GPU node needed).  t1 = the whole frame
     rendered in place with `inflight` frames in flight, and for each N every rank r's share of
     the N-way block deal (tile_begin r, tile_step N, tile-major, the same frames in flight) alone
     on this GPU — ALL timed over the same `steps` steps after the same warm-up, with one set of
     render streams (each rank of an N-GPU run creates its streams in a fresh process).  The N-GPU
-    step can be no shorter than the slowest share: t1 / (N * max_r t_share) bounds the
-    efficiency from above (the gather to rank 0 and its untile are not included)."""
+    step can be no shorter than the slowest share, nor than rank 0's share plus its assembly of
+    the others' (the RGB untile, or the records' resolve with exchange="records"): t1 / (N *
+    that step) bounds the efficiency from above (the link transfer, overlapped with the
+    rendering of the frames in flight, is reported in bytes, not timed)."""
     from ceng795_amd import dist_tiles
     streams = dist_tiles.render_streams(inflight)  # one set for every run (pool streams)
 
@@ -397,29 +400,244 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8)):
 
     one = dist_tiles.FrameRenderer(scene, stream, inflight=inflight, streams=streams)
     t1 = timed(one)
+    records = exchange == "records" and dist_tiles.records_ok(scene)
+    costs = dist_tiles.measure_tile_costs(scene)
     out = {}
     for n in ns:
+        # the band split (bench default): each rank's cost-balanced row band alone, in place;
+        # rank 0 receives the others' bands into its frame (no extra kernel there)
+        plan = dist_tiles.BandRenderPlan(scene, n, 0, dist_tiles.BandPlan.from_costs(
+            [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)],
+            n, 0, costs).cuts)
+        bands = [timed(BandProbe(scene, plan, r, stream, inflight, streams)) for r in range(n)]
+        bc = plan.band_costs(costs)
+        band = {"band_ms_per_rank": [round(x, 4) for x in bands],
+                "band_ms_max": round(max(bands), 4),
+                "band_cost_max_over_mean": round(float(bc.max() / bc.mean()), 4),
+                "band_tile_row_cuts": plan.cuts[0] if len(plan.cuts) == 1 else plan.cuts,
+                "predicted_efficiency": round(t1 / (n * max(bands)), 4),
+                "peer_link_MB_per_step_max": round(max(
+                    12 * sum((b.y1 - b.y0) * plan.sizes[b.camera][0] for b in plan.per_rank[r])
+                    for r in range(1, n)) / 1e6, 3)}
+        # ranks > 0 render what the N-GPU bench exchanges (RGB or pixel records); rank 0's
+        # share is the same tile work (it renders in place)
         per = [timed(dist_tiles.ShareRenderer(scene, n, r, stream, inflight=inflight,
-                                              streams=streams))
+                                              streams=streams, records=records and r > 0))
                for r in range(n)]
-        slow = max(per)
-        out[str(n)] = {"share_ms_max": round(slow, 4), "share_ms_min": round(min(per), 4),
+        # rank 0 also assembles the other ranks' shares into its frame: the RGB untile
+        # (rt_untile_device) or the records' shading (rt_resolve_device) — both timed
+        untile = timed(ResolveProbe(scene, n, stream, inflight, streams, records=False))
+        resolve = (timed(ResolveProbe(scene, n, stream, inflight, streams, records=True))
+                   if dist_tiles.records_ok(scene) else None)
+        root = resolve if records else untile
+        slow = max(max(per), per[0] + root)
+        L = dist_tiles.TilePlan(scene, n, 0)
+        link = sum(sh.slot for sh in L.shares) * 64 * 4  # bytes per peer per step, per 4 B/px
+        tiles = {"share_ms_max": round(max(per), 4), "share_ms_min": round(min(per), 4),
                        "share_ms_per_rank": [round(x, 4) for x in per],
-                       "predicted_efficiency": round(t1 / (n * slow), 4),
-                       "predicted_Mrays_s_factor": round(t1 / slow, 3)}
+                       "root_untile_ms": round(untile, 4),
+                       "root_resolve_ms": None if resolve is None else round(resolve, 4),
+                       "peer_link_MB_per_step": {"rgb": round(3 * link / 1e6, 3),
+                                                 "records": round(link / 1e6, 3)},
+                       "predicted_step_ms": round(slow, 4),
+                       "predicted_efficiency": round(t1 / (n * slow), 4)}
+        step = max(bands) if split == "bands" else slow
+        out[str(n)] = {"split": split, "predicted_step_ms": round(step, 4),
+                       "predicted_efficiency": round(t1 / (n * step), 4),
+                       "predicted_Mrays_s_factor": round(t1 / step, 3),
+                       "bands": band, "tiles": tiles}
     cam = scene.camera(0)
     return {"frame": f"{cam.width}x{cam.height}", "t1_ms": round(t1, 4), "steps": steps,
-            "frames_in_flight": inflight, "per_n": out,
-            "note": "PREDICTION from one GPU: t1 and each rank's block share of one frame timed "
-                    "over the same number of steps with the same frames in flight and render "
-                    "streams; t1 / (N * slowest share); the exchange to rank 0 and its untile "
-                    "are not included"}
+            "frames_in_flight": inflight, "split": split,
+            "tiles_exchange": "records" if records else "rgb",
+            "per_n": out,
+            "note": "PREDICTION from one GPU: t1 and every rank's work of one frame, timed over "
+                    "the same number of steps with the same frames in flight and render streams. "
+                    "bands (the bench's N>1 split): each rank's cost-balanced row band in place; "
+                    "step = the slowest band.  tiles: each rank's block share, plus rank 0's "
+                    "untile (or resolve of pixel records) of the others; step = max(slowest "
+                    "share, rank 0's share + untile).  Efficiency t1 / (N * step); the transfer "
+                    "to rank 0 (MB per xGMI link per step, overlapped with the rendering of the "
+                    "frames in flight) is not included"}
+
+
+class BandProbe:
+    """Rank r's bands of a BandPlan rendered in place (no exchange): the per-rank render work of
+    the band split, on one GPU."""
+
+    def __init__(self, scene, plan, r, stream, inflight, streams):
+        import torch
+        from ceng795_amd import dist_tiles
+        self.scene, self.stream, self.streams = scene, stream, streams
+        self.bands = plan.per_rank[r]
+        self.render = dist_tiles.scene_band_renderer(scene)
+        self.frames = [[torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
+                        for (w, h) in plan.sizes] for _ in range(inflight)]
+        for st in streams:
+            st.wait_stream(stream)
+        self.k = 0
+
+    def step(self, events=None):
+        s = self.k % len(self.streams)
+        self.k += 1
+        for c, b in enumerate(self.bands):
+            if b.rows > 0:
+                self.render(b, self.frames[s][c], self.streams[s])
+
+    def finish(self):
+        for st in self.streams:
+            self.stream.wait_stream(st)
+
+
+class ResolveProbe:
+    """Rank 0's shading of the other n-1 ranks' pixel records (rt_resolve_device with skip_root,
+    every camera), on records rendered once beforehand: the exchange's extra GPU work on rank 0
+    (records=False: the RGB untile, rt_untile_device, instead)."""
+
+    def __init__(self, scene, n, stream, inflight, streams, records=True):
+        import torch
+        from ceng795_amd import dist_tiles
+        self.scene, self.stream = scene, stream
+        self.layout = L = dist_tiles.TilePlan(scene, n, 0)
+        self.streams = streams
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.gathered = []
+        for c, sh in enumerate(L.shares):
+            g = torch.zeros((n, sh.slot, dist_tiles.TILE_RECORDS if records else
+                             dist_tiles.TILE_FLOATS), dtype=torch.float32, device=dev)
+            for r in range(1, n):
+                sr = L.per_rank[r][c]
+                if sr.count:
+                    scene.render_device(c, g[r].data_ptr(), tile_begin=sr.tile_begin,
+                                        tile_step=sr.tile_step, tile_major=True,
+                                        blocks=sr.blocks, records=records,
+                                        stream=torch.cuda.current_stream().cuda_stream)
+            self.gathered.append(g)
+        self.frames = [[torch.empty((h, w, 3), dtype=torch.float32, device=dev)
+                        for (w, h) in L.sizes] for _ in range(inflight)]
+        torch.cuda.synchronize()
+        self.untile = dist_tiles.scene_tile_untiler(scene, L, records=records)
+        for st in streams:
+            st.wait_stream(stream)
+        self.k = 0
+
+    def step(self, events=None):
+        s = self.k % len(self.streams)
+        self.k += 1
+        st = self.streams[s]
+        for c in range(len(self.gathered)):
+            self.untile(c, self.gathered[c], self.frames[s][c], st, skip_root=True)
+
+    def finish(self):
+        for st in self.streams:
+            self.stream.wait_stream(st)
+
+
+def band_bytes(plan) -> int:
+    """Bytes rank 0 receives per step in the band split: the other ranks' bands as fp32 RGB."""
+    return int(sum(12 * (b.y1 - b.y0) * plan.sizes[b.camera][0]
+                   for r in range(1, plan.world) for b in plan.per_rank[r]))
+
+
+def band_exchange_text(world, comm, renderer, band_costs):
+    import numpy as np
+    plan = renderer.plan
+    txt = ("rank 0 renders its row band in place; batch_isend_irecv (RCCL send / receive) of "
+           "the other ranks' bands straight into rank 0's frame rows (no untile)" if world > 1
+           else "one-rank rehearsal: rank 0's row band through an RCCL self send / receive pair "
+                "(batch_isend_irecv) into the frame")
+    out = {"how": txt + ("" if comm == "rccl" else " (gloo: through host copies)"),
+           "band_tile_row_cuts": plan.cuts}
+    if band_costs is not None and len(band_costs) > 1:
+        out["band_cost_max_over_mean"] = round(float(max(band_costs) / np.mean(band_costs)), 4)
+    return out
+
+
+def renderer_records(renderer) -> bool:
+    return getattr(renderer, "tile_words", 0) == 64
+
+
+def exchange_bytes(renderer) -> int:
+    """Bytes rank 0 receives per step in the tile split: every other rank's slots."""
+    L = renderer.layout
+    return int(4 * renderer.tile_words * sum(sh.slot for sh in L.shares) * (L.world - 1))
 
 
 def synthetic_frame(w: int, h: int, seed: int = 795):
     """Stand-in framebuffer for the CPU rehearsal: deterministic fp32 values per pixel."""
     import numpy as np
     return np.random.default_rng(seed).standard_normal((h, w, 3)).astype(np.float32)
+
+
+def cpu_rehearsal_bands(args, truth, world, rank, desc) -> int:
+    """cpu_rehearsal of the band split: bands cut from a synthetic cost map (the frame's own
+    values per tile, so the bands are uneven), each rank's band copied from the synthetic frame
+    into its frame instead of rendered, the BandGatherRenderer exchange over gloo, and rank 0's
+    frame checked bit for bit."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from ceng795_amd import dist_tiles
+    h, w, _ = truth.shape
+    tx, ty = dist_tiles.tiles_of((w, h))
+    pad = np.zeros((ty * 8, tx * 8), np.float64)
+    pad[:h, :w] = np.abs(truth).sum(2)
+    costs = pad.reshape(ty, 8, tx, 8).sum((1, 3)).reshape(-1) + 1.0
+    plan = dist_tiles.BandPlan.from_costs([(w, h)], world, rank, [costs])
+    src = torch.from_numpy(truth)
+    rendered = []
+
+    def render(b, frame, stream):
+        rendered.append(b.y1 - b.y0)
+        frame[b.y0:b.y1].copy_(src[b.y0:b.y1])
+
+    R = dist_tiles.BandGatherRenderer(plan, None, render, host_staging=True, device="cpu")
+    for _ in range(args.warmup):
+        R.step()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frames = R.step()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    b = plan.bands[0]
+    assert sum(rendered) == (args.warmup + args.steps) * (b.y1 - b.y0)
+    if rank == 0:
+        ok = bool(np.array_equal(frames[0].numpy().view(np.uint32), truth.view(np.uint32)))
+        print(json.dumps({"metric": "cpu rehearsal of the N>1 exchange (no rendering)",
+                          "value": round(w * h * args.steps / float(el.item()) / 1e6, 3),
+                          "unit": "Mpixels/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "scaling": "strong",
+                          "data": "synthetic frame, cpu-rehearsal",
+                          "config": {"workload": desc, "parallelism": f"bands{world}+gloo_p2p",
+                                     "band_cuts": plan.cuts[0],
+                                     "band_costs": [round(x, 1) for x in plan.band_costs([costs])],
+                                     "gather_verified": ok}}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0
+
+
+def band_cuts_for(scene, world: int, rank: int, coll_dev: str):
+    """Rank 0 measures every camera's tile costs (whole frames on this GPU) and cuts the bands;
+    the cuts are broadcast so every rank holds the same plan.  Returns (cuts, tile costs or None)."""
+    import torch
+    import torch.distributed as dist
+    from ceng795_amd import dist_tiles
+    sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
+    costs = None
+    flat = []
+    if rank == 0:
+        costs = dist_tiles.measure_tile_costs(scene)
+        plan = dist_tiles.BandPlan.from_costs(sizes, world, 0, costs)
+        flat = [x for cc in plan.cuts for x in cc]
+    t = torch.tensor(flat if rank == 0 else [0] * (len(sizes) * (world + 1)),
+                     dtype=torch.int64, device=coll_dev)
+    if world > 1:
+        dist.broadcast(t, 0)
+    v = t.cpu().tolist()
+    return [v[c * (world + 1):(c + 1) * (world + 1)] for c in range(len(sizes))], costs
 
 
 def cpu_rehearsal(args) -> int:
@@ -441,6 +659,8 @@ def cpu_rehearsal(args) -> int:
     dist.init_process_group("gloo")
     _, w, h, desc = WORKLOADS[args.workload]
     truth = synthetic_frame(w, h)
+    if args.split == "bands":
+        return cpu_rehearsal_bands(args, truth, world, rank, desc)
     L = dist_tiles.TileLayout([(w, h)], world, rank)
     tx, ty = dist_tiles.tiles_of((w, h))
     pad = np.zeros((ty * 8, tx * 8, 3), np.float32)
@@ -510,13 +730,21 @@ def main() -> int:
                     help="frames (cameras) per step; --split tiles deals their tiles over the "
                          "ranks (strong scaling at 1 frame), --split frames gives each rank "
                          "whole frames (default then: one per rank)")
-    ap.add_argument("--split", default="tiles", choices=["tiles", "frames"])
+    ap.add_argument("--split", default="bands", choices=["bands", "tiles", "frames"],
+                    help="N>1: bands = each frame cut into one row band per rank at measured-"
+                         "cost-balanced cuts, received by rank 0 straight into its frame; tiles = "
+                         "2x2 tile blocks dealt round-robin, gathered and untiled by rank 0; "
+                         "frames = whole frames per rank (weak scaling)")
     ap.add_argument("--no-weak", action="store_true",
                     help="N>1: skip the extra weak-scaling measurement (one frame per rank)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--gather-stream", choices=("render", "comm"), default="render",
                     help="N>1 tile split: enqueue a step's gather + untile on its own render "
                          "stream (default) or on one communication stream")
+    ap.add_argument("--exchange", choices=("rgb", "records"), default="rgb",
+                    help="N>1 tile split: the shares travel as fp32 RGB (12 B per pixel, untiled "
+                         "by rank 0) or as 32-bit pixel records (4 B, shaded by rank 0: a third "
+                         "of the link bytes for rank 0 re-reading the hit primitives)")
     ap.add_argument("--root-gather", action="store_true",
                     help="N>1 tile split: rank 0 renders its share tile-major and gathers it "
                          "with the others (default: in place, point-to-point receives only)")
@@ -604,7 +832,8 @@ def main() -> int:
         args.frames = world
     n_cams = max(1, args.frames)
     tiled = use_pg and args.split == "tiles"
-    strong = tiled and n_cams < world  # one frame (or a few) split over more ranks
+    banded = use_pg and args.split == "bands"
+    strong = (tiled or banded) and n_cams < world  # one frame (or a few) split over more ranks
     if rank == 0:
         xml = scene_path(args.workload, n_cams)
     if world > 1:
@@ -616,19 +845,35 @@ def main() -> int:
         f"BVH depth {scene.bvh_depth}")
     stream = torch.cuda.current_stream()
     dev = torch.device("cuda", device)
+    band_costs = None
     if not use_pg:
         renderer = dist_tiles.FrameRenderer(scene, stream, inflight=args.inflight)
+    elif banded:
+        cuts, costs = band_cuts_for(scene, world, rank, coll_dev)
+        plan = dist_tiles.BandRenderPlan(scene, world, rank, cuts)
+        if costs is not None:
+            band_costs = plan.band_costs(costs)
+        renderer = dist_tiles.BandGatherRenderer(
+            plan, stream, dist_tiles.scene_band_renderer(scene), inflight=args.inflight,
+            host_staging=host_staging, device=dev,
+            # one-rank rehearsal: rank 0's band through a real RCCL self send / receive
+            self_exchange=args.gather_rehearsal and world == 1)
     elif tiled:
         layout = dist_tiles.TilePlan(scene, world, rank)
+        # shares travel as 32-bit pixel records (a third of RGB's bytes) where the scene allows;
+        # rank 0 shades them into the frame (rt_resolve_device)
+        records = (not host_staging and args.exchange == "records"
+                   and dist_tiles.records_ok(scene))
         renderer = dist_tiles.TileGatherRenderer(
-            layout, stream, dist_tiles.scene_tile_renderer(scene), inflight=args.inflight,
+            layout, stream, dist_tiles.scene_tile_renderer(scene, records), inflight=args.inflight,
             host_staging=host_staging, device=dev,
-            untile=None if host_staging else dist_tiles.scene_tile_untiler(scene, layout),
+            untile=None if host_staging else dist_tiles.scene_tile_untiler(scene, layout, records),
             gather_stream=args.gather_stream,
             render_inplace=None if (host_staging or args.root_gather)
             else dist_tiles.scene_inplace_renderer(scene),
             # one-rank rehearsal: rank 0's share through a real RCCL self send / receive + untile
-            self_exchange=args.gather_rehearsal and world == 1)
+            self_exchange=args.gather_rehearsal and world == 1,
+            tile_words=dist_tiles.TILE_RECORDS if records else dist_tiles.TILE_FLOATS)
     else:
         owners = dist_tiles.FrameOwners(n_cams, world, rank)
         sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
@@ -753,12 +998,14 @@ def main() -> int:
                 single = one_frame_ms(scene, stream, max(10, args.steps // 2))
                 cold = cold_frame_ms(scene)
                 if not args.no_share_probe:
-                    probe = share_probe(scene, stream, max(20, args.steps), args.inflight)
+                    probe = share_probe(scene, stream, max(20, args.steps), args.inflight,
+                                        exchange=args.exchange, split=args.split)
                     if args.workload == "c3":
                         # the north star's 8-GPU configuration: C4 (3840x2160), same mesh
                         with ceng795_amd.Scene(scene_path("c4", 1), device=device,
                                                traversal=args.traversal) as s4:
-                            probe_c4 = share_probe(s4, stream, max(20, args.steps), args.inflight)
+                            probe_c4 = share_probe(s4, stream, max(20, args.steps), args.inflight,
+                                               exchange=args.exchange, split=args.split)
             except Exception as e:
                 log(f"one-frame / share probe failed: {e!r}")
         host_rate = None
@@ -788,19 +1035,26 @@ def main() -> int:
                        "triangles": 2 * (n - 1) ** 2, "rays_per_step": int(rays_step),
                        "traversal": args.traversal,
                        "parallelism": (f"tiles{world}+{comm}_gather" if tiled else
+                                       f"bands{world}+{comm}_p2p" if banded else
                                        f"frames{world}+{comm}_gather" if use_pg else "frames1"),
                        "frames_in_flight": renderer.inflight,
                        "dispatch": "heavy-first per XCD region; the primary kernel by the tile "
                                    "costs of the previous frame on its stream (warm order, "
                                    "DESIGN.md 4.8), every frame's rays all traced",
                        "gather_verified": verified,
-                       "exchange": None if not tiled else (
-                           "dist.gather (RCCL) of every rank's tile-major share, whole-frame untile"
-                           if args.root_gather or host_staging else
-                           "rank 0 in place + batch_isend_irecv (RCCL send / receive) of the other "
-                           "ranks' shares, untile around rank 0's units" if world > 1 else
-                           "one-rank rehearsal: rank 0's tile-major share through an RCCL self "
-                           "send / receive pair (batch_isend_irecv), whole-frame untile"),
+                       "exchange": band_exchange_text(world, comm, renderer, band_costs)
+                       if banded else None if not tiled else (
+                           ("dist.gather (RCCL) of every rank's tile-major share, whole-frame untile"
+                            if args.root_gather or host_staging else
+                            "rank 0 in place + batch_isend_irecv (RCCL send / receive) of the other "
+                            "ranks' shares, untile around rank 0's units" if world > 1 else
+                            "one-rank rehearsal: rank 0's tile-major share through an RCCL self "
+                            "send / receive pair (batch_isend_irecv), whole-frame untile")
+                           + ("; shares as 32-bit pixel records (hit primitive + shadow bits, "
+                              "4 B per pixel) shaded on rank 0 (rt_resolve_device)"
+                              if renderer_records(renderer) else "; shares as fp32 RGB")),
+                       "exchange_bytes_per_step": (exchange_bytes(renderer) if tiled else
+                                                   band_bytes(renderer.plan) if banded else None),
                        "render_ms_avg": round(sum(render_ms) / len(render_ms), 4) if ev else None,
                        "timed_region": "the steps alone: no timing events inside it (kernel "
                                        "and one-frame times are measured after it)",

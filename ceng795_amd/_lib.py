@@ -96,6 +96,10 @@ SIGNATURES = {
                                    C.c_int, C.c_void_p, C.c_void_p]),
     "rt_render_device_range": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                          C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
+    "rt_scene_records_ok": (C.c_int, [C.c_void_p, C.c_int]),
+    "rt_tile_costs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
+    "rt_resolve_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                    C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     "rt_set_kernel_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "rt_read_kernel_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_double),
                                        C.POINTER(C.c_longlong)]),
@@ -136,7 +140,7 @@ def _share_torch_hip_runtime() -> None:
         pass
 
 
-ABI_VERSION = 4  # CENG795_RT_ABI_VERSION of include/ceng795_rt.h
+ABI_VERSION = 6  # CENG795_RT_ABI_VERSION of include/ceng795_rt.h
 
 
 def lib() -> C.CDLL:

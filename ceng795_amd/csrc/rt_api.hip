@@ -28,6 +28,8 @@ hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevP
 int max_supported_depth();
 hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream);
 hipError_t launch_untile(const UntileParams& U, hipStream_t stream);
+hipError_t launch_resolve(const RenderParams& P, const UntileParams& U, bool spheres,
+                          hipStream_t stream);
 unsigned long long read_reset_exact_fallbacks();
 hipError_t launch_quot_check(unsigned long long seed, long long count, unsigned long long* counts,
                              hipStream_t stream);
@@ -453,6 +455,7 @@ RenderParams make_params(const rt_scene* s, const Replica& r, int cam, int row0,
   const int sel_units = tile_begin < units ? (units - tile_begin + tile_step - 1) / tile_step : 0;
   P.num_sel_tiles = P.block_deal ? 4 * sel_units : sel_units;
   P.tile_major = tile_major & RT_TILE_MAJOR;
+  P.records = (tile_major & RT_TILE_RECORDS) ? 1 : 0;
   P.out = out;
   P.occ_words = occ_words(h);
   P.counters = counters;
@@ -467,6 +470,13 @@ void limit_rows(RenderParams& P, int rows) {
   P.num_sel_tiles = P.tile_begin < P.tiles_total
                         ? (P.tiles_total - P.tile_begin + P.tile_step - 1) / P.tile_step
                         : 0;
+}
+
+// Pixel records (RT_TILE_RECORDS) carry the primary hit and up to kRecMaxLights shadow bits:
+// pixel-centre cameras of scenes without mirror/dielectric recursion.
+bool records_ok(const rt_scene* s, int cam) {
+  return s->host.cameras[cam].num_samples <= 1 && !s->needs_recursion &&
+         (int)s->host.lights.size() <= kRecMaxLights;
 }
 
 void check_render_args(const rt_scene* s, int cam, int row0, int row_stride) {
@@ -802,8 +812,10 @@ void render_multi_msaa(rt_scene* s, CtxSet& cx, int cam, float* d_frame, hipStre
 // stream s0.  The frame's 2x2-tile blocks are dealt round-robin over the D devices in deal
 // order (the reference's row interleave over threads, HW2/main.cpp:33-36, at block
 // granularity; block d -> device d mod D, deal_block_tile); each device renders its blocks
-// tile-major into a slot of 4 ceil(B / D) tiles on its context's stream; one RCCL group of send / receive pairs (single process, one communicator
-// per device) gathers the slots onto the first device, whose untile kernel writes the rows.
+// tile-major into a slot of 4 ceil(B / D) tiles on its context's stream — as 32-bit pixel
+// records where records_ok (a third of RGB's bytes), else RGB; one RCCL group of send / receive
+// pairs (single process, one communicator per device) gathers the slots onto the first device,
+// whose resolve kernel shades the records into the rows (or untile kernel copies the RGB).
 // Counters: `per_call` adds each device's rays to its context's counters (rt_render's stats),
 // else to the replica's (rt_collect_stats).  Caller holds s->multi_mu.
 void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, float* d_frame,
@@ -814,6 +826,9 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
   if (tp.tiles_total == 0) return;
   const int blocks = deal_blocks(tp.tiles_x, tp.tiles_total / tp.tiles_x);
   const int slot = 4 * ((blocks + D - 1) / D);  // tiles: whole 2x2 blocks (block deal)
+  // the other devices' shares travel as 32-bit pixel records where the scene allows, else as RGB
+  const bool records = records_ok(s, cam);
+  const size_t tile_words = records ? (size_t)kTile * kTile : (size_t)kTileFloats;
   RenderCtx* x0 = cx.x[0];
   {
     DeviceGuard g(s->rep[0]->device);
@@ -829,16 +844,17 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
     // copy gather: the previous frame's peer copy out of d_out (on the first device's stream)
     // has finished before this frame renders into it
     if (d > 0 && s->copy_gather) hip_check(hipStreamWaitEvent(x->stream, x0->ev_gathered, 0), "wait event");
-    if (d > 0) ensure(x->d_out, x->out_floats, (size_t)slot * kTileFloats, "alloc tile slot");
+    if (d > 0) ensure(x->d_out, x->out_floats, (size_t)slot * tile_words, "alloc tile slot");
     RenderParams P = make_params(s, r, cam, row0, row_stride, d, D,
-                                 d == 0 ? RT_TILE_BLOCKS : RT_TILE_MAJOR | RT_TILE_BLOCKS,
+                                 d == 0 ? RT_TILE_BLOCKS
+                                        : RT_TILE_MAJOR | RT_TILE_BLOCKS | (records ? RT_TILE_RECORDS : 0),
                                  d == 0 ? d_frame : x->d_out, per_call ? x->d_cnt : r.d_counters);
     bind_ctx(s, x, P, c);
     enqueue_frame(s, r, P, 1, nullptr, x->stream, d == 0);
   }
   DeviceGuard g(s->rep[0]->device);
-  ensure(x0->d_recv, x0->recv_floats, (size_t)D * slot * kTileFloats, "alloc gathered slots");
-  const size_t count = (size_t)slot * kTileFloats;
+  ensure(x0->d_recv, x0->recv_floats, (size_t)D * slot * tile_words, "alloc gathered slots");
+  const size_t count = (size_t)slot * tile_words;  // 4-B words (floats or pixel records)
   if (D == 1) {
     // nothing to gather: the one device rendered the frame in place
   } else if (s->copy_gather) {
@@ -880,7 +896,14 @@ void render_multi(rt_scene* s, CtxSet& cx, int cam, int row0, int row_stride, fl
   U.blocks = 1;
   U.skip_root = 1;  // the first device's blocks are already in d_frame
   U.vec = untile_vec(U);
-  if (D > 1) hip_check(launch_untile(U, x0->stream), "untile launch");
+  if (D > 1 && records) {  // the others' pixel records shaded into the frame
+    const RenderParams P0 = make_params(s, *s->rep[0], cam, row0, row_stride, 0, 1, 0, d_frame,
+                                        nullptr);
+    U.vec = 0;
+    hip_check(launch_resolve(P0, U, s->has_spheres, x0->stream), "resolve launch");
+  } else if (D > 1) {
+    hip_check(launch_untile(U, x0->stream), "untile launch");
+  }
   if (s0 != x0->stream) {
     hip_check(hipEventRecord(x0->ev_out, x0->stream), "event record");
     hip_check(hipStreamWaitEvent(s0, x0->ev_out, 0), "wait event");
@@ -1138,8 +1161,14 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
                            void* stream) {
   return guarded([&] {
     check_render_args(s, cam, row0, row_stride);
-    if (tile_begin < 0 || tile_step < 1 || !d_out || (tile_major & ~(RT_TILE_MAJOR | RT_TILE_BLOCKS)))
+    if (tile_begin < 0 || tile_step < 1 || !d_out ||
+        (tile_major & ~(RT_TILE_MAJOR | RT_TILE_BLOCKS | RT_TILE_RECORDS)))
       throw std::invalid_argument("rt_render_device: bad tile selection / output");
+    if ((tile_major & RT_TILE_RECORDS) && !(tile_major & RT_TILE_MAJOR))
+      throw std::invalid_argument("rt_render_device: RT_TILE_RECORDS needs RT_TILE_MAJOR");
+    if ((tile_major & RT_TILE_RECORDS) && !records_ok(s, cam))
+      throw std::domain_error("rt_render_device: pixel records need a pixel-centre camera, no "
+                              "mirror/dielectric recursion and at most 4 lights");
     const rt_camera& c = s->host.cameras[cam];
     if (s->multi) {
       // a multi-device scene renders whole frames (rows subsets allowed) split over its devices
@@ -1223,6 +1252,77 @@ int rt_untile_device(rt_scene* s, int cam, int row0, int row_stride, int devices
     U.skip_root = (flags & RT_UNTILE_SKIP_ROOT) ? 1 : 0;
     U.vec = untile_vec(U);
     hip_check(launch_untile(U, (hipStream_t)stream), "untile launch");
+    return RT_OK;
+  });
+}
+
+int rt_tile_costs(rt_scene* s, void* stream, unsigned* host_out, int capacity) {
+  if (!s || !host_out || capacity < 0) return set_error(RT_E_INVALID, "rt_tile_costs: bad argument");
+  return guarded([&]() -> int {
+    if (s->multi) throw std::domain_error("rt_tile_costs: single-device scenes only");
+    Replica& r = *s->rep[0];
+    DeviceGuard g(r.device);
+    StreamScratch* x = nullptr;
+    std::unique_lock<std::mutex> held;
+    {
+      std::lock_guard<std::mutex> lk(r.mu);
+      for (auto& p : r.streams)
+        if (p->stream == stream) x = p.get();
+      if (x) held = std::unique_lock<std::mutex>(x->mu);
+    }
+    if (!x || !x->order_valid)
+      throw std::domain_error("rt_tile_costs: no ordered frame was rendered on this stream");
+    const long long n = x->order_key[5];  // the last selection's tiles
+    if (n > capacity) throw std::invalid_argument("rt_tile_costs: capacity below the frame's tiles");
+    hip_check(hipStreamSynchronize((hipStream_t)stream), "synchronize stream");
+    hip_check(hipMemcpy(host_out, x->sched + sched_snap_offset((unsigned long long)n),
+                        (size_t)n * sizeof(unsigned), hipMemcpyDeviceToHost),
+              "read tile costs");
+    return (int)n;
+  });
+}
+
+int rt_scene_records_ok(const rt_scene* s, int cam) {
+  if (!s || cam < 0 || cam >= (int)s->host.cameras.size())
+    return set_error(RT_E_INVALID, "rt_scene_records_ok: bad argument");
+  return records_ok(s, cam) ? 1 : 0;
+}
+
+int rt_resolve_device(rt_scene* s, int cam, int row0, int row_stride, int devices, int slot,
+                      int tile_offset, int flags, const unsigned* d_gathered, float* d_out,
+                      void* stream) {
+  return guarded([&] {
+    check_render_args(s, cam, row0, row_stride);
+    if (devices < 1 || slot < 0 || tile_offset < 0 || !d_gathered || !d_out ||
+        (flags & ~(RT_UNTILE_BLOCKS | RT_UNTILE_SKIP_ROOT)) ||
+        ((flags & RT_UNTILE_BLOCKS) && slot % 4))
+      throw std::invalid_argument("rt_resolve_device: bad argument");
+    if (!records_ok(s, cam)) throw std::domain_error("rt_resolve_device: no pixel records here");
+    const rt_camera& c = s->host.cameras[cam];
+    const TilePlan tp = plan(c, row0, row_stride);
+    const int blocks = (flags & RT_UNTILE_BLOCKS) ? 1 : 0;
+    const long long units = blocks ? deal_blocks(tp.tiles_x, tp.tiles_total / tp.tiles_x) : tp.tiles_total;
+    if ((long long)devices * (blocks ? slot / 4 : slot) < units)
+      throw std::invalid_argument("rt_resolve_device: devices * slot is smaller than the frame's share");
+    Replica& r = *s->rep[0];
+    DeviceGuard g(r.device);
+    const RenderParams P = make_params(s, r, cam, row0, row_stride, 0, 1, 0, d_out, nullptr);
+    UntileParams U;
+    U.recv = reinterpret_cast<const float*>(d_gathered);
+    U.out = d_out;
+    U.width = c.width;
+    U.row0 = row0;
+    U.row_stride = row_stride;
+    U.rows = tp.rows;
+    U.tiles_x = tp.tiles_x;
+    U.tiles_total = tp.tiles_total;
+    U.devices = devices;
+    U.slot = slot;
+    U.tile_offset = tile_offset % devices;
+    U.blocks = blocks;
+    U.skip_root = (flags & RT_UNTILE_SKIP_ROOT) ? 1 : 0;
+    U.vec = 0;
+    hip_check(launch_resolve(P, U, s->has_spheres, (hipStream_t)stream), "resolve launch");
     return RT_OK;
   });
 }

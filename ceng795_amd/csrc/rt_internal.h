@@ -171,6 +171,18 @@ struct MsaaResolveParams {
 #define RT_HD
 #endif
 
+// Pixel record (rt_render_device with RT_TILE_RECORDS; rt_resolve_device): what a share of a
+// multi-GPU frame sends to the gathering rank instead of 12 B of colour — the primary hit's DFS
+// leaf index (bits 0..25) and the shadow bits of lights 0..3 (bits 26..29); or a miss (the
+// background) or a pixel outside the image.  The gathering rank re-derives the hit's t with the
+// same intersection arithmetic (bit for bit) and shades it there.
+constexpr unsigned kRecLeafMask = (1u << 26) - 1u;
+constexpr int kRecLightShift = 26;
+constexpr unsigned kRecLightMask = 15u;  // lights 0..3
+constexpr int kRecMaxLights = 4;
+constexpr unsigned kRecMiss = 1u << 30;
+constexpr unsigned kRecOutside = 2u << 30;
+
 // Block deal (rt_render_device with RT_TILE_BLOCKS, multi-device frames): the unit dealt over
 // devices is a 2x2 block of tiles (the traversal workgroup's unit, so a share keeps the
 // in-place frame's coherence), numbered with each block row rotated by its row index —
@@ -207,8 +219,10 @@ struct UntileParams {
 };
 
 // Words of the per-stream schedule buffer for a launch of `tiles` selected tiles: tile costs
-// + the unit order lists (order_layout in rt_kernels.hip stays within this).
-inline unsigned long long sched_words_for(unsigned long long tiles) { return 10 * tiles + 64; }
+// + the unit order lists (order_layout in rt_kernels.hip stays below sched_snap_offset), then
+// the snapshot of the tile costs the order kernel read (rt_tile_costs) in the last `tiles` words.
+constexpr unsigned long long sched_words_for(unsigned long long tiles) { return 10 * tiles + 64; }
+constexpr unsigned long long sched_snap_offset(unsigned long long tiles) { return 9 * tiles + 64; }
 
 struct RenderParams {
   const DevNode* nodes;
@@ -269,6 +283,7 @@ struct RenderParams {
   int use_order;
   int primary_order;  // the primary kernel too dispatches by unit_order: the order the previous
                       // frame of the same selection left on this stream (rt_api.hip warm order)
+  int records;    // RT_TILE_RECORDS: the shading phase writes 32-bit pixel records, not RGB
   float* frames;  // recursive scenes only: (max_depth+1) * 28 * lanes ray-tree frames, else null
   // kCounterRows rows of kCounterWidth u64 (columns: kCnt*)
   unsigned long long* counters;

@@ -1080,6 +1080,39 @@ __device__ __forceinline__ float phong_pow(float c, float p) {
   return phong_pow_f64(c, p);
 }
 
+// The colour of a primary hit (leaf, t) of pixel (px, py): ambient, then per unoccluded light
+// diffuse and specular, in the reference's order.  occluded(li): light li's shadow bit.
+template <bool SPHERES, typename Occ>
+__device__ __forceinline__ V3 shade_hit(const RenderParams& P, const DevPrim* __restrict__ prims,
+                                        const float* __restrict__ normals,
+                                        const DevMaterial* __restrict__ mats,
+                                        const DevLight* __restrict__ lights, int leaf, V3 p,
+                                        Occ occluded) {
+  V3 color = v3(0.0f, 0.0f, 0.0f);
+  const V3 e = ld3(P.cam_e);
+  const float4 nm = *reinterpret_cast<const float4*>(normals + 4 * leaf);
+  const bool tri = !SPHERES || prims[leaf].kind == kPrimTriangle;
+  const V3 n = tri ? v3(nm.x, nm.y, nm.z) : normalize(p - ld3(prims[leaf].v0));
+  const DevMaterial& m = mats[__float_as_int(nm.w)];
+  const V3 w0 = normalize(e - p);  // (ray.o - intersection_point).normalize()
+  color = color + ld3(m.ambient) * ld3(P.ambient);
+  for (int li = 0; li < P.num_lights; li++) {
+    if (occluded(li)) continue;
+    const DevLight& Lt = lights[li];
+    const V3 ld = ld3(Lt.position) - p;
+    const V3 wi = normalize(ld);
+    const float dist = length(ld);
+    const V3 I = ld3(Lt.intensity);
+    const float d2 = dist * dist;
+    const float cos_d = dot(n, wi);
+    color = color + ((ld3(m.diffuse) * I) * cos_d) / d2;
+    const float cos_s = __builtin_fmaxf(dot(n, normalize(w0 + wi)), 0.0f);
+    const float pw = phong_pow(cos_s, m.phong_exponent);
+    color = color + ((ld3(m.specular) * I) * pw) / d2;
+  }
+  return color;
+}
+
 template <bool SPHERES>
 __device__ __forceinline__ void shade_pixel(const RenderParams& P,
                                             const DevPrim* __restrict__ prims,
@@ -1092,31 +1125,22 @@ __device__ __forceinline__ void shade_pixel(const RenderParams& P,
   const int2_t rec = P.hits[pix];
   const bool valid = q.own && hit_leaf(rec) != -2;
   const bool hit = q.own && hit_leaf(rec) >= 0;
+  if (P.records) {  // RT_TILE_RECORDS: the pixel record instead of its colour (rt_resolve_device)
+    if (!q.own) return;
+    unsigned r = kRecOutside;
+    if (hit)
+      r = (unsigned)hit_leaf(rec) | ((P.occ[pix * P.occ_words] & kRecLightMask) << kRecLightShift);
+    else if (valid)
+      r = kRecMiss;
+    reinterpret_cast<unsigned*>(P.out)[pix] = r;
+    return;
+  }
   V3 color = v3(0.0f, 0.0f, 0.0f);
   if (hit) {
-    const int leaf = hit_leaf(rec);
-    const V3 e = ld3(P.cam_e);
-    const V3 p = hit_point(P, q, hit_t(rec));
-    const float4 nm = *reinterpret_cast<const float4*>(normals + 4 * leaf);
-    const bool tri = !SPHERES || prims[leaf].kind == kPrimTriangle;
-    const V3 n = tri ? v3(nm.x, nm.y, nm.z) : normalize(p - ld3(prims[leaf].v0));
-    const DevMaterial& m = mats[__float_as_int(nm.w)];
-    const V3 w0 = normalize(e - p);  // (ray.o - intersection_point).normalize()
-    color = color + ld3(m.ambient) * ld3(P.ambient);
-    for (int li = 0; li < P.num_lights; li++) {
-      if ((P.occ[pix * P.occ_words + (li >> 5)] >> (li & 31)) & 1u) continue;
-      const DevLight& Lt = lights[li];
-      const V3 ld = ld3(Lt.position) - p;
-      const V3 wi = normalize(ld);
-      const float dist = length(ld);
-      const V3 I = ld3(Lt.intensity);
-      const float d2 = dist * dist;
-      const float cos_d = dot(n, wi);
-      color = color + ((ld3(m.diffuse) * I) * cos_d) / d2;
-      const float cos_s = __builtin_fmaxf(dot(n, normalize(w0 + wi)), 0.0f);
-      const float pw = phong_pow(cos_s, m.phong_exponent);
-      color = color + ((ld3(m.specular) * I) * pw) / d2;
-    }
+    const unsigned* occ = P.occ + pix * P.occ_words;
+    color = shade_hit<SPHERES>(P, prims, normals, mats, lights, hit_leaf(rec),
+                               hit_point(P, q, hit_t(rec)),
+                               [&](int li) { return ((occ[li >> 5] >> (li & 31)) & 1u) != 0; });
   } else if (valid) {
     color = ld3(P.background);  // primary miss: max_recursion_depth == depth
   }
@@ -1437,14 +1461,14 @@ __device__ __forceinline__ int packet_sel(const RenderParams& P, int p) {
   const int w = p % kTraceWaves, b = p / kTraceWaves;
   const int nbx = (P.tiles_x + kBlockW - 1) / kBlockW;
   const int tx = (b % nbx) * kBlockW + w % kBlockW, ty = (b / nbx) * kBlockH + w / kBlockW;
-  const int tiles_y = P.tiles_total / P.tiles_x;
+  const int tiles_y = P.num_sel_tiles / P.tiles_x;  // the selection's tile rows
   return (tx < P.tiles_x && ty < tiles_y) ? ty * P.tiles_x + tx : -1;
 }
 
 // Logical packets of a traversal launch (with tile_block, padded to whole blocks).
 __host__ __device__ __forceinline__ int trace_packets(const RenderParams& P) {
   if (!P.tile_block) return P.num_sel_tiles;
-  const int tiles_y = P.tiles_total / P.tiles_x;
+  const int tiles_y = P.num_sel_tiles / P.tiles_x;
   return ((P.tiles_x + kBlockW - 1) / kBlockW) * ((tiles_y + kBlockH - 1) / kBlockH) * kTraceWaves;
 }
 
@@ -1599,8 +1623,13 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(RenderParams P) {
   }
   __syncthreads();
   const int nsplit = split_info[1];
+  unsigned* snap = P.tile_cost + sched_snap_offset((unsigned long long)P.num_sel_tiles);
   for (int i = tid; i < n; i += kOrderThreads) {
     const int u = region_unit(P, x, i);
+    for (int w = 0; w < kTraceWaves; w++) {  // this frame's costs, kept for rt_tile_costs
+      const int sel = unit_sel(P, u, w);
+      if (sel >= 0) snap[sel] = P.tile_cost[sel];
+    }
     const int r = atomicAdd(&hist[cost_bucket(unit_cost(P, u))], 1);
     if (r < nsplit) {  // one entry per tile, -1 for a padding tile of an edge block
       for (int w = 0; w < kTraceWaves; w++) {
@@ -1718,7 +1747,10 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
     return;
   }
   RenderParams T = P;
-  T.tile_block = P.tile_begin == 0 && P.tile_step == 1 && !P.block_deal;
+  // 2-D blocks of tiles for a selection of whole tile rows: the whole frame, or a row band
+  // (dist_tiles.BandPlan: tiles tile_begin .. tile_begin + num_sel_tiles - 1)
+  T.tile_block = P.tile_step == 1 && !P.block_deal && P.tile_begin % P.tiles_x == 0 &&
+                 P.num_sel_tiles % P.tiles_x == 0;
   const int tblocks = (trace_packets(T) + kTraceWaves - 1) / kTraceWaves;
   const size_t tlds = DEEP ? sizeof(int) * kDeepWords * kDeepStack * kTraceWaves : 0;
   // dispatch order: units of one traversal workgroup, `regions` regions of
@@ -1747,7 +1779,7 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
     T.order_stride = per_region + (kTraceWaves - 1) * T.order_split;
     ordered = (unsigned long long)T.num_sel_tiles +
                   (unsigned long long)T.order_regions * T.order_stride <=
-              sched_words_for((unsigned long long)T.num_sel_tiles);
+              sched_snap_offset((unsigned long long)T.num_sel_tiles);
   }
   const int oblocks = ordered ? T.order_regions * T.order_stride : tblocks;
   const RenderParams S = T;
@@ -1824,14 +1856,22 @@ hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream) {
 // of a tile is 96 contiguous bytes in both layouts: six 16-B chunks, one per thread (a wave
 // covers 10 tile rows); a tile row on the frame's right edge, or a frame whose rows are not
 // 16-B aligned (width % 4 != 0), is copied by pixel instead.
-// (nullptr: a unit of rank 0 under skip_root)
-__device__ __forceinline__ const float* untile_src(const UntileParams& U, int t, int tx, int ty) {
+// Gathered tile of frame tile t: rank r's slot tile k (false: a unit of rank 0 under skip_root).
+__device__ __forceinline__ bool untile_slot(const UntileParams& U, int t, int tx, int ty, int& r,
+                                            int& k) {
   int w = 0;
   const int u = U.blocks ? deal_block_index(U.tiles_x, tx, ty, w) : t;  // deal unit
-  const int r = (u + U.tile_offset) % U.devices;
-  if (U.skip_root && r == 0) return nullptr;
+  r = (u + U.tile_offset) % U.devices;
+  if (U.skip_root && r == 0) return false;
   const int b = ((r - U.tile_offset) % U.devices + U.devices) % U.devices;  // rank r's first unit
-  const int k = U.blocks ? 4 * ((u - b) / U.devices) + w : (u - b) / U.devices;  // slot tile
+  k = U.blocks ? 4 * ((u - b) / U.devices) + w : (u - b) / U.devices;  // slot tile
+  return true;
+}
+
+// (nullptr: a unit of rank 0 under skip_root)
+__device__ __forceinline__ const float* untile_src(const UntileParams& U, int t, int tx, int ty) {
+  int r, k;
+  if (!untile_slot(U, t, tx, ty, r, k)) return nullptr;
   return U.recv + (size_t)(r * U.slot + k) * (kTile * kTile * 3);
 }
 
@@ -1866,6 +1906,55 @@ hipError_t launch_untile(const UntileParams& U, hipStream_t stream) {
   if (U.tiles_total <= 0) return hipSuccess;
   const long long threads = (long long)U.tiles_total * kTile * kUntileChunks;
   hipLaunchKernelGGL(untile_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, U);
+  return hipGetLastError();
+}
+
+// rt_resolve_device: the gathered pixel records of RT_TILE_RECORDS shares (rt_internal.h) into
+// colours of the row-major frame — the shading the frame kernel would have done on the rank that
+// traced them, done on the gathering rank.  One thread per pixel, 64 per tile, 4 tiles per
+// workgroup.  The hit's t is re-derived by the intersection test the traversal ran (the same ray
+// from the same camera arithmetic, the same primitive record, the same operations: the same
+// bits), the hit point is o + t * d as trace_ray computes it, and shade_hit is the frame kernel's.
+template <bool SPHERES>
+__global__ __launch_bounds__(256) void resolve_kernel(RenderParams P, UntileParams U) {
+  const int t = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (t >= U.tiles_total) return;
+  const int lane = (int)(threadIdx.x & 63);
+  const int tx = t % U.tiles_x, ty = t / U.tiles_x;
+  const int px = tx * kTile + (lane & 7), lr = ty * kTile + (lane >> 3);
+  if (px >= U.width || lr >= U.rows) return;
+  int r, k;
+  if (!untile_slot(U, t, tx, ty, r, k)) return;
+  const unsigned rec = reinterpret_cast<const unsigned*>(U.recv)[(size_t)(r * U.slot + k) * (kTile * kTile) + lane];
+  if (rec & kRecOutside) return;
+  const int py = U.row0 + lr * U.row_stride;
+  V3 color;
+  if (rec & kRecMiss) {
+    color = ld3(P.background);
+  } else {
+    const int leaf = (int)(rec & kRecLeafMask);
+    const V3 e = ld3(P.cam_e), d = primary_dir(P, px, py);
+    const LaneRay ray = make_ray(e, d, P.quot_ok);
+    float th = 0.0f;
+    (void)leaf_test<SPHERES>(P.prims, leaf, ray, th);
+    const unsigned occ = (rec >> kRecLightShift) & kRecLightMask;
+    color = shade_hit<SPHERES>(P, P.prims, P.normals, P.materials, P.lights, leaf, e + d * th,
+                               [&](int li) { return ((occ >> li) & 1u) != 0; });
+  }
+  float* o = U.out + 3 * ((size_t)py * U.width + px);
+  o[0] = 0.0f + color.x;
+  o[1] = 0.0f + color.y;
+  o[2] = 0.0f + color.z;
+}
+
+hipError_t launch_resolve(const RenderParams& P, const UntileParams& U, bool spheres,
+                          hipStream_t stream) {
+  if (U.tiles_total <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((U.tiles_total + 3) / 4));
+  if (spheres)
+    hipLaunchKernelGGL(resolve_kernel<true>, grid, dim3(256), 0, stream, P, U);
+  else
+    hipLaunchKernelGGL(resolve_kernel<false>, grid, dim3(256), 0, stream, P, U);
   return hipGetLastError();
 }
 

@@ -33,6 +33,7 @@ import numpy as np
 
 TILE = 8
 TILE_FLOATS = TILE * TILE * 3
+TILE_RECORDS = TILE * TILE  # 32-bit pixel records per tile (RT_TILE_RECORDS shares)
 ROW_FLOATS = TILE * 3  # one pixel row of a tile
 
 
@@ -170,14 +171,16 @@ def untile_camera(gathered_c, layout: TileLayout, c: int, index=None, out=None):
     return out[:h, :w]
 
 
-def scene_tile_untiler(scene, layout: TileLayout) -> Callable:
+def scene_tile_untiler(scene, layout: TileLayout, records: bool = False) -> Callable:
     """The GPU untile: rt_untile_device of camera c's gathered shares straight into its
-    row-major frame, on `stream`; skip_root: rank 0's own units are already in the frame."""
+    row-major frame, on `stream`; skip_root: rank 0's own units are already in the frame.
+    records: the shares are pixel records, shaded into the frame by rt_resolve_device."""
     def untile(c, gathered_c, frame, stream, skip_root=False):
         sh = layout.shares[c]
-        scene.untile_device(c, layout.world, sh.slot, gathered_c.data_ptr(), frame.data_ptr(),
-                            tile_offset=int(layout.offsets[c] % layout.world),
-                            blocks=layout.blocks, skip_root=skip_root, stream=stream.cuda_stream)
+        fn = scene.resolve_device if records else scene.untile_device
+        fn(c, layout.world, sh.slot, gathered_c.data_ptr(), frame.data_ptr(),
+           tile_offset=int(layout.offsets[c] % layout.world), blocks=layout.blocks,
+           skip_root=skip_root, stream=stream.cuda_stream)
     return untile
 
 
@@ -190,13 +193,19 @@ def scene_inplace_renderer(scene) -> Callable:
     return render
 
 
-def scene_tile_renderer(scene) -> Callable:
-    """The GPU tile renderer: rt_render_device of camera c's share, tile-major into `slot`."""
+def scene_tile_renderer(scene, records: bool = False) -> Callable:
+    """The GPU tile renderer: rt_render_device of camera c's share, tile-major into `slot`
+    (records: 64 pixel records per tile, RT_TILE_RECORDS, instead of RGB)."""
     def render(sh: CameraShare, slot, stream):
         scene.render_device(sh.camera, slot.data_ptr(), tile_begin=sh.tile_begin,
                             tile_step=sh.tile_step, tile_major=True, blocks=sh.blocks,
-                            stream=stream.cuda_stream)
+                            stream=stream.cuda_stream, records=records)
     return render
+
+
+def records_ok(scene) -> bool:
+    """Every camera of the scene may send its shares as pixel records (rt_scene_records_ok)."""
+    return all(scene.records_ok(c) for c in range(scene.num_cameras))
 
 
 class FrameRenderer:
@@ -258,7 +267,8 @@ class TileGatherRenderer:
     def __init__(self, layout: TileLayout, stream, render: Callable, inflight: int = 2,
                  host_staging: bool = False, device=None, untile: Optional[Callable] = None,
                  gather_stream: str = "render", render_inplace: Optional[Callable] = None,
-                 cpu_fakes: bool = False, self_exchange: bool = False):
+                 cpu_fakes: bool = False, self_exchange: bool = False,
+                 tile_words: int = TILE_FLOATS):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -299,8 +309,10 @@ class TileGatherRenderer:
         else:
             self.rstreams = render_streams(F, dev)  # (pool streams, one per frame in flight)
             self.comm = torch.cuda.Stream(device=dev)
-        self.local = [torch.zeros((L.buffer_tiles, TILE_FLOATS), dtype=torch.float32, device=dev)
-                      for _ in range(F)]
+        # tile_words: 4-B words per tile in the slots (TILE_FLOATS RGB, TILE_RECORDS records)
+        self.tile_words = int(tile_words)
+        self.local = [torch.zeros((L.buffer_tiles, self.tile_words), dtype=torch.float32,
+                                  device=dev) for _ in range(F)]
         if not host_staging:
             # the zero fill above ran on the allocating (current) stream: every stream that
             # writes or reads these buffers first waits for it
@@ -315,7 +327,7 @@ class TileGatherRenderer:
         self.k = 0
         self.frames = None
         if self.rank == 0:
-            self.gathered = [[torch.empty((L.world, sh.slot, TILE_FLOATS), dtype=torch.float32,
+            self.gathered = [[torch.empty((L.world, sh.slot, self.tile_words), dtype=torch.float32,
                                           device=dev) for sh in L.shares] for _ in range(F)]
             self.index = [torch.as_tensor(L.row_index(c).reshape(-1), device=dev)
                           for c in range(len(L.shares))]
@@ -350,7 +362,7 @@ class TileGatherRenderer:
                     for req in dist.batch_isend_irecv(ops):
                         req.wait()
             elif self.host_staging:
-                glist = list(torch.empty((L.world, sh.slot, TILE_FLOATS))) if root else None
+                glist = list(torch.empty((L.world, sh.slot, self.tile_words))) if root else None
                 dist.gather(self._slot(s, sh).cpu(), glist, dst=0)
                 if root:
                     self.gathered[s][c].copy_(torch.stack(glist))
@@ -523,9 +535,11 @@ class ShareRenderer:
     strong scaling before an N-GPU node is available (bench.py share probe).  Steps go to
     `inflight` streams / buffer sets in turn, as in TileGatherRenderer."""
 
-    def __init__(self, scene, world: int, rank: int, stream, inflight: int = 1, streams=None):
+    def __init__(self, scene, world: int, rank: int, stream, inflight: int = 1, streams=None,
+                 records: bool = False):
         import torch
         self.layout = L = TilePlan(scene, world, rank)
+        self.records = records
         self.scene, self.stream = scene, stream
         dev = torch.device("cuda", torch.cuda.current_device())
         self.inflight = max(1, int(inflight))
@@ -547,10 +561,260 @@ class ShareRenderer:
                 slot = self.local[s][sh.offset:sh.offset + sh.slot]
                 self.scene.render_device(sh.camera, slot.data_ptr(), tile_begin=sh.tile_begin,
                                          tile_step=sh.tile_step, tile_major=True,
-                                         blocks=sh.blocks, stream=st.cuda_stream)
+                                         blocks=sh.blocks, stream=st.cuda_stream,
+                                         records=self.records)
 
     def finish(self):
         for st in self.streams:
+            self.stream.wait_stream(st)
+
+
+# ------------------------------------------------------------------ row bands
+# The band split: camera c's frame is cut into `world` bands of whole 8-pixel tile rows, band r
+# to rank r, the cuts placed so the bands' measured costs (rt_tile_costs of a whole frame) are
+# as equal as contiguous rows allow.  A band of tile rows is one contiguous run of the row-major
+# frame, so a rank renders its band in place (a tile range of rt_render_device_range) and
+# rank 0 receives every other band straight into its frame: no untile, nothing extra on rank 0.
+
+def band_cuts(row_costs: Sequence[float], world: int) -> List[int]:
+    """Cuts 0 = c_0 <= c_1 <= ... <= c_world = len(row_costs) of the rows into `world` contiguous
+    bands (band r = rows [c_r, c_r+1)) whose heaviest band is as light as possible (a binary
+    search over the band capacity with the greedy left-to-right cut)."""
+    w = np.maximum(np.asarray(row_costs, dtype=np.float64), 0.0)
+    n = len(w)
+    if n == 0:
+        return [0] * (world + 1)
+    if w.sum() <= 0:
+        w = np.ones(n)
+
+    def greedy(cap):
+        cuts, acc = [0], 0.0
+        for i, x in enumerate(w):
+            if acc + x > cap and acc > 0:
+                cuts.append(i)
+                acc = 0.0
+            acc += x
+        return cuts
+
+    lo, hi = float(w.max()), float(w.sum())
+    for _ in range(60):
+        mid = 0.5 * (lo + hi)
+        if len(greedy(mid)) <= world:
+            hi = mid
+        else:
+            lo = mid
+    cuts = greedy(hi)
+    # exactly `world` bands: split the longest bands (in rows) until there are enough; ranks
+    # beyond the row count get empty bands at the end
+    while len(cuts) < world and len(cuts) < n:
+        edges = cuts + [n]
+        k = int(np.argmax(np.diff(edges)))
+        if edges[k + 1] - edges[k] < 2:
+            break
+        cuts.insert(k + 1, (edges[k] + edges[k + 1]) // 2)
+    cuts = sorted(cuts) + [n] * (world + 1 - len(cuts))
+    return [int(c) for c in cuts]
+
+
+@dataclass
+class CameraBand:
+    camera: int
+    row0: int        # first tile row
+    rows: int        # tile rows
+    tiles_x: int
+    y0: int          # pixel rows [y0, y1) of the frame (clipped to its height)
+    y1: int
+
+    @property
+    def tile_begin(self) -> int:
+        return self.row0 * self.tiles_x
+
+    @property
+    def tile_count(self) -> int:
+        return self.rows * self.tiles_x
+
+
+class BandPlan:
+    """Row bands of every camera over `world` ranks.  cuts[c] = the world + 1 tile-row cuts of
+    camera c (band_cuts of its measured row costs; equal rows when no costs are given).  Every
+    rank must hold the same cuts: rank 0 measures them and broadcasts (bench.py)."""
+
+    def __init__(self, sizes: Sequence[Tuple[int, int]], world: int, rank: int,
+                 cuts: Optional[Sequence[Sequence[int]]] = None):
+        self.sizes = [tuple(s) for s in sizes]
+        self.world, self.rank = world, rank
+        txy = [tiles_of(s) for s in self.sizes]
+        if cuts is None:
+            cuts = [band_cuts(np.ones(ty), world) for _, ty in txy]
+        self.cuts = [[int(x) for x in c] for c in cuts]
+        for c, (cc, (tx, ty)) in enumerate(zip(self.cuts, txy)):
+            assert len(cc) == world + 1 and cc[0] == 0 and cc[-1] == ty and \
+                all(a <= b for a, b in zip(cc, cc[1:])), f"bad cuts for camera {c}: {cc}"
+        self.per_rank = [[CameraBand(c, cc[r], cc[r + 1] - cc[r], tx, min(h, TILE * cc[r]),
+                                     min(h, TILE * cc[r + 1]))
+                          for c, (cc, (tx, _), (_, h)) in enumerate(zip(self.cuts, txy, self.sizes))]
+                         for r in range(world)]
+        self.bands = self.per_rank[rank]
+
+    @classmethod
+    def from_costs(cls, sizes, world: int, rank: int, tile_costs: Sequence[np.ndarray]):
+        """tile_costs[c]: camera c's row-major per-tile costs (rt_tile_costs of a whole frame)."""
+        cuts = []
+        for (w, h), cost in zip(sizes, tile_costs):
+            tx, ty = tiles_of((w, h))
+            cuts.append(band_cuts(np.asarray(cost, np.float64).reshape(ty, tx).sum(1), world))
+        return cls(sizes, world, rank, cuts)
+
+    def band_costs(self, tile_costs: Sequence[np.ndarray]) -> np.ndarray:
+        """[world] summed tile costs of each rank's bands (all cameras)."""
+        out = np.zeros(self.world)
+        for c, ((w, h), cost) in enumerate(zip(self.sizes, tile_costs)):
+            tx, ty = tiles_of((w, h))
+            rows = np.asarray(cost, np.float64).reshape(ty, tx).sum(1)
+            for r in range(self.world):
+                out[r] += rows[self.cuts[c][r]:self.cuts[c][r + 1]].sum()
+        return out
+
+
+def measure_tile_costs(scene, frames: int = 5) -> List[np.ndarray]:
+    """Every camera's per-tile costs: `frames` whole frames rendered one at a time on a fresh
+    stream (rt_tile_costs after each), the element-wise median of the maps."""
+    import torch
+    st = torch.cuda.Stream()
+    out = []
+    for c in range(scene.num_cameras):
+        cam = scene.camera(c)
+        buf = torch.empty((cam.height, cam.width, 3), dtype=torch.float32, device="cuda")
+        n = scene.num_tiles(c)
+        maps = []
+        for _ in range(max(1, frames)):
+            scene.render_device(c, buf.data_ptr(), stream=st.cuda_stream)
+            maps.append(scene.tile_costs(st.cuda_stream, n))
+        out.append(np.median(np.stack(maps), axis=0))
+    st.synchronize()
+    scene.release_stream(st.cuda_stream)
+    return out
+
+
+def scene_band_renderer(scene) -> Callable:
+    """Band b of camera b.camera rendered in place into its row-major frame (a tile range)."""
+    def render(b: CameraBand, frame, stream):
+        scene.render_device(b.camera, frame.data_ptr(), tile_begin=b.tile_begin, tile_step=1,
+                            tile_count=b.tile_count, stream=stream.cuda_stream)
+    return render
+
+
+def BandRenderPlan(scene, world: int, rank: int, cuts=None) -> BandPlan:
+    sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
+    return BandPlan(sizes, world, rank, cuts)
+
+
+class BandGatherRenderer:
+    """One step = every camera split over the ranks in row bands (BandPlan), each rank's bands
+    rendered in place into its own frames, and every band of ranks > 0 sent to rank 0 straight
+    into its frames (point-to-point, batch_isend_irecv: RCCL send / receive over xGMI with backend
+    "nccl").  No untile: a band is a contiguous run of rows.  Steps go to `inflight` render
+    streams / frame sets in turn; a step's exchange is enqueued on its own render stream after its
+    render, so a set is rendered again only after its exchange `inflight` steps earlier.
+    host_staging=True (gloo, CPU tensors): the same exchange through the host, one set.
+    self_exchange (one-rank rehearsal): rank 0 renders its band into a separate buffer and sends
+    it to itself into the frame (RCCL self send / receive; a local copy with gloo).
+    frames: rank 0's frames of the last step (complete after finish())."""
+
+    def __init__(self, plan: BandPlan, stream, render: Callable, inflight: int = 2,
+                 host_staging: bool = False, device=None, self_exchange: bool = False):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.plan = self.layout = plan
+        self.stream, self.render = stream, render
+        self.host_staging = host_staging
+        self.inflight = 1 if host_staging else max(1, int(inflight))
+        self.rank = plan.rank
+        self.self_loop = bool(self_exchange) and plan.world == 1
+        dev = device if device is not None else (
+            "cpu" if host_staging else torch.device("cuda", torch.cuda.current_device()))
+        self.rstreams = [stream] if host_staging else render_streams(self.inflight, dev)
+        self.frame_sets = [[torch.zeros((h, w, 3), dtype=torch.float32, device=dev)
+                            for (w, h) in plan.sizes] for _ in range(self.inflight)]
+        self.local = ([[torch.zeros((h, w, 3), dtype=torch.float32, device=dev)
+                        for (w, h) in plan.sizes] for _ in range(self.inflight)]
+                      if self.self_loop else None)
+        if not host_staging:
+            cur = torch.cuda.current_stream(dev)
+            for st in self.rstreams:
+                st.wait_stream(cur)
+                if stream is not None:
+                    st.wait_stream(stream)
+        self.k = 0
+        self.frames = None
+
+    def _exchange(self, s: int):
+        dist, P = self.dist, self.plan
+        ops = []
+        if P.world > 1 and self.host_staging:  # gloo: host tensors, the receives copied in
+            for c in range(len(P.sizes)):
+                if self.rank == 0:
+                    for r in range(1, P.world):
+                        b = P.per_rank[r][c]
+                        if b.y1 > b.y0:
+                            dst = self.frame_sets[s][c][b.y0:b.y1]
+                            tmp = self.torch.empty(dst.shape, dtype=dst.dtype)
+                            dist.recv(tmp, r)
+                            dst.copy_(tmp)
+                else:
+                    b = P.bands[c]
+                    if b.y1 > b.y0:
+                        dist.send(self.frame_sets[s][c][b.y0:b.y1].cpu(), 0)
+        elif P.world > 1:
+            for c in range(len(P.sizes)):
+                if self.rank == 0:
+                    for r in range(1, P.world):
+                        b = P.per_rank[r][c]
+                        if b.y1 > b.y0:
+                            ops.append(dist.P2POp(dist.irecv, self.frame_sets[s][c][b.y0:b.y1], r))
+                else:
+                    b = P.bands[c]
+                    if b.y1 > b.y0:
+                        ops.append(dist.P2POp(dist.isend, self.frame_sets[s][c][b.y0:b.y1], 0))
+        elif self.self_loop:
+            for c, b in enumerate(P.bands):
+                if b.y1 <= b.y0:
+                    continue
+                src, dst = self.local[s][c][b.y0:b.y1], self.frame_sets[s][c][b.y0:b.y1]
+                if self.host_staging:  # (gloo has no pair to itself)
+                    dst.copy_(src)
+                else:
+                    ops += [dist.P2POp(dist.isend, src, 0), dist.P2POp(dist.irecv, dst, 0)]
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+
+    def step(self, events=None):
+        s = self.k % self.inflight
+        self.k += 1
+        st = self.rstreams[s]
+        if events is not None:
+            events[0].record(st)
+        target = self.local[s] if self.self_loop else self.frame_sets[s]
+        for c, b in enumerate(self.plan.bands):
+            if b.rows > 0:
+                self.render(b, target[c], st)
+        if events is not None:
+            events[1].record(st)
+        if self.host_staging:
+            self._exchange(s)
+        else:
+            with self.torch.cuda.stream(st):
+                self._exchange(s)
+        if self.rank == 0:
+            self.frames = self.frame_sets[s]
+        return self.frames
+
+    def finish(self):
+        if self.host_staging:
+            return
+        for st in self.rstreams:
             self.stream.wait_stream(st)
 
 

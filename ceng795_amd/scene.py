@@ -10,7 +10,8 @@ import numpy as np
 from . import _lib
 from ._lib import check, lib
 
-RT_TILE_MAJOR, RT_TILE_BLOCKS = 1, 2  # rt_render_device tile_major flags (include/ceng795_rt.h)
+# rt_render_device tile_major flags (include/ceng795_rt.h)
+RT_TILE_MAJOR, RT_TILE_BLOCKS, RT_TILE_RECORDS = 1, 2, 4
 RT_UNTILE_BLOCKS, RT_UNTILE_SKIP_ROOT = 1, 2  # rt_untile_device flags
 
 
@@ -142,12 +143,14 @@ class Scene:
     def render_device(self, camera_index: int, out_ptr: int, *, starting_row: int = 0,
                       row_stride: int = 1, tile_begin: int = 0, tile_step: int = 1,
                       tile_major: bool = False, blocks: bool = False, stream: int = 0,
-                      tile_count: int = -1) -> None:
+                      tile_count: int = -1, records: bool = False) -> None:
         """Asynchronous render into device memory at ``out_ptr`` on HIP stream ``stream``
         (deal units tile_begin + k*tile_step, k < tile_count; tile_count < 0: all of them; a
         unit is a tile, or with ``blocks`` a 2x2 block of tiles in deal order —
-        RT_TILE_BLOCKS of include/ceng795_rt.h)."""
-        flags = (RT_TILE_MAJOR if tile_major else 0) | (RT_TILE_BLOCKS if blocks else 0)
+        RT_TILE_BLOCKS of include/ceng795_rt.h).  ``records`` (with ``tile_major``): 64
+        32-bit pixel records per tile instead of RGB (RT_TILE_RECORDS)."""
+        flags = ((RT_TILE_MAJOR if tile_major else 0) | (RT_TILE_BLOCKS if blocks else 0) |
+                 (RT_TILE_RECORDS if records else 0))
         check(lib().rt_render_device_range(self._h, camera_index, starting_row, row_stride,
                                            tile_begin, tile_step, tile_count, flags,
                                            C.c_void_p(out_ptr), C.c_void_p(stream)))
@@ -163,6 +166,28 @@ class Scene:
         check(lib().rt_untile_device(self._h, camera_index, 0, 1, devices, slot, tile_offset,
                                      flags, C.c_void_p(gathered_ptr), C.c_void_p(out_ptr),
                                      C.c_void_p(stream)))
+
+    def tile_costs(self, stream: int, capacity: int) -> "np.ndarray":
+        """rt_tile_costs: every tile's measured time (100 MHz ticks) in the last frame enqueued on
+        HIP stream ``stream``, in that call's selection order (waits for the stream)."""
+        out = np.zeros(max(1, capacity), dtype=np.uint32)
+        n = check(lib().rt_tile_costs(self._h, C.c_void_p(stream),
+                                      out.ctypes.data_as(C.c_void_p), capacity))
+        return out[:n]
+
+    def records_ok(self, camera_index: int) -> bool:
+        """rt_scene_records_ok: may this camera's shares travel as pixel records?"""
+        return bool(check(lib().rt_scene_records_ok(self._h, camera_index)))
+
+    def resolve_device(self, camera_index: int, devices: int, slot: int, gathered_ptr: int,
+                       out_ptr: int, *, tile_offset: int = 0, blocks: bool = False,
+                       skip_root: bool = False, stream: int = 0) -> None:
+        """rt_resolve_device: gathered pixel records [devices][slot][64] (RT_TILE_RECORDS
+        shares) shaded into the row-major frame (the layout and flags of untile_device)."""
+        flags = (RT_UNTILE_BLOCKS if blocks else 0) | (RT_UNTILE_SKIP_ROOT if skip_root else 0)
+        check(lib().rt_resolve_device(self._h, camera_index, 0, 1, devices, slot, tile_offset,
+                                      flags, C.c_void_p(gathered_ptr), C.c_void_p(out_ptr),
+                                      C.c_void_p(stream)))
 
     def release_stream(self, stream: int) -> None:
         """Frees the scratch the library keeps for HIP stream ``stream`` (after waiting for it)."""

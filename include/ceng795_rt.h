@@ -24,9 +24,10 @@
 extern "C" {
 #endif
 
-#define CENG795_RT_ABI_VERSION 4  /* 2: MSAA cameras + rt_set_msaa_seed; 3: tile ranges,
+#define CENG795_RT_ABI_VERSION 6  /* 2: MSAA cameras + rt_set_msaa_seed; 3: tile ranges,
                                       kernel timing; 4: multi-device scenes, stream scratch
-                                      release, no CULL mode */
+                                      release, no CULL mode; 5: pixel records
+                                      (RT_TILE_RECORDS, rt_resolve_device); 6: rt_tile_costs */
 
 enum {
   RT_OK = 0,
@@ -182,7 +183,12 @@ int rt_render(rt_scene* scene, int camera_index, int starting_row, int row_strid
               float* out_rgb, rt_stats* stats);
 
 /* tile_major flags of rt_render_device / rt_render_device_range */
-enum { RT_TILE_MAJOR = 1, RT_TILE_BLOCKS = 2 };
+enum { RT_TILE_MAJOR = 1, RT_TILE_BLOCKS = 2,
+       RT_TILE_RECORDS = 4  /* with RT_TILE_MAJOR: each pixel as one 32-bit pixel record (the
+                               primary hit's primitive and the shadow bits) instead of 3 floats —
+                               a third of the bytes for the framebuffer gather; rank 0 shades the
+                               gathered records with rt_resolve_device.  Only where
+                               rt_scene_records_ok. */ };
 
 /* Device-resident variant (the building block of the one-process-per-GPU image tiling, and
  * of frames kept in HBM).  The image (rows starting_row +
@@ -238,6 +244,26 @@ enum { RT_UNTILE_BLOCKS = 1,    /* the units are 2x2 blocks (shares rendered wit
        RT_UNTILE_SKIP_ROOT = 2  /* rank 0's units are not touched: the gathering rank rendered its
                                    own share in place into d_out (tile_major without
                                    RT_TILE_MAJOR), so its slot need not be gathered */ };
+/* 1 when camera_index of the scene can exchange pixel records (RT_TILE_RECORDS): a pixel-centre
+ * camera, no mirror/dielectric recursion, at most 4 point lights; else 0. */
+int rt_scene_records_ok(const rt_scene* scene, int camera_index);
+/* rt_untile_device for shares rendered with RT_TILE_RECORDS: d_gathered holds
+ * [devices][slot][8*8] 32-bit pixel records; each is shaded into its pixel of the row-major
+ * frame d_out — the colour the rank that traced it would have written, bit for bit (the hit's
+ * distance is re-derived by the same intersection arithmetic).  Same layout and flags as
+ * rt_untile_device.  This is the shading step of Scene::trace_ray (HW2/Scene.cpp:101-138)
+ * moved to the gathering GPU. */
+int rt_resolve_device(rt_scene* scene, int camera_index, int starting_row, int row_stride,
+                      int devices, int slot, int tile_offset, int flags,
+                      const unsigned* d_gathered, float* d_out, void* hip_stream);
+/* The measured cost of every tile of the last frame rt_render_device enqueued on `hip_stream`
+ * (single-device scenes, pixel-centre cameras without recursion): each 8x8 packet's time from
+ * its first traversal step to its shading, in ticks of the 100 MHz device clock, in the order
+ * of that call's tile selection (row-major tiles for a whole frame).  Waits for the stream;
+ * writes at most `capacity` values to host memory and returns how many it wrote.  The row bands
+ * of the multi-GPU frame split are cut from these (dist_tiles.BandPlan).  Nothing in the
+ * reference measures work; its threads take interleaved rows (HW2/main.cpp:33-36). */
+int rt_tile_costs(rt_scene* scene, void* hip_stream, unsigned* host_out, int capacity);
 /* Waits for `hip_stream` and frees the scratch rt_render_device keeps for it (no-op for a
  * stream the scene never rendered on).  Streams that come and go should release theirs. */
 int rt_release_stream_scratch(rt_scene* scene, void* hip_stream);

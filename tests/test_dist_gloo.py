@@ -294,11 +294,12 @@ def test_root_inplace_exchange(tmp_path, world, sizes, self_exchange):
     assert (tmp_path / "result").read_text() == "ok"
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_bench_self_launches_ranks(tmp_path, world):
+@pytest.mark.parametrize("world,split", [(2, "bands"), (3, "bands"), (2, "tiles"), (3, "tiles")])
+def test_bench_self_launches_ranks(tmp_path, world, split):
     """`python bench.py --gpus N` with no launcher: bench.py starts N ranks itself (before
-    any GPU call) and rank 0 prints one JSON line with n_gpus == N; the default N>1 path (tile
-    deal, TileGatherRenderer exchange, untile) reassembles the frame bit for bit."""
+    any GPU call) and rank 0 prints one JSON line with n_gpus == N; the default N>1 path (row
+    bands received into rank 0's frame) and the tile deal (TileGatherRenderer exchange, untile)
+    reassemble the frame bit for bit."""
     import json
     import subprocess
     import sys
@@ -306,15 +307,110 @@ def test_bench_self_launches_ranks(tmp_path, world):
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world),
-                        "--cpu-rehearsal", "--workload", "c2", "--steps", "2", "--warmup", "1"],
+                        "--cpu-rehearsal", "--workload", "c2", "--steps", "2", "--warmup", "1",
+                        "--split", split],
                        capture_output=True, text=True, env=env, timeout=300, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
     assert line["n_gpus"] == world and line["scaling"] == "strong"
-    assert line["config"]["parallelism"] == f"tiles{world}+gloo_gather"
+    assert line["config"]["parallelism"] == (f"tiles{world}+gloo_gather" if split == "tiles"
+                                             else f"bands{world}+gloo_p2p")
     assert line["config"]["gather_verified"] is True
+    if split == "bands":  # cost-balanced cuts of the synthetic cost map: uneven bands
+        cuts = line["config"]["band_cuts"]
+        assert len(cuts) == world + 1 and cuts[0] == 0 and all(a < b for a, b in zip(cuts, cuts[1:]))
+
+
+# --------------------------------------------------------------------------- row bands
+def _brute_min_max(w, world):
+    """The lightest possible heaviest band over every way to cut w into `world` contiguous bands."""
+    import itertools
+    n = len(w)
+    best = float("inf")
+    for cuts in itertools.combinations_with_replacement(range(n + 1), world - 1):
+        edges = (0,) + cuts + (n,)
+        best = min(best, max(sum(w[a:b]) for a, b in zip(edges, edges[1:])))
+    return best
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("world", [1, 2, 3, 5])
+def test_band_cuts_minimise_the_heaviest_band(seed, world):
+    rng = np.random.default_rng(seed)
+    w = rng.integers(1, 50, size=int(rng.integers(1, 9))).astype(float)
+    cuts = dist_tiles.band_cuts(w, world)
+    assert len(cuts) == world + 1 and cuts[0] == 0 and cuts[-1] == len(w)
+    assert all(a <= b for a, b in zip(cuts, cuts[1:]))
+    heaviest = max(w[a:b].sum() for a, b in zip(cuts, cuts[1:]))
+    assert heaviest <= _brute_min_max(list(w), world) * (1 + 1e-9)
+
+
+def test_band_plan_covers_every_row_once():
+    costs = [np.random.default_rng(c).random(dist_tiles.tiles_of(s)[0] * dist_tiles.tiles_of(s)[1])
+             for c, s in enumerate(SIZES)]
+    for world in (1, 2, 3, 8):
+        P = dist_tiles.BandPlan.from_costs(SIZES, world, 0, costs)
+        for c, (w, h) in enumerate(SIZES):
+            rows = np.zeros(h, int)
+            for r in range(world):
+                b = P.per_rank[r][c]
+                assert b.tile_begin == b.row0 * b.tiles_x and b.tile_count == b.rows * b.tiles_x
+                rows[b.y0:b.y1] += 1
+            assert (rows == 1).all()
+        assert np.isclose(P.band_costs(costs).sum(), sum(x.sum() for x in costs))
+
+
+def _band_worker(rank, world, port, outdir, sizes, steps, self_exchange=False):
+    """The band split's exchange (BandGatherRenderer): each rank writes its bands into its own
+    frames (in place, as rt_render_device_range does), the other ranks' bands land in rank 0's
+    frames; uneven bands from a random cost map."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ceng795_amd.dist_tiles import BandGatherRenderer, BandPlan, tiles_of
+    costs = [np.random.default_rng(40 + c).random(tiles_of(s)[0] * tiles_of(s)[1]) ** 4
+             for c, s in enumerate(sizes)]
+    P = BandPlan.from_costs(sizes, world, rank, costs)
+    state = {"step": 0, "rows": 0}
+
+    def truth(step):
+        return [np.random.default_rng(500 + step).standard_normal((h, w, 3)).astype(np.float32)
+                for (w, h) in sizes]
+
+    def render(b, frame, stream):
+        state["rows"] += b.y1 - b.y0
+        frame[b.y0:b.y1] = torch.from_numpy(truth(state["step"])[b.camera][b.y0:b.y1])
+
+    R = BandGatherRenderer(P, None, render, host_staging=True, device="cpu",
+                           self_exchange=self_exchange)
+    ok = True
+    for step in range(steps):
+        state["step"] = step
+        frames = R.step()
+        if rank == 0:
+            ok &= all(_same(frames[c].numpy(), truth(step)[c]) for c in range(len(sizes)))
+    R.finish()
+    ok &= state["rows"] == steps * sum(b.y1 - b.y0 for b in P.bands)
+    flag = torch.tensor([1 if ok else 0])
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        with open(os.path.join(outdir, "result"), "w") as fh:
+            fh.write("ok" if flag.item() else "mismatch")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,sizes,self_exchange", [(2, [(64, 40), (37, 21)], False),
+                                                       (3, [(96, 64)], False),
+                                                       (3, [(5, 9)], False),
+                                                       (1, [(40, 24), (17, 9)], True)])
+def test_band_exchange(tmp_path, world, sizes, self_exchange):
+    """world 3 on a one-tile-row frame: two ranks get empty bands and send nothing."""
+    mp.spawn(_band_worker, args=(world, _free_port(), str(tmp_path), sizes, 2, self_exchange),
+             nprocs=world, join=True)
+    assert (tmp_path / "result").read_text() == "ok"
 
 
 # --------------------------------------------------------------------------- whole frames per rank

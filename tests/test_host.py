@@ -37,7 +37,7 @@ def test_library_exports_every_declared_function():
     for n in names:
         assert hasattr(L, n), n
         assert n in _lib.SIGNATURES, f"{n} missing from the ctypes table"
-    assert L.rt_abi_version() == _lib.ABI_VERSION == 4
+    assert L.rt_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_oracle_is_not_linked_into_the_product():
