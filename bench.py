@@ -376,49 +376,96 @@ def cold_frame_ms(scene, frames: int = 3):
     return round(sorted(out)[len(out) // 2], 4)
 
 
+def timed_probe(scene, R, steps: int) -> float:
+    """ms per step of probe renderer R (3 untimed steps first), one GPU."""
+    for _ in range(3):
+        R.step()
+    R.finish()
+    ms = timed_steps(R, steps, 1, "cuda") / steps * 1e3
+    scene.collect_stats()
+    return ms
+
+
+def record_band_plan(scene, n: int, costs, rho: float, stream, inflight: int, streams,
+                     steps: int = 20, rounds: int = 3):
+    """Row bands for the pixel-record exchange: rank 0's band starts at root_band_weights(n, rho)
+    and is then calibrated on this GPU — rank 0's work (its band + the resolve of the others')
+    and rank 1's band are timed with `inflight` frames in flight, and rank 0's weight moves by
+    their difference over one band's time (linear in the weight), up to `rounds` times or until
+    they agree within 3 %.  Returns (plan, rank-0 weight, [(t0, t1) per round])."""
+    from ceng795_amd import dist_tiles
+    sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
+    w0 = dist_tiles.root_band_weights(n, rho)[0]
+    hist = []
+    plan = None
+    for _ in range(rounds if n > 1 else 1):
+        plan = dist_tiles.BandPlan.from_costs(sizes, n, 0, costs, [w0] + [1.0] * (n - 1))
+        if n == 1:
+            break
+        t0 = timed_probe(scene, BandProbe(scene, plan, 0, stream, inflight, streams, True), steps)
+        t1 = timed_probe(scene, BandProbe(scene, plan, 1, stream, inflight, streams, True), steps)
+        hist.append((round(t0, 4), round(t1, 4)))
+        if abs(t0 - t1) <= 0.03 * t1:
+            break
+        w0 = min(1.0, max(0.0, w0 + (t1 - t0) / t1))
+    return plan, w0, hist
+
+
 def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange: str = "rgb",
                 split: str = "bands"):
     """Prediction of strong scaling on one GPU (no N-GPU node needed).  t1 = the whole frame
-    rendered in place with `inflight` frames in flight, and for each N every rank r's share of
-    the N-way block deal (tile_begin r, tile_step N, tile-major, the same frames in flight) alone
-    on this GPU — ALL timed over the same `steps` steps after the same warm-up, with one set of
-    render streams (each rank of an N-GPU run creates its streams in a fresh process).  The N-GPU
-    step can be no shorter than the slowest share, nor than rank 0's share plus its assembly of
-    the others' (the RGB untile, or the records' resolve with exchange="records"): t1 / (N *
-    that step) bounds the efficiency from above (the link transfer, overlapped with the
-    rendering of the frames in flight, is reported in bytes, not timed)."""
+    rendered in place with `inflight` frames in flight, and for each N every rank's work of the
+    N-way split alone on this GPU — ALL timed over the same `steps` steps after the same warm-up,
+    with one set of render streams (each rank of an N-GPU run creates its streams in a fresh
+    process).  bands: rank r's cost-balanced row band in place (payload rgb; payload records:
+    ranks > 0 render pixel records, rank 0 its smaller band plus the resolve of the others');
+    tiles: rank r's block share, plus rank 0's untile / resolve of the others.  The N-GPU step
+    can be no shorter than the slowest rank's work: t1 / (N * that step) bounds the efficiency
+    from above (the link transfer, overlapped with the rendering of the frames in flight, is
+    reported in bytes, not timed)."""
     from ceng795_amd import dist_tiles
     streams = dist_tiles.render_streams(inflight)  # one set for every run (pool streams)
 
     def timed(R):
-        for _ in range(3):
-            R.step()
-        R.finish()
-        ms = timed_steps(R, steps, 1, "cuda") / steps * 1e3
-        scene.collect_stats()
-        return ms
+        return timed_probe(scene, R, steps)
 
     one = dist_tiles.FrameRenderer(scene, stream, inflight=inflight, streams=streams)
     t1 = timed(one)
     records = exchange == "records" and dist_tiles.records_ok(scene)
     costs = dist_tiles.measure_tile_costs(scene)
+    rho = dist_tiles.measure_resolve_frac(scene) if dist_tiles.records_ok(scene) else None
+    sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
     out = {}
     for n in ns:
         # the band split (bench default): each rank's cost-balanced row band alone, in place;
-        # rank 0 receives the others' bands into its frame (no extra kernel there)
-        plan = dist_tiles.BandRenderPlan(scene, n, 0, dist_tiles.BandPlan.from_costs(
-            [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)],
-            n, 0, costs).cuts)
-        bands = [timed(BandProbe(scene, plan, r, stream, inflight, streams)) for r in range(n)]
-        bc = plan.band_costs(costs)
-        band = {"band_ms_per_rank": [round(x, 4) for x in bands],
-                "band_ms_max": round(max(bands), 4),
-                "band_cost_max_over_mean": round(float(bc.max() / bc.mean()), 4),
-                "band_tile_row_cuts": plan.cuts[0] if len(plan.cuts) == 1 else plan.cuts,
-                "predicted_efficiency": round(t1 / (n * max(bands)), 4),
-                "peer_link_MB_per_step_max": round(max(
-                    12 * sum((b.y1 - b.y0) * plan.sizes[b.camera][0] for b in plan.per_rank[r])
-                    for r in range(1, n)) / 1e6, 3)}
+        # rank 0 receives the others' bands into its frame (records: and shades them, its own
+        # band shrunk by that work) — both payloads
+        bands_by = {}
+        for rec in ((False, True) if rho is not None else (False,)):
+            if rec:  # rank 0's band calibrated against its resolve of the others' records
+                plan, w0, hist = record_band_plan(scene, n, costs, rho, stream, inflight, streams,
+                                                  steps)
+            else:
+                plan = dist_tiles.BandPlan.from_costs(sizes, n, 0, costs)
+            bands = [timed(BandProbe(scene, plan, r, stream, inflight, streams, rec))
+                     for r in range(n)]
+            bc = plan.band_costs(costs)
+            band = {"band_ms_per_rank": [round(x, 4) for x in bands],
+                    "band_ms_max": round(max(bands), 4),
+                    "band_cost_max_over_mean": round(float(
+                        bc[1:].max() / bc[1:].mean() if rec and n > 1 else bc.max() / bc.mean()), 4),
+                    "band_tile_row_cuts": plan.cuts[0] if len(plan.cuts) == 1 else plan.cuts,
+                    "predicted_efficiency": round(t1 / (n * max(bands)), 4),
+                    "peer_link_MB_per_step_max": round(max(
+                        (4 if rec else 12) *
+                        sum((b.y1 - b.y0) * plan.sizes[b.camera][0] for b in plan.per_rank[r])
+                        for r in range(1, n)) / 1e6, 3)}
+            if rec:
+                band["resolve_frac_of_frame"] = round(rho, 4)
+                band["root_weight"] = round(w0, 4)
+                band["root_calibration_ms"] = hist
+            bands_by["records" if rec else "rgb"] = (band, max(bands))
+        band_step = bands_by["records" if records else "rgb"][1]
         # ranks > 0 render what the N-GPU bench exchanges (RGB or pixel records); rank 0's
         # share is the same tile work (it renders in place)
         per = [timed(dist_tiles.ShareRenderer(scene, n, r, stream, inflight=inflight,
@@ -434,18 +481,21 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange
         L = dist_tiles.TilePlan(scene, n, 0)
         link = sum(sh.slot for sh in L.shares) * 64 * 4  # bytes per peer per step, per 4 B/px
         tiles = {"share_ms_max": round(max(per), 4), "share_ms_min": round(min(per), 4),
-                       "share_ms_per_rank": [round(x, 4) for x in per],
-                       "root_untile_ms": round(untile, 4),
-                       "root_resolve_ms": None if resolve is None else round(resolve, 4),
-                       "peer_link_MB_per_step": {"rgb": round(3 * link / 1e6, 3),
-                                                 "records": round(link / 1e6, 3)},
-                       "predicted_step_ms": round(slow, 4),
-                       "predicted_efficiency": round(t1 / (n * slow), 4)}
-        step = max(bands) if split == "bands" else slow
-        out[str(n)] = {"split": split, "predicted_step_ms": round(step, 4),
+                 "share_ms_per_rank": [round(x, 4) for x in per],
+                 "root_untile_ms": round(untile, 4),
+                 "root_resolve_ms": None if resolve is None else round(resolve, 4),
+                 "peer_link_MB_per_step": {"rgb": round(3 * link / 1e6, 3),
+                                           "records": round(link / 1e6, 3)},
+                 "predicted_step_ms": round(slow, 4),
+                 "predicted_efficiency": round(t1 / (n * slow), 4)}
+        step = band_step if split == "bands" else slow
+        out[str(n)] = {"split": split, "payload": "records" if records else "rgb",
+                       "predicted_step_ms": round(step, 4),
                        "predicted_efficiency": round(t1 / (n * step), 4),
                        "predicted_Mrays_s_factor": round(t1 / step, 3),
-                       "bands": band, "tiles": tiles}
+                       "bands": bands_by["rgb"][0], "tiles": tiles}
+        if "records" in bands_by:
+            out[str(n)]["bands_records"] = bands_by["records"][0]
     cam = scene.camera(0)
     return {"frame": f"{cam.width}x{cam.height}", "t1_ms": round(t1, 4), "steps": steps,
             "frames_in_flight": inflight, "split": split,
@@ -463,16 +513,30 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange
 
 class BandProbe:
     """Rank r's bands of a BandPlan rendered in place (no exchange): the per-rank render work of
-    the band split, on one GPU."""
+    the band split, on one GPU.  records: ranks > 0 render pixel records, and rank 0 renders RGB
+    and then shades every other band's records (from a whole-frame record buffer rendered once)."""
 
-    def __init__(self, scene, plan, r, stream, inflight, streams):
+    def __init__(self, scene, plan, r, stream, inflight, streams, records=False):
         import torch
         from ceng795_amd import dist_tiles
         self.scene, self.stream, self.streams = scene, stream, streams
         self.bands = plan.per_rank[r]
-        self.render = dist_tiles.scene_band_renderer(scene)
-        self.frames = [[torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
+        self.records = records and r > 0
+        self.resolve = dist_tiles.scene_row_resolver(scene) if records and r == 0 else None
+        self.render = dist_tiles.scene_band_renderer(scene, self.records)
+        shape = (lambda w, h: (h, w)) if self.records else (lambda w, h: (h, w, 3))
+        dt = torch.int32 if self.records else torch.float32
+        self.frames = [[torch.empty(shape(w, h), dtype=dt, device="cuda")
                         for (w, h) in plan.sizes] for _ in range(inflight)]
+        self.recs = None
+        if self.resolve is not None:
+            self.recs = []
+            for c, (w, h) in enumerate(plan.sizes):
+                t = torch.empty((h, w), dtype=torch.int32, device="cuda")
+                scene.render_device(c, t.data_ptr(), records=True,
+                                    stream=torch.cuda.current_stream().cuda_stream)
+                self.recs.append(t)
+            torch.cuda.synchronize()
         for st in streams:
             st.wait_stream(stream)
         self.k = 0
@@ -480,9 +544,15 @@ class BandProbe:
     def step(self, events=None):
         s = self.k % len(self.streams)
         self.k += 1
+        st = self.streams[s]
         for c, b in enumerate(self.bands):
             if b.rows > 0:
-                self.render(b, self.frames[s][c], self.streams[s])
+                self.render(b, self.frames[s][c], st)
+            if self.resolve is not None:
+                h = self.frames[s][c].shape[0]
+                for y0, y1 in ((0, b.y0), (b.y1, h)):
+                    if y1 > y0:
+                        self.resolve(c, y0, y1, self.recs[c], self.frames[s][c], st)
 
     def finish(self):
         for st in self.streams:
@@ -533,9 +603,12 @@ class ResolveProbe:
             self.stream.wait_stream(st)
 
 
-def band_bytes(plan) -> int:
-    """Bytes rank 0 receives per step in the band split: the other ranks' bands as fp32 RGB."""
-    return int(sum(12 * (b.y1 - b.y0) * plan.sizes[b.camera][0]
+def band_bytes(renderer) -> int:
+    """Bytes rank 0 receives per step in the band split: the other ranks' bands as fp32 RGB (12 B
+    per pixel) or as pixel records (4 B)."""
+    plan = renderer.plan
+    per_px = 4 if renderer.records else 12
+    return int(sum(per_px * (b.y1 - b.y0) * plan.sizes[b.camera][0]
                    for r in range(1, plan.world) for b in plan.per_rank[r]))
 
 
@@ -546,8 +619,14 @@ def band_exchange_text(world, comm, renderer, band_costs):
            "the other ranks' bands straight into rank 0's frame rows (no untile)" if world > 1
            else "one-rank rehearsal: rank 0's row band through an RCCL self send / receive pair "
                 "(batch_isend_irecv) into the frame")
+    if renderer.records:
+        txt += ("; the bands travel as 32-bit pixel records (hit primitive + shadow bits, 4 B per "
+                "pixel) that rank 0 shades into its frame (rt_resolve_rows); rank 0's band is "
+                "shrunk by that work")
     out = {"how": txt + ("" if comm == "rccl" else " (gloo: through host copies)"),
-           "band_tile_row_cuts": plan.cuts}
+           "band_tile_row_cuts": plan.cuts, "payload": "records" if renderer.records else "rgb"}
+    if getattr(renderer, "resolve_frac", None) is not None:
+        out["resolve_frac_of_frame"] = round(renderer.resolve_frac, 4)
     if band_costs is not None and len(band_costs) > 1:
         out["band_cost_max_over_mean"] = round(float(max(band_costs) / np.mean(band_costs)), 4)
     return out
@@ -619,25 +698,34 @@ def cpu_rehearsal_bands(args, truth, world, rank, desc) -> int:
     return 0
 
 
-def band_cuts_for(scene, world: int, rank: int, coll_dev: str):
-    """Rank 0 measures every camera's tile costs (whole frames on this GPU) and cuts the bands;
-    the cuts are broadcast so every rank holds the same plan.  Returns (cuts, tile costs or None)."""
+def band_cuts_for(scene, world: int, rank: int, coll_dev: str, records: bool = False,
+                  inflight: int = 4):
+    """Rank 0 measures every camera's tile costs (whole frames on this GPU) and cuts the bands
+    (records: rank 0's band shrunk by its resolve of the others', root_band_weights); the cuts
+    are broadcast so every rank holds the same plan.  Returns (cuts, tile costs or None, the
+    resolve fraction or None)."""
     import torch
     import torch.distributed as dist
     from ceng795_amd import dist_tiles
     sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
-    costs = None
+    costs = rho = None
     flat = []
     if rank == 0:
         costs = dist_tiles.measure_tile_costs(scene)
-        plan = dist_tiles.BandPlan.from_costs(sizes, world, 0, costs)
+        if records:  # rank 0's band sized against its resolve of the others' records
+            rho = dist_tiles.measure_resolve_frac(scene)
+            st = torch.cuda.current_stream()
+            plan, _, _ = record_band_plan(scene, world, costs, rho, st, inflight,
+                                          dist_tiles.render_streams(inflight))
+        else:
+            plan = dist_tiles.BandPlan.from_costs(sizes, world, 0, costs)
         flat = [x for cc in plan.cuts for x in cc]
     t = torch.tensor(flat if rank == 0 else [0] * (len(sizes) * (world + 1)),
                      dtype=torch.int64, device=coll_dev)
     if world > 1:
         dist.broadcast(t, 0)
     v = t.cpu().tolist()
-    return [v[c * (world + 1):(c + 1) * (world + 1)] for c in range(len(sizes))], costs
+    return [v[c * (world + 1):(c + 1) * (world + 1)] for c in range(len(sizes))], costs, rho
 
 
 def cpu_rehearsal(args) -> int:
@@ -741,10 +829,11 @@ def main() -> int:
     ap.add_argument("--gather-stream", choices=("render", "comm"), default="render",
                     help="N>1 tile split: enqueue a step's gather + untile on its own render "
                          "stream (default) or on one communication stream")
-    ap.add_argument("--exchange", choices=("rgb", "records"), default="rgb",
-                    help="N>1 tile split: the shares travel as fp32 RGB (12 B per pixel, untiled "
-                         "by rank 0) or as 32-bit pixel records (4 B, shaded by rank 0: a third "
-                         "of the link bytes for rank 0 re-reading the hit primitives)")
+    ap.add_argument("--exchange", choices=("rgb", "records"), default="records",
+                    help="N>1: the bands / shares travel as 32-bit pixel records (default where "
+                         "the scene allows: 4 B per pixel, shaded by rank 0 — a third of the link "
+                         "bytes for rank 0 re-reading the hit primitives; with bands, rank 0's "
+                         "band is calibrated smaller by that work) or as fp32 RGB (12 B)")
     ap.add_argument("--root-gather", action="store_true",
                     help="N>1 tile split: rank 0 renders its share tile-major and gathers it "
                          "with the others (default: in place, point-to-point receives only)")
@@ -849,7 +938,11 @@ def main() -> int:
     if not use_pg:
         renderer = dist_tiles.FrameRenderer(scene, stream, inflight=args.inflight)
     elif banded:
-        cuts, costs = band_cuts_for(scene, world, rank, coll_dev)
+        # the bands travel as 32-bit pixel records (a third of RGB's link bytes) shaded by rank 0
+        # (rt_resolve_rows), whose band is shrunk by that work
+        records = args.exchange == "records" and dist_tiles.records_ok(scene)
+        cuts, costs, resolve_frac = band_cuts_for(scene, world, rank, coll_dev, records,
+                                                  args.inflight)
         plan = dist_tiles.BandRenderPlan(scene, world, rank, cuts)
         if costs is not None:
             band_costs = plan.band_costs(costs)
@@ -857,7 +950,10 @@ def main() -> int:
             plan, stream, dist_tiles.scene_band_renderer(scene), inflight=args.inflight,
             host_staging=host_staging, device=dev,
             # one-rank rehearsal: rank 0's band through a real RCCL self send / receive
-            self_exchange=args.gather_rehearsal and world == 1)
+            self_exchange=args.gather_rehearsal and world == 1,
+            render_records=dist_tiles.scene_band_renderer(scene, True) if records else None,
+            resolve=dist_tiles.scene_row_resolver(scene) if records else None)
+        renderer.resolve_frac = resolve_frac
     elif tiled:
         layout = dist_tiles.TilePlan(scene, world, rank)
         # shares travel as 32-bit pixel records (a third of RGB's bytes) where the scene allows;
@@ -1054,7 +1150,7 @@ def main() -> int:
                               "4 B per pixel) shaded on rank 0 (rt_resolve_device)"
                               if renderer_records(renderer) else "; shares as fp32 RGB")),
                        "exchange_bytes_per_step": (exchange_bytes(renderer) if tiled else
-                                                   band_bytes(renderer.plan) if banded else None),
+                                                   band_bytes(renderer) if banded else None),
                        "render_ms_avg": round(sum(render_ms) / len(render_ms), 4) if ev else None,
                        "timed_region": "the steps alone: no timing events inside it (kernel "
                                        "and one-frame times are measured after it)",

@@ -98,6 +98,8 @@ SIGNATURES = {
                                          C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
     "rt_scene_records_ok": (C.c_int, [C.c_void_p, C.c_int]),
     "rt_tile_costs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
+    "rt_resolve_rows": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                  C.c_void_p]),
     "rt_resolve_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     "rt_set_kernel_timing": (C.c_int, [C.c_void_p, C.c_int]),

@@ -28,6 +28,8 @@ hipError_t launch_render(const RenderParams& P, const DevNode* nodes, const DevP
 int max_supported_depth();
 hipError_t launch_msaa_resolve(const MsaaResolveParams& M, hipStream_t stream);
 hipError_t launch_untile(const UntileParams& U, hipStream_t stream);
+hipError_t launch_resolve_rows(const RenderParams& P, const unsigned* rec, int row_begin,
+                               int row_end, bool spheres, hipStream_t stream);
 hipError_t launch_resolve(const RenderParams& P, const UntileParams& U, bool spheres,
                           hipStream_t stream);
 unsigned long long read_reset_exact_fallbacks();
@@ -1164,8 +1166,6 @@ int rt_render_device_range(rt_scene* s, int cam, int row0, int row_stride, int t
     if (tile_begin < 0 || tile_step < 1 || !d_out ||
         (tile_major & ~(RT_TILE_MAJOR | RT_TILE_BLOCKS | RT_TILE_RECORDS)))
       throw std::invalid_argument("rt_render_device: bad tile selection / output");
-    if ((tile_major & RT_TILE_RECORDS) && !(tile_major & RT_TILE_MAJOR))
-      throw std::invalid_argument("rt_render_device: RT_TILE_RECORDS needs RT_TILE_MAJOR");
     if ((tile_major & RT_TILE_RECORDS) && !records_ok(s, cam))
       throw std::domain_error("rt_render_device: pixel records need a pixel-centre camera, no "
                               "mirror/dielectric recursion and at most 4 lights");
@@ -1323,6 +1323,24 @@ int rt_resolve_device(rt_scene* s, int cam, int row0, int row_stride, int device
     U.skip_root = (flags & RT_UNTILE_SKIP_ROOT) ? 1 : 0;
     U.vec = 0;
     hip_check(launch_resolve(P, U, s->has_spheres, (hipStream_t)stream), "resolve launch");
+    return RT_OK;
+  });
+}
+
+int rt_resolve_rows(rt_scene* s, int cam, int row_begin, int row_end, const unsigned* d_records,
+                    float* d_out, void* stream) {
+  return guarded([&] {
+    check_render_args(s, cam, 0, 1);
+    const rt_camera& c = s->host.cameras[cam];
+    if (row_begin < 0 || row_end < row_begin || row_end > c.height || !d_records || !d_out)
+      throw std::invalid_argument("rt_resolve_rows: bad argument");
+    if (s->multi) throw std::domain_error("rt_resolve_rows: single-device scenes only");
+    if (!records_ok(s, cam)) throw std::domain_error("rt_resolve_rows: no pixel records here");
+    Replica& r = *s->rep[0];
+    DeviceGuard g(r.device);
+    const RenderParams P = make_params(s, r, cam, 0, 1, 0, 1, 0, d_out, nullptr);
+    hip_check(launch_resolve_rows(P, d_records, row_begin, row_end, s->has_spheres,
+                                  (hipStream_t)stream), "resolve launch");
     return RT_OK;
   });
 }

@@ -1125,14 +1125,15 @@ __device__ __forceinline__ void shade_pixel(const RenderParams& P,
   const int2_t rec = P.hits[pix];
   const bool valid = q.own && hit_leaf(rec) != -2;
   const bool hit = q.own && hit_leaf(rec) >= 0;
-  if (P.records) {  // RT_TILE_RECORDS: the pixel record instead of its colour (rt_resolve_device)
-    if (!q.own) return;
+  if (P.records) {  // RT_TILE_RECORDS: the pixel record instead of its colour (rt_resolve_*)
+    if (!q.own || (!P.tile_major && !valid)) return;
     unsigned r = kRecOutside;
     if (hit)
       r = (unsigned)hit_leaf(rec) | ((P.occ[pix * P.occ_words] & kRecLightMask) << kRecLightShift);
     else if (valid)
       r = kRecMiss;
-    reinterpret_cast<unsigned*>(P.out)[pix] = r;
+    unsigned* o = reinterpret_cast<unsigned*>(P.out);
+    o[P.tile_major ? pix : (size_t)q.py * P.width + q.px] = r;  // tile-major, or row-major
     return;
   }
   V3 color = v3(0.0f, 0.0f, 0.0f);
@@ -1915,6 +1916,49 @@ hipError_t launch_untile(const UntileParams& U, hipStream_t stream) {
 // workgroup.  The hit's t is re-derived by the intersection test the traversal ran (the same ray
 // from the same camera arithmetic, the same primitive record, the same operations: the same
 // bits), the hit point is o + t * d as trace_ray computes it, and shade_hit is the frame kernel's.
+// The colour of pixel (px, py) from its record (not kRecOutside).
+template <bool SPHERES>
+__device__ __forceinline__ V3 resolve_pixel(const RenderParams& P, unsigned rec, int px, int py) {
+  if (rec & kRecMiss) return ld3(P.background);
+  const int leaf = (int)(rec & kRecLeafMask);
+  const V3 e = ld3(P.cam_e), d = primary_dir(P, px, py);
+  const LaneRay ray = make_ray(e, d, P.quot_ok);
+  float th = 0.0f;
+  (void)leaf_test<SPHERES>(P.prims, leaf, ray, th);
+  const unsigned occ = (rec >> kRecLightShift) & kRecLightMask;
+  return shade_hit<SPHERES>(P, P.prims, P.normals, P.materials, P.lights, leaf, e + d * th,
+                            [&](int li) { return ((occ >> li) & 1u) != 0; });
+}
+
+// rt_resolve_rows: row-major pixel records (a row band's, received whole) into the row-major
+// frame, rows [row_begin, row_end) of the camera's own frame; one thread per pixel.
+template <bool SPHERES>
+__global__ __launch_bounds__(256) void resolve_rows_kernel(RenderParams P, const unsigned* rec,
+                                                           int row_begin, int row_end) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long py = row_begin + i / P.width;
+  if (py >= row_end) return;
+  const int px = (int)(i % P.width);
+  const size_t pix = (size_t)py * P.width + px;
+  const V3 color = resolve_pixel<SPHERES>(P, rec[pix], px, (int)py);
+  float* o = P.out + 3 * pix;
+  o[0] = 0.0f + color.x;
+  o[1] = 0.0f + color.y;
+  o[2] = 0.0f + color.z;
+}
+
+hipError_t launch_resolve_rows(const RenderParams& P, const unsigned* rec, int row_begin,
+                               int row_end, bool spheres, hipStream_t stream) {
+  const long long n = (long long)(row_end - row_begin) * P.width;
+  if (n <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (spheres)
+    hipLaunchKernelGGL(resolve_rows_kernel<true>, grid, dim3(256), 0, stream, P, rec, row_begin, row_end);
+  else
+    hipLaunchKernelGGL(resolve_rows_kernel<false>, grid, dim3(256), 0, stream, P, rec, row_begin, row_end);
+  return hipGetLastError();
+}
+
 template <bool SPHERES>
 __global__ __launch_bounds__(256) void resolve_kernel(RenderParams P, UntileParams U) {
   const int t = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -1928,19 +1972,7 @@ __global__ __launch_bounds__(256) void resolve_kernel(RenderParams P, UntilePara
   const unsigned rec = reinterpret_cast<const unsigned*>(U.recv)[(size_t)(r * U.slot + k) * (kTile * kTile) + lane];
   if (rec & kRecOutside) return;
   const int py = U.row0 + lr * U.row_stride;
-  V3 color;
-  if (rec & kRecMiss) {
-    color = ld3(P.background);
-  } else {
-    const int leaf = (int)(rec & kRecLeafMask);
-    const V3 e = ld3(P.cam_e), d = primary_dir(P, px, py);
-    const LaneRay ray = make_ray(e, d, P.quot_ok);
-    float th = 0.0f;
-    (void)leaf_test<SPHERES>(P.prims, leaf, ray, th);
-    const unsigned occ = (rec >> kRecLightShift) & kRecLightMask;
-    color = shade_hit<SPHERES>(P, P.prims, P.normals, P.materials, P.lights, leaf, e + d * th,
-                               [&](int li) { return ((occ >> li) & 1u) != 0; });
-  }
+  const V3 color = resolve_pixel<SPHERES>(P, rec, px, py);
   float* o = U.out + 3 * ((size_t)py * U.width + px);
   o[0] = 0.0f + color.x;
   o[1] = 0.0f + color.y;

@@ -576,43 +576,40 @@ class ShareRenderer:
 # frame, so a rank renders its band in place (a tile range of rt_render_device_range) and
 # rank 0 receives every other band straight into its frame: no untile, nothing extra on rank 0.
 
-def band_cuts(row_costs: Sequence[float], world: int) -> List[int]:
+def band_cuts(row_costs: Sequence[float], world: int,
+              weights: Optional[Sequence[float]] = None) -> List[int]:
     """Cuts 0 = c_0 <= c_1 <= ... <= c_world = len(row_costs) of the rows into `world` contiguous
-    bands (band r = rows [c_r, c_r+1)) whose heaviest band is as light as possible (a binary
-    search over the band capacity with the greedy left-to-right cut)."""
-    w = np.maximum(np.asarray(row_costs, dtype=np.float64), 0.0)
-    n = len(w)
+    bands (band r = rows [c_r, c_r+1)) minimising the heaviest band's cost / weights[r] (weights:
+    each band's share of the work, default equal; rank 0's band is lighter when it also shades the
+    others' pixel records): a binary search over the scale with the greedy in-order fill."""
+    x = np.maximum(np.asarray(row_costs, dtype=np.float64), 0.0)
+    n = len(x)
     if n == 0:
         return [0] * (world + 1)
-    if w.sum() <= 0:
-        w = np.ones(n)
+    if x.sum() <= 0:
+        x = np.ones(n)
+    wt = np.ones(world) if weights is None else np.maximum(np.asarray(weights, np.float64), 0.0)
+    assert len(wt) == world and wt.max() > 0
+    pre = np.concatenate([[0.0], np.cumsum(x)])
 
-    def greedy(cap):
-        cuts, acc = [0], 0.0
-        for i, x in enumerate(w):
-            if acc + x > cap and acc > 0:
-                cuts.append(i)
-                acc = 0.0
-            acc += x
+    def fill(lam):  # each band in turn takes rows while its cost stays within lam * weight
+        cuts, i = [0], 0
+        for r in range(world):
+            # the last row index j with pre[j] - pre[i] <= cap (at least i)
+            j = int(np.searchsorted(pre, pre[i] + lam * wt[r] * (1 + 1e-12), side="right")) - 1
+            i = max(i, min(n, j))
+            cuts.append(i)
         return cuts
 
-    lo, hi = float(w.max()), float(w.sum())
-    for _ in range(60):
+    lo, hi = 0.0, float(pre[-1]) / float(wt.max()) * (1 + 1e-9)
+    for _ in range(80):
         mid = 0.5 * (lo + hi)
-        if len(greedy(mid)) <= world:
+        if fill(mid)[-1] >= n:
             hi = mid
         else:
             lo = mid
-    cuts = greedy(hi)
-    # exactly `world` bands: split the longest bands (in rows) until there are enough; ranks
-    # beyond the row count get empty bands at the end
-    while len(cuts) < world and len(cuts) < n:
-        edges = cuts + [n]
-        k = int(np.argmax(np.diff(edges)))
-        if edges[k + 1] - edges[k] < 2:
-            break
-        cuts.insert(k + 1, (edges[k] + edges[k + 1]) // 2)
-    cuts = sorted(cuts) + [n] * (world + 1 - len(cuts))
+    cuts = fill(hi)
+    cuts[-1] = n
     return [int(c) for c in cuts]
 
 
@@ -657,12 +654,15 @@ class BandPlan:
         self.bands = self.per_rank[rank]
 
     @classmethod
-    def from_costs(cls, sizes, world: int, rank: int, tile_costs: Sequence[np.ndarray]):
-        """tile_costs[c]: camera c's row-major per-tile costs (rt_tile_costs of a whole frame)."""
+    def from_costs(cls, sizes, world: int, rank: int, tile_costs: Sequence[np.ndarray],
+                   weights: Optional[Sequence[float]] = None):
+        """tile_costs[c]: camera c's row-major per-tile costs (rt_tile_costs of a whole frame);
+        weights: each rank's share of the render work (band_cuts)."""
         cuts = []
         for (w, h), cost in zip(sizes, tile_costs):
             tx, ty = tiles_of((w, h))
-            cuts.append(band_cuts(np.asarray(cost, np.float64).reshape(ty, tx).sum(1), world))
+            cuts.append(band_cuts(np.asarray(cost, np.float64).reshape(ty, tx).sum(1), world,
+                                  weights))
         return cls(sizes, world, rank, cuts)
 
     def band_costs(self, tile_costs: Sequence[np.ndarray]) -> np.ndarray:
@@ -696,12 +696,59 @@ def measure_tile_costs(scene, frames: int = 5) -> List[np.ndarray]:
     return out
 
 
-def scene_band_renderer(scene) -> Callable:
-    """Band b of camera b.camera rendered in place into its row-major frame (a tile range)."""
+def measure_resolve_frac(scene, frames: int = 5) -> float:
+    """rt_resolve_rows of a whole frame's pixel records over the frame's in-place render, camera
+    0, each timed alone on one stream (HIP events, median of `frames`): how much of a frame's
+    work rank 0 adds per frame when it shades the others' records."""
+    import torch
+    cam = scene.camera(0)
+    st = torch.cuda.Stream()
+    buf = torch.empty((cam.height, cam.width, 3), dtype=torch.float32, device="cuda")
+    rec = torch.empty((cam.height, cam.width), dtype=torch.int32, device="cuda")
+    scene.render_device(0, rec.data_ptr(), stream=st.cuda_stream, records=True)
+    ren, res = [], []
+    for _ in range(max(1, frames) + 1):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record(st)
+        scene.render_device(0, buf.data_ptr(), stream=st.cuda_stream)
+        e[1].record(st)
+        scene.resolve_rows(0, 0, cam.height, rec.data_ptr(), buf.data_ptr(), stream=st.cuda_stream)
+        e[2].record(st)
+        st.synchronize()
+        ren.append(e[0].elapsed_time(e[1]))
+        res.append(e[1].elapsed_time(e[2]))
+    scene.release_stream(st.cuda_stream)
+    return float(np.median(res[1:]) / max(1e-9, np.median(ren[1:])))
+
+
+def scene_band_renderer(scene, records: bool = False) -> Callable:
+    """Band b of camera b.camera rendered in place into its row-major frame (a tile range);
+    records: as row-major 32-bit pixel records (RT_TILE_RECORDS) into a [h, w] word buffer."""
     def render(b: CameraBand, frame, stream):
         scene.render_device(b.camera, frame.data_ptr(), tile_begin=b.tile_begin, tile_step=1,
-                            tile_count=b.tile_count, stream=stream.cuda_stream)
+                            tile_count=b.tile_count, stream=stream.cuda_stream, records=records)
     return render
+
+
+def scene_row_resolver(scene) -> Callable:
+    """rt_resolve_rows: rows [y0, y1) of camera c's row-major records shaded into its frame."""
+    def resolve(c, y0, y1, records, frame, stream):
+        scene.resolve_rows(c, y0, y1, records.data_ptr(), frame.data_ptr(),
+                           stream=stream.cuda_stream)
+    return resolve
+
+
+def root_band_weights(world: int, resolve_frac: float) -> List[float]:
+    """Band weights when rank 0 also shades the other ranks' pixel records: resolve_frac = the
+    resolve of a whole frame / its render.  Rank 0's band shrinks so that its render plus its
+    resolve of the other (world - 1) / world of the frame takes as long as another rank's band:
+    with T the per-rank time in frame renders, T = (1 + rho (N - 1) / N) / N and rank 0's band
+    is T - rho (N - 1) / N (at least 0)."""
+    if world <= 1:
+        return [1.0]
+    rho = max(0.0, float(resolve_frac)) * (world - 1) / world
+    T = (1.0 + rho) / world
+    return [max(0.0, T - rho) / T] + [1.0] * (world - 1)
 
 
 def BandRenderPlan(scene, world: int, rank: int, cuts=None) -> BandPlan:
@@ -722,7 +769,8 @@ class BandGatherRenderer:
     frames: rank 0's frames of the last step (complete after finish())."""
 
     def __init__(self, plan: BandPlan, stream, render: Callable, inflight: int = 2,
-                 host_staging: bool = False, device=None, self_exchange: bool = False):
+                 host_staging: bool = False, device=None, self_exchange: bool = False,
+                 render_records: Optional[Callable] = None, resolve: Optional[Callable] = None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -740,6 +788,15 @@ class BandGatherRenderer:
         self.local = ([[torch.zeros((h, w, 3), dtype=torch.float32, device=dev)
                         for (w, h) in plan.sizes] for _ in range(self.inflight)]
                       if self.self_loop else None)
+        # pixel records (render_records + resolve): ranks > 0 (and rank 0 in the rehearsal)
+        # render their bands as 32-bit records into a [h, w] word buffer and send those rows;
+        # rank 0 receives them into its own record buffer and shades them into the frame
+        self.records = render_records is not None and resolve is not None
+        self.render_records, self.resolve = render_records, resolve
+        self.rec_sets = ([[torch.zeros((h, w), dtype=torch.int32, device=dev)
+                           for (w, h) in plan.sizes] for _ in range(self.inflight)]
+                         if self.records else None)
+        self.rec_recv = {}  # (set, camera) -> the rehearsal's received record rows
         if not host_staging:
             cur = torch.cuda.current_stream(dev)
             for st in self.rstreams:
@@ -748,6 +805,12 @@ class BandGatherRenderer:
                     st.wait_stream(stream)
         self.k = 0
         self.frames = None
+
+    def _payload(self, s: int, c: int, b: CameraBand, local: bool = False):
+        """What travels for band b: its frame rows (RGB) or its record rows."""
+        if self.records:
+            return self.rec_sets[s][c][b.y0:b.y1]
+        return (self.local if local else self.frame_sets)[s][c][b.y0:b.y1]
 
     def _exchange(self, s: int):
         dist, P = self.dist, self.plan
@@ -758,30 +821,35 @@ class BandGatherRenderer:
                     for r in range(1, P.world):
                         b = P.per_rank[r][c]
                         if b.y1 > b.y0:
-                            dst = self.frame_sets[s][c][b.y0:b.y1]
+                            dst = self._payload(s, c, b)
                             tmp = self.torch.empty(dst.shape, dtype=dst.dtype)
                             dist.recv(tmp, r)
                             dst.copy_(tmp)
                 else:
                     b = P.bands[c]
                     if b.y1 > b.y0:
-                        dist.send(self.frame_sets[s][c][b.y0:b.y1].cpu(), 0)
+                        dist.send(self._payload(s, c, b).cpu(), 0)
         elif P.world > 1:
             for c in range(len(P.sizes)):
                 if self.rank == 0:
                     for r in range(1, P.world):
                         b = P.per_rank[r][c]
                         if b.y1 > b.y0:
-                            ops.append(dist.P2POp(dist.irecv, self.frame_sets[s][c][b.y0:b.y1], r))
+                            ops.append(dist.P2POp(dist.irecv, self._payload(s, c, b), r))
                 else:
                     b = P.bands[c]
                     if b.y1 > b.y0:
-                        ops.append(dist.P2POp(dist.isend, self.frame_sets[s][c][b.y0:b.y1], 0))
+                        ops.append(dist.P2POp(dist.isend, self._payload(s, c, b), 0))
         elif self.self_loop:
             for c, b in enumerate(P.bands):
                 if b.y1 <= b.y0:
                     continue
-                src, dst = self.local[s][c][b.y0:b.y1], self.frame_sets[s][c][b.y0:b.y1]
+                if self.records:  # the record rows travel; the resolve below shades them
+                    src = self._payload(s, c, b)
+                    dst = self.torch.empty_like(src)
+                    self.rec_recv[(s, c)] = dst
+                else:
+                    src, dst = self._payload(s, c, b, local=True), self._payload(s, c, b)
                 if self.host_staging:  # (gloo has no pair to itself)
                     dst.copy_(src)
                 else:
@@ -789,6 +857,22 @@ class BandGatherRenderer:
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
+
+    def _resolve(self, s: int, stream):
+        """Rank 0: shade the received record rows (every band but its own) into the frames."""
+        P = self.plan
+        for c, (w, h) in enumerate(P.sizes):
+            if self.self_loop:
+                b = P.bands[c]
+                if b.y1 > b.y0:
+                    rec = self.rec_sets[s][c]  # the received rows replace the sent ones
+                    rec[b.y0:b.y1].copy_(self.rec_recv[(s, c)])
+                    self.resolve(c, b.y0, b.y1, rec, self.frame_sets[s][c], stream)
+                continue
+            own = P.bands[c]
+            for y0, y1 in ((0, own.y0), (own.y1, h)):
+                if y1 > y0:
+                    self.resolve(c, y0, y1, self.rec_sets[s][c], self.frame_sets[s][c], stream)
 
     def step(self, events=None):
         s = self.k % self.inflight
@@ -799,14 +883,21 @@ class BandGatherRenderer:
         target = self.local[s] if self.self_loop else self.frame_sets[s]
         for c, b in enumerate(self.plan.bands):
             if b.rows > 0:
-                self.render(b, target[c], st)
+                if self.records and (self.rank > 0 or self.self_loop):
+                    self.render_records(b, self.rec_sets[s][c], st)
+                else:  # rank 0's own band: RGB in place
+                    self.render(b, target[c], st)
         if events is not None:
             events[1].record(st)
         if self.host_staging:
             self._exchange(s)
+            if self.records and self.rank == 0:
+                self._resolve(s, st)
         else:
             with self.torch.cuda.stream(st):
                 self._exchange(s)
+                if self.records and self.rank == 0:
+                    self._resolve(s, st)
         if self.rank == 0:
             self.frames = self.frame_sets[s]
         return self.frames

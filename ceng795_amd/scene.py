@@ -175,6 +175,14 @@ class Scene:
                                       out.ctypes.data_as(C.c_void_p), capacity))
         return out[:n]
 
+    def resolve_rows(self, camera_index: int, row_begin: int, row_end: int, records_ptr: int,
+                     out_ptr: int, *, stream: int = 0) -> None:
+        """rt_resolve_rows: row-major pixel records (one 32-bit word per pixel of the frame)
+        shaded into rows [row_begin, row_end) of the row-major frame at ``out_ptr``."""
+        check(lib().rt_resolve_rows(self._h, camera_index, row_begin, row_end,
+                                    C.c_void_p(records_ptr), C.c_void_p(out_ptr),
+                                    C.c_void_p(stream)))
+
     def records_ok(self, camera_index: int) -> bool:
         """rt_scene_records_ok: may this camera's shares travel as pixel records?"""
         return bool(check(lib().rt_scene_records_ok(self._h, camera_index)))

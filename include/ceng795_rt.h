@@ -27,7 +27,8 @@ extern "C" {
 #define CENG795_RT_ABI_VERSION 6  /* 2: MSAA cameras + rt_set_msaa_seed; 3: tile ranges,
                                       kernel timing; 4: multi-device scenes, stream scratch
                                       release, no CULL mode; 5: pixel records
-                                      (RT_TILE_RECORDS, rt_resolve_device); 6: rt_tile_costs */
+                                      (RT_TILE_RECORDS, rt_resolve_device); 6: rt_tile_costs,
+                                      row-major records + rt_resolve_rows */
 
 enum {
   RT_OK = 0,
@@ -184,11 +185,12 @@ int rt_render(rt_scene* scene, int camera_index, int starting_row, int row_strid
 
 /* tile_major flags of rt_render_device / rt_render_device_range */
 enum { RT_TILE_MAJOR = 1, RT_TILE_BLOCKS = 2,
-       RT_TILE_RECORDS = 4  /* with RT_TILE_MAJOR: each pixel as one 32-bit pixel record (the
-                               primary hit's primitive and the shadow bits) instead of 3 floats —
-                               a third of the bytes for the framebuffer gather; rank 0 shades the
-                               gathered records with rt_resolve_device.  Only where
-                               rt_scene_records_ok. */ };
+       RT_TILE_RECORDS = 4  /* each pixel as one 32-bit pixel record (the primary hit's
+                               primitive and the shadow bits) instead of 3 floats — a third of the
+                               bytes for the framebuffer exchange; the gathering rank shades the
+                               records: tile-major shares with rt_resolve_device, row-major ones
+                               (no RT_TILE_MAJOR: a 4-B word per pixel at py * width + px) with
+                               rt_resolve_rows.  Only where rt_scene_records_ok. */ };
 
 /* Device-resident variant (the building block of the one-process-per-GPU image tiling, and
  * of frames kept in HBM).  The image (rows starting_row +
@@ -264,6 +266,12 @@ int rt_resolve_device(rt_scene* scene, int camera_index, int starting_row, int r
  * of the multi-GPU frame split are cut from these (dist_tiles.BandPlan).  Nothing in the
  * reference measures work; its threads take interleaved rows (HW2/main.cpp:33-36). */
 int rt_tile_costs(rt_scene* scene, void* hip_stream, unsigned* host_out, int capacity);
+/* Row-major pixel records (rt_render_device with RT_TILE_RECORDS and no RT_TILE_MAJOR: one
+ * 32-bit word per pixel at py * width + px of d_records) shaded into rows [row_begin, row_end)
+ * of the row-major frame d_out — bit for bit the colours the tracing rank would have written.
+ * The band split's rank 0 runs it over the rows the other ranks sent (dist_tiles.BandPlan). */
+int rt_resolve_rows(rt_scene* scene, int camera_index, int row_begin, int row_end,
+                    const unsigned* d_records, float* d_out, void* hip_stream);
 /* Waits for `hip_stream` and frees the scratch rt_render_device keeps for it (no-op for a
  * stream the scene never rendered on).  Streams that come and go should release theirs. */
 int rt_release_stream_scratch(rt_scene* scene, void* hip_stream);

@@ -324,27 +324,47 @@ def test_bench_self_launches_ranks(tmp_path, world, split):
 
 
 # --------------------------------------------------------------------------- row bands
-def _brute_min_max(w, world):
-    """The lightest possible heaviest band over every way to cut w into `world` contiguous bands."""
+def _brute_min_max(w, world, wt):
+    """The lightest possible heaviest band (cost / weight) over every way to cut w into `world`
+    contiguous bands."""
     import itertools
     n = len(w)
     best = float("inf")
     for cuts in itertools.combinations_with_replacement(range(n + 1), world - 1):
         edges = (0,) + cuts + (n,)
-        best = min(best, max(sum(w[a:b]) for a, b in zip(edges, edges[1:])))
+        best = min(best, max(_load(sum(w[a:b]), x) for a, b, x in zip(edges, edges[1:], wt)))
     return best
 
 
+def _load(cost, weight):
+    return cost / weight if weight > 0 else (float("inf") if cost > 0 else 0.0)
+
+
+@pytest.mark.parametrize("weighted", [False, True])
 @pytest.mark.parametrize("seed", range(6))
 @pytest.mark.parametrize("world", [1, 2, 3, 5])
-def test_band_cuts_minimise_the_heaviest_band(seed, world):
+def test_band_cuts_minimise_the_heaviest_band(seed, world, weighted):
     rng = np.random.default_rng(seed)
     w = rng.integers(1, 50, size=int(rng.integers(1, 9))).astype(float)
-    cuts = dist_tiles.band_cuts(w, world)
+    wt = ([float(rng.choice([0.0, 0.3, 0.6]))] + [1.0] * (world - 1)) if weighted else [1.0] * world
+    if world == 1:
+        wt = [1.0]
+    cuts = dist_tiles.band_cuts(w, world, wt if weighted else None)
     assert len(cuts) == world + 1 and cuts[0] == 0 and cuts[-1] == len(w)
     assert all(a <= b for a, b in zip(cuts, cuts[1:]))
-    heaviest = max(w[a:b].sum() for a, b in zip(cuts, cuts[1:]))
-    assert heaviest <= _brute_min_max(list(w), world) * (1 + 1e-9)
+    heaviest = max(_load(w[a:b].sum(), x) for a, b, x in zip(cuts, cuts[1:], wt))
+    assert heaviest <= _brute_min_max(list(w), world, wt) * (1 + 1e-9)
+
+
+def test_root_band_weights():
+    """Rank 0's band shrinks by its resolve of the others' records: with rho the resolve of a
+    whole frame over its render, every rank's time (in frames) is (1 + rho (N-1)/N) / N."""
+    assert dist_tiles.root_band_weights(1, 0.3) == [1.0]
+    for n, rho in [(2, 0.0), (8, 0.08), (4, 0.5), (8, 5.0)]:
+        wt = dist_tiles.root_band_weights(n, rho)
+        T = (1 + rho * (n - 1) / n) / n
+        assert len(wt) == n and wt[1:] == [1.0] * (n - 1)
+        assert wt[0] == pytest.approx(max(0.0, T - rho * (n - 1) / n) / T)
 
 
 def test_band_plan_covers_every_row_once():
@@ -362,7 +382,7 @@ def test_band_plan_covers_every_row_once():
         assert np.isclose(P.band_costs(costs).sum(), sum(x.sum() for x in costs))
 
 
-def _band_worker(rank, world, port, outdir, sizes, steps, self_exchange=False):
+def _band_worker(rank, world, port, outdir, sizes, steps, self_exchange=False, records=False):
     """The band split's exchange (BandGatherRenderer): each rank writes its bands into its own
     frames (in place, as rt_render_device_range does), the other ranks' bands land in rank 0's
     frames; uneven bands from a random cost map."""
@@ -383,8 +403,20 @@ def _band_worker(rank, world, port, outdir, sizes, steps, self_exchange=False):
         state["rows"] += b.y1 - b.y0
         frame[b.y0:b.y1] = torch.from_numpy(truth(state["step"])[b.camera][b.y0:b.y1])
 
+    def render_records(b, rec, stream):  # a "record" = the pixel's index in the frame
+        state["rows"] += b.y1 - b.y0
+        h, w = rec.shape
+        rec[b.y0:b.y1] = torch.arange(b.y0 * w, b.y1 * w, dtype=torch.int32).view(-1, w)
+
+    def resolve(c, y0, y1, rec, frame, stream):  # ... shaded = looked up in this step's truth
+        flat = torch.from_numpy(truth(state["step"])[c]).view(-1, 3)
+        frame[y0:y1] = flat[rec[y0:y1].reshape(-1).long()].view(y1 - y0, -1, 3)
+
     R = BandGatherRenderer(P, None, render, host_staging=True, device="cpu",
-                           self_exchange=self_exchange)
+                           self_exchange=self_exchange,
+                           render_records=render_records if records else None,
+                           resolve=resolve if records else None)
+    assert R.records == records
     ok = True
     for step in range(steps):
         state["step"] = step
@@ -402,14 +434,16 @@ def _band_worker(rank, world, port, outdir, sizes, steps, self_exchange=False):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("records", [False, True])
 @pytest.mark.parametrize("world,sizes,self_exchange", [(2, [(64, 40), (37, 21)], False),
                                                        (3, [(96, 64)], False),
                                                        (3, [(5, 9)], False),
                                                        (1, [(40, 24), (17, 9)], True)])
-def test_band_exchange(tmp_path, world, sizes, self_exchange):
-    """world 3 on a one-tile-row frame: two ranks get empty bands and send nothing."""
-    mp.spawn(_band_worker, args=(world, _free_port(), str(tmp_path), sizes, 2, self_exchange),
-             nprocs=world, join=True)
+def test_band_exchange(tmp_path, world, sizes, self_exchange, records):
+    """world 3 on a one-tile-row frame: two ranks get empty bands and send nothing.  records:
+    the bands travel as pixel records that rank 0 resolves (every band but its own)."""
+    mp.spawn(_band_worker, args=(world, _free_port(), str(tmp_path), sizes, 2, self_exchange,
+                                 records), nprocs=world, join=True)
     assert (tmp_path / "result").read_text() == "ok"
 
 

@@ -78,3 +78,51 @@ def test_c3_band_costs_balance(scene_dir):
     rows = costs[0].reshape(135, 240).sum(1)
     assert bc.max() - bc.min() <= 2 * rows.max()
     assert bc.max() / bc.mean() < 1.05
+
+
+@pytest.mark.parametrize("name", ["c1", "soup2", "single_sphere", "graze_plane", "c2"])
+def test_record_bands_assemble_the_oracle_frame(scene_dir, name):
+    """Bands as row-major pixel records (RT_TILE_RECORDS without RT_TILE_MAJOR) from ranks > 0,
+    rank 0's (smaller) band in place as RGB, then rt_resolve_rows over every other row: the
+    oracle's frame bit for bit."""
+    import torch
+    import ceng795_amd
+    from ceng795_amd import dist_tiles
+    xml = scenes.write(name, scene_dir)
+    o = OracleScene(xml)
+    with ceng795_amd.Scene(xml) as s:
+        assert dist_tiles.records_ok(s)
+        refs = [o.render(c, threads=8)[0] for c in range(s.num_cameras)]
+        costs = dist_tiles.measure_tile_costs(s, frames=2)
+        rho = dist_tiles.measure_resolve_frac(s, frames=2)
+        assert 0.0 < rho < 5.0
+        rgb = dist_tiles.scene_band_renderer(s)
+        rec_render = dist_tiles.scene_band_renderer(s, records=True)
+        resolve = dist_tiles.scene_row_resolver(s)
+        st = torch.cuda.current_stream()
+        for world in (1, 2, 3, 8):
+            plan = dist_tiles.BandPlan.from_costs(plan_sizes(s), world, 0, costs,
+                                                  dist_tiles.root_band_weights(world, rho))
+            for c, ref in enumerate(refs):
+                h, w, _ = ref.shape
+                frame = torch.full(ref.shape, -1.0, dtype=torch.float32, device="cuda")
+                recs = torch.full((h, w), -1, dtype=torch.int32, device="cuda")
+                own = plan.per_rank[0][c]
+                if own.rows:
+                    rgb(own, frame, st)
+                for r in range(1, world):
+                    b = plan.per_rank[r][c]
+                    if b.rows:
+                        rec_render(b, recs, st)
+                for y0, y1 in ((0, own.y0), (own.y1, h)):
+                    if y1 > y0:
+                        resolve(c, y0, y1, recs, frame, st)
+                torch.cuda.synchronize()
+                what = f"{name}/cam{c}/world{world}"
+                assert assert_parity(frame.cpu().numpy(), ref, what) == 0, what
+                if world == 1:  # and a whole frame of records alone
+                    full = dist_tiles.BandPlan(plan_sizes(s), 1, 0).bands[c]
+                    rec_render(full, recs, st)
+                    resolve(c, 0, h, recs, frame, st)
+                    torch.cuda.synchronize()
+                    assert assert_parity(frame.cpu().numpy(), ref, what + "/all") == 0
