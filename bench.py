@@ -35,6 +35,10 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 METRIC = "Mrays/s at 1920×1080 (primary+shadow); fraction of HBM roofline"
+# frames in flight: whole frames on one GPU gain from six (10,918-10,989 vs 10,635-10,700
+# Mrays/s with four, same box), a rank's 1/N-frame launches from four
+# (profiles/r05/hwq_inflight/runs.txt)
+INFLIGHT_N1, INFLIGHT_SPLIT = 6, 4
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 WORKLOADS = {
     # name: (grid n, width, height, description)
@@ -412,7 +416,7 @@ def record_band_plan(scene, n: int, costs, rho: float, stream, inflight: int, st
 
 
 def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange: str = "rgb",
-                split: str = "bands"):
+                split: str = "bands", streams=None, inflight_n: int = INFLIGHT_SPLIT):
     """Prediction of strong scaling on one GPU (no N-GPU node needed).  t1 = the whole frame
     rendered in place with `inflight` frames in flight, and for each N every rank's work of the
     N-way split alone on this GPU — ALL timed over the same `steps` steps after the same warm-up,
@@ -424,19 +428,24 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange
     from above (the link transfer, overlapped with the rendering of the frames in flight, is
     reported in bytes, not timed)."""
     from ceng795_amd import dist_tiles
-    streams = dist_tiles.render_streams(inflight)  # one set for every run (pool streams)
+    # t1 on the bench's own render streams (`streams`) with the N = 1 line's frames in flight;
+    # every rank's work of an N-way split with the split's frames in flight (`inflight_n`) on
+    # a stream set picked the way a rank of the N-GPU run picks its own (pick_render_streams)
+    streams = dist_tiles.render_streams(inflight, streams=streams)
 
     def timed(R):
         return timed_probe(scene, R, steps)
 
     one = dist_tiles.FrameRenderer(scene, stream, inflight=inflight, streams=streams)
     t1 = timed(one)
+    inflight = inflight_n
     records = exchange == "records" and dist_tiles.records_ok(scene)
     costs = dist_tiles.measure_tile_costs(scene)
     rho = dist_tiles.measure_resolve_frac(scene) if dist_tiles.records_ok(scene) else None
     sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
     out = {}
     for n in ns:
+        streams, set_ms = dist_tiles.pick_render_streams(scene, inflight, n)
         # the band split (bench default): each rank's cost-balanced row band alone, in place;
         # rank 0 receives the others' bands into its frame (records: and shades them, its own
         # band shrunk by that work) — both payloads
@@ -490,6 +499,7 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange
                  "predicted_efficiency": round(t1 / (n * slow), 4)}
         step = band_step if split == "bands" else slow
         out[str(n)] = {"split": split, "payload": "records" if records else "rgb",
+                       "render_stream_sets_ms": set_ms,
                        "predicted_step_ms": round(step, 4),
                        "predicted_efficiency": round(t1 / (n * step), 4),
                        "predicted_Mrays_s_factor": round(t1 / step, 3),
@@ -498,7 +508,8 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange
             out[str(n)]["bands_records"] = bands_by["records"][0]
     cam = scene.camera(0)
     return {"frame": f"{cam.width}x{cam.height}", "t1_ms": round(t1, 4), "steps": steps,
-            "frames_in_flight": inflight, "split": split,
+            "frames_in_flight": {"t1": one.inflight, "per_rank": inflight_n},
+            "split": split,
             "tiles_exchange": "records" if records else "rgb",
             "per_n": out,
             "note": "PREDICTION from one GPU: t1 and every rank's work of one frame, timed over "
@@ -627,6 +638,8 @@ def band_exchange_text(world, comm, renderer, band_costs):
            "band_tile_row_cuts": plan.cuts, "payload": "records" if renderer.records else "rgb"}
     if getattr(renderer, "resolve_frac", None) is not None:
         out["resolve_frac_of_frame"] = round(renderer.resolve_frac, 4)
+    if getattr(renderer, "stream_set_ms", None) is not None:
+        out["render_stream_sets_ms"] = renderer.stream_set_ms
     if band_costs is not None and len(band_costs) > 1:
         out["band_cost_max_over_mean"] = round(float(max(band_costs) / np.mean(band_costs)), 4)
     return out
@@ -699,7 +712,7 @@ def cpu_rehearsal_bands(args, truth, world, rank, desc) -> int:
 
 
 def band_cuts_for(scene, world: int, rank: int, coll_dev: str, records: bool = False,
-                  inflight: int = 4):
+                  inflight: int = 4, streams=None):
     """Rank 0 measures every camera's tile costs (whole frames on this GPU) and cuts the bands
     (records: rank 0's band shrunk by its resolve of the others', root_band_weights); the cuts
     are broadcast so every rank holds the same plan.  Returns (cuts, tile costs or None, the
@@ -716,7 +729,7 @@ def band_cuts_for(scene, world: int, rank: int, coll_dev: str, records: bool = F
             rho = dist_tiles.measure_resolve_frac(scene)
             st = torch.cuda.current_stream()
             plan, _, _ = record_band_plan(scene, world, costs, rho, st, inflight,
-                                          dist_tiles.render_streams(inflight))
+                                          dist_tiles.render_streams(inflight, streams=streams))
         else:
             plan = dist_tiles.BandPlan.from_costs(sizes, world, 0, costs)
         flat = [x for cc in plan.cuts for x in cc]
@@ -851,10 +864,12 @@ def main() -> int:
     ap.add_argument("--precondition-ms", type=float, default=100.0,
                     help="untimed steps for this long before the warm-up steps (the GPU's clock "
                          "ramp; 0 = none)")
-    ap.add_argument("--inflight", type=int, default=4,
+    ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight per GPU: consecutive steps on that many streams / "
                          "buffer sets, so one frame's sparsely occupied last waves (and, N>1, "
-                         "its gather) overlap the next frame; 1 = one frame at a time")
+                         "its exchange) overlap the next frame; 1 = one frame at a time "
+                         "(default: 6 for one GPU's whole frames, 4 for the N>1 split's "
+                         "smaller per-rank launches; profiles/r05/hwq_inflight/)")
     args = ap.parse_args()
     if args.workload == "c5" and (int(os.environ.get("WORLD_SIZE", "1")) > 1
                                   or args.gather_rehearsal):
@@ -902,6 +917,8 @@ def main() -> int:
     device = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     use_pg = world > 1 or args.gather_rehearsal
+    if args.inflight is None:
+        args.inflight = INFLIGHT_N1 if not use_pg else INFLIGHT_SPLIT
     if use_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(29577))
@@ -941,8 +958,13 @@ def main() -> int:
         # the bands travel as 32-bit pixel records (a third of RGB's link bytes) shaded by rank 0
         # (rt_resolve_rows), whose band is shrunk by that work
         records = args.exchange == "records" and dist_tiles.records_ok(scene)
+        # the render streams first, picked by measurement (pick_render_streams): the
+        # calibration runs on the streams the steps will use
+        rstreams, stream_ms = ((None, None) if host_staging else
+                               dist_tiles.pick_render_streams(scene, args.inflight, world,
+                                                              device=dev))
         cuts, costs, resolve_frac = band_cuts_for(scene, world, rank, coll_dev, records,
-                                                  args.inflight)
+                                                  args.inflight, rstreams)
         plan = dist_tiles.BandRenderPlan(scene, world, rank, cuts)
         if costs is not None:
             band_costs = plan.band_costs(costs)
@@ -952,8 +974,10 @@ def main() -> int:
             # one-rank rehearsal: rank 0's band through a real RCCL self send / receive
             self_exchange=args.gather_rehearsal and world == 1,
             render_records=dist_tiles.scene_band_renderer(scene, True) if records else None,
-            resolve=dist_tiles.scene_row_resolver(scene) if records else None)
+            resolve=dist_tiles.scene_row_resolver(scene) if records else None,
+            streams=rstreams)
         renderer.resolve_frac = resolve_frac
+        renderer.stream_set_ms = stream_ms
     elif tiled:
         layout = dist_tiles.TilePlan(scene, world, rank)
         # shares travel as 32-bit pixel records (a third of RGB's bytes) where the scene allows;
@@ -1095,13 +1119,15 @@ def main() -> int:
                 cold = cold_frame_ms(scene)
                 if not args.no_share_probe:
                     probe = share_probe(scene, stream, max(20, args.steps), args.inflight,
-                                        exchange=args.exchange, split=args.split)
+                                        exchange=args.exchange, split=args.split,
+                                        streams=renderer.streams)
                     if args.workload == "c3":
                         # the north star's 8-GPU configuration: C4 (3840x2160), same mesh
                         with ceng795_amd.Scene(scene_path("c4", 1), device=device,
                                                traversal=args.traversal) as s4:
                             probe_c4 = share_probe(s4, stream, max(20, args.steps), args.inflight,
-                                               exchange=args.exchange, split=args.split)
+                                               exchange=args.exchange, split=args.split,
+                                               streams=renderer.streams)
             except Exception as e:
                 log(f"one-frame / share probe failed: {e!r}")
         host_rate = None

@@ -41,10 +41,10 @@ def render_streams(n: int, device=None, streams=None) -> list:
     """`n` render streams for frames in flight: `streams` when given (reused, e.g. one set for
     every renderer of a probe), else n consecutive streams of torch's per-device stream pool —
     never the caller's default stream.  HIP hands the process's hardware queues
-    (GPU_MAX_HW_QUEUES, 4 on this pool) to streams in turn at creation, and two streams on one
-    queue serialise their kernels; the pool's streams were created together, so n <= 4
-    consecutive ones sit on n different queues, whereas the default stream shares its queue with
-    one pool stream in four.  (Rendering on the default stream plus three pool streams made the
+    (GPU_MAX_HW_QUEUES: HIP's default 4, bench.py sets 8) to streams in turn at creation, and two
+    streams on one queue serialise their kernels; streams created together sit on different
+    queues as long as there are enough, whereas the default stream shares its queue with one of
+    them.  (Rendering on the default stream plus three pool streams made the
     one-GPU share probe bimodal: 0.056 or 0.093 ms for the same 1/8 share)"""
     import torch
     if streams is not None:
@@ -52,6 +52,48 @@ def render_streams(n: int, device=None, streams=None) -> list:
         assert len(out) == n, "need one stream per frame in flight"
         return out
     return [torch.cuda.Stream(device=device) for _ in range(n)]
+
+
+def pick_render_streams(scene, inflight: int, world: int, sets: int = 3, steps: int = 12,
+                        device=None):
+    """The render streams for a rank's small per-step launches, chosen by measurement: `sets`
+    fresh stream sets, each timed rendering the middle 1/world of camera 0's tile rows in place
+    with `inflight` frames in flight, the fastest kept.  HIP maps streams to hardware queues
+    when they are created, and which set a rank gets decides the time of its small launches: a
+    1/8 band of the C3 frame took 0.071-0.085 ms per step on the first set a process created and
+    0.055-0.060 on the next ones, with GPU_MAX_HW_QUEUES 4 (whole frames: within 1 %;
+    profiles/r05/stream_sets/).  Returns (streams, ms per step of each set)."""
+    import time
+    import torch
+    cam = scene.camera(0)
+    tx, ty = tiles_of((cam.width, cam.height))
+    rows = max(1, ty // max(1, world))
+    b = CameraBand(0, (ty - rows) // 2, rows, tx, 0, 0)
+    frames = [torch.empty((cam.height, cam.width, 3), dtype=torch.float32, device="cuda")
+              for _ in range(inflight)]
+    best, best_ms, times = None, float("inf"), []
+    for _ in range(max(1, sets)):
+        S = render_streams(inflight, device)
+        for st in S:
+            st.wait_stream(torch.cuda.current_stream())
+
+        def run(k):
+            for i in range(k):
+                scene.render_device(0, frames[i % inflight].data_ptr(), tile_begin=b.tile_begin,
+                                    tile_step=1, tile_count=b.tile_count,
+                                    stream=S[i % inflight].cuda_stream)
+            for st in S:
+                torch.cuda.current_stream().wait_stream(st)
+            torch.cuda.synchronize()
+        run(2 * inflight)
+        t0 = time.perf_counter()
+        run(steps)
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        times.append(round(ms, 4))
+        if ms < best_ms:
+            best, best_ms = S, ms
+    scene.collect_stats()
+    return best, times
 
 
 def tiles_of(size: Tuple[int, int]) -> Tuple[int, int]:
@@ -770,7 +812,8 @@ class BandGatherRenderer:
 
     def __init__(self, plan: BandPlan, stream, render: Callable, inflight: int = 2,
                  host_staging: bool = False, device=None, self_exchange: bool = False,
-                 render_records: Optional[Callable] = None, resolve: Optional[Callable] = None):
+                 render_records: Optional[Callable] = None, resolve: Optional[Callable] = None,
+                 streams=None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -782,7 +825,7 @@ class BandGatherRenderer:
         self.self_loop = bool(self_exchange) and plan.world == 1
         dev = device if device is not None else (
             "cpu" if host_staging else torch.device("cuda", torch.cuda.current_device()))
-        self.rstreams = [stream] if host_staging else render_streams(self.inflight, dev)
+        self.rstreams = [stream] if host_staging else render_streams(self.inflight, dev, streams)
         self.frame_sets = [[torch.zeros((h, w, 3), dtype=torch.float32, device=dev)
                             for (w, h) in plan.sizes] for _ in range(self.inflight)]
         self.local = ([[torch.zeros((h, w, 3), dtype=torch.float32, device=dev)
