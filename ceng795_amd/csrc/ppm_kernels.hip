@@ -1438,17 +1438,10 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(PPM
       }
       __syncthreads();
       PPM_PHASE(4)
-      // (4) the exact recurrence, in photon order: a candidate is applied up to its
-      // multiplicity times while it stays inside the shrinking radius (the update count is
-      // derived from cnt afterwards, so the loop carries no counter of its own)
-      // Packed fp32: (flux.x, flux.y) and (flux.z, r^2) are updated by v_pk_add/v_pk_mul
-      // pairs, each element rounded as its scalar op; r^2 + 0 = r^2 exactly (r^2 > 0).
-      // Candidates go in batches of kB: all their LDS operands are loaded up front, and the
-      // batch is applied branch-free on the assumption that each candidate is accepted, so
-      // candidate k uses the staged rr(n) k places on.  The first rejected candidate ends the
-      // batch (it changes nothing; the ones after it are redone with the right rr).  A batch
-      // holding a multiplicity > 1, or reaching past the staged rr(n), takes the scalar path
-      // for its first candidate.
+      // (4) the exact recurrence, in photon order: wave gw applies this round's candidates of
+      // its hit point (gate_round: radius table, acceptance runs, flux chains; a candidate of
+      // multiplicity > 1 sends the round through the one-at-a-time loop), after sliding its
+      // staged rr(n) cache to the hit point's count when the round could run past it
       if (gw < nh && S.diag != 1) {
         const int gb = s_wc[gw * nwords];
         const int ge = gw + 1 < nh ? s_wc[(gw + 1) * nwords] : ncand;
