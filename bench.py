@@ -1063,9 +1063,11 @@ def main() -> int:
                 verified &= bool(torch.equal(ref.view(torch.int32), f.view(torch.int32)))
             log(f"[rank 0] gathered frames bit-identical to single-GPU renders: {verified}")
         if strong:
-            # t1: the same job rendered by this GPU alone, in place, with the same frames in
-            # flight (the N = 1 bench path)
-            one = dist_tiles.FrameRenderer(scene, stream, inflight=args.inflight)
+            # t1: the same job rendered by this GPU alone, in place, as the N = 1 bench renders
+            # it (its frames in flight, a picked stream set)
+            one_streams, _ = dist_tiles.pick_render_streams(scene, INFLIGHT_N1, 1, device=dev)
+            one = dist_tiles.FrameRenderer(scene, stream, inflight=INFLIGHT_N1,
+                                           streams=one_streams)
             for _ in range(max(1, args.warmup)):
                 one.step()
             one.finish()
