@@ -419,11 +419,14 @@ __device__ __forceinline__ bool advance(WaveStack<DEEP>& st, int c0, int c1, uin
 // implies every enclosing reference box accepts, else guard_exact over the
 // ancestry — so exactly the leaves the reference reaches are tested.  Without CULL (reference
 // walk) an entry is a DFS leaf whose boxes the walk has already decided.
-#ifndef RT_BATCH_FLUSH
-#define RT_BATCH_FLUSH 160
-#endif
-constexpr int kBatchFlush = RT_BATCH_FLUSH;   // run the queue once this many tests are pending
-constexpr int kBatchCap = kBatchFlush + 256;  // a wide visit flushes before a slot could overflow
+// The queue is flushed only between visits, once kBatchFlush tests are pending, and holds a whole
+// wide visit's pushes (8 slots x 2 leaves x 64 lanes) above that: no flush inside the slot loop.
+// (Round 5: the in-loop check inlined the batch test into every slot and held 69 SGPRs in VGPR
+// lanes; without it 7 spill and the C3 frame kernel runs 0.406 -> 0.395 ms, four in flight
+// 0.385 -> 0.374, profiles/r05/ab_visit_flush.json.  LDS: 22.6 KB per 4-wave workgroup, seven
+// workgroups per CU.)
+constexpr int kBatchFlush = 128;
+constexpr int kBatchCap = kBatchFlush + kWideSlots * 2 * 64;
 constexpr int kShadowFlush = kBatchFlush;
 
 // The primary traversal's queue pushes write every lane: lanes outside the push mask write a
@@ -662,10 +665,6 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
     if (kinds & (kSlotLeafy << c)) {
       const int leaf = leaf_base + (int)((offs >> (4 * c)) & 15u);
       const bool pair = (kinds & (kSlotPair << c)) != 0;
-      if (pending > kBatchCap - 128) {
-        batch_flush<SHADOW, SPHERES, true, SKIP>(P, L, pending, r, thr, dg);
-        pending = 0;
-      }
       // (the shadow kernel keeps the exec-mask pushes: junk writes cost it VGPR spills)
       if (pair)
         batch_push_pair<!SHADOW>(L, pending, leaf, hm);
