@@ -856,6 +856,9 @@ def main() -> int:
     ap.add_argument("--kernel-timing", action="store_true",
                     help="HIP events around the kernels inside the timed region too (the "
                          "roofline always uses one-frame-at-a-time times after it)")
+    ap.add_argument("--split-inflight", type=int, default=INFLIGHT_SPLIT,
+                    help="frames in flight per rank of the N>1 split (and of the N=1 line's "
+                         "prediction of it)")
     ap.add_argument("--no-share-probe", action="store_true",
                     help="N=1: skip the one-GPU prediction of strong scaling (share probe)")
     ap.add_argument("--cpu-rehearsal", action="store_true",
@@ -918,7 +921,7 @@ def main() -> int:
     torch.cuda.set_device(device)
     use_pg = world > 1 or args.gather_rehearsal
     if args.inflight is None:
-        args.inflight = INFLIGHT_N1 if not use_pg else INFLIGHT_SPLIT
+        args.inflight = INFLIGHT_N1 if not use_pg else args.split_inflight
     if use_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(29577))
@@ -1127,14 +1130,16 @@ def main() -> int:
                 if not args.no_share_probe:
                     probe = share_probe(scene, stream, max(20, args.steps), args.inflight,
                                         exchange=args.exchange, split=args.split,
-                                        streams=renderer.streams)
+                                        streams=renderer.streams,
+                                        inflight_n=args.split_inflight)
                     if args.workload == "c3":
                         # the north star's 8-GPU configuration: C4 (3840x2160), same mesh
                         with ceng795_amd.Scene(scene_path("c4", 1), device=device,
                                                traversal=args.traversal) as s4:
                             probe_c4 = share_probe(s4, stream, max(20, args.steps), args.inflight,
                                                exchange=args.exchange, split=args.split,
-                                               streams=renderer.streams)
+                                               streams=renderer.streams,
+                                               inflight_n=args.split_inflight)
             except Exception as e:
                 log(f"one-frame / share probe failed: {e!r}")
         host_rate = None
