@@ -315,6 +315,7 @@ void create_device(ppm_scene* s, int device) {
   S.materials = own(s, h.materials, "upload materials");
   S.top_root = h.top_root;
   S.max_depth = h.max_depth;
+  S.lds_stack = (h.top_depth + 1 <= kLdsStack && h.mesh_depth + 1 <= kLdsStack) ? 1 : 0;
   S.eps = h.eps;
 #ifdef PPM_DIAG_LEVEL  // experiment builds (make ppm-exp EXTRA=-DPPM_DIAG_LEVEL=2): diag counters
   S.diag = PPM_DIAG_LEVEL;

@@ -11,6 +11,8 @@ constexpr int kMatDiffuse = 0, kMatMirror = 1, kMatRefractive = 2;  // Material.
 constexpr int kObjSphere = 0, kObjInstance = 1;
 constexpr int kTopStack = 48;   // per-lane traversal stacks (host checks the BVH depths)
 constexpr int kMeshStack = 64;
+constexpr int kLdsStack = 12;   // ... in LDS when both BVHs fit this many levels (PScene::lds_stack)
+constexpr int kPpmThreads = 256;  // workgroup size of the eye and photon kernels
 constexpr int kEyeStack = 24;   // eye-ray tree: <= MaxRecursionDepth (<= 20) + 1 pending
 constexpr int kStatSlots = 36;  // device counter words (ppm_collect_stats)
 constexpr int kMaxCells = 27;
@@ -91,6 +93,7 @@ struct PScene {  // device pointers + scalars, passed by value to every kernel
   float light_pos[3], light_intensity[3];
   int diag;  // timing experiments only (CENG795_PPM_DIAG): 1 = skip the update recurrence
   int compact_seg;  // update pass: deposits per compaction segment (ppm_set_update_segment)
+  int lds_stack;    // 1: both BVHs fit kLdsStack levels, the traversal stacks live in LDS
 };
 
 struct PCamera {

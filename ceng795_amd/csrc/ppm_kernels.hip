@@ -174,9 +174,30 @@ struct Hit {
   float beta, gamma;
 };
 
+// Per-lane traversal stacks.  LDS (the launchers' choice when both BVHs fit kLdsStack levels,
+// PScene::lds_stack): thread t's entry d at s[d][t], consecutive threads in consecutive banks,
+// 24 KiB per 256-thread workgroup for the top-level and mesh stacks together.  Else a private
+// array, which the compiler keeps in scratch (dynamically indexed).  Round 5: the C5 photon pass
+// 16.4-16.7 -> 15.9-16.0 ms with LDS stacks (photon kernel scratch 464 -> 60 B per lane).
+template <bool LDS, int N, int WHICH>
+struct TraceStack {
+  int s[N];
+  __device__ __forceinline__ int& operator[](int d) { return s[d]; }
+};
+template <int N, int WHICH>
+struct TraceStack<true, N, WHICH> {
+  int* base;
+  __device__ __forceinline__ TraceStack() {
+    __shared__ int s_stk[kLdsStack][kPpmThreads];
+    base = &s_stk[0][threadIdx.x];
+  }
+  __device__ __forceinline__ int& operator[](int d) { return base[d * kPpmThreads]; }
+};
+
 // Mesh::intersect -> the mesh's BVH with the local ray (Mesh.h:21-27, BVH.cpp:30-52): the
 // first triangle in DFS order with the smallest t > 0.  A one-triangle mesh (create_bvh
 // returns the triangle itself) gives the raw test, t > -1e-4 included.
+template <bool LDS>
 __device__ bool mesh_closest(const PScene& S, int root, const Ray& rl, bool culling, Hit& h) {
   float t, b, g;
   if (root < 0) {
@@ -184,7 +205,7 @@ __device__ bool mesh_closest(const PScene& S, int root, const Ray& rl, bool cull
     h.t = t, h.tri = ~root, h.beta = b, h.gamma = g;
     return true;
   }
-  int stack[kMeshStack];
+  TraceStack<LDS, kMeshStack, 1> stack;
   int sp = 0;
   stack[sp++] = root;
   bool any = false;
@@ -205,6 +226,7 @@ __device__ bool mesh_closest(const PScene& S, int root, const Ray& rl, bool cull
 }
 
 // Shape::intersect of a top-level object, unfiltered (the parent BVH node filters t > 0).
+template <bool LDS>
 __device__ __forceinline__ bool object_test(const PScene& S, int obj, const Ray& r,
                                             bool culling, Hit& h) {
   const PObject& o = S.objects[obj];
@@ -217,14 +239,15 @@ __device__ __forceinline__ bool object_test(const PScene& S, int obj, const Ray&
   // refractive instances are never culled.
   if (!box_accept(o.lo, o.hi, r)) return false;
   const Ray rl{mul_point(o.inv, r.o), mul_vector(o.inv, 4, r.d)};
-  return mesh_closest(S, S.meshes[o.mesh].root, rl, o.refractive ? false : culling, h);
+  return mesh_closest<LDS>(S, S.meshes[o.mesh].root, rl, o.refractive ? false : culling, h);
 }
 
 // bvh->intersect(ray, intersection, true) at the top level (BVH.cpp:30-52).
+template <bool LDS>
 __device__ bool closest(const PScene& S, const Ray& r, Hit& best) {
   if (S.top_root == INT_MIN) return false;
-  if (S.top_root < 0) return object_test(S, ~S.top_root, r, true, best);  // root = one object
-  int stack[kTopStack];
+  if (S.top_root < 0) return object_test<LDS>(S, ~S.top_root, r, true, best);  // root = one object
+  TraceStack<LDS, kTopStack, 0> stack;
   int sp = 0;
   stack[sp++] = S.top_root;
   bool any = false;
@@ -239,7 +262,7 @@ __device__ bool closest(const PScene& S, const Ray& r, Hit& best) {
       continue;
     }
     Hit h;
-    if (object_test(S, ~e, r, true, h) && h.t > 0.0f && h.t < best.t) {
+    if (object_test<LDS>(S, ~e, r, true, h) && h.t > 0.0f && h.t < best.t) {
       best = h;
       any = true;
     }
@@ -319,7 +342,7 @@ struct EyeItem {
 
 // eye_trace (Scene.cpp:286-361) of one primary ray, depth first (reflection subtree before
 // the refraction one).  WRITE: store the hit points at out[k++]; always counts them.
-template <bool WRITE>
+template <bool WRITE, bool LDS>
 __device__ int eye_trace(const PScene& S, const Ray& primary, int pixel, PHitPoint* out, int k,
                          unsigned long long& rays) {
   EyeItem stack[kEyeStack];
@@ -329,7 +352,7 @@ __device__ int eye_trace(const PScene& S, const Ray& primary, int pixel, PHitPoi
     const EyeItem it = stack[--sp];
     Hit h;
     rays++;
-    if (!closest(S, it.ray, h)) continue;
+    if (!closest<LDS>(S, it.ray, h)) continue;
     const V x = point_at(it.ray, h.t);
     const V normal = hit_normal(S, it.ray, h);
     const int mid = S.objects[h.obj].material;
@@ -390,9 +413,11 @@ __device__ __forceinline__ int cell(float v) { const int i = (int)v; return i < 
 
 // ------------------------------------------------------------------ eye pass
 // counts != null: pass 1 (hit points per pixel); else pass 2 writes at offsets[pixel].
-__global__ __launch_bounds__(256) void eye_kernel(PScene S, PCamera C, unsigned long long seed,
-                                                  int* counts, const int* offsets,
-                                                  PHitPoint* out, unsigned long long* stats) {
+template <bool LDS>
+__global__ __launch_bounds__(kPpmThreads) void eye_kernel(PScene S, PCamera C,
+                                                          unsigned long long seed, int* counts,
+                                                          const int* offsets, PHitPoint* out,
+                                                          unsigned long long* stats) {
   const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   const bool active = p < C.width * C.height;
   unsigned long long rays = 0;
@@ -402,7 +427,8 @@ __global__ __launch_bounds__(256) void eye_kernel(PScene S, PCamera C, unsigned 
     int k = write ? offsets[p] : 0;
     if (C.samples == 1) {  // Scene.cpp:257-263
       const Ray r = camera_ray(C, i + 0.5f, j + 0.5f);
-      k = write ? eye_trace<true>(S, r, p, out, k, rays) : eye_trace<false>(S, r, p, out, k, rays);
+      k = write ? eye_trace<true, LDS>(S, r, p, out, k, rays)
+                : eye_trace<false, LDS>(S, r, p, out, k, rays);
     } else {  // Scene.cpp:264-284: at most 2x2 jittered samples
       const int n = C.samples < 2 ? C.samples : 2;
       ppm_math::Rng rng(seed, ppm_math::kEyeStream | (unsigned long long)p);
@@ -413,8 +439,8 @@ __global__ __launch_bounds__(256) void eye_kernel(PScene S, PCamera C, unsigned 
           const float sx = (x + ex) / n;
           const float sy = (y + ey) / n;
           const Ray r = camera_ray(C, i + sx, j + sy);
-          k = write ? eye_trace<true>(S, r, p, out, k, rays)
-                    : eye_trace<false>(S, r, p, out, k, rays);
+          k = write ? eye_trace<true, LDS>(S, r, p, out, k, rays)
+                    : eye_trace<false, LDS>(S, r, p, out, k, rays);
         }
     }
     if (!write) counts[p] = k;
@@ -529,6 +555,7 @@ __device__ __forceinline__ void emit_photon(const PScene& S, unsigned long long 
 }
 
 // One segment of photon_trace (Scene.cpp:106-249) for photon i; false when the chain ends.
+template <bool LDS>
 __device__ __forceinline__ bool photon_segment(const PScene& S, int i, int count, PDeposit* slots,
                                                PhotonState& P, unsigned long long& rays,
                                                unsigned long long& deps) {
@@ -537,7 +564,7 @@ __device__ __forceinline__ bool photon_segment(const PScene& S, int i, int count
   Hit h;
   rays++;
   const Ray ray = P.ray;
-  if (!closest(S, ray, h)) return false;
+  if (!closest<LDS>(S, ray, h)) return false;
   const V x = point_at(ray, h.t);
   const V normal = hit_normal(S, ray, h);
   const PMaterial& m = S.materials[S.objects[h.obj].material];
@@ -589,10 +616,11 @@ __device__ __forceinline__ bool photon_segment(const PScene& S, int i, int count
   return true;
 }
 
-__global__ __launch_bounds__(256) void photon_kernel(PScene S, unsigned long long seed,
-                                                     long long first, int count, int K,
-                                                     PDeposit* slots, int* ndep,
-                                                     unsigned long long* stats) {
+template <bool LDS>
+__global__ __launch_bounds__(kPpmThreads) void photon_kernel(PScene S, unsigned long long seed,
+                                                             long long first, int count, int K,
+                                                             PDeposit* slots, int* ndep,
+                                                             unsigned long long* stats) {
   unsigned long long rays = 0, deps = 0;
   PhotonState P;
   __shared__ int s_next;
@@ -619,7 +647,7 @@ __global__ __launch_bounds__(256) void photon_kernel(PScene S, unsigned long lon
       }
     }
     if (!__ballot(i >= 0)) break;  // range exhausted and every chain ended
-    if (i >= 0 && !photon_segment(S, i, count, slots, P, rays, deps)) {
+    if (i >= 0 && !photon_segment<LDS>(S, i, count, slots, P, rays, deps)) {
       ndep[i] = P.k;
       i = -1;
     }
@@ -1526,14 +1554,19 @@ __global__ __launch_bounds__(256) void density_kernel(const PHitPoint* hps, cons
 }
 
 // ------------------------------------------------------------------ launchers (ppm_api.hip)
-constexpr int kThreads = 256;
+constexpr int kThreads = kPpmThreads;
 static int blocks_for(long long n) { return (int)((n + kThreads - 1) / kThreads); }
 
 hipError_t launch_eye(const PScene& S, const PCamera& C, unsigned long long seed, int* counts,
                       const int* offsets, PHitPoint* out, unsigned long long* stats,
                       hipStream_t st) {
-  hipLaunchKernelGGL(eye_kernel, dim3(blocks_for((long long)C.width * C.height)), dim3(kThreads),
-                     0, st, S, C, seed, counts, offsets, out, stats);
+  const dim3 grid(blocks_for((long long)C.width * C.height));
+  if (S.lds_stack)
+    hipLaunchKernelGGL(eye_kernel<true>, grid, dim3(kThreads), 0, st, S, C, seed, counts, offsets,
+                       out, stats);
+  else
+    hipLaunchKernelGGL(eye_kernel<false>, grid, dim3(kThreads), 0, st, S, C, seed, counts,
+                       offsets, out, stats);
   return hipGetLastError();
 }
 hipError_t launch_grid(const PHitPoint* hps, int n, int w, int h, PGrid* grid, float4* state,
@@ -1547,8 +1580,12 @@ hipError_t launch_photons(const PScene& S, unsigned long long seed, long long fi
   // workgroups of a contiguous photon range each (2048: 3.99 ms, 4096: 3.72 ms on C5)
   const int blocks = std::min(blocks_for(count), PPM_PHOTON_BLOCKS);
   if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(photon_kernel, dim3(blocks), dim3(kThreads), 0, st, S, seed,
-                     first, count, K, slots, ndep, stats);
+  if (S.lds_stack)
+    hipLaunchKernelGGL(photon_kernel<true>, dim3(blocks), dim3(kThreads), 0, st, S, seed, first,
+                       count, K, slots, ndep, stats);
+  else
+    hipLaunchKernelGGL(photon_kernel<false>, dim3(blocks), dim3(kThreads), 0, st, S, seed, first,
+                       count, K, slots, ndep, stats);
   return hipGetLastError();
 }
 hipError_t launch_deposit_keys(const PDeposit* slots, const int* ndep, const int* offsets,

@@ -97,13 +97,20 @@ PPM = {
                     "MaxRecursionDepth 3 cuts eye and photon paths"),
 }
 
+# GPU-vs-oracle only (no reference goldens): a mesh BVH deeper than the kernels' LDS traversal
+# stacks, so the eye and photon kernels take their scratch-stack variants.
+PPM_DEEP = {
+    "ppm_deep": (lambda: GP.cornell(40, 40, photons=6000, iterations=10, variant="deep"),
+                 "4,608-triangle floor mesh: BVH deeper than the LDS stacks (scratch stacks)"),
+}
+
 
 def write_ppm(name: str, directory: str) -> str:
     path = os.path.join(directory, f"{name}.xml")
     if not os.path.exists(path):
         tmp = path + ".tmp"
         with open(tmp, "w") as f:
-            f.write(PPM[name][0]())
+            f.write({**PPM, **PPM_DEEP}[name][0]())
         os.replace(tmp, path)
     return path
 

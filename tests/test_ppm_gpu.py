@@ -24,7 +24,7 @@ def bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
-@pytest.mark.parametrize("name", list(scenes.PPM))
+@pytest.mark.parametrize("name", list(scenes.PPM) + list(scenes.PPM_DEEP))
 def test_eye_pass_and_grid_match_oracle(ppm, scene_dir, name):
     xml = scenes.write_ppm(name, scene_dir)
     o = OraclePPM(xml)
@@ -39,7 +39,7 @@ def test_eye_pass_and_grid_match_oracle(ppm, scene_dir, name):
         assert np.array_equal(np.float32(info), np.float32(oinfo))
 
 
-@pytest.mark.parametrize("name", list(scenes.PPM))
+@pytest.mark.parametrize("name", list(scenes.PPM) + list(scenes.PPM_DEEP))
 def test_photon_updates_match_oracle(ppm, scene_dir, name):
     xml = scenes.write_ppm(name, scene_dir)
     o = OraclePPM(xml)

@@ -113,6 +113,17 @@ def cornell(width: int = 256, height: int = 256, photons: int = 10000, iteration
                 add((0.0, 0.05, 0.0))]
         prism = [(base[0], base[1], base[2]), (base[0], base[3], base[1]),  # outward normals
                  (base[1], base[3], base[2]), (base[2], base[3], base[0])]
+    grid = []
+    if variant == "deep":  # the floor as a 48 x 48 grid of quads: a mesh BVH of 13+ levels
+        n = 48
+        idx = {}
+        for j in range(n + 1):
+            for i in range(n + 1):
+                idx[(i, j)] = add((-1 + 2 * i / n, -1.0, 1 - 2 * j / n))
+        for j in range(n):
+            for i in range(n):
+                a, b, cc, d = idx[(i, j)], idx[(i + 1, j)], idx[(i + 1, j + 1)], idx[(i, j + 1)]
+                grid += [(a, b, cc), (a, cc, d)]
     lines.append("  <VertexData>")
     lines += ["    " + _v(v) for v in verts]
     lines.append("  </VertexData>")
@@ -122,6 +133,12 @@ def cornell(width: int = 256, height: int = 256, photons: int = 10000, iteration
     for name, quad in walls.items():
         a, b, cc, d = (c[q] for q in quad)
         mesh_id += 1
+        if name == "floor" and grid:
+            lines += [f"    <Mesh id=\"{mesh_id}\">", f"      <Material>{wall_mat[name]}</Material>",
+                      "      <Faces>"]
+            lines += [f"        {x} {y} {z}" for x, y, z in grid]
+            lines += ["      </Faces>", "    </Mesh>"]
+            continue
         lines += [f"    <Mesh id=\"{mesh_id}\">", f"      <Material>{wall_mat[name]}</Material>",
                   "      <Faces>", f"        {a} {b} {cc}", f"        {a} {cc} {d}",
                   "      </Faces>", "    </Mesh>"]
@@ -152,7 +169,7 @@ def main(argv=None) -> int:
     ap.add_argument("--size", type=int, nargs=2, default=(256, 256))
     ap.add_argument("--photons", type=int, default=10000)
     ap.add_argument("--iterations", type=int, default=1000)
-    ap.add_argument("--variant", default="plain", choices=["plain", "transforms"])
+    ap.add_argument("--variant", default="plain", choices=["plain", "transforms", "deep"])
     ap.add_argument("--num-samples", type=int, default=None)
     a = ap.parse_args(argv)
     with open(a.out, "w") as f:
