@@ -10,14 +10,18 @@ dominant kernel and the reference CPU path timed on this box's host cores.
 One step = one full render of every camera in the job (default: one 1920x1080 C3 frame).
 `--gpus N` with N > 1 and no launcher starts N rank processes itself (torch.distributed.run,
 before any GPU call).  N = 1: the step is one C3 frame rendered in place, `--inflight`
-consecutive steps on as many streams.  N > 1 (default `--split tiles`): the frame's 8x8-pixel
-tiles are dealt round-robin over the ranks (the reference deals rows round-robin over threads,
-HW2/main.cpp:33-36), each rank renders its share tile-major into HBM, and the shares are
-gathered to rank 0 over RCCL (torch.distributed "nccl" = RCCL over xGMI) and untiled there,
-with `--inflight` steps in flight per rank ("scaling": "strong"); rank 0 also times the same
-frame rendered alone to report t1 / (N * tN), and the line carries a weak-scaling measurement
-(one whole frame per rank per step) as an extra key.  At N = 1 the line also carries the C5
-photon-mapping benchmark (tools/bench_ppm.py) as a `c5` sub-object.
+consecutive steps (default 6) on as many render streams, picked by timing.  N > 1 (default
+`--split bands`, "scaling": "strong"): each frame is cut into one row band per rank at cuts
+balanced by the frame's measured tile costs (the reference deals rows round-robin over
+threads, HW2/main.cpp:33-36); each rank renders its band in place, ranks > 0 send it to rank 0
+point to point over RCCL (torch.distributed "nccl" = RCCL over xGMI) as 32-bit pixel records
+that rank 0 shades into its frame (`--exchange rgb`: as RGB), four steps in flight per rank;
+`--split tiles` deals 2x2-tile blocks and untiles on rank 0, `--split frames` gives each rank
+whole frames.  Rank 0 verifies the frame bit for bit, times the same frame rendered alone to
+report t1 / (N * tN), and the line carries a weak-scaling measurement (one whole frame per
+rank per step) as an extra key.  At N = 1 the line predicts the split's efficiency for N = 2,
+4, 8 from every rank's work timed on this GPU (C3 and C4) and carries the C5 photon-mapping
+benchmark (tools/bench_ppm.py) as a `c5` sub-object.
 
 Printed by rank 0: ONE JSON line (see the contract in the task statement).
 """
