@@ -56,12 +56,18 @@ MSAA = {
     "msaa16": (lambda: G.soup_scene(11, 32, 24, num_samples=16), "n = 4"),
 }
 
+# The multi-GPU split paths (row bands, pixel records) on a frame whose sides are no multiple of
+# the 8x8 tile: partial tile rows and columns, pixels outside the frame in the last tiles.
+SPLIT = {
+    "ragged": (lambda: G.soup_scene(12, 75, 53), "75x53: ragged tiles, 4 lights, spheres"),
+}
+
 SMALL = ["c1", "hf_small", "hf_side", "soup1", "soup2", "soup3", "single_sphere",
          "single_triangle", "graze_plane", "graze_hf"]
 
 
 def write(name: str, directory: str) -> str:
-    table = {**CATALOGUE, **RECURSIVE, **MSAA}
+    table = {**CATALOGUE, **RECURSIVE, **MSAA, **SPLIT}
     path = os.path.join(directory, f"{name}.xml")
     if not os.path.exists(path):
         text = table[name][0]().to_xml()

@@ -34,7 +34,7 @@ def test_tile_costs_of_a_whole_frame(scene_dir):
         s.release_stream(st.cuda_stream)
 
 
-@pytest.mark.parametrize("name", ["c1", "hf_side", "soup2", "single_sphere", "c2"])
+@pytest.mark.parametrize("name", ["c1", "hf_side", "soup2", "single_sphere", "c2", "ragged"])
 def test_bands_assemble_the_oracle_frame(scene_dir, name):
     import torch
     import ceng795_amd
@@ -80,7 +80,7 @@ def test_c3_band_costs_balance(scene_dir):
     assert bc.max() / bc.mean() < 1.05
 
 
-@pytest.mark.parametrize("name", ["c1", "soup2", "single_sphere", "graze_plane", "c2"])
+@pytest.mark.parametrize("name", ["c1", "soup2", "single_sphere", "graze_plane", "c2", "ragged"])
 def test_record_bands_assemble_the_oracle_frame(scene_dir, name):
     """Bands as row-major pixel records (RT_TILE_RECORDS without RT_TILE_MAJOR) from ranks > 0,
     rank 0's (smaller) band in place as RGB, then rt_resolve_rows over every other row: the

@@ -15,7 +15,8 @@ from oracle.cpu_ref import OracleScene
 
 pytestmark = pytest.mark.gpu
 
-NAMES = ["c1", "hf_side", "soup2", "single_sphere", "single_triangle", "graze_plane", "c2"]
+NAMES = ["c1", "hf_side", "soup2", "single_sphere", "single_triangle", "graze_plane", "c2",
+         "ragged"]
 
 
 def assembled(s, world, *, root_inplace):
