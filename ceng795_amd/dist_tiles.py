@@ -1,7 +1,12 @@
-"""Image-tile sharding over GPUs + framebuffer gather, one process per GPU.
+"""Frame sharding over GPUs + framebuffer exchange, one process per GPU.
 
 The reference splits a frame over host threads by interleaved rows (HW2/main.cpp:33-36,
-HW2/Scene.cpp:25).  Here the deal units of every camera's frame — 2x2 blocks of 8x8-pixel tiles
+HW2/Scene.cpp:25).  Two splits live here.  The default of bench.py (BandPlan,
+BandGatherRenderer, further down): each camera's frame cut into one band of whole 8-pixel tile
+rows per rank at cuts balanced by the frame's measured tile costs (rt_tile_costs), rendered in
+place and sent to rank 0 straight into its frame rows — as 32-bit pixel records that rank 0
+shades (rt_resolve_rows), or as RGB.  The tile deal (TileLayout, TileGatherRenderer): the deal
+units of every camera's frame — 2x2 blocks of 8x8-pixel tiles
 (one wavefront per tile, one traversal workgroup per block), block rows rotated by their row
 index (RT_TILE_BLOCKS, include/ceng795_rt.h) — are numbered globally, camera after camera, and
 dealt round-robin over ranks: rank r renders global units g = r (mod world), diagonal stripes
