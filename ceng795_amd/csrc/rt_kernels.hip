@@ -602,9 +602,12 @@ __device__ __forceinline__ float half_hi(int w) {
 // host's margin the test never culls a treelet the reference would enter, so no decision band
 // is needed); the valid slots come first and the visit stops at the first invalid one (whose
 // NaN planes would fail the test anyway).  A leafy slot's leaves go to the leaf queue (the exact
-// guard decision is taken there); of the entered inner slots one becomes `node` (SHADOW: the
-// nearest by the entry distance of the first entering lane, so occluders turn up early) and the
+// guard decision is taken there); of the entered inner slots the first becomes `node` and the
 // others are pushed.  `alive`: lanes still searching.  Returns false when the walk is over.
+// (Round 5: shadow rays used to enter the nearest slot by the first entering lane's entry
+// distance, so occluders would turn up early; the readlane and compare per entered slot cost
+// more than it saved — C3 frame kernel 0.397 -> 0.392 ms, four in flight 0.374 -> 0.369 ms,
+// profiles/r05/ab_shadow_first.json.  Any-hit: the visiting order does not change the answer.)
 // Plane order per lane: a slot word holds the lo plane in its low half and the hi plane in its
 // high half; one v_alignbit by the ray's sh (16 where 1/d < 0) puts the lane's ENTRY plane low,
 // so a slot costs 3 alignbit + 6 fma_mix + max3 + min3 + 2 compares instead of a min and a max
@@ -612,9 +615,9 @@ __device__ __forceinline__ float half_hi(int w) {
 // skipped axis (SKIP) gets S = 0 and planes -inf / +inf, once per visit.
 template <bool SKIP, bool SHADOW, bool DEEP, bool SPHERES>
 __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode* __restrict__ nodes,
-                                           WaveLeafLds& L, int& pending, const LaneRay& r, float thr,
-                                           int& node, uint64_t& m, uint64_t alive,
-                                           WaveStack<DEEP>& st, Diag& dg) {
+                                           WaveLeafLds& L, int& pending, const LaneRay& r, int& node,
+                                           uint64_t& m, uint64_t alive, WaveStack<DEEP>& st,
+                                           Diag& dg) {
   v16i a, b;
   load_node8(nodes, node, a, b);
   const unsigned scale = (unsigned)a[3];
@@ -640,7 +643,6 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
   }
   int nxt = -1;
   uint64_t nm = 0;
-  unsigned nkey = 0;
 #pragma unroll
   for (int c = 0; c < kWideSlots; c++) {
     // the valid slots come first (check_accel): stop at the first invalid one (its NaN planes
@@ -674,18 +676,7 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
       continue;
     }
     const int ch = (inner_base + 2 * __builtin_popcount(inner & ((1u << c) - 1u))) | kWideTag;
-    if (SHADOW) {
-      const unsigned key = (unsigned)__builtin_amdgcn_readlane(
-          __float_as_int(__builtin_fmaxf(tn, 0.0f)), (int)__builtin_ctzll(hm));
-      if (nxt < 0 || key < nkey) {
-        if (nxt >= 0) st.push(nxt, nm);
-        nxt = ch;
-        nm = hm;
-        nkey = key;
-      } else {
-        st.push(ch, hm);
-      }
-    } else if (nxt < 0) {
+    if (nxt < 0) {
       nxt = ch;
       nm = hm;
     } else {
@@ -744,7 +735,7 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
       pending = 0;
     }
     if constexpr (FAST) {
-      if (!visit_wide<SKIP, false, DEEP, SPHERES>(P, nodes, L, pending, r, 0.0f, node, m, ~0ull, st, dg))
+      if (!visit_wide<SKIP, false, DEEP, SPHERES>(P, nodes, L, pending, r, node, m, ~0ull, st, dg))
         break;
     } else {
       const DevNode N = nodes[node];
@@ -808,7 +799,7 @@ __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* _
       if (!m && !st.pop_live(node, m, alive)) break;
     }
     if constexpr (FAST) {
-      if (!visit_wide<SKIP, true, DEEP, SPHERES>(P, nodes, L, pending, r, thr, node, m, alive, st, dg))
+      if (!visit_wide<SKIP, true, DEEP, SPHERES>(P, nodes, L, pending, r, node, m, alive, st, dg))
         break;
     } else {
       const DevNode N = nodes[node];
