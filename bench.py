@@ -347,6 +347,27 @@ def timed_steps(renderer, steps: int, world: int, coll_dev: str, events=None):
     return float(el.item())
 
 
+def n1_steps(scene, stream, inflight: int, steps: int, warmup: int, precondition_ms: float, dev):
+    """The N = 1 bench of another scene exactly as main() times its own: render streams picked
+    by timing, `inflight` frames in flight, preconditioned for `precondition_ms`, `warmup`
+    untimed steps, then `steps` timed steps.  Returns ms per step and Mrays/s."""
+    from ceng795_amd import dist_tiles
+    rstreams, _ = dist_tiles.pick_render_streams(scene, inflight, 1, device=dev)
+    R = dist_tiles.FrameRenderer(scene, stream, inflight=inflight, streams=rstreams)
+    precondition(R, precondition_ms)
+    scene.collect_stats()
+    for _ in range(max(1, warmup)):
+        R.step()
+    R.finish()
+    st = scene.collect_stats()
+    rays = (st.primary_rays + st.shadow_rays + st.secondary_rays) / max(1, warmup)
+    el = timed_steps(R, steps, 1, "cuda")
+    scene.collect_stats()
+    return {"ms_per_step": round(el / steps * 1e3, 4),
+            "Mrays_s": round(rays * steps / el / 1e6, 2), "steps": steps,
+            "frames_in_flight": inflight, "precondition_ms": precondition_ms}
+
+
 def one_frame_ms(scene, stream, frames: int):
     """Wall time per frame of camera 0 rendered ONE frame at a time (one stream, nothing else
     in flight): the single-frame latency beside the pipelined `value`."""
@@ -384,11 +405,25 @@ def cold_frame_ms(scene, frames: int = 3):
     return round(sorted(out)[len(out) // 2], 4)
 
 
-def timed_probe(scene, R, steps: int) -> float:
-    """ms per step of probe renderer R (3 untimed steps first), one GPU."""
-    for _ in range(3):
-        R.step()
-    R.finish()
+def precondition(R, ms: float):
+    """Untimed steps of renderer R for `ms` of wall time (the GPU's clock ramp after an idle
+    gap: profiles/r05/warmup_sweep.txt measured 7.5 % on 3 warm-up steps), then its queue
+    drained."""
+    import torch
+    t0 = time.perf_counter()
+    while True:
+        for _ in range(8):
+            R.step()
+        R.finish()
+        torch.cuda.synchronize()
+        if (time.perf_counter() - t0) * 1e3 >= ms:
+            return
+
+
+def timed_probe(scene, R, steps: int, precondition_ms: float = 30.0) -> float:
+    """ms per step of probe renderer R, one GPU: preconditioned like the bench's own timed
+    region (untimed steps of R for `precondition_ms`), then `steps` timed steps."""
+    precondition(R, precondition_ms)
     ms = timed_steps(R, steps, 1, "cuda") / steps * 1e3
     scene.collect_stats()
     return ms
@@ -420,7 +455,8 @@ def record_band_plan(scene, n: int, costs, rho: float, stream, inflight: int, st
 
 
 def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange: str = "rgb",
-                split: str = "bands", streams=None, inflight_n: int = INFLIGHT_SPLIT):
+                split: str = "bands", streams=None, inflight_n: int = INFLIGHT_SPLIT,
+                t1_line_ms=None):
     """Prediction of strong scaling on one GPU (no N-GPU node needed).  t1 = the whole frame
     rendered in place with `inflight` frames in flight, and for each N every rank's work of the
     N-way split alone on this GPU — ALL timed over the same `steps` steps after the same warm-up,
@@ -430,7 +466,12 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange
     tiles: rank r's block share, plus rank 0's untile / resolve of the others.  The N-GPU step
     can be no shorter than the slowest rank's work: t1 / (N * that step) bounds the efficiency
     from above (the link transfer, overlapped with the rendering of the frames in flight, is
-    reported in bytes, not timed)."""
+    reported in bytes, not timed).
+
+    t1_line_ms: the N = 1 line's own ms_per_step for this frame (its timed region, after its
+    preconditioning), the t1 every efficiency is priced against; the re-probed t1 is reported
+    beside it (`t1_probe_ms`) as a check of the probe conditions.  Every probe is preconditioned
+    (timed_probe)."""
     from ceng795_amd import dist_tiles
     # t1 on the bench's own render streams (`streams`) with the N = 1 line's frames in flight;
     # every rank's work of an N-way split with the split's frames in flight (`inflight_n`) on
@@ -441,7 +482,8 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange
         return timed_probe(scene, R, steps)
 
     one = dist_tiles.FrameRenderer(scene, stream, inflight=inflight, streams=streams)
-    t1 = timed(one)
+    t1_probe = timed(one)
+    t1 = t1_line_ms if t1_line_ms else t1_probe
     inflight = inflight_n
     records = exchange == "records" and dist_tiles.records_ok(scene)
     costs = dist_tiles.measure_tile_costs(scene)
@@ -511,13 +553,23 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange
         if "records" in bands_by:
             out[str(n)]["bands_records"] = bands_by["records"][0]
     cam = scene.camera(0)
-    return {"frame": f"{cam.width}x{cam.height}", "t1_ms": round(t1, 4), "steps": steps,
+    eff = [v["predicted_efficiency"] for v in out.values()]
+    return {"frame": f"{cam.width}x{cam.height}", "t1_ms": round(t1, 4),
+            "t1_source": ("the N = 1 line's ms_per_step (same process, same preconditioning)"
+                          if t1_line_ms else "re-probed"),
+            "t1_probe_ms": round(t1_probe, 4),
+            "t1_probe_over_t1": round(t1_probe / t1, 4),
+            "efficiency_check": ("ok: no prediction above 1.0" if max(eff) <= 1.0 else
+                                 "SUSPECT: a prediction above 1.0 (no measured cause; treat "
+                                 "as a probe artifact)"),
+            "steps": steps,
             "frames_in_flight": {"t1": one.inflight, "per_rank": inflight_n},
             "split": split,
             "tiles_exchange": "records" if records else "rgb",
             "per_n": out,
             "note": "PREDICTION from one GPU: t1 and every rank's work of one frame, timed over "
-                    "the same number of steps with the same frames in flight and render streams. "
+                    "the same number of steps with the same frames in flight and render streams, "
+                    "each preconditioned; efficiencies priced against the line's own N = 1 step. "
                     "bands (the bench's N>1 split): each rank's cost-balanced row band in place; "
                     "step = the slowest band.  tiles: each rank's block share, plus rank 0's "
                     "untile (or resolve of pixel records) of the others; step = max(slowest "
@@ -1132,18 +1184,25 @@ def main() -> int:
                 single = one_frame_ms(scene, stream, max(10, args.steps // 2))
                 cold = cold_frame_ms(scene)
                 if not args.no_share_probe:
+                    # every efficiency is priced against this line's own N = 1 step
                     probe = share_probe(scene, stream, max(20, args.steps), args.inflight,
                                         exchange=args.exchange, split=args.split,
                                         streams=renderer.streams,
-                                        inflight_n=args.split_inflight)
+                                        inflight_n=args.split_inflight,
+                                        t1_line_ms=elapsed / args.steps * 1e3)
                     if args.workload == "c3":
-                        # the north star's 8-GPU configuration: C4 (3840x2160), same mesh
+                        # the north star's 8-GPU configuration: C4 (3840x2160), same mesh; its
+                        # t1 = the C4 frame's N = 1 steps timed here exactly as this line's
                         with ceng795_amd.Scene(scene_path("c4", 1), device=device,
                                                traversal=args.traversal) as s4:
+                            c4_n1 = n1_steps(s4, stream, args.inflight, args.steps, args.warmup,
+                                             args.precondition_ms, dev)
                             probe_c4 = share_probe(s4, stream, max(20, args.steps), args.inflight,
-                                               exchange=args.exchange, split=args.split,
-                                               streams=renderer.streams,
-                                               inflight_n=args.split_inflight)
+                                                   exchange=args.exchange, split=args.split,
+                                                   streams=renderer.streams,
+                                                   inflight_n=args.split_inflight,
+                                                   t1_line_ms=c4_n1["ms_per_step"])
+                            probe_c4["n1_line"] = c4_n1
             except Exception as e:
                 log(f"one-frame / share probe failed: {e!r}")
         host_rate = None

@@ -117,6 +117,7 @@ SIGNATURES = {
     "rt_host_check_accel_xml": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_longlong)]),
     "rt_debug_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong)]),
     "rt_debug_timeline": (C.c_longlong, [C.POINTER(C.c_ulonglong), C.c_longlong]),
+    "rt_debug_phases": (C.c_longlong, [C.POINTER(C.c_ulonglong), C.c_longlong]),
     "rt_debug_quotient_check": (C.c_int, [C.c_int, C.c_ulonglong, C.c_longlong,
                                           C.POINTER(C.c_longlong)]),
 }

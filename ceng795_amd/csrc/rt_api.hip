@@ -37,6 +37,7 @@ hipError_t launch_quot_check(unsigned long long seed, long long count, unsigned 
                              hipStream_t stream);
 bool diag_build();
 long long read_reset_timeline(unsigned long long* out, long long max_values);
+long long read_reset_phases(unsigned long long* out, long long max_values);
 void write_png(const std::string& path, const float* rgb, int w, int h);
 }  // namespace rt
 
@@ -1417,6 +1418,13 @@ int rt_debug_counters(rt_scene* s, long long* out16) {
     out16[kCntExactBox] = (long long)read_reset_exact_fallbacks();
     return diag_build() ? 1 : 0;
   });
+}
+
+long long rt_debug_phases(unsigned long long* out, long long max_values) {
+  if (!out || max_values < 0) return set_error(RT_E_INVALID, "rt_debug_phases: bad argument");
+  const long long n = read_reset_phases(out, max_values);
+  if (n < 0) return set_error(RT_E_INVALID, "rt_debug_phases: buffer too small or copy failed");
+  return n;
 }
 
 long long rt_debug_timeline(unsigned long long* out, long long max_values) {

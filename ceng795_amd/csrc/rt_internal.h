@@ -33,6 +33,19 @@ enum : int {
   kCntPrimWide = 14, kCntShadWide = 15
 };
 
+// RT_DIAG per-phase attribution (rt_debug_phases, tools/phases.py): per traversal kind (primary,
+// shadow) the visit loop's events, then shader-clock cycle sums.
+enum : int {
+  kPhVisits = 0, kPhSlotsTested = 1, kPhSlotHits = 2, kPhLeafyHits = 3, kPhPairHits = 4,
+  kPhInnerHits = 5, kPhPushes = 6, kPhPops = 7, kPhFlushes = 8, kPhFlushIters = 9,
+  kPhaseEvents = 10
+};
+enum : int {
+  kPhCycPrimTotal = 2 * kPhaseEvents, kPhCycPrimVisit, kPhCycPrimLoad, kPhCycPrimFlush,
+  kPhCycShadTotal, kPhCycShadVisit, kPhCycShadLoad, kPhCycShadFlush, kPhCycShade,
+  kPhCycFrame, kPhWaves, kPhaseSlots
+};
+
 constexpr int kDefaultTreeletLeaves = 2;  // culling-tree treelets: lone leaves and leaf pairs
 
 struct alignas(16) DevNode {

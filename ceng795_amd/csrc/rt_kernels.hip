@@ -42,7 +42,21 @@ constexpr int kCounterSlots = kCounterRows;
 #endif
 struct Diag {  // per-wave traversal work (RT_DIAG builds)
   unsigned long long nodes = 0, node_lanes = 0, leaves = 0, leaf_lanes = 0, wide = 0, guard = 0;
+  // per-phase attribution (rt_debug_phases): events of the visit loop, and shader-clock cycles
+  // (s_memrealtime, 100 MHz) of this wave spent in its phases
+  unsigned long long ev[kPhaseEvents] = {};
+  unsigned long long cyc_visit = 0, cyc_load = 0, cyc_flush = 0;
 };
+#ifdef RT_DIAG
+// [0, kPhaseEvents): primary events, [kPhaseEvents, 2 kPhaseEvents): shadow events, then the
+// cycle counters (kPhCyc*)
+__device__ unsigned long long g_phase[kPhaseSlots];
+__device__ __forceinline__ unsigned long long clock_now() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  return t;
+}
+#endif
 
 // ------------------------------------------------------------------ vector helpers
 struct V3 {
@@ -291,6 +305,7 @@ struct WaveStack {
   unsigned mlo = 0, mhi = 0;
   int sp = 0;  // wave-uniform
   int* lds = nullptr;
+  DIAG(unsigned long long pushes = 0; unsigned long long pops = 0;)
 
   __device__ __forceinline__ void push(int n, uint64_t m) {
     if (!DEEP) {
@@ -304,9 +319,11 @@ struct WaveStack {
       lds[kDeepWords * sp + 2] = (int)(unsigned)(m >> 32);
     }
     sp++;
+    DIAG(pushes++);
   }
   __device__ __forceinline__ void pop(int& n, uint64_t& m) {
     sp--;
+    DIAG(pops++);
     if (!DEEP) {
       n = __builtin_amdgcn_readlane(node, sp);
       m = (uint64_t)(unsigned)__builtin_amdgcn_readlane(mlo, sp) |
@@ -425,7 +442,10 @@ __device__ __forceinline__ bool advance(WaveStack<DEEP>& st, int c0, int c1, uin
 // lanes; without it 7 spill and the C3 frame kernel runs 0.406 -> 0.395 ms, four in flight
 // 0.385 -> 0.374, profiles/r05/ab_visit_flush.json.  LDS: 22.6 KB per 4-wave workgroup, seven
 // workgroups per CU.)
-constexpr int kBatchFlush = 128;
+#ifndef RT_BATCH_FLUSH  // (A/B builds)
+#define RT_BATCH_FLUSH 128
+#endif
+constexpr int kBatchFlush = RT_BATCH_FLUSH;
 constexpr int kBatchCap = kBatchFlush + kWideSlots * 2 * 64;
 constexpr int kShadowFlush = kBatchFlush;
 
@@ -619,7 +639,9 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
                                            uint64_t& m, uint64_t alive, WaveStack<DEEP>& st,
                                            Diag& dg) {
   v16i a, b;
+  DIAG(const unsigned long long tl0 = clock_now());
   load_node8(nodes, node, a, b);
+  DIAG(dg.cyc_load += clock_now() - tl0);
   const unsigned scale = (unsigned)a[3];
   const int inner_base = a[4], leaf_base = a[5], kinds = a[6];
   const unsigned offs = (unsigned)a[7];
@@ -648,6 +670,7 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
     // the valid slots come first (check_accel): stop at the first invalid one (its NaN planes
     // would fail the test anyway)
     if (!(kinds & (kSlotValid << c))) break;
+    DIAG(dg.ev[kPhSlotsTested]++);
     float n3[3], f3[3];
 #pragma unroll
     for (int x = 0; x < 3; x++) {
@@ -664,9 +687,12 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
     // fp16 planes, finite scales, skipped axes at -inf / +inf)
     const uint64_t hm = m & alive & ~lanes_nge(tf, __builtin_fmaxf(tn, 0.0f));
     if (!hm) continue;
+    DIAG(dg.ev[kPhSlotHits]++);
     if (kinds & (kSlotLeafy << c)) {
+      DIAG(dg.ev[kPhLeafyHits]++);
       const int leaf = leaf_base + (int)((offs >> (4 * c)) & 15u);
       const bool pair = (kinds & (kSlotPair << c)) != 0;
+      DIAG(dg.ev[kPhPairHits] += pair);
       // (the shadow kernel keeps the exec-mask pushes: junk writes cost it VGPR spills)
       if (pair)
         batch_push_pair<!SHADOW>(L, pending, leaf, hm);
@@ -676,6 +702,7 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
       continue;
     }
     const int ch = (inner_base + 2 * __builtin_popcount(inner & ((1u << c) - 1u))) | kWideTag;
+    DIAG(dg.ev[kPhInnerHits]++);
     if (nxt < 0) {
       nxt = ch;
       nm = hm;
@@ -692,6 +719,28 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
 }
 #undef RT_NODE_WORD
 
+// Wave priority (s_setprio) by phase (round 6).  A node visit is the traversal's dependent chain
+// — scalar node load -> slot tests -> lane masks -> next node — of short VALU -> SALU -> branch
+// steps, each waiting on the one before; the leaf-batch flushes are long runs of independent
+// VALU work on loaded records.  With the visits at the highest priority the arbiter issues a
+// ready visit instruction first and the flushes (lowest) fill the slots the chains leave idle;
+// setup and shading sit between.  Same box, three interleaved rounds
+// (profiles/r06/ab_priority*.json): C3 frame kernel 0.390 -> 0.362 ms one frame at a time,
+// six in flight 0.352 -> 0.333 ms per frame; the flushes above the visits, or at the visits'
+// level, measured slower.  (A/B builds: -DRT_PRIO_V=.. -DRT_PRIO_F=.. -DRT_PRIO_REST=..)
+#ifndef RT_PRIO_V
+#define RT_PRIO_V 3
+#endif
+#ifndef RT_PRIO_F
+#define RT_PRIO_F 0
+#endif
+#ifndef RT_PRIO_REST
+#define RT_PRIO_REST 1
+#endif
+#define RT_PRIO_VISIT_BEGIN __builtin_amdgcn_s_setprio(RT_PRIO_V)
+#define RT_PRIO_VISIT_END __builtin_amdgcn_s_setprio(RT_PRIO_REST)
+#define RT_PRIO_FLUSH_BEGIN __builtin_amdgcn_s_setprio(RT_PRIO_F)
+#define RT_PRIO_FLUSH_END __builtin_amdgcn_s_setprio(RT_PRIO_REST)
 // ------------------------------------------------------------------ closest hit
 // The reference's (t, leaf) for every active ray: leaf < 0 = miss.  FAST: the 8-wide culling
 // tree over reference treelets (the launch takes it only when the scene has one); otherwise
@@ -731,12 +780,22 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
   int node = FAST ? P.accel_root : P.root_ref;
   for (;;) {
     if (pending >= kBatchFlush) {  // between visits: only the ray and the stack are live
+      DIAG(const unsigned long long tf0 = clock_now());
+      RT_PRIO_FLUSH_BEGIN;
       batch_flush<false, SPHERES, FAST, SKIP>(P, L, pending, r, 0.0f, dg);
+      RT_PRIO_FLUSH_END;
+      DIAG(dg.cyc_flush += clock_now() - tf0; dg.ev[kPhFlushes]++;
+           dg.ev[kPhFlushIters] += (pending + 63) / 64);
       pending = 0;
     }
     if constexpr (FAST) {
-      if (!visit_wide<SKIP, false, DEEP, SPHERES>(P, nodes, L, pending, r, node, m, ~0ull, st, dg))
-        break;
+      DIAG(const unsigned long long tv0 = clock_now(); dg.ev[kPhVisits]++);
+      RT_PRIO_VISIT_BEGIN;
+      const bool more =
+          visit_wide<SKIP, false, DEEP, SPHERES>(P, nodes, L, pending, r, node, m, ~0ull, st, dg);
+      RT_PRIO_VISIT_END;
+      DIAG(dg.cyc_visit += clock_now() - tv0);
+      if (!more) break;
     } else {
       const DevNode N = nodes[node];
       bool h0, h1;
@@ -750,7 +809,15 @@ __device__ __forceinline__ void closest_hit(const RenderParams& P, const DevNode
       if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, ~0ull)) break;
     }
   }
-  if (pending) batch_flush<false, SPHERES, FAST, SKIP>(P, L, pending, r, 0.0f, dg);
+  if (pending) {
+    DIAG(const unsigned long long tf0 = clock_now());
+    RT_PRIO_FLUSH_BEGIN;
+    batch_flush<false, SPHERES, FAST, SKIP>(P, L, pending, r, 0.0f, dg);
+    RT_PRIO_FLUSH_END;
+    DIAG(dg.cyc_flush += clock_now() - tf0; dg.ev[kPhFlushes]++;
+         dg.ev[kPhFlushIters] += (pending + 63) / 64);
+  }
+  DIAG(dg.ev[kPhPushes] += st.pushes; dg.ev[kPhPops] += st.pops);
   const unsigned long long key = L.key[lane];
   best_t = __uint_as_float((unsigned)(key >> 32));
   best_leaf = (int)(unsigned)key;
@@ -792,15 +859,25 @@ __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* _
   int node = FAST ? P.accel_root : P.root_ref;
   for (;;) {
     if (pending >= kShadowFlush) {  // between visits; a lane found occluded stops entering nodes
+      DIAG(const unsigned long long tf0 = clock_now());
+      RT_PRIO_FLUSH_BEGIN;
       batch_flush<true, SPHERES, FAST, SKIP>(P, L, pending, r, thr, dg);
+      RT_PRIO_FLUSH_END;
+      DIAG(dg.cyc_flush += clock_now() - tf0; dg.ev[kPhFlushes]++;
+           dg.ev[kPhFlushIters] += (pending + 63) / 64);
       pending = 0;
       alive &= ~ballot(L.key[lane] != 0ull);
       m &= alive;
       if (!m && !st.pop_live(node, m, alive)) break;
     }
     if constexpr (FAST) {
-      if (!visit_wide<SKIP, true, DEEP, SPHERES>(P, nodes, L, pending, r, node, m, alive, st, dg))
-        break;
+      DIAG(const unsigned long long tv0 = clock_now(); dg.ev[kPhVisits]++);
+      RT_PRIO_VISIT_BEGIN;
+      const bool more =
+          visit_wide<SKIP, true, DEEP, SPHERES>(P, nodes, L, pending, r, node, m, alive, st, dg);
+      RT_PRIO_VISIT_END;
+      DIAG(dg.cyc_visit += clock_now() - tv0);
+      if (!more) break;
     } else {
       const DevNode N = nodes[node];
       bool h0, h1;
@@ -813,7 +890,15 @@ __device__ __forceinline__ bool occluded(const RenderParams& P, const DevNode* _
       if (!advance(st, N.child[0], N.child[1], m0, m1, t0, t1, node, m, alive)) break;
     }
   }
-  if (pending) batch_flush<true, SPHERES, FAST, SKIP>(P, L, pending, r, thr, dg);
+  if (pending) {
+    DIAG(const unsigned long long tf0 = clock_now());
+    RT_PRIO_FLUSH_BEGIN;
+    batch_flush<true, SPHERES, FAST, SKIP>(P, L, pending, r, thr, dg);
+    RT_PRIO_FLUSH_END;
+    DIAG(dg.cyc_flush += clock_now() - tf0; dg.ev[kPhFlushes]++;
+         dg.ev[kPhFlushIters] += (pending + 63) / 64);
+  }
+  DIAG(dg.ev[kPhPushes] += st.pushes; dg.ev[kPhPops] += st.pops);
   return L.key[lane] != 0ull;
 }
 
@@ -979,6 +1064,10 @@ __device__ __forceinline__ void primary_packet(const RenderParams& P,
     atomicAdd(&c[kCntPrimLeafLanes], dg.leaf_lanes);
     atomicAdd(&c[kCntPrimWide], dg.wide);
     atomicAdd(&c[kCntGuardTests], dg.guard);
+    for (int k = 0; k < kPhaseEvents; k++) atomicAdd(&g_phase[k], dg.ev[k]);
+    atomicAdd(&g_phase[kPhCycPrimVisit], dg.cyc_visit);
+    atomicAdd(&g_phase[kPhCycPrimLoad], dg.cyc_load);
+    atomicAdd(&g_phase[kPhCycPrimFlush], dg.cyc_flush);
 #endif
   }
 }
@@ -1047,6 +1136,10 @@ __device__ __forceinline__ void shadow_packet(const RenderParams& P0,
       atomicAdd(&c[kCntShadLeafLanes], dg.leaf_lanes);
       atomicAdd(&c[kCntShadWide], dg.wide);
       atomicAdd(&c[kCntGuardTests], dg.guard);
+      for (int k = 0; k < kPhaseEvents; k++) atomicAdd(&g_phase[kPhaseEvents + k], dg.ev[k]);
+      atomicAdd(&g_phase[kPhCycShadVisit], dg.cyc_visit);
+      atomicAdd(&g_phase[kPhCycShadLoad], dg.cyc_load);
+      atomicAdd(&g_phase[kPhCycShadFlush], dg.cyc_flush);
 #endif
     }
   }
@@ -1683,11 +1776,24 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_FRAME_OCCUPANCY void trace_fra
     // the packet's start time waits in LDS (kept in SGPRs across the traversals it spilled)
     __shared__ unsigned long long start[kTraceWaves];
     start[threadIdx.x >> 6] = __builtin_amdgcn_s_memrealtime();
+    DIAG(const unsigned long long c0 = clock_now());
     primary_packet<FAST, DEEP, SPHERES>(Q, nodes, sel, spill, L);
+    DIAG(const unsigned long long c1 = clock_now());
     if (fresh_params(P).num_lights > 0)
       shadow_packet<FAST, DEEP, SPHERES>(fresh_params(P), nodes, lights, sel, spill, L);
+    DIAG(const unsigned long long c2 = clock_now());
     const RenderParams& Ps = fresh_params(P);
     shade_pixel<SPHERES>(Ps, Ps.prims, Ps.normals, Ps.materials, lights, sel, wave_sub(L));
+#ifdef RT_DIAG
+    const unsigned long long c3 = clock_now();
+    if (lane_id() == 0) {
+      atomicAdd(&g_phase[kPhCycPrimTotal], c1 - c0);
+      atomicAdd(&g_phase[kPhCycShadTotal], c2 - c1);
+      atomicAdd(&g_phase[kPhCycShade], c3 - c2);
+      atomicAdd(&g_phase[kPhCycFrame], c3 - c0);
+      atomicAdd(&g_phase[kPhWaves], 1ull);
+    }
+#endif
     const RenderParams& Pw = fresh_params(P);
     if (Pw.tile_cost && lane_id() == 0) {  // the next frame's dispatch order
       const unsigned c = (unsigned)min(__builtin_amdgcn_s_memrealtime() - start[threadIdx.x >> 6],
@@ -2077,6 +2183,21 @@ long long read_reset_timeline(unsigned long long* out, long long max_values) {
   std::vector<unsigned long long> z((size_t)n, 0ull);
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_timeline), z.data(), n * sizeof *out) != hipSuccess) return -1;
   return n;
+#else
+  (void)out;
+  (void)max_values;
+  return 0;
+#endif
+}
+
+// Copies (and clears) the RT_DIAG phase counters (kPhaseSlots values); 0 in other builds.
+long long read_reset_phases(unsigned long long* out, long long max_values) {
+#ifdef RT_DIAG
+  if (max_values < kPhaseSlots) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), kPhaseSlots * sizeof *out) != hipSuccess) return -1;
+  unsigned long long z[kPhaseSlots] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z) != hipSuccess) return -1;
+  return kPhaseSlots;
 #else
   (void)out;
   (void)max_values;

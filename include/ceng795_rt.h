@@ -304,6 +304,13 @@ int rt_debug_counters(rt_scene* scene, long long* out16);
  * Returns the number of values written (0 in other builds) or a negative RT_E_* code. */
 long long rt_debug_timeline(unsigned long long* out, long long max_values);
 
+/* RT_DIAG builds (tools/phases.py): copies and clears the per-phase attribution of the frame
+ * kernel — per traversal kind (primary, shadow) the visit loop's events (visits, slots tested,
+ * slot hits, leafy / pair / inner hits, stack pushes and pops, leaf-batch flushes and their
+ * 64-test iterations), then shader-clock cycle sums per phase (rt_internal.h kPh*).  Returns the
+ * number of values written (0 in other builds) or a negative RT_E_* code. */
+long long rt_debug_phases(unsigned long long* out, long long max_values);
+
 /* Device self-check of the triangle test's shared-reciprocal quotients (rt_kernels.hip,
  * tri_quotients) against IEEE division on `count` seeded random operand pairs of the fast
  * range; out2[0] = mismatching quotients (must be 0), out2[1] = cases run. */

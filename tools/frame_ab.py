@@ -5,7 +5,7 @@
 
 Each (round, variant) runs in its own process with CENG795_LIB=<variant> ("base" = the
 production build): 100 ms of untimed frames (the GPU's clock ramp), then the frame kernel's
-HIP-event time one frame at a time (median of 20), and the bench's pipelined rate (4 frames in
+HIP-event time one frame at a time (median of 20), and the bench's pipelined rate (6 frames in
 flight, `--steps` steps).  Rounds interleave the variants (A B C A B C ...).  Prints one JSON
 object: per variant the runs and the medians."""
 import argparse
@@ -27,7 +27,7 @@ def one(workload: str, steps: int) -> dict:
     from ceng795_amd import dist_tiles
     with ceng795_amd.Scene(bench.scene_path(workload, 1), device=0) as s:
         st = torch.cuda.current_stream()
-        R = dist_tiles.FrameRenderer(s, st, inflight=4)
+        R = dist_tiles.FrameRenderer(s, st, inflight=6)
         t0 = time.perf_counter()
         while time.perf_counter() - t0 < 0.1:
             for _ in range(16):
@@ -39,7 +39,7 @@ def one(workload: str, steps: int) -> dict:
         for _ in range(8):
             R.step()
         R.finish()
-        out["ms_per_frame_4inflight"] = round(bench.timed_steps(R, steps, 1, "cuda") / steps * 1e3, 4)
+        out["ms_per_frame_6inflight"] = round(bench.timed_steps(R, steps, 1, "cuda") / steps * 1e3, 4)
         st_ = s.collect_stats()
     return out
 
