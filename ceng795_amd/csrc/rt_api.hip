@@ -48,6 +48,21 @@ using namespace rt;
 // thread per camera (HW2/main.cpp:33-36), so a drop-in pays hipMalloc / hipFree only the first
 // time a call of that size runs.  Calls on several host threads each take their own context
 // (rt_render stays reentrant).
+// rt_render into a caller buffer in pinned host memory: the frame kernel writes it directly
+// (its device-visible address; C3 one frame at a time 0.94-0.97 -> 0.67-0.69 ms).  Into a
+// pageable buffer: the frame as RT_RENDER_CHUNKS bands of tile rows, one launch each, each band
+// copied out on a second stream as soon as it is done.  (The copies are blit kernels here,
+// which wait for CU slots the render holds: pageable 1.00-1.05 ms unbanded, 0.89 with 2 bands,
+// 0.98 with 4, 1.36 with 8; a high-priority copy stream changed nothing —
+// profiles/r06/host_rate_bands.jsonl.)
+#ifndef RT_DIRECT_PINNED  // (A/B builds)
+#define RT_DIRECT_PINNED 1
+#endif
+#ifndef RT_RENDER_CHUNKS  // (A/B builds)
+#define RT_RENDER_CHUNKS 2
+#endif
+constexpr int kRenderChunks = RT_RENDER_CHUNKS;
+
 struct RenderCtx {
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -73,6 +88,10 @@ struct RenderCtx {
   // has copied the shares out of the other contexts' buffers; a context renders its next share
   // only after it (the copy reads d_out / d_image on another stream: write-after-read)
   hipEvent_t ev_gathered = nullptr;
+  // rt_render's chunked copy-out (render_to_host): a second stream for the device-to-host copies
+  // and one event per row chunk (created on first use)
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t ev_chunk[kRenderChunks] = {};
 };
 
 // rt_render_device scratch of one stream (hit records, occlusion bits, tile schedule, ray-tree
@@ -230,6 +249,9 @@ void free_ctx(RenderCtx* c) {
   if (c->ev_gathered) (void)hipEventDestroy(c->ev_gathered);
   if (c->e0) (void)hipEventDestroy(c->e0);
   if (c->e1) (void)hipEventDestroy(c->e1);
+  for (hipEvent_t e : c->ev_chunk)
+    if (e) (void)hipEventDestroy(e);
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1485,22 +1507,74 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
                 "zero counters");
     }
     hip_check(hipEventRecord(x->e0, x->stream), "event record");
-    if (multi && c.num_samples > 1) {
-      render_multi_msaa(s, cx, cam, d_frame, x->stream, true);
-    } else if (multi) {
-      render_multi(s, cx, cam, row0, row_stride, d_frame, x->stream, true);
-    } else {
-      RenderParams P = make_params(s, r, cam, row0, row_stride, 0, 1, 0, d_frame, x->d_cnt);
-      bind_ctx(s, x, P, c);
-      enqueue_frame(s, r, P, c.num_samples, x->d_samples, x->stream, true);
-    }
-    hip_check(hipEventRecord(x->e1, x->stream), "event record");
-    // rows j = row0 + k*row_stride only: a strided 2D copy leaves the others untouched
+    // rows j = row0 + k*row_stride only: strided 2D copies leave the others untouched
     const size_t row_bytes = (size_t)c.width * 3 * sizeof(float);
-    hip_check(hipMemcpy2DAsync(out_rgb + (size_t)row0 * c.width * 3, row_bytes * row_stride,
-                               d_frame + (size_t)row0 * c.width * 3, row_bytes * row_stride,
-                               row_bytes, tp.rows, hipMemcpyDeviceToHost, x->stream),
-              "copy rows");
+    auto copy_rows = [&](int lr0, int lr1, hipStream_t st) {  // logical rows [lr0, lr1)
+      if (lr1 <= lr0) return;
+      const size_t off = (size_t)(row0 + (size_t)lr0 * row_stride) * c.width * 3;
+      hip_check(hipMemcpy2DAsync(out_rgb + off, row_bytes * row_stride, d_frame + off,
+                                 row_bytes * row_stride, row_bytes, (size_t)(lr1 - lr0),
+                                 hipMemcpyDeviceToHost, st),
+                "copy rows");
+    };
+    const int tiles_y = tp.tiles_total / tp.tiles_x;
+    const int chunks = std::min(kRenderChunks, tiles_y);
+    // a caller buffer in pinned host memory (hipHostMalloc / registered, e.g. torch pin_memory)
+    // is written by the frame kernel itself, through its device-visible address: no copy
+    float* direct = nullptr;
+    if (!multi && c.num_samples <= 1 && RT_DIRECT_PINNED) {
+      void* dp = nullptr;
+      if (hipHostGetDevicePointer(&dp, out_rgb, 0) == hipSuccess && dp)
+        direct = static_cast<float*>(dp);
+      else
+        (void)hipGetLastError();  // pageable memory: not an error here
+    }
+    if (direct) {
+      RenderParams P = make_params(s, r, cam, row0, row_stride, 0, 1, 0, direct, x->d_cnt);
+      bind_ctx(s, x, P, c);
+      P.tile_cost = nullptr;
+      enqueue_frame(s, r, P, c.num_samples, x->d_samples, x->stream, true);
+      hip_check(hipEventRecord(x->e1, x->stream), "event record");
+    } else if (!multi && c.num_samples <= 1 && chunks > 1) {
+      // the drop-in seam: the frame as `chunks` bands of tile rows, one
+      // launch each on the context's stream; each band goes to the caller's buffer on the copy
+      // stream as soon as its launch is done, while the next bands render
+      if (!x->copy_stream)
+        hip_check(hipStreamCreateWithFlags(&x->copy_stream, hipStreamNonBlocking), "copy stream");
+      for (int k = 0; k < chunks; k++) {
+        const int ty0 = (int)((long long)tiles_y * k / chunks);
+        const int ty1 = (int)((long long)tiles_y * (k + 1) / chunks);
+        RenderParams P = make_params(s, r, cam, row0, row_stride, ty0 * tp.tiles_x, 1, 0, d_frame,
+                                     x->d_cnt);
+        P.num_sel_tiles = (ty1 - ty0) * tp.tiles_x;
+        bind_ctx(s, x, P, c);
+        P.tile_cost = nullptr;  // no dispatch order for a next frame (nothing reuses it here)
+        enqueue_frame(s, r, P, c.num_samples, x->d_samples, x->stream, true);
+        if (!x->ev_chunk[k])
+          hip_check(hipEventCreateWithFlags(&x->ev_chunk[k], hipEventDisableTiming), "event");
+        hip_check(hipEventRecord(x->ev_chunk[k], x->stream), "event record");
+      }
+      hip_check(hipEventRecord(x->e1, x->stream), "event record");
+      for (int k = 0; k < chunks; k++) {
+        const int ty0 = (int)((long long)tiles_y * k / chunks);
+        const int ty1 = (int)((long long)tiles_y * (k + 1) / chunks);
+        hip_check(hipStreamWaitEvent(x->copy_stream, x->ev_chunk[k], 0), "wait band");
+        copy_rows(kTile * ty0, std::min(tp.rows, kTile * ty1), x->copy_stream);
+      }
+      hip_check(hipStreamSynchronize(x->copy_stream), "synchronize copies");
+    } else {
+      if (multi && c.num_samples > 1) {
+        render_multi_msaa(s, cx, cam, d_frame, x->stream, true);
+      } else if (multi) {
+        render_multi(s, cx, cam, row0, row_stride, d_frame, x->stream, true);
+      } else {
+        RenderParams P = make_params(s, r, cam, row0, row_stride, 0, 1, 0, d_frame, x->d_cnt);
+        bind_ctx(s, x, P, c);
+        enqueue_frame(s, r, P, c.num_samples, x->d_samples, x->stream, true);
+      }
+      hip_check(hipEventRecord(x->e1, x->stream), "event record");
+      copy_rows(0, tp.rows, x->stream);
+    }
     std::vector<std::vector<unsigned long long>> cnt(cx.x.size(),
                                                      std::vector<unsigned long long>(kCounterAlloc));
     for (size_t d = 0; d < cx.x.size(); d++) {
