@@ -137,6 +137,36 @@ def cpu_baseline(xml: str, threads: int, how: str, reps: int = 5, warm: int = 1)
                       f"HW2/main.cpp:26-41; threads: {how}"}
 
 
+def dropin_ms(xml: str, threads: int):
+    """The drop-in at the reference's own seam: oracle/_ref/hw2_gpu — the unmodified HW2 Scene /
+    Pixel / lodepng sources with the binding of INTEGRATION.md §2 (the reference's parsed Scene
+    and its own BVH handed over as an rt_scene_desc) — timed by its own clock over HW2/main.cpp's
+    region (:26-41: T threads of render_image_gpu, i.e. rt_render into a pinned frame plus the
+    reference's Pixel::add_color per pixel).  One render per camera, as the reference does (a
+    cold frame).  Returns {threads: ms} for T = 1 and `threads`, or None without the binary."""
+    import re
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "oracle", "_ref", "hw2_gpu")
+    if not os.path.exists(exe):
+        return None
+    out = {}
+    for t in sorted({1, threads}):
+        with tempfile.TemporaryDirectory() as d:
+            r = subprocess.run([exe, xml, "--threads", str(t)], cwd=d, capture_output=True,
+                               text=True, timeout=300)
+        m = re.search(r"in ([0-9.eE+-]+) ms", r.stdout)
+        if r.returncode or not m:
+            log(f"hw2_gpu failed ({r.returncode}): {r.stderr[-500:]}")
+            return None
+        out[str(t)] = round(float(m.group(1)), 3)
+    return {"ms_by_threads": out,
+            "binary": "oracle/_ref/hw2_gpu (reference HW2 sources + oracle/ref/Scene_gpu.cpp)",
+            "region": "HW2/main.cpp:26-41 as the reference times it: render_image_gpu on T "
+                      "threads (rt_render into a pinned frame, then Pixel::add_color per pixel); "
+                      "one cold frame per camera"}
+
+
 def stream_copy_gbps(device) -> float:
     """Measured device-to-device copy bandwidth (read + write bytes / time) on this GPU: the
     attainable-HBM reference SURVEY.md §8(d) asks for beside the 8 TB/s spec peak."""
@@ -1217,6 +1247,12 @@ def main() -> int:
                 cpu = cpu_baseline(xml, threads, how)
             except Exception as e:
                 log(f"cpu baseline failed: {e!r}")
+        dropin = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                dropin = dropin_ms(xml, threads)
+            except Exception as e:
+                log(f"drop-in timing failed: {e!r}")
         n, w, h, desc = WORKLOADS[args.workload]
         ms_step = elapsed / args.steps * 1e3
         comm = "rccl" if coll_dev == "cuda" else "gloo"
@@ -1260,6 +1296,7 @@ def main() -> int:
                                            "note": "untimed steps before the warm-up: the "
                                                    "GPU's clock ramp"}},
             "roofline": roof, "cpu_baseline": cpu, "pcie_inclusive": host_rate,
+            "dropin_ms": dropin,
         }
         if single is not None:
             line["one_frame_ms"] = single

@@ -57,6 +57,10 @@ class rt_scene_desc(C.Structure):
         ("triangle_material", C.POINTER(C.c_int)),
         ("num_spheres", C.c_int), ("sphere_center", C.POINTER(C.c_int)),
         ("sphere_radius", C.POINTER(C.c_float)), ("sphere_material", C.POINTER(C.c_int)),
+        # ABI 7: the caller's own BVH (zero = the library builds the reference's)
+        ("bvh_num_nodes", C.c_int), ("bvh_children", C.POINTER(C.c_int)),
+        ("bvh_boxes", C.POINTER(C.c_float)), ("bvh_num_leaves", C.c_int),
+        ("bvh_leaf_object", C.POINTER(C.c_int)), ("bvh_leaf_normals", C.POINTER(C.c_float)),
     ]
 
 
@@ -114,6 +118,9 @@ SIGNATURES = {
     "rt_last_error": (C.c_char_p, []),
     "rt_abi_version": (C.c_int, []),
     "rt_host_dump_bvh_xml": (C.c_int, [C.c_char_p, C.c_char_p]),
+    "rt_host_dump_bvh_desc": (C.c_int, [C.POINTER(rt_scene_desc), C.c_char_p]),
+    "rt_host_alloc": (C.c_void_p, [C.c_size_t]),
+    "rt_host_free": (None, [C.c_void_p]),
     "rt_host_check_accel_xml": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_longlong)]),
     "rt_debug_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong)]),
     "rt_debug_timeline": (C.c_longlong, [C.POINTER(C.c_ulonglong), C.c_longlong]),
@@ -143,7 +150,7 @@ def _share_torch_hip_runtime() -> None:
         pass
 
 
-ABI_VERSION = 6  # CENG795_RT_ABI_VERSION of include/ceng795_rt.h
+ABI_VERSION = 7  # CENG795_RT_ABI_VERSION of include/ceng795_rt.h
 
 
 def lib() -> C.CDLL:

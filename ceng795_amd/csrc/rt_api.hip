@@ -1141,6 +1141,34 @@ int rt_host_dump_bvh_xml(const char* xml_path, const char* out_path) {
   });
 }
 
+int rt_host_dump_bvh_desc(const rt_scene_desc* desc, const char* out_path) {
+  if (!desc || !out_path) return set_error(RT_E_INVALID, "rt_host_dump_bvh_desc: NULL argument");
+  return guarded([&] {
+    HostScene h;
+    build_host_scene(*desc, h);
+    FILE* f = std::fopen(out_path, "w");
+    if (!f) throw std::ios_base::failure(std::string("cannot open ") + out_path);
+    const std::string text = dump_bvh(h);
+    std::fwrite(text.data(), 1, text.size(), f);
+    std::fclose(f);
+    return RT_OK;
+  });
+}
+
+void* rt_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  const int rc = guarded([&] {
+    hip_check(hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault),
+              "rt_host_alloc");
+    return RT_OK;
+  });
+  return rc == RT_OK ? p : nullptr;
+}
+
+void rt_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 int rt_host_check_accel_xml(const char* xml_path, int treelet_leaves, long long* stats4) {
   if (!xml_path || !stats4) return set_error(RT_E_INVALID, "rt_host_check_accel_xml: NULL argument");
   return guarded([&] {

@@ -236,6 +236,114 @@ void camera_from_view(const float pos[3], const float gaze[3], const float up[3]
   c.num_samples = ns;
 }
 
+namespace {
+
+// One leaf of the flattened scene (DevPrim + normal/material record + its source), appended in
+// leaf order; returns its leaf index.  Triangle: v0, a1 = v0 - v1, a2 = v0 - v2 as
+// HW2/Triangle.cpp:43-44 computes them.
+template <typename Vtx>
+int append_leaf(HostScene& s, const LeafSource& ls, F3 n, Vtx vtx) {
+  DevPrim p{};
+  p.kind = ls.kind;
+  p.material = ls.material;
+  if (ls.kind == kPrimTriangle) {
+    const F3 v0 = vtx(ls.i0), v1 = vtx(ls.i1), v2 = vtx(ls.i2);
+    const F3 a1 = v0 - v1, a2 = v0 - v2;
+    const float rec[9] = {v0.x, v0.y, v0.z, a1.x, a1.y, a1.z, a2.x, a2.y, a2.z};
+    std::memcpy(p.v0, rec, sizeof rec);
+    p.cx = a1.y * a2.z - a2.y * a1.z;  // c1.y*c2.z - c2.y*c1.z with c1 = a1, c2 = a2
+    s.quot_ok &= quot_coord_ok(v0.x) & quot_coord_ok(v0.y) & quot_coord_ok(v0.z);
+  } else {
+    std::memcpy(p.v0, ls.center, 12);
+    p.a1[0] = ls.radius;
+  }
+  const int index = (int)s.prims.size();
+  s.prims.push_back(p);
+  int mat_bits = ls.material;
+  float mat_f;
+  std::memcpy(&mat_f, &mat_bits, 4);
+  s.normals.insert(s.normals.end(), {n.x, n.y, n.z, mat_f});
+  s.leaf_src.push_back(ls);
+  return index;
+}
+
+// rt_scene_desc with the caller's own BVH (bvh_*, ABI 7): adopted as given.  The walk checks
+// that nodes are numbered in DFS preorder and leaves in DFS (left-first) order, each exactly
+// once, and that every primitive of the object lists is exactly one leaf.
+template <typename Vtx>
+void adopt_tree(const rt_scene_desc& d, HostScene& s, const std::vector<LeafSource>& objects,
+                const std::vector<F3>& normals, Vtx vtx) {
+  const int nn = d.bvh_num_nodes, nl = d.bvh_num_leaves;
+  if (nn < 0 || nl <= 0) fail("bvh_num_nodes < 0 or bvh_num_leaves <= 0");
+  if (!d.bvh_leaf_object) fail("bvh_leaf_object == NULL");
+  if (nn > 0 && (!d.bvh_children || !d.bvh_boxes)) fail("bvh_children / bvh_boxes == NULL");
+  if ((size_t)nl != objects.size())
+    fail("bvh_num_leaves (" + std::to_string(nl) + ") is not the number of primitives (" +
+         std::to_string(objects.size()) + ")");
+  if (nn != nl - 1) fail("a binary tree of " + std::to_string(nl) + " leaves has " +
+                         std::to_string(nl - 1) + " internal nodes, not " + std::to_string(nn));
+  std::vector<char> used(objects.size(), 0);
+  for (int k = 0; k < nl; k++) {
+    const int o = d.bvh_leaf_object[k];
+    if (o < 0 || (size_t)o >= objects.size()) fail("bvh_leaf_object out of range");
+    if (used[o]++) fail("primitive " + std::to_string(o) + " is two leaves");
+    F3 n = normals[o];
+    if (d.bvh_leaf_normals && objects[o].kind == kPrimTriangle)
+      n = {d.bvh_leaf_normals[3 * k], d.bvh_leaf_normals[3 * k + 1], d.bvh_leaf_normals[3 * k + 2]};
+    append_leaf(s, objects[o], n, vtx);
+  }
+  if (nn == 0) {  // the root is the one primitive (BVH::create_bvh, .h:13-14)
+    s.root_kind = s.prims[0].kind == kPrimTriangle ? kRootTriangle : kRootSphere;
+    s.root_ref = 0;
+    s.depth = 0;
+    return;
+  }
+  s.root_kind = kRootNode;
+  s.root_ref = 0;
+  std::memcpy(s.root_box, d.bvh_boxes, sizeof s.root_box);
+  s.nodes.assign((size_t)nn, DevNode{});
+  const float kAll[6] = {-1e30f, -1e30f, -1e30f, 1e30f, 1e30f, 1e30f};  // a leaf's slot
+  int next_node = 1, next_leaf = 0;
+  s.depth = 1;
+  struct Frame {
+    int node, side, depth;
+  };
+  std::vector<Frame> st{{0, 0, 1}};
+  while (!st.empty()) {
+    Frame& f = st.back();
+    if (f.side == 2) {
+      st.pop_back();
+      continue;
+    }
+    const int side = f.side++, node = f.node, depth = f.depth;
+    const int c = d.bvh_children[2 * node + side];
+    DevNode& dn = s.nodes[node];
+    dn.axis = (depth - 1) % 3;
+    const float* b = kAll;
+    if (c >= 0) {
+      if (c != next_node) fail("bvh nodes are not numbered in DFS preorder (node " +
+                               std::to_string(node) + " child " + std::to_string(c) + ")");
+      next_node++;
+      b = d.bvh_boxes + 6 * (size_t)c;
+      dn.child[side] = c;
+      s.depth = std::max(s.depth, depth + 1);
+      st.push_back({c, 0, depth + 1});  // invalidates f
+    } else {
+      if (~c != next_leaf) fail("bvh leaves are not numbered in DFS order (leaf " +
+                                std::to_string(~c) + ")");
+      next_leaf++;
+      dn.child[side] = c;
+    }
+    for (int a = 0; a < 3; a++) {
+      s.nodes[node].lo[a][side] = b[a];
+      s.nodes[node].hi[a][side] = b[a + 3];
+    }
+  }
+  if (next_node != nn || next_leaf != nl) fail("bvh tree does not reach every node and leaf");
+}
+
+}  // namespace
+
 void build_host_scene(const rt_scene_desc& d, HostScene& s) {
   if (d.num_vertices < 0 || d.num_materials < 0 || d.num_lights < 0 || d.num_cameras < 0 ||
       d.num_meshes < 0 || d.num_triangles < 0 || d.num_spheres < 0)
@@ -278,6 +386,58 @@ void build_host_scene(const rt_scene_desc& d, HostScene& s) {
   auto check_material = [&](int m) {
     if (m < 0 || m >= d.num_materials) fail("material id out of range");
   };
+
+  if (d.bvh_num_leaves > 0 || d.bvh_num_nodes > 0) {
+    // the caller's own tree: the primitives in object-list order, then adopt_tree
+    std::vector<LeafSource> objects;
+    std::vector<F3> normals;
+    auto tri = [&](int i0, int i1, int i2, int mat) {
+      check_material(mat);
+      const F3 v0 = vtx(i0), v1 = vtx(i1), v2 = vtx(i2);
+      LeafSource ls{};
+      ls.kind = kPrimTriangle;
+      ls.i0 = i0;
+      ls.i1 = i1;
+      ls.i2 = i2;
+      ls.material = mat;
+      objects.push_back(ls);
+      normals.push_back(unit(cross(v1 - v0, v2 - v0)));  // Triangle.cpp:14
+    };
+    long long fb = 0;
+    for (int m = 0; m < d.num_meshes; m++) {
+      const int nf = d.mesh_face_count[m];
+      if (nf <= 0) fail("mesh without faces (the reference dereferences a NULL bvh)");
+      for (int f = 0; f < nf; f++) {
+        const int* idx = d.mesh_faces + 3 * (fb + f);
+        tri(idx[0], idx[1], idx[2], d.mesh_material[m]);
+      }
+      fb += nf;
+    }
+    for (int t = 0; t < d.num_triangles; t++) {
+      const int* idx = d.triangle_indices + 3 * t;
+      tri(idx[0], idx[1], idx[2], d.triangle_material[t]);
+    }
+    for (int k = 0; k < d.num_spheres; k++) {
+      check_material(d.sphere_material[k]);
+      const F3 c = vtx(d.sphere_center[k]);
+      LeafSource ls{};
+      ls.kind = kPrimSphere;
+      ls.center[0] = c.x;
+      ls.center[1] = c.y;
+      ls.center[2] = c.z;
+      ls.radius = d.sphere_radius[k];
+      ls.material = d.sphere_material[k];
+      objects.push_back(ls);
+      normals.push_back({0, 0, 0});
+    }
+    s.nodes.clear();
+    s.prims.clear();
+    s.normals.clear();
+    s.leaf_src.clear();
+    s.quot_ok = 1;
+    adopt_tree(d, s, objects, normals, vtx);
+    return;
+  }
 
   Builder B;
   auto add_triangle = [&](int i0, int i1, int i2, int mat) {
@@ -360,30 +520,7 @@ void build_host_scene(const rt_scene_desc& d, HostScene& s) {
   };
   auto emit_leaf = [&](int id) {
     const Obj& o = B.objs[id];
-    const LeafSource& ls = B.leaves[o.leaf];
-    DevPrim p{};
-    p.kind = ls.kind;
-    p.material = ls.material;
-    if (ls.kind == kPrimTriangle) {
-      const F3 v0 = vtx(ls.i0), v1 = vtx(ls.i1), v2 = vtx(ls.i2);
-      const F3 a1 = v0 - v1, a2 = v0 - v2;
-      const float rec[9] = {v0.x, v0.y, v0.z, a1.x, a1.y, a1.z, a2.x, a2.y, a2.z};
-      std::memcpy(p.v0, rec, sizeof rec);
-      p.cx = a1.y * a2.z - a2.y * a1.z;  // c1.y*c2.z - c2.y*c1.z with c1 = a1, c2 = a2
-      s.quot_ok &= quot_coord_ok(v0.x) & quot_coord_ok(v0.y) & quot_coord_ok(v0.z);
-    } else {
-      std::memcpy(p.v0, ls.center, 12);
-      p.a1[0] = ls.radius;
-    }
-    const int index = (int)s.prims.size();
-    s.prims.push_back(p);
-    const F3 n = B.normals[o.leaf];
-    int mat_bits = ls.material;
-    float mat_f;
-    std::memcpy(&mat_f, &mat_bits, 4);
-    s.normals.insert(s.normals.end(), {n.x, n.y, n.z, mat_f});
-    s.leaf_src.push_back(ls);
-    return ~index;
+    return ~append_leaf(s, B.leaves[o.leaf], B.normals[o.leaf], vtx);
   };
   auto put_box = [](float* dst, const Aabb& b) {
     dst[0] = b.lo.x;

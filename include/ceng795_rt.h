@@ -20,15 +20,18 @@
  */
 #ifndef CENG795_RT_H_
 #define CENG795_RT_H_
+#include <stddef.h>
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define CENG795_RT_ABI_VERSION 6  /* 2: MSAA cameras + rt_set_msaa_seed; 3: tile ranges,
+#define CENG795_RT_ABI_VERSION 7  /* 2: MSAA cameras + rt_set_msaa_seed; 3: tile ranges,
                                       kernel timing; 4: multi-device scenes, stream scratch
                                       release, no CULL mode; 5: pixel records
                                       (RT_TILE_RECORDS, rt_resolve_device); 6: rt_tile_costs,
-                                      row-major records + rt_resolve_rows */
+                                      row-major records + rt_resolve_rows; 7: the caller's own
+                                      BVH in rt_scene_desc (bvh_*), rt_host_dump_bvh_desc,
+                                      rt_host_alloc / rt_host_free */
 
 enum {
   RT_OK = 0,
@@ -99,6 +102,31 @@ typedef struct rt_scene_desc {
   const int* sphere_center;     /* int32[num_spheres], vertex id         */
   const float* sphere_radius;   /* fp32[num_spheres]                     */
   const int* sphere_material;   /* int32[num_spheres]                    */
+
+  /* Optional (ABI 7): the caller's own BVH — e.g. the reference's Scene::bvh walked through
+   * its public members (BVH::left / right / bounding_box, Mesh::bvh, Triangle::index_* /
+   * normal, Sphere::center / radius; HW2/Bounding_volume_hierarchy.h:39-41, Mesh.h:12,
+   * Triangle.h:12-14).  bvh_num_leaves == 0 (zero-initialised desc): the library builds the
+   * reference's tree itself from the object lists (HW2/Bounding_volume_hierarchy.cpp:3-29).
+   * Otherwise the library adopts this tree as given, Mesh wrappers spliced out (Mesh::intersect
+   * delegates to its BVH with no box test of its own, Mesh.h:13-15):
+   *   internal nodes in DFS preorder, node 0 the root (none when the root is one primitive);
+   *   bvh_children[2 i + s] = child s (0 left, 1 right) of node i: >= 0 an internal node
+   *     (> i), < 0 ~k for leaf k;  leaves numbered in DFS (left-first) order, which is the
+   *     closest-hit tie-break order (appendix A.5 of SURVEY.md);
+   *   bvh_boxes[6 i ..] = node i's Bounding_box (min xyz, max xyz) exactly as the caller holds
+   *     it — these are the boxes the slab tests see;
+   *   bvh_leaf_object[k] = leaf k's primitive: an index into the triangles of the object lists
+   *     (mesh faces in mesh order, then loose triangles) or, past them, into the spheres;
+   *   bvh_leaf_normals: NULL, or fp32[3 bvh_num_leaves] = each triangle leaf's flat normal as
+   *     the caller computed it (Triangle.cpp:14; sphere leaves: ignored).
+   * Every leaf index and every primitive must occur exactly once. */
+  int bvh_num_nodes;
+  const int* bvh_children;      /* int32[2*bvh_num_nodes]                */
+  const float* bvh_boxes;       /* fp32[6*bvh_num_nodes]                 */
+  int bvh_num_leaves;
+  const int* bvh_leaf_object;   /* int32[bvh_num_leaves]                 */
+  const float* bvh_leaf_normals;/* fp32[3*bvh_num_leaves] or NULL        */
 } rt_scene_desc;
 
 /* Work counters for one render call. */
@@ -155,6 +183,9 @@ int rt_scene_dump_bvh(const rt_scene* scene, const char* path);
 /* Host-only variant for tests without a GPU: XML ingest + BVH build + flatten, then the
  * same dump.  Touches no HIP API. */
 int rt_host_dump_bvh_xml(const char* xml_path, const char* out_path);
+/* Host-only, for tests without a GPU: the same dump for a scene description (with or without
+ * the caller's own BVH, bvh_*).  Touches no HIP API. */
+int rt_host_dump_bvh_desc(const rt_scene_desc* desc, const char* out_path);
 /* Host-only, for tests: XML ingest + BVH build + the culling tree over reference treelets of
  * <= treelet_leaves leaves, then a check of the invariants the kernels'
  * exactness rests on (every leaf in exactly one treelet, guard boxes = the reference boxes
@@ -182,6 +213,13 @@ int rt_set_traversal(rt_scene* scene, int mode);
  * reproducible.  rt_stats counts every sample's rays. */
 int rt_render(rt_scene* scene, int camera_index, int starting_row, int row_stride,
               float* out_rgb, rt_stats* stats);
+
+/* Page-locked host memory for rt_render's out_rgb (ABI 7): the frame kernel writes such a buffer
+ * directly through its device-visible address, with no device-to-host copy afterwards (any
+ * pinned buffer, e.g. torch's pin_memory, gets the same path).  NULL on failure
+ * (rt_last_error). */
+void* rt_host_alloc(size_t bytes);
+void rt_host_free(void* ptr);
 
 /* tile_major flags of rt_render_device / rt_render_device_range */
 enum { RT_TILE_MAJOR = 1, RT_TILE_BLOCKS = 2,

@@ -1,6 +1,7 @@
 // ORACLE TEST INFRASTRUCTURE — HW2's driver with the two-line patch of INTEGRATION.md §2:
-// the reference's Scene parses the XML, render_image_gpu (oracle/ref/Scene_gpu.cpp) fills the
-// reference's Pixel array through libceng795_rt.so, and the reference's own Pixel::get_color +
+// the reference's Scene parses the XML and builds its BVH, gpu_scene_open hands that Scene (its
+// objects and its own BVH, walked through public members) to libceng795_rt.so, render_image_gpu
+// (oracle/ref/Scene_gpu.cpp) fills the reference's Pixel array, and the reference's own Pixel::get_color +
 // lodepng::encode write the PNG named by <ImageName> (HW2/main.cpp:17-57).  Linked against the
 // UNMODIFIED reference HW2 sources by oracle/Makefile (`make -C oracle binding`).
 //
@@ -23,7 +24,7 @@
 #include "Scene.h"
 #include "lodepng/lodepng.h"
 
-void gpu_scene_open(const char* xml, int devices);
+void gpu_scene_open(const Scene& scene, const char* xml, int devices);
 void gpu_scene_close();
 void render_image_gpu(const Scene& scene, int camera_index, Pixel* result, int starting_row,
                       int height_increase);
@@ -42,7 +43,7 @@ int main(int argc, char* argv[]) {
   }
   try {
     Scene scene(argv[1]);
-    gpu_scene_open(argv[1], gpus);
+    gpu_scene_open(scene, argv[1], gpus);
     for (size_t cam = 0; cam < scene.cameras.size(); cam++) {
       const Camera& camera = scene.cameras[cam];
       const int w = camera.get_image_plane().width, h = camera.get_image_plane().height;

@@ -1,7 +1,8 @@
 """The reference-side binding of INTEGRATION.md §2, compiled and run.
 
 oracle/_ref/hw2_gpu is the UNMODIFIED reference HW2 Scene / Pixel / tinyxml2 / lodepng sources
-linked with oracle/ref/Scene_gpu.cpp (render_image_gpu over libceng795_rt.so) and
+linked with oracle/ref/Scene_gpu.cpp (the reference's Scene and its own BVH handed to
+libceng795_rt.so as an rt_scene_desc with bvh_*, render_image_gpu over rt_render) and
 oracle/ref/hw2_gpu_main.cpp (HW2/main.cpp:17-57 with the two-line patch).  Its Pixel::color
 must hash to the reference's own frame hashes (tests/golden/golden.json, written by the
 reference's Scene::render_image), and its PNG files — the reference's Pixel::get_color and
@@ -60,6 +61,23 @@ def test_binding_frames_and_pngs_match_the_reference(scene_dir, tmp_path, name):
     png = open(os.path.join(str(tmp_path), image_name(xml)), "rb").read()
     assert hashlib.sha256(png).hexdigest() == pngs["png_sha256"]
     assert png == open(os.path.join(GOLDEN, "png", f"{name}_cam0.png"), "rb").read()
+
+
+def test_binding_renders_every_golden_scene(scene_dir, tmp_path):
+    """Every golden scene (C3 apart: its own test) through the binding, which hands the
+    reference's parsed Scene and its own BVH to the library (rt_scene_desc bvh_*, no library XML
+    loader): Pixel::color hash-equal to the reference's frames (recursion, spheres at the root,
+    grazing rays and C2 included)."""
+    golden = json.load(open(os.path.join(GOLDEN, "golden.json")))
+    names = [n for n in golden if not n.startswith("_") and n != "c3"]
+    assert len(names) >= 12
+    for name in names:
+        xml = scenes.write(name, scene_dir)
+        (tmp_path / name).mkdir()
+        frames = run_binding(xml, str(tmp_path / name))
+        assert len(frames) == len(golden[name]["cameras"]), name
+        for cam, gc in enumerate(golden[name]["cameras"]):
+            assert hashlib.sha256(frames[cam].tobytes()).hexdigest() == gc["frame_sha256"], name
 
 
 def test_binding_with_the_reference_threads(scene_dir, tmp_path):

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_function():
     for n in names:
         assert hasattr(L, n), n
         assert n in _lib.SIGNATURES, f"{n} missing from the ctypes table"
-    assert L.rt_abi_version() == _lib.ABI_VERSION == 6
+    assert L.rt_abi_version() == _lib.ABI_VERSION == 7
 
 
 def test_oracle_is_not_linked_into_the_product():
@@ -307,3 +307,74 @@ def test_culling_tree_on_c3(scene_dir):
     assert rc == 0, _lib.lib().rt_last_error().decode()
     treelets, culling_nodes, depth, lone = list(st)
     assert treelets > 300000 and (treelets + 6) // 7 <= culling_nodes < treelets // 3 and depth < 32
+
+
+# ---- the caller's own BVH in rt_scene_desc (ABI 7) ----------------------
+def _dump_desc(desc, path) -> str:
+    rc = _lib.lib().rt_host_dump_bvh_desc(C.byref(desc.d), str(path).encode())
+    assert rc == 0, _lib.lib().rt_last_error()
+    return open(path).read()
+
+
+@pytest.mark.parametrize("name", ["c1", "hf_small", "soup1", "soup3", "single_sphere",
+                                  "single_triangle", "graze_plane"])
+def test_prebuilt_tree_is_adopted_exactly(scene_dir, tmp_path, name):
+    """A desc carrying its own tree (children, boxes, leaf objects in DFS order, as the binding
+    walks the reference's Scene::bvh) flattens to the same preorder dump as the library's own
+    build — which is the reference's tree (its golden topology hash) — and a desc without one
+    still builds that tree from the object lists."""
+    import desc_xml
+    xml = scenes.write(name, scene_dir)
+    host_dump_bvh(xml, str(tmp_path / "xml.txt"))
+    ref = (tmp_path / "xml.txt").read_text()
+    assert hashlib.sha256(ref.encode()).hexdigest() == GOLDEN[name]["bvh_sha256"]
+    d = desc_xml.Desc(xml)
+    assert _dump_desc(d, tmp_path / "built.txt") == ref
+    children, boxes, objs = desc_xml.tree_from_dump(ref, d)
+    d.set_tree(children, boxes, objs)
+    assert _dump_desc(d, tmp_path / "adopted.txt") == ref
+
+
+def test_prebuilt_tree_normals_are_the_callers(scene_dir, tmp_path):
+    """bvh_leaf_normals: the caller's flat normals are taken as given (the binding passes the
+    reference's Triangle::normal); a desc with them builds the same tree (the dump carries no
+    normals; the GPU binding test checks the shading with the reference's own)."""
+    import desc_xml
+    xml = scenes.write("soup1", scene_dir)
+    host_dump_bvh(xml, str(tmp_path / "xml.txt"))
+    ref = (tmp_path / "xml.txt").read_text()
+    d = desc_xml.Desc(xml)
+    children, boxes, objs = desc_xml.tree_from_dump(ref, d)
+    d.set_tree(children, boxes, objs, normals=np.ones(3 * len(objs), np.float32))
+    assert _dump_desc(d, tmp_path / "n.txt") == ref
+
+
+def test_prebuilt_tree_is_validated(scene_dir, tmp_path):
+    """Malformed trees are refused with RT_E_INVALID: a leaf out of DFS order, a primitive used
+    twice, nodes not in preorder, a wrong node count."""
+    import desc_xml
+    xml = scenes.write("hf_small", scene_dir)
+    host_dump_bvh(xml, str(tmp_path / "xml.txt"))
+    d = desc_xml.Desc(xml)
+    children, boxes, objs = desc_xml.tree_from_dump((tmp_path / "xml.txt").read_text(), d)
+    L = _lib.lib()
+
+    def refused(ch, bx, ob, what):
+        d.set_tree(ch, bx, ob)
+        rc = L.rt_host_dump_bvh_desc(C.byref(d.d), str(tmp_path / "bad.txt").encode())
+        assert rc == _lib.RT_E_INVALID, what
+        assert what in L.rt_last_error().decode(), L.rt_last_error()
+
+    swapped = list(children)
+    i = swapped.index(-1)  # leaf 0's slot
+    j = swapped.index(-2)
+    swapped[i], swapped[j] = swapped[j], swapped[i]
+    refused(swapped, boxes, objs, "DFS order")
+    dup = list(objs)
+    dup[1] = dup[0]
+    refused(children, boxes, dup, "two leaves")
+    k = next(k for k, c in enumerate(children) if c > 1)
+    bad = list(children)
+    bad[k] += 1
+    refused(bad, boxes, objs, "preorder")
+    refused(children[:-2], boxes[:-6], objs, "internal nodes")
