@@ -459,29 +459,34 @@ def timed_probe(scene, R, steps: int, precondition_ms: float = 30.0) -> float:
     return ms
 
 
-def record_band_plan(scene, n: int, costs, rho: float, stream, inflight: int, streams,
-                     steps: int = 20, rounds: int = 3):
-    """Row bands for the pixel-record exchange: rank 0's band starts at root_band_weights(n, rho)
-    and is then calibrated on this GPU — rank 0's work (its band + the resolve of the others')
-    and rank 1's band are timed with `inflight` frames in flight, and rank 0's weight moves by
-    their difference over one band's time (linear in the weight), up to `rounds` times or until
-    they agree within 3 %.  Returns (plan, rank-0 weight, [(t0, t1) per round])."""
+def calibrated_band_plan(scene, n: int, costs, rho, stream, inflight: int, streams,
+                        records: bool, steps: int = 20, rounds: int = 4):
+    """Row bands balanced on measured band times.  The cuts start from the measured tile costs
+    (records: rank 0's band shrunk by its resolve of the others', root_band_weights(n, rho));
+    then every rank's band is timed on this GPU (`inflight` frames in flight, preconditioned) and
+    each rank's weight — its share of the tile costs, band_cuts — is scaled by mean / its time,
+    up to `rounds` times or until the slowest band is within 1.5 % of the mean.  The plan with
+    the smallest slowest band is kept.  Returns (plan, weights, [per-round band times])."""
     from ceng795_amd import dist_tiles
     sizes = [(scene.camera(c).width, scene.camera(c).height) for c in range(scene.num_cameras)]
-    w0 = dist_tiles.root_band_weights(n, rho)[0]
+    w = list(dist_tiles.root_band_weights(n, rho)) if records and rho is not None else [1.0] * n
+    plan = dist_tiles.BandPlan.from_costs(sizes, n, 0, costs, w)
+    if n == 1:
+        return plan, w, []
+    best = (float("inf"), plan, list(w))
     hist = []
-    plan = None
-    for _ in range(rounds if n > 1 else 1):
-        plan = dist_tiles.BandPlan.from_costs(sizes, n, 0, costs, [w0] + [1.0] * (n - 1))
-        if n == 1:
+    for _ in range(rounds):
+        t = [timed_probe(scene, BandProbe(scene, plan, r, stream, inflight, streams, records), steps)
+             for r in range(n)]
+        hist.append([round(x, 4) for x in t])
+        if max(t) < best[0]:
+            best = (max(t), plan, list(w))
+        mean = sum(t) / n
+        if max(t) <= 1.015 * mean:
             break
-        t0 = timed_probe(scene, BandProbe(scene, plan, 0, stream, inflight, streams, True), steps)
-        t1 = timed_probe(scene, BandProbe(scene, plan, 1, stream, inflight, streams, True), steps)
-        hist.append((round(t0, 4), round(t1, 4)))
-        if abs(t0 - t1) <= 0.03 * t1:
-            break
-        w0 = min(1.0, max(0.0, w0 + (t1 - t0) / t1))
-    return plan, w0, hist
+        w = [wi * mean / ti for wi, ti in zip(w, t)]
+        plan = dist_tiles.BandPlan.from_costs(sizes, n, 0, costs, w)
+    return best[1], best[2], hist
 
 
 def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange: str = "rgb",
@@ -527,11 +532,10 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange
         # band shrunk by that work) — both payloads
         bands_by = {}
         for rec in ((False, True) if rho is not None else (False,)):
-            if rec:  # rank 0's band calibrated against its resolve of the others' records
-                plan, w0, hist = record_band_plan(scene, n, costs, rho, stream, inflight, streams,
-                                                  steps)
-            else:
-                plan = dist_tiles.BandPlan.from_costs(sizes, n, 0, costs)
+            # cuts calibrated on measured band times (records: rank 0's band against its
+            # resolve of the others' records too)
+            plan, wts, hist = calibrated_band_plan(scene, n, costs, rho, stream, inflight, streams,
+                                                   rec, steps)
             bands = [timed(BandProbe(scene, plan, r, stream, inflight, streams, rec))
                      for r in range(n)]
             bc = plan.band_costs(costs)
@@ -545,10 +549,10 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange
                         (4 if rec else 12) *
                         sum((b.y1 - b.y0) * plan.sizes[b.camera][0] for b in plan.per_rank[r])
                         for r in range(1, n)) / 1e6, 3)}
+            band["weights"] = [round(x, 4) for x in wts]
+            band["calibration_band_ms"] = hist
             if rec:
                 band["resolve_frac_of_frame"] = round(rho, 4)
-                band["root_weight"] = round(w0, 4)
-                band["root_calibration_ms"] = hist
             bands_by["records" if rec else "rgb"] = (band, max(bands))
         band_step = bands_by["records" if records else "rgb"][1]
         # ranks > 0 render what the N-GPU bench exchanges (RGB or pixel records); rank 0's
@@ -800,8 +804,9 @@ def cpu_rehearsal_bands(args, truth, world, rank, desc) -> int:
 def band_cuts_for(scene, world: int, rank: int, coll_dev: str, records: bool = False,
                   inflight: int = 4, streams=None):
     """Rank 0 measures every camera's tile costs (whole frames on this GPU) and cuts the bands
-    (records: rank 0's band shrunk by its resolve of the others', root_band_weights); the cuts
-    are broadcast so every rank holds the same plan.  Returns (cuts, tile costs or None, the
+    (records: rank 0's band shrunk by its resolve of the others', root_band_weights), then
+    balances them on measured band times (calibrated_band_plan); the cuts are broadcast so
+    every rank holds the same plan.  Returns (cuts, tile costs or None, the
     resolve fraction or None)."""
     import torch
     import torch.distributed as dist
@@ -813,11 +818,11 @@ def band_cuts_for(scene, world: int, rank: int, coll_dev: str, records: bool = F
         costs = dist_tiles.measure_tile_costs(scene)
         if records:  # rank 0's band sized against its resolve of the others' records
             rho = dist_tiles.measure_resolve_frac(scene)
-            st = torch.cuda.current_stream()
-            plan, _, _ = record_band_plan(scene, world, costs, rho, st, inflight,
-                                          dist_tiles.render_streams(inflight, streams=streams))
-        else:
-            plan = dist_tiles.BandPlan.from_costs(sizes, world, 0, costs)
+        st = torch.cuda.current_stream()
+        # the cuts balanced on this GPU's measured band times (calibrated_band_plan)
+        plan, _, _ = calibrated_band_plan(scene, world, costs, rho, st, inflight,
+                                          dist_tiles.render_streams(inflight, streams=streams),
+                                          records)
         flat = [x for cc in plan.cuts for x in cc]
     t = torch.tensor(flat if rank == 0 else [0] * (len(sizes) * (world + 1)),
                      dtype=torch.int64, device=coll_dev)
