@@ -46,7 +46,7 @@ def render_streams(n: int, device=None, streams=None) -> list:
     """`n` render streams for frames in flight: `streams` when given (reused, e.g. one set for
     every renderer of a probe), else n consecutive streams of torch's per-device stream pool —
     never the caller's default stream.  HIP hands the process's hardware queues
-    (GPU_MAX_HW_QUEUES: HIP's default 4, bench.py sets 8) to streams in turn at creation, and two
+    (GPU_MAX_HW_QUEUES: 4, HIP's default and the GPU box's setting) to streams in turn at creation, and two
     streams on one queue serialise their kernels; streams created together sit on different
     queues as long as there are enough, whereas the default stream shares its queue with one of
     them.  (Rendering on the default stream plus three pool streams made the
