@@ -435,6 +435,12 @@ def cold_frame_ms(scene, frames: int = 3):
     return round(sorted(out)[len(out) // 2], 4)
 
 
+# Steps per timed probe of the one-GPU scaling prediction (at least): a 1/8 band of C3 takes
+# ~0.045 ms, so 20 steps timed 1 ms of work and the per-rank times scattered by several % from
+# run to run; 100 steps (each probe also preconditioned, precondition()) hold them within ~1-2 %.
+PROBE_STEPS = 100
+
+
 def precondition(R, ms: float):
     """Untimed steps of renderer R for `ms` of wall time (the GPU's clock ramp after an idle
     gap: profiles/r05/warmup_sweep.txt measured 7.5 % on 3 warm-up steps), then its queue
@@ -460,7 +466,7 @@ def timed_probe(scene, R, steps: int, precondition_ms: float = 30.0) -> float:
 
 
 def calibrated_band_plan(scene, n: int, costs, rho, stream, inflight: int, streams,
-                        records: bool, steps: int = 20, rounds: int = 4):
+                        records: bool, steps: int = PROBE_STEPS, rounds: int = 4):
     """Row bands balanced on measured band times.  The cuts start from the measured tile costs
     (records: rank 0's band shrunk by its resolve of the others', root_band_weights(n, rho));
     then every rank's band is timed on this GPU (`inflight` frames in flight, preconditioned) and
@@ -1220,7 +1226,7 @@ def main() -> int:
                 cold = cold_frame_ms(scene)
                 if not args.no_share_probe:
                     # every efficiency is priced against this line's own N = 1 step
-                    probe = share_probe(scene, stream, max(20, args.steps), args.inflight,
+                    probe = share_probe(scene, stream, max(PROBE_STEPS, args.steps), args.inflight,
                                         exchange=args.exchange, split=args.split,
                                         streams=renderer.streams,
                                         inflight_n=args.split_inflight,
@@ -1232,7 +1238,7 @@ def main() -> int:
                                                traversal=args.traversal) as s4:
                             c4_n1 = n1_steps(s4, stream, args.inflight, args.steps, args.warmup,
                                              args.precondition_ms, dev)
-                            probe_c4 = share_probe(s4, stream, max(20, args.steps), args.inflight,
+                            probe_c4 = share_probe(s4, stream, max(PROBE_STEPS, args.steps), args.inflight,
                                                    exchange=args.exchange, split=args.split,
                                                    streams=renderer.streams,
                                                    inflight_n=args.split_inflight,
