@@ -292,7 +292,7 @@ struct RenderParams {
   unsigned* tile_cost;
   int* unit_order;
   int order_regions, order_chunk, order_stride, order_units;
-  int order_split;  // units per region the order kernel may split tile by tile (quadrant waves)
+  int order_split;  // units per region the order kernel may split into quadrant waves per tile
   int use_order;
   int primary_order;  // the primary kernel too dispatches by unit_order: the order the previous
                       // frame of the same selection left on this stream (rt_api.hip warm order)

@@ -58,6 +58,18 @@ __device__ __forceinline__ unsigned long long clock_now() {
 }
 #endif
 
+// Packets (8x8 tiles, one wave each) per traversal workgroup.  Two: at 3 waves per SIMD (158
+// VGPRs) a CU takes six 2-wave workgroups, and a freed pair of wave slots takes new work where a
+// 4-wave workgroup would wait for four (C3: frame 0.335 -> 0.327 ms with six in flight, a 1/8
+// band 0.047 -> 0.045 ms; profiles/r06/ab_trace_waves.json).  (A/B builds: 1, 2 or 4.)
+#ifndef RT_TRACE_WAVES
+#define RT_TRACE_WAVES 2
+#endif
+constexpr int kTraceWaves = RT_TRACE_WAVES;
+static_assert(kTraceWaves == 1 || kTraceWaves == 2 || kTraceWaves == 4, "1, 2 or 4 waves");
+// A split tile's quadrants take kSplitEntries workgroups of kTraceWaves waves.
+constexpr int kQuadrants = 4, kSplitEntries = kQuadrants / kTraceWaves;
+
 // ------------------------------------------------------------------ vector helpers
 struct V3 {
   float x, y, z;
@@ -694,10 +706,16 @@ __device__ __forceinline__ bool visit_wide(const RenderParams& P, const DevNode*
       const bool pair = (kinds & (kSlotPair << c)) != 0;
       DIAG(dg.ev[kPhPairHits] += pair);
       // (the shadow kernel keeps the exec-mask pushes: junk writes cost it VGPR spills)
+#ifdef RT_PRIO_PUSH  // (A/B builds: the leaf pushes at another priority; +0.3 %, in the noise)
+      __builtin_amdgcn_s_setprio(RT_PRIO_PUSH);
+#endif
       if (pair)
         batch_push_pair<!SHADOW>(L, pending, leaf, hm);
       else
         batch_push<!SHADOW>(L, pending, leaf, hm);
+#ifdef RT_PRIO_PUSH
+      __builtin_amdgcn_s_setprio(3);  // (RT_PRIO_V)
+#endif
       DIAG(dg.leaves += 1 + pair; dg.leaf_lanes += (1 + pair) * __builtin_popcountll(hm));
       continue;
     }
@@ -922,9 +940,9 @@ __device__ __forceinline__ const RenderParams& fresh_params(const RenderParams& 
 // (occupancy is what hides the dependent node loads).
 //
 // A packet is normally one wave's 64 lanes = the tile's 8x8 pixels.  A heavy tile can instead
-// be split over its workgroup's four waves (sub = 0..3: wave `sub` takes quadrant `sub` of the
-// tile, 4x4 pixels in lanes 0..15): fewer rays per wave walk a smaller union
-// of BVH paths, and the four quadrants run side by side.
+// be split over four waves (sub = 0..3: wave `sub` takes quadrant `sub` of the tile, 4x4 pixels
+// in lanes 0..15): fewer rays per wave walk a smaller union of BVH paths, and the
+// four quadrants run side by side (kSplitEntries workgroups of kTraceWaves waves).
 struct PacketPixel {
   int lane;  // pixel lane: the pixel's index within the tile's 8x8 (its record's slot)
   int px, py;
@@ -1533,11 +1551,7 @@ __device__ __forceinline__ int packet_index() {
 // its scalar cache.  With P.tile_block the workgroup's packets form a kBlockW x kBlockH block
 // of tiles (blocks row-major over the frame) instead of a run along a tile row: neighbouring
 // rays walk the same nodes, and the cache serves them once.
-#ifndef RT_TRACE_WAVES  // (A/B builds: 2 = 1x2-tile workgroups)
-#define RT_TRACE_WAVES 4
-#endif
-constexpr int kTraceWaves = RT_TRACE_WAVES;
-constexpr int kBlockW = 2, kBlockH = kTraceWaves / kBlockW;
+constexpr int kBlockW = kTraceWaves >= 2 ? 2 : 1, kBlockH = kTraceWaves / kBlockW;
 
 // Tile (= sel, tile_step 1) of logical packet p; -1 for a padding packet of an edge block.
 __device__ __forceinline__ int packet_sel(const RenderParams& P, int p) {
@@ -1575,8 +1589,9 @@ __device__ __forceinline__ int unit_sel(const RenderParams& P, int unit, int w) 
 
 // Selected tile of this wave in a traversal launch, and its quadrant (sub, -1: the whole
 // packet): ordered (block b of the grid takes entry b / regions of region b mod regions' list,
-// heaviest first: a unit, -1 = none, or -2 - (4 u + w) = tile w of unit u split over the
-// workgroup's four waves, wave k taking quadrant k), else the XCD-remapped block order.
+// heaviest first: a unit, -1 = none, or -2 - (p kSplitEntries + j) = quadrants j kTraceWaves ..
+// of logical packet p's tile, wave k taking quadrant j kTraceWaves + k), else the XCD-remapped
+// block order.
 __device__ __forceinline__ int order_entry(const RenderParams& Q) {
   const int b = (int)blockIdx.x;
   return uniform(Q.unit_order[(b % Q.order_regions) * Q.order_stride + b / Q.order_regions]);
@@ -1588,8 +1603,8 @@ __device__ __forceinline__ int dispatch_sel(const RenderParams& Q) {
     const int e = order_entry(Q);
     if (e >= 0) return uniform(unit_sel(Q, e, w));
     if (e == -1) return -1;
-    const int k = -2 - e;
-    return uniform(unit_sel(Q, k >> 2, k & 3));
+    const int p = (-2 - e) / kSplitEntries;  // the split tile's logical packet
+    return uniform(unit_sel(Q, p / kTraceWaves, p % kTraceWaves));
   }
   const int p = packet_index<kTraceWaves>();
   const int sel = p < trace_packets(Q) ? packet_sel(Q, p) : -1;
@@ -1635,25 +1650,26 @@ __device__ __forceinline__ unsigned unit_cost(const RenderParams& P, int u) {
 //
 // Split: the heaviest units — at most order_split per region, each costing at
 // least kSplitBuckets buckets (2^(kSplitBuckets/8)) above the region's median — are listed as
-// one entry per tile (-2 - (4 u + w)), so each of their tiles gets a workgroup whose four waves
-// take one quadrant each.  Those tiles' costs are zeroed here: the next frame's quadrant waves
+// kSplitEntries entries per tile, so each of their tiles gets kSplitEntries workgroups whose
+// waves take one quadrant each.  Those tiles' costs are zeroed here: the next frame's quadrant waves
 // add their times into them (the tile's cost = the sum of its quadrants).
 constexpr int kOrderThreads = 256;
 // Split tuning (A/B builds): threshold in buckets above the median (8 per octave: 11 = 2.6 x),
-// units split per region at most (1 / RT_SPLIT_DIV of the region), and only in launches whose
-// regions hold at most RT_SPLIT_MAX_UNITS units (the shares of a frame split over GPUs: a whole
-// frame's tail is already hidden by the frames in flight, and splitting adds work)
+// tiles split per region at most (1 / RT_SPLIT_DIV of the region's tiles, at most kMaxSplit), and
+// only in launches whose regions hold at most RT_SPLIT_MAX_TILES tiles (the shares of a frame
+// split over GPUs: a whole frame's tail is already hidden by the frames in flight, and splitting
+// adds work).  Counted in tiles, so the split covers the same share whatever the workgroup size.
 #ifndef RT_SPLIT_BUCKETS
 #define RT_SPLIT_BUCKETS 11
 #endif
 #ifndef RT_SPLIT_DIV
 #define RT_SPLIT_DIV 16
 #endif
-#ifndef RT_SPLIT_MAX_UNITS
-#define RT_SPLIT_MAX_UNITS 192
+#ifndef RT_SPLIT_MAX_TILES
+#define RT_SPLIT_MAX_TILES 768
 #endif
 constexpr int kSplitBuckets = RT_SPLIT_BUCKETS;
-constexpr int kMaxSplit = 32;  // units split per region at most
+constexpr int kMaxSplit = 128;  // tiles split per region at most
 __global__ __launch_bounds__(kOrderThreads) void order_kernel(RenderParams P) {
   __shared__ int hist[kOrderBuckets];
   __shared__ int split_info[2];  // [0] = split threshold bucket, [1] = units split
@@ -1715,17 +1731,19 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(RenderParams P) {
       if (sel >= 0) snap[sel] = P.tile_cost[sel];
     }
     const int r = atomicAdd(&hist[cost_bucket(unit_cost(P, u))], 1);
-    if (r < nsplit) {  // one entry per tile, -1 for a padding tile of an edge block
+    if (r < nsplit) {  // kSplitEntries entries per tile, -1 for a padding tile of an edge block
       for (int w = 0; w < kTraceWaves; w++) {
         const int sel = unit_sel(P, u, w);
-        out[kTraceWaves * r + w] = sel >= 0 ? -2 - (kTraceWaves * u + w) : -1;
+        for (int j = 0; j < kSplitEntries; j++)
+          out[kQuadrants * r + kSplitEntries * w + j] =
+              sel >= 0 ? -2 - ((kTraceWaves * u + w) * kSplitEntries + j) : -1;
         if (sel >= 0) P.tile_cost[sel] = 0u;
       }
     } else {
-      out[r + (kTraceWaves - 1) * nsplit] = u;
+      out[r + (kQuadrants - 1) * nsplit] = u;
     }
   }
-  for (int i = n + (kTraceWaves - 1) * nsplit + tid; i < P.order_stride; i += kOrderThreads)
+  for (int i = n + (kQuadrants - 1) * nsplit + tid; i < P.order_stride; i += kOrderThreads)
     out[i] = -1;
 }
 
@@ -1772,7 +1790,8 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_FRAME_OCCUPANCY void trace_fra
   const int sel = dispatch_sel(Q);
   TL_SEL(sel);
   if (sel >= 0) {
-    L.sub = Q.use_order && order_entry(Q) <= -2 ? (int)threadIdx.x >> 6 : -1;
+    const int e = Q.use_order ? order_entry(Q) : -1;
+    L.sub = e <= -2 ? ((-2 - e) % kSplitEntries) * kTraceWaves + ((int)threadIdx.x >> 6) : -1;
     // the packet's start time waits in LDS (kept in SGPRs across the traversals it spilled)
     __shared__ unsigned long long start[kTraceWaves];
     start[threadIdx.x >> 6] = __builtin_amdgcn_s_memrealtime();
@@ -1871,9 +1890,10 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
     const int chunks = (T.order_units + T.order_chunk - 1) / T.order_chunk;
     const int per_region = ((chunks + T.order_regions - 1) / T.order_regions) * T.order_chunk;
     // room for order_split units per region listed tile by tile (kTraceWaves entries each)
-    T.order_split = RT_ORDER_SPLIT && per_region <= RT_SPLIT_MAX_UNITS
-                        ? min(kMaxSplit, max(1, per_region / RT_SPLIT_DIV)) : 0;
-    T.order_stride = per_region + (kTraceWaves - 1) * T.order_split;
+    const int region_tiles = per_region * kTraceWaves;
+    T.order_split = RT_ORDER_SPLIT && region_tiles <= RT_SPLIT_MAX_TILES
+                        ? max(1, min(kMaxSplit, region_tiles / RT_SPLIT_DIV) / kTraceWaves) : 0;
+    T.order_stride = per_region + (kQuadrants - 1) * T.order_split;
     ordered = (unsigned long long)T.num_sel_tiles +
                   (unsigned long long)T.order_regions * T.order_stride <=
               sched_snap_offset((unsigned long long)T.num_sel_tiles);
