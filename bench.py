@@ -495,6 +495,26 @@ def calibrated_band_plan(scene, n: int, costs, rho, stream, inflight: int, strea
     return best[1], best[2], hist
 
 
+# Measured causes of band efficiencies above 1.0, by frame: per-launch PMC of the frame kernel
+# (tools/band_pmc.py, dispatches serialised) for the whole frame and every band of the cut.
+BAND_LOCALITY = {
+    "3840x2160": "profiles/r06/band_locality.json: the C4 bands' launches together fetch 0.78x "
+                 "(N = 2) / 0.73x (N = 8) of the whole frame's HBM bytes, L2 hit rate 0.71 -> "
+                 "0.75 / 0.77 (a band's rays walk a smaller part of the tree, which stays in L2); "
+                 "C3's bands fetch 1.11x at N = 8 and predict below 1.0",
+}
+
+
+def efficiency_check(frame: str, per_n: dict) -> str:
+    over = [n for n, v in per_n.items() if v["predicted_efficiency"] > 1.0]
+    if not over:
+        return "ok: no prediction above 1.0"
+    if frame in BAND_LOCALITY:
+        return f"above 1.0 at N = {', '.join(over)}, measured cause: {BAND_LOCALITY[frame]}"
+    return (f"SUSPECT: above 1.0 at N = {', '.join(over)} with no measured cause; treat as a "
+            "probe artifact")
+
+
 def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange: str = "rgb",
                 split: str = "bands", streams=None, inflight_n: int = INFLIGHT_SPLIT,
                 t1_line_ms=None):
@@ -599,9 +619,7 @@ def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange
                           if t1_line_ms else "re-probed"),
             "t1_probe_ms": round(t1_probe, 4),
             "t1_probe_over_t1": round(t1_probe / t1, 4),
-            "efficiency_check": ("ok: no prediction above 1.0" if max(eff) <= 1.0 else
-                                 "SUSPECT: a prediction above 1.0 (no measured cause; treat "
-                                 "as a probe artifact)"),
+            "efficiency_check": efficiency_check(f"{cam.width}x{cam.height}", out),
             "steps": steps,
             "frames_in_flight": {"t1": one.inflight, "per_rank": inflight_n},
             "split": split,
