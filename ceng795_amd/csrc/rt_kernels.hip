@@ -58,10 +58,12 @@ __device__ __forceinline__ unsigned long long clock_now() {
 }
 #endif
 
-// Packets (8x8 tiles, one wave each) per traversal workgroup.  Two: at 3 waves per SIMD (158
-// VGPRs) a CU takes six 2-wave workgroups, and a freed pair of wave slots takes new work where a
-// 4-wave workgroup would wait for four (C3: frame 0.335 -> 0.327 ms with six in flight, a 1/8
-// band 0.047 -> 0.045 ms; profiles/r06/ab_trace_waves.json).  (A/B builds: 1, 2 or 4.)
+// Packets (8x8 tiles, one wave each) per traversal workgroup.  Two: a workgroup's LDS (leaf
+// queues, ~5.6 KiB per wave, which like the VGPRs caps a CU at 28 waves) stays allocated until
+// its slowest wave ends, so the finished waves of a 4-wave workgroup hold slots a new workgroup
+// cannot use; with two, half as much sits idle behind a heavy packet (C3: frame 0.335 -> 0.327
+// ms with six in flight, a 1/8 band 0.047 -> 0.045 ms; profiles/r06/ab_trace_waves.json).
+// (A/B builds: 1, 2 or 4.)
 #ifndef RT_TRACE_WAVES
 #define RT_TRACE_WAVES 2
 #endif
