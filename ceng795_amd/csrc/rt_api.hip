@@ -328,16 +328,19 @@ int occ_words(const HostScene& h) { return std::max(1, ((int)h.lights.size() + 3
 // A counter buffer: kCounterRows x kCounterWidth ray counters.
 constexpr size_t kCounterAlloc = (size_t)kCounterWidth * kCounterRows;
 // Dispatch order of the traversal kernels: heavy first within each XCD's
-// part of the frame (RT_ORDER_REGIONS regions, one per XCD; 0 = block order), each region one
-// contiguous band of the frame (RT_ORDER_CHUNKS chunks per region: its L2 then holds that
-// band's part of the tree — shadow kernel reads 91 vs 130 MB per C3 frame with interleaved
-// half-row chunks, profiles/r03/ab_order_chunks.jsonl).  The order never changes a result,
-// only which tiles start first.  (Macros: A/B builds, `make exp EXTRA=-D...`.)
+// part of the frame (RT_ORDER_REGIONS regions, one per XCD; 0 = block order), each region
+// RT_ORDER_CHUNKS contiguous bands of the frame, chunk c in region c mod regions.  Two: an XCD's
+// L2 still holds its bands' part of the tree (shadow kernel reads 91 vs 130 MB per C3 frame with
+// interleaved half-row chunks, profiles/r03/ab_order_chunks.jsonl), and two bands half a frame
+// apart even out the XCDs' shares of the heavy rows (C3 frame kernel 0.352 -> 0.339 ms one at a
+// time, 0.327 -> 0.319 six in flight; 4 / 8 / 16 chunks 0.343 / 0.343 / 0.346;
+// profiles/r06/ab_order_chunks.json).  The order never changes a result, only which tiles start
+// first.  (Macros: A/B builds, `make exp EXTRA=-D...`.)
 #ifndef RT_ORDER_REGIONS
 #define RT_ORDER_REGIONS 8
 #endif
 #ifndef RT_ORDER_CHUNKS
-#define RT_ORDER_CHUNKS 1
+#define RT_ORDER_CHUNKS 2
 #endif
 // sched: sched_words_for(num_sel_tiles) words — tile costs, then the unit order lists
 // The untile kernel copies 16-B chunks when every frame row and both buffers are 16-B aligned.
