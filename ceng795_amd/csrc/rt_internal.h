@@ -294,6 +294,11 @@ struct RenderParams {
   int order_regions, order_chunk, order_stride, order_units;
   int order_split;  // units per region the order kernel may split into quadrant waves per tile
   int use_order;
+  // cold_order: the camera's whole-frame unit order seeded at scene creation from estimated tile
+  // costs (rt_api.hip seed_cold_orders), for a frame without a previous one (no split entries);
+  // used when the launch selects cold_tiles tiles (the whole frame), else nullptr
+  const int* cold_order;
+  int cold_tiles;
   int primary_order;  // the primary kernel too dispatches by unit_order: the order the previous
                       // frame of the same selection left on this stream (rt_api.hip warm order)
   int records;    // RT_TILE_RECORDS: the shading phase writes 32-bit pixel records, not RGB

@@ -1848,6 +1848,56 @@ static inline void mark(const hipEvent_t* marks, int k, hipStream_t stream) {
   if (marks) (void)hipEventRecord(marks[k], stream);
 }
 
+// Dispatch-order geometry of a traversal launch: units of one traversal
+// workgroup, `regions` regions of `chunk`-unit chunks (tile_block: half a row of 2x1 blocks), LPT
+// within each region.  Sets T's tile_block and order_* fields, the launch's unit count (tblocks)
+// and the units per region; false: the launch runs in block order (no order kernel).
+#ifndef RT_ORDER_MIN_TILES  // launches selecting fewer tiles run in block order (no order kernel)
+#define RT_ORDER_MIN_TILES 0
+#endif
+#ifndef RT_ORDER_SPLIT  // (A/B builds: 0 = no heavy-tile split)
+#define RT_ORDER_SPLIT 1
+#endif
+static bool order_geometry(RenderParams& T, int& tblocks, int& per_region) {
+  // 2-D blocks of tiles for a selection of whole tile rows: the whole frame, or a row band
+  // (dist_tiles.BandPlan: tiles tile_begin .. tile_begin + num_sel_tiles - 1)
+  T.tile_block = T.tile_step == 1 && !T.block_deal && T.tile_begin % T.tiles_x == 0 &&
+                 T.num_sel_tiles % T.tiles_x == 0;
+  tblocks = (trace_packets(T) + kTraceWaves - 1) / kTraceWaves;
+  per_region = 0;
+  T.use_order = 0;
+  if (!(T.tile_cost != nullptr && T.unit_order != nullptr && T.order_regions > 0 &&
+        T.num_sel_tiles >= RT_ORDER_MIN_TILES))
+    return false;
+  T.order_units = tblocks;
+  const int nbx = (T.tiles_x + kBlockW - 1) / kBlockW;
+  if (T.order_chunk > 0)  // host-set: that many chunks per region
+    T.order_chunk = max(1, (tblocks + T.order_regions * T.order_chunk - 1) / (T.order_regions * T.order_chunk));
+  else
+    T.order_chunk = T.tile_block ? max(1, (nbx + 1) / 2) : 64;
+  const int chunks = (T.order_units + T.order_chunk - 1) / T.order_chunk;
+  per_region = ((chunks + T.order_regions - 1) / T.order_regions) * T.order_chunk;
+  // room for order_split units per region listed quadrant group by quadrant group
+  const int region_tiles = per_region * kTraceWaves;
+  T.order_split = RT_ORDER_SPLIT && region_tiles <= RT_SPLIT_MAX_TILES
+                      ? max(1, min(kMaxSplit, region_tiles / RT_SPLIT_DIV) / kTraceWaves) : 0;
+  T.order_stride = per_region + (kQuadrants - 1) * T.order_split;
+  return (unsigned long long)T.num_sel_tiles + (unsigned long long)T.order_regions * T.order_stride <=
+         sched_snap_offset((unsigned long long)T.num_sel_tiles);
+}
+
+// The cold order of a camera's whole frame (rt_api.hip seed_cold_orders): P's tile_cost holds
+// the estimated tile costs; the order kernel lists the units heaviest first into P's
+// unit_order, without split entries.  Returns 1 if the launch is ordered (a list was made).
+int launch_cold_order(RenderParams P, hipStream_t stream) {
+  int tblocks = 0, per_region = 0;
+  if (P.num_sel_tiles <= 0 || !order_geometry(P, tblocks, per_region)) return 0;
+  P.order_split = 0;
+  P.order_stride = per_region;
+  hipLaunchKernelGGL(order_kernel, dim3(P.order_regions), dim3(kOrderThreads), 0, stream, P);
+  return hipGetLastError() == hipSuccess ? 1 : 0;
+}
+
 template <bool FAST, bool DEEP, bool SPHERES>
 static void launch_variant(const RenderParams& P, const DevNode* nodes, const DevPrim* prims,
                            const float* normals, const DevMaterial* mats,
@@ -1865,49 +1915,25 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
     return;
   }
   RenderParams T = P;
-  // 2-D blocks of tiles for a selection of whole tile rows: the whole frame, or a row band
-  // (dist_tiles.BandPlan: tiles tile_begin .. tile_begin + num_sel_tiles - 1)
-  T.tile_block = P.tile_step == 1 && !P.block_deal && P.tile_begin % P.tiles_x == 0 &&
-                 P.num_sel_tiles % P.tiles_x == 0;
-  const int tblocks = (trace_packets(T) + kTraceWaves - 1) / kTraceWaves;
+  int tblocks = 0, per_region = 0;
+  bool ordered = order_geometry(T, tblocks, per_region);
   const size_t tlds = DEEP ? sizeof(int) * kDeepWords * kDeepStack * kTraceWaves : 0;
-  // dispatch order: units of one traversal workgroup, `regions` regions of
-  // `chunk`-unit chunks (tile_block: half a row of 2x2 blocks), LPT within each region
-  T.use_order = 0;
-#ifndef RT_ORDER_MIN_TILES  // launches selecting fewer tiles run in block order (no order kernel)
-#define RT_ORDER_MIN_TILES 0
-#endif
-#ifndef RT_ORDER_SPLIT  // (A/B builds: 0 = no heavy-tile split)
-#define RT_ORDER_SPLIT 1
-#endif
-  bool ordered = T.tile_cost != nullptr && T.unit_order != nullptr && T.order_regions > 0 &&
-                 T.num_sel_tiles >= RT_ORDER_MIN_TILES;
-  if (ordered) {
-    T.order_units = tblocks;
-    const int nbx = (T.tiles_x + kBlockW - 1) / kBlockW;
-    if (T.order_chunk > 0)  // host-set: that many chunks per region
-      T.order_chunk = max(1, (tblocks + T.order_regions * T.order_chunk - 1) / (T.order_regions * T.order_chunk));
-    else
-      T.order_chunk = T.tile_block ? max(1, (nbx + 1) / 2) : 64;
-    const int chunks = (T.order_units + T.order_chunk - 1) / T.order_chunk;
-    const int per_region = ((chunks + T.order_regions - 1) / T.order_regions) * T.order_chunk;
-    // room for order_split units per region listed tile by tile (kTraceWaves entries each)
-    const int region_tiles = per_region * kTraceWaves;
-    T.order_split = RT_ORDER_SPLIT && region_tiles <= RT_SPLIT_MAX_TILES
-                        ? max(1, min(kMaxSplit, region_tiles / RT_SPLIT_DIV) / kTraceWaves) : 0;
-    T.order_stride = per_region + (kQuadrants - 1) * T.order_split;
-    ordered = (unsigned long long)T.num_sel_tiles +
-                  (unsigned long long)T.order_regions * T.order_stride <=
-              sched_snap_offset((unsigned long long)T.num_sel_tiles);
-  }
-  const int oblocks = ordered ? T.order_regions * T.order_stride : tblocks;
+  int oblocks = ordered ? T.order_regions * T.order_stride : tblocks;
   const RenderParams S = T;
   // one kernel per frame, dispatched by the previous frame's heavy-first order when there is one
-  // (warm order: same selection, same stream); the order kernel then sorts this frame's packet
-  // costs for the next frame
+  // (warm order: same selection, same stream), else — a camera's whole frame — by the order
+  // seeded at scene creation (cold order, no split); the order kernel then sorts this frame's
+  // packet costs for the next frame
   mark(marks, 0, stream);
   if (!ordered) T.tile_cost = nullptr;
   T.use_order = ordered && P.primary_order ? 1 : 0;
+  if (ordered && !T.use_order && P.cold_order && P.num_sel_tiles == P.cold_tiles) {
+    T.order_split = 0;
+    T.order_stride = per_region;
+    T.unit_order = const_cast<int*>(P.cold_order);
+    T.use_order = 1;
+    oblocks = T.order_regions * T.order_stride;
+  }
   hipLaunchKernelGGL((trace_frame_kernel<FAST, DEEP, SPHERES>), dim3(T.use_order ? oblocks : tblocks),
                      dim3(kTraceWaves * 64), tlds, stream, T, nodes, lights);
   mark(marks, 1, stream);
