@@ -299,7 +299,6 @@ struct RenderParams {
   // used when the launch selects cold_tiles tiles (the whole frame), else nullptr
   const int* cold_order;
   int cold_tiles;
-  int no_next_order;  // no order kernel after the frame (nothing renders this selection again)
   int primary_order;  // the primary kernel too dispatches by unit_order: the order the previous
                       // frame of the same selection left on this stream (rt_api.hip warm order)
   int records;    // RT_TILE_RECORDS: the shading phase writes 32-bit pixel records, not RGB

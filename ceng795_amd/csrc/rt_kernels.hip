@@ -1937,8 +1937,7 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
   hipLaunchKernelGGL((trace_frame_kernel<FAST, DEEP, SPHERES>), dim3(T.use_order ? oblocks : tblocks),
                      dim3(kTraceWaves * 64), tlds, stream, T, nodes, lights);
   mark(marks, 1, stream);
-  if (ordered && !P.no_next_order)
-    hipLaunchKernelGGL(order_kernel, dim3(S.order_regions), dim3(kOrderThreads), 0, stream, S);
+  if (ordered) hipLaunchKernelGGL(order_kernel, dim3(S.order_regions), dim3(kOrderThreads), 0, stream, S);
   mark(marks, 2, stream);
   mark(marks, 3, stream);
 }
