@@ -1679,6 +1679,10 @@ int rt_render(rt_scene* s, int cam, int row0, int row_stride, float* out_rgb, rt
       // block order: the frame is bound by its writes over PCIe, which the heavy-first (cold)
       // order scatters (0.674 -> 0.742 ms per C3 frame, profiles/r06/ab_dropin_cold.jsonl)
       P.tile_cost = nullptr;
+#ifndef RT_PAIR_ROWS  // (A/B builds: 0 = each wave writes its own tile)
+#define RT_PAIR_ROWS 1
+#endif
+      P.pair_rows = RT_PAIR_ROWS;
       enqueue_frame(s, r, P, c.num_samples, x->d_samples, x->stream, true);
       hip_check(hipEventRecord(x->e1, x->stream), "event record");
     } else if (!multi && c.num_samples <= 1 && chunks > 1) {

@@ -299,6 +299,10 @@ struct RenderParams {
   // used when the launch selects cold_tiles tiles (the whole frame), else nullptr
   const int* cold_order;
   int cold_tiles;
+  // pair_rows: a row-major frame in host memory written over PCIe (rt_render, pinned): the two
+  // tiles of a workgroup are written together as whole rows of 16 pixels (launch_variant
+  // checks the layout; 0 = each wave writes its own tile)
+  int pair_rows;
   int primary_order;  // the primary kernel too dispatches by unit_order: the order the previous
                       // frame of the same selection left on this stream (rt_api.hip warm order)
   int records;    // RT_TILE_RECORDS: the shading phase writes 32-bit pixel records, not RGB

@@ -1222,7 +1222,7 @@ __device__ __forceinline__ void shade_pixel(const RenderParams& P,
                                             const float* __restrict__ normals,
                                             const DevMaterial* __restrict__ mats,
                                             const DevLight* __restrict__ lights, int sel,
-                                            int sub) {
+                                            int sub, float* stage = nullptr) {
   const PacketPixel q = packet_pixel(P, sel, sub);
   const size_t pix = (size_t)sel * (kTile * kTile) + q.lane;
   const int2_t rec = P.hits[pix];
@@ -1248,7 +1248,11 @@ __device__ __forceinline__ void shade_pixel(const RenderParams& P,
   } else if (valid) {
     color = ld3(P.background);  // primary miss: max_recursion_depth == depth
   }
-  if (valid) {
+  if (valid && stage) {  // pair_rows: the colour waits in LDS for the workgroup's row writes
+    stage[3 * q.lane] = 0.0f + color.x;
+    stage[3 * q.lane + 1] = 0.0f + color.y;
+    stage[3 * q.lane + 2] = 0.0f + color.z;
+  } else if (valid) {
     float* o;
     if (P.tile_major)
       o = P.out + 3 * pix;
@@ -1260,6 +1264,32 @@ __device__ __forceinline__ void shade_pixel(const RenderParams& P,
   } else if (P.tile_major && q.own) {
     float* o = P.out + 3 * pix;
     o[0] = o[1] = o[2] = 0.0f;
+  }
+}
+
+// pair_rows (rt_render into pinned host memory): the frame kernel's stores cross PCIe, where a
+// wave's 8 rows of 96 B each end in a half-filled 64-B line.  The workgroup's two tiles (a 2x1
+// unit, tx even) instead leave their colours in their waves' LDS; the second wave to arrive
+// writes both tiles as 8 rows of 192 B — whole 64-B lines, 16-B stores.  (Same values, same
+// pixels: only who stores them changes.)
+__device__ __forceinline__ void pair_write(const RenderParams& P, WaveLeafLds* lds, int sel,
+                                           int* arrived) {
+  __threadfence_block();  // this wave's staged colours before its arrival
+  int first = 0;
+  if (lane_id() == 0) first = atomicAdd(arrived, 1) == 0;
+  if (__builtin_amdgcn_readfirstlane(first)) return;  // the partner writes both tiles
+  __threadfence_block();
+  const int w = (int)threadIdx.x >> 6;
+  const int tile = P.tile_begin + sel - w;  // the unit's left tile
+  const int tx0 = tile % P.tiles_x, ty = tile / P.tiles_x;
+  for (int f = lane_id(); f < 96; f += 64) {  // 8 rows x 12 float4
+    const int r = f / 12, k = f % 12;
+    const int lr = ty * kTile + r;
+    if (lr >= P.rows) continue;
+    const float* src = reinterpret_cast<const float*>(lds[k / 6].q) + r * 24 + (k % 6) * 4;
+    const size_t y = (size_t)(P.row0 + lr * P.row_stride);
+    float4* dst = reinterpret_cast<float4*>(P.out + 3 * (y * P.width + (size_t)tx0 * kTile) + 4 * k);
+    *dst = make_float4(src[0], src[1], src[2], src[3]);
   }
 }
 
@@ -1787,6 +1817,11 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_FRAME_OCCUPANCY void trace_fra
   __shared__ WaveLeafLds leaf_lds[kTraceWaves];
   int* spill = DEEP ? deep_stack + ((int)threadIdx.x >> 6) * kDeepWords * kDeepStack : nullptr;
   WaveLeafLds& L = leaf_lds[threadIdx.x >> 6];
+  __shared__ int pair_arrived;
+  if (P.pair_rows) {
+    if (threadIdx.x == 0) pair_arrived = 0;
+    __syncthreads();
+  }
   TL_BEGIN;
   const RenderParams& Q = fresh_params(P);
   const int sel = dispatch_sel(Q);
@@ -1804,7 +1839,13 @@ __global__ __launch_bounds__(kTraceWaves * 64) RT_FRAME_OCCUPANCY void trace_fra
       shadow_packet<FAST, DEEP, SPHERES>(fresh_params(P), nodes, lights, sel, spill, L);
     DIAG(const unsigned long long c2 = clock_now());
     const RenderParams& Ps = fresh_params(P);
-    shade_pixel<SPHERES>(Ps, Ps.prims, Ps.normals, Ps.materials, lights, sel, wave_sub(L));
+    if (Ps.pair_rows) {
+      shade_pixel<SPHERES>(Ps, Ps.prims, Ps.normals, Ps.materials, lights, sel, -1,
+                           reinterpret_cast<float*>(L.q));
+      pair_write(fresh_params(P), leaf_lds, sel, &pair_arrived);
+    } else {
+      shade_pixel<SPHERES>(Ps, Ps.prims, Ps.normals, Ps.materials, lights, sel, wave_sub(L));
+    }
 #ifdef RT_DIAG
     const unsigned long long c3 = clock_now();
     if (lane_id() == 0) {
@@ -1934,6 +1975,10 @@ static void launch_variant(const RenderParams& P, const DevNode* nodes, const De
     T.use_order = 1;
     oblocks = T.order_regions * T.order_stride;
   }
+  // every workgroup holds two tiles of one tile row (tiles_x even, whole 16-pixel rows)
+  T.pair_rows = P.pair_rows && kTraceWaves == 2 && kBlockW == 2 && T.tile_block && !T.use_order &&
+                !T.tile_major && !T.records && T.tiles_x % 2 == 0 && T.width % 16 == 0 &&
+                (reinterpret_cast<uintptr_t>(T.out) & 15) == 0 ? 1 : 0;
   hipLaunchKernelGGL((trace_frame_kernel<FAST, DEEP, SPHERES>), dim3(T.use_order ? oblocks : tblocks),
                      dim3(kTraceWaves * 64), tlds, stream, T, nodes, lights);
   mark(marks, 1, stream);

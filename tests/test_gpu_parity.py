@@ -63,6 +63,43 @@ def test_row_subset_like_render_image(rt, scene_dir, start, stride):
         assert np.all(got[~sel] == -7.0)
 
 
+@pytest.mark.parametrize("name", ["hf_side", "soup3", "ragged"])
+@pytest.mark.parametrize("start,stride", [(0, 1), (3, 5), (0, 2), (47, 1)])
+def test_pinned_host_buffer_like_render_image(rt, scene_dir, name, start, stride):
+    """render_image into page-locked host memory: the frame kernel writes the caller's buffer
+    itself over PCIe (rt_api.hip rt_render), whole 16-pixel rows per workgroup where the frame
+    allows (pair_rows: hf_side 96 x 64, soup3 64 x 72; ragged, 75 x 53, is not a multiple of 16
+    wide: each wave writes its own tile) — the same bits and rows as the oracle's."""
+    import torch
+    xml = scenes.write(name, scene_dir)
+    ref, _ = oracle_frame(xml, 0)
+    if start >= ref.shape[0]:
+        pytest.skip("starting row past the frame")
+    with rt.Scene(xml) as s:
+        buf = torch.full(ref.shape, -7.0, dtype=torch.float32).pin_memory()
+        got, _ = s.render_image(0, buf.numpy(), start, stride)
+        rows = np.arange(ref.shape[0])
+        sel = (rows >= start) & ((rows - start) % stride == 0)
+        assert np.array_equal(got[sel].view(np.uint32), ref[sel].view(np.uint32))
+        assert np.all(got[~sel] == -7.0)
+
+
+def test_c3_pinned_host_buffer_matches_reference_golden_hash(rt, scene_dir):
+    """The drop-in's fast path on C3: rt_render into pinned memory (pair_rows) equals the
+    reference's own frame."""
+    import hashlib
+    import json
+    import torch
+    golden = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+    xml = scenes.write_c3(scene_dir)
+    gc = golden["c3"]["cameras"][0]
+    with rt.Scene(xml) as s:
+        buf = torch.zeros((gc["height"], gc["width"], 3), dtype=torch.float32).pin_memory()
+        for _ in range(2):
+            got, _ = s.render_image(0, buf.numpy())
+            assert hashlib.sha256(got.tobytes()).hexdigest() == gc["frame_sha256"]
+
+
 def test_tile_major_device_render(rt, scene_dir):
     """Multi-GPU building block: tiles tile_begin + k*tile_step, tile-major, in HBM."""
     import torch
