@@ -365,15 +365,19 @@ void set_schedule(RenderParams& P, unsigned* sched) {
 }
 
 // Estimated cost of every tile of camera c's whole frame, for the dispatch order of a frame
-// without a previous one (the cold frame): 1 + the number of primitives whose
-// projected bounds touch the tile.  Where many primitives project into one tile — surfaces seen
-// edge-on — its rays walk more of the tree (C3: correlation 0.58 with measured tile times).  A
-// point X projects to the image-plane point tl + su fx - sv fy that e + l (X - e) reaches
-// (Cramer's rule; l > 0: in front of the camera); a primitive with a point not in front is
-// left out.  Only the order depends on it, never a pixel.
+// without a previous one (the cold frame): 16 x (1 + the primitives whose
+// projected bounds touch the tile, each weighted by 1 / |cos| of the angle between its normal
+// and the view direction, at most 20).  Where many primitives project into one tile — surfaces
+// seen edge-on — its rays walk more of the tree (C3: correlation 0.62 with measured tile times,
+// 0.59 unweighted).  A point X projects to the image-plane point tl + su fx - sv fy that
+// e + l (X - e) reaches (Cramer's rule; l > 0: in front of the camera); a primitive with a point
+// not in front is left out.  Only the order depends on it, never a pixel.
+#ifndef RT_COLD_WEIGHT  // (A/B builds: 0 = every primitive counts 1)
+#define RT_COLD_WEIGHT 1
+#endif
 std::vector<unsigned> cold_costs(const HostScene& h, const rt_camera& c) {
   const int tx = (c.width + kTile - 1) / kTile, ty = (c.height + kTile - 1) / kTile;
-  std::vector<unsigned> est((size_t)tx * ty, 1u);
+  std::vector<double> acc((size_t)tx * ty, 1.0);
   const double e[3] = {c.e[0], c.e[1], c.e[2]};
   const double nu[3] = {-c.s_u[0], -c.s_u[1], -c.s_u[2]}, sv[3] = {c.s_v[0], c.s_v[1], c.s_v[2]};
   const double r[3] = {c.top_left[0] - e[0], c.top_left[1] - e[1], c.top_left[2] - e[2]};
@@ -399,6 +403,7 @@ std::vector<unsigned> cold_costs(const HostScene& h, const rt_camera& c) {
   for (const DevPrim& p : h.prims) {
     double pts[8][3];
     int n = 0;
+    double weight = 1.0;
     if (p.kind == kPrimTriangle) {
       for (int k = 0; k < 3; k++) {
         pts[0][k] = p.v0[k];
@@ -406,6 +411,17 @@ std::vector<unsigned> cold_costs(const HostScene& h, const rt_camera& c) {
         pts[2][k] = (double)p.v0[k] - p.a2[k];
       }
       n = 3;
+      if (RT_COLD_WEIGHT) {
+        const double a1[3] = {p.a1[0], p.a1[1], p.a1[2]}, a2[3] = {p.a2[0], p.a2[1], p.a2[2]};
+        double nrm[3];
+        cross(a1, a2, nrm);
+        const double d[3] = {(pts[0][0] + pts[1][0] + pts[2][0]) / 3 - e[0],
+                             (pts[0][1] + pts[1][1] + pts[2][1]) / 3 - e[1],
+                             (pts[0][2] + pts[1][2] + pts[2][2]) / 3 - e[2]};
+        const double len = std::sqrt(dot(nrm, nrm) * dot(d, d));
+        const double cosv = len > 0.0 ? std::fabs(dot(nrm, d)) / len : 1.0;
+        weight = 1.0 / std::max(cosv, 0.05);
+      }
     } else {
       const double rad = std::fabs((double)p.a1[0]);
       for (int m = 0; m < 8; m++)
@@ -426,8 +442,10 @@ std::vector<unsigned> cold_costs(const HostScene& h, const rt_camera& c) {
     const int a0 = std::max(0, (int)(x0 / kTile)), a1 = std::min(tx - 1, (int)(x1 / kTile));
     const int b0 = std::max(0, (int)(y0 / kTile)), b1 = std::min(ty - 1, (int)(y1 / kTile));
     for (int b = b0; b <= b1; b++)
-      for (int a = a0; a <= a1; a++) est[(size_t)b * tx + a]++;
+      for (int a = a0; a <= a1; a++) acc[(size_t)b * tx + a] += weight;
   }
+  std::vector<unsigned> est(acc.size());
+  for (size_t i = 0; i < acc.size(); i++) est[i] = (unsigned)std::min(16.0 * acc[i], 4e9);
   return est;
 }
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Offline study of the cold-frame order (CPU only, development tool): how well the projected-
-primitive count per tile (rt_api.hip cold_costs) orders a C3 frame, replayed against measured
-per-tile times.
+primitive count per tile (rt_api.hip cold_costs: each primitive weighted by 1 / |cos| of its
+view angle, or unweighted) orders a C3 frame, replayed against measured per-tile times.
 
   python tools/cold_study.py [--costs profiles/r05/tile_cost_map_split_w1.npz]
 
@@ -25,7 +25,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
-def estimate(n=708, width=1920, height=1080):
+def estimate(n=708, width=1920, height=1080, weighted=True):
     import gen_scene as G
     from ceng795_amd import _lib
     V = np.array([[float(x) for x in ln.split()] for ln in G.heightfield_vertices(n)])
@@ -47,9 +47,15 @@ def estimate(n=708, width=1920, height=1080):
     x1 = np.clip(np.floor(fx[T].max(1) / 8).astype(int), 0, tx - 1)
     y0 = np.clip(np.floor(fy[T].min(1) / 8).astype(int), 0, ty - 1)
     y1 = np.clip(np.floor(fy[T].max(1) / 8).astype(int), 0, ty - 1)
+    w = np.ones(len(T))
+    if weighted:  # 1 / |cos(normal, view direction)|, at most 20 (as cold_costs)
+        nrm = np.cross(V[T[:, 0]] - V[T[:, 1]], V[T[:, 0]] - V[T[:, 2]])
+        d = V[T].mean(1) - e
+        cosv = np.abs((nrm * d).sum(1)) / (np.linalg.norm(nrm, axis=1) * np.linalg.norm(d, axis=1))
+        w = 1.0 / np.maximum(cosv, 0.05)
     est = np.ones((ty, tx))
     for i in np.nonzero(ok)[0]:
-        est[y0[i]:y1[i] + 1, x0[i]:x1[i] + 1] += 1
+        est[y0[i]:y1[i] + 1, x0[i]:x1[i] + 1] += w[i]
     return est
 
 
@@ -80,10 +86,12 @@ def main():
     a = ap.parse_args()
     m = np.load(a.costs)
     cost = m["trace_primary_kernel"] + m["trace_shadow_kernel"]
-    est = estimate()
-    print({"corr": round(float(np.corrcoef(est.ravel(), cost.ravel())[0, 1]), 3),
+    est, cnt = estimate(), estimate(weighted=False)
+    print({"corr_weighted": round(float(np.corrcoef(est.ravel(), cost.ravel())[0, 1]), 3),
+           "corr_count": round(float(np.corrcoef(cnt.ravel(), cost.ravel())[0, 1]), 3),
            "block_order": round(float(replay(cost, None, chunks=1)), 1),  # (one run per XCD)
-           "estimate_order": round(float(replay(cost, est)), 1),
+           "count_order": round(float(replay(cost, cnt)), 1),
+           "weighted_order": round(float(replay(cost, est)), 1),
            "measured_order": round(float(replay(cost, cost)), 1)})
 
 
