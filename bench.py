@@ -506,13 +506,22 @@ BAND_LOCALITY = {
 
 
 def efficiency_check(frame: str, per_n: dict) -> str:
-    over = [n for n, v in per_n.items() if v["predicted_efficiency"] > 1.0]
+    """Every prediction of the line (the chosen split and payload, and the RGB bands, record
+    bands and tile deal beside it) above 1.0, with its measured cause or flagged."""
+    over = []
+    for n, v in per_n.items():
+        for name, e in (("line", v.get("predicted_efficiency")),
+                        ("rgb bands", v.get("bands", {}).get("predicted_efficiency")),
+                        ("record bands", v.get("bands_records", {}).get("predicted_efficiency")),
+                        ("tile deal", v.get("tiles", {}).get("predicted_efficiency"))):
+            if e is not None and e > 1.0:
+                over.append(f"N = {n} {name} {e}")
     if not over:
         return "ok: no prediction above 1.0"
     if frame in BAND_LOCALITY:
-        return f"above 1.0 at N = {', '.join(over)}, measured cause: {BAND_LOCALITY[frame]}"
-    return (f"SUSPECT: above 1.0 at N = {', '.join(over)} with no measured cause; treat as a "
-            "probe artifact")
+        return f"above 1.0 ({'; '.join(over)}), measured cause: {BAND_LOCALITY[frame]}"
+    return (f"SUSPECT: above 1.0 ({'; '.join(over)}) with no measured cause; treat as a probe "
+            "artifact")
 
 
 def share_probe(scene, stream, steps: int, inflight: int, ns=(2, 4, 8), exchange: str = "rgb",
