@@ -2121,13 +2121,23 @@ __device__ __forceinline__ V3 resolve_pixel(const RenderParams& P, unsigned rec,
 
 // rt_resolve_rows: row-major pixel records (a row band's, received whole) into the row-major
 // frame, rows [row_begin, row_end) of the camera's own frame; one thread per pixel.
+#ifndef RT_RESOLVE_PATCH  // (A/B builds: 0 = 256 consecutive pixels of a row per workgroup)
+#define RT_RESOLVE_PATCH 1
+#endif
 template <bool SPHERES>
 __global__ __launch_bounds__(256) void resolve_rows_kernel(RenderParams P, const unsigned* rec,
                                                            int row_begin, int row_end) {
+#if RT_RESOLVE_PATCH
+  // a 32 x 8 patch of pixels per workgroup: neighbouring rows' hits share primitives
+  const int px = (int)blockIdx.x * 32 + (int)(threadIdx.x & 31);
+  const long long py = row_begin + (long long)blockIdx.y * 8 + (threadIdx.x >> 5);
+  if (px >= P.width || py >= row_end) return;
+#else
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   const long long py = row_begin + i / P.width;
   if (py >= row_end) return;
   const int px = (int)(i % P.width);
+#endif
   const size_t pix = (size_t)py * P.width + px;
   const V3 color = resolve_pixel<SPHERES>(P, rec[pix], px, (int)py);
   float* o = P.out + 3 * pix;
@@ -2140,7 +2150,9 @@ hipError_t launch_resolve_rows(const RenderParams& P, const unsigned* rec, int r
                                int row_end, bool spheres, hipStream_t stream) {
   const long long n = (long long)(row_end - row_begin) * P.width;
   if (n <= 0) return hipSuccess;
-  const dim3 grid((unsigned)((n + 255) / 256));
+  const dim3 grid = RT_RESOLVE_PATCH ? dim3((unsigned)((P.width + 31) / 32),
+                                            (unsigned)((row_end - row_begin + 7) / 8))
+                                     : dim3((unsigned)((n + 255) / 256));
   if (spheres)
     hipLaunchKernelGGL(resolve_rows_kernel<true>, grid, dim3(256), 0, stream, P, rec, row_begin, row_end);
   else
