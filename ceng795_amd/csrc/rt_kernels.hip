@@ -2124,13 +2124,17 @@ __device__ __forceinline__ V3 resolve_pixel(const RenderParams& P, unsigned rec,
 #ifndef RT_RESOLVE_PATCH  // (A/B builds: 0 = 256 consecutive pixels of a row per workgroup)
 #define RT_RESOLVE_PATCH 1
 #endif
+#ifndef RT_RESOLVE_PW  // patch width (A/B builds); height 256 / width
+#define RT_RESOLVE_PW 32
+#endif
+constexpr int kResolvePW = RT_RESOLVE_PW, kResolvePH = 256 / RT_RESOLVE_PW;
 template <bool SPHERES>
 __global__ __launch_bounds__(256) void resolve_rows_kernel(RenderParams P, const unsigned* rec,
                                                            int row_begin, int row_end) {
 #if RT_RESOLVE_PATCH
   // a 32 x 8 patch of pixels per workgroup: neighbouring rows' hits share primitives
-  const int px = (int)blockIdx.x * 32 + (int)(threadIdx.x & 31);
-  const long long py = row_begin + (long long)blockIdx.y * 8 + (threadIdx.x >> 5);
+  const int px = (int)blockIdx.x * kResolvePW + (int)(threadIdx.x % kResolvePW);
+  const long long py = row_begin + (long long)blockIdx.y * kResolvePH + (threadIdx.x / kResolvePW);
   if (px >= P.width || py >= row_end) return;
 #else
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -2150,8 +2154,8 @@ hipError_t launch_resolve_rows(const RenderParams& P, const unsigned* rec, int r
                                int row_end, bool spheres, hipStream_t stream) {
   const long long n = (long long)(row_end - row_begin) * P.width;
   if (n <= 0) return hipSuccess;
-  const dim3 grid = RT_RESOLVE_PATCH ? dim3((unsigned)((P.width + 31) / 32),
-                                            (unsigned)((row_end - row_begin + 7) / 8))
+  const dim3 grid = RT_RESOLVE_PATCH ? dim3((unsigned)((P.width + kResolvePW - 1) / kResolvePW),
+                                            (unsigned)((row_end - row_begin + kResolvePH - 1) / kResolvePH))
                                      : dim3((unsigned)((n + 255) / 256));
   if (spheres)
     hipLaunchKernelGGL(resolve_rows_kernel<true>, grid, dim3(256), 0, stream, P, rec, row_begin, row_end);
