@@ -378,3 +378,23 @@ def test_prebuilt_tree_is_validated(scene_dir, tmp_path):
     bad[k] += 1
     refused(bad, boxes, objs, "preorder")
     refused(children[:-2], boxes[:-6], objs, "internal nodes")
+
+
+def test_bench_efficiency_check_names_every_prediction_above_one():
+    """bench.py's efficiency_check: any predicted efficiency above 1.0 —
+    the line's own split or the RGB bands, record bands and tile deal beside it — is either
+    tied to its measured cause (C4's band locality, profiles/r06/band_locality.json) or
+    flagged SUSPECT; none above 1.0 reads ok."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    ok = {"8": {"predicted_efficiency": 0.85, "bands": {"predicted_efficiency": 0.9},
+                "tiles": {"predicted_efficiency": 0.6}}}
+    assert bench.efficiency_check("1920x1080", ok).startswith("ok")
+    c3 = {"2": {"predicted_efficiency": 0.97, "bands": {"predicted_efficiency": 1.003}}}
+    msg = bench.efficiency_check("1920x1080", c3)
+    assert msg.startswith("SUSPECT") and "N = 2 rgb bands 1.003" in msg
+    c4 = {"2": {"predicted_efficiency": 1.01, "bands_records": {"predicted_efficiency": 1.01}}}
+    msg = bench.efficiency_check("3840x2160", c4)
+    assert msg.startswith("above 1.0") and "band_locality.json" in msg
+    assert os.path.exists(os.path.join(os.path.dirname(bench.__file__), "profiles", "r06",
+                                       "band_locality.json"))
